@@ -1,0 +1,261 @@
+// Python bindings for the gfx950 kernel library (torch tensors -> raw launchers).
+// Every entry point validates shapes/dtypes/devices on the host BEFORE launching, so a
+// mis-shaped call raises instead of faulting the GPU, and launches on torch's current HIP
+// stream (graph-capturable: no allocation, no sync inside).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int dllm_norm(const void*, const void*, void*, const void*, const void*, void*, int, int, long, long, float, int,
+              hipStream_t);
+int dllm_rope_kv(const void*, long, const int*, const float*, const int*, void*, void*, void*, int, int, int, int, int,
+                 hipStream_t);
+int dllm_kv_write(const void*, const void*, long, const int*, void*, void*, int, int, int, int, hipStream_t);
+int dllm_paged_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*,
+                         const int*, const int*, void*, float*, float*, int, int, int, int, int, int, int, float,
+                         hipStream_t);
+int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
+int dllm_gelu(const void*, void*, long, hipStream_t);
+int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
+int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
+int dllm_argmax(const void*, long, int, int, int, int*, hipStream_t);
+int dllm_sample_topp(const float*, const long*, int, int, const float*, const float*, const float*, int*, hipStream_t);
+int dllm_cosine_scores(const float*, const float*, float*, int, int, int, hipStream_t);
+int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
+                              unsigned long long*, hipStream_t);
+}
+
+namespace {
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_dev(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_bf16(const torch::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bf16");
+}
+void check_i32(const torch::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kInt32 && t.is_contiguous(), name, " must be contiguous int32");
+}
+void check_f32(const torch::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32 && t.is_contiguous(), name, " must be contiguous f32");
+}
+void ok(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " launch failed, code ", rc); }
+
+// y = norm(x (+ residual)) * w (+ b); residual (if given) is updated in place to x + residual.
+void norm(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor w, c10::optional<torch::Tensor> b,
+          torch::Tensor y, double eps, bool layernorm) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.stride(1) == 1 && y.stride(1) == 1, "x, y: 2-D row-major");
+  const int rows = x.size(0), H = x.size(1);
+  TORCH_CHECK(y.size(0) == rows && y.size(1) == H && w.numel() == H, "shape mismatch");
+  const void* rp = nullptr;
+  if (residual) {
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == rows && residual->size(1) == H, "residual shape");
+    rp = residual->data_ptr();
+  }
+  const void* bp = nullptr;
+  if (layernorm) {
+    TORCH_CHECK(b.has_value(), "layernorm needs bias");
+    check_bf16(*b, "b");
+    bp = b->data_ptr();
+  }
+  ok(dllm_norm(x.data_ptr(), rp, residual ? residual->data_ptr() : nullptr, w.data_ptr(), bp, y.data_ptr(), rows, H,
+               x.stride(0), y.stride(0), (float)eps, layernorm ? 1 : 0, stream()),
+     "norm");
+}
+
+void rope_kv(torch::Tensor qkv, torch::Tensor pos, torch::Tensor cos_sin, torch::Tensor slots, torch::Tensor q_out,
+             torch::Tensor kc, torch::Tensor vc, int64_t nq, int64_t nkv, int64_t d) {
+  check_bf16(qkv, "qkv");
+  check_i32(pos, "positions");
+  check_f32(cos_sin, "cos_sin");
+  check_i32(slots, "slot_mapping");
+  check_bf16(q_out, "q_out");
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (nq + 2 * nkv) * d, "qkv shape");
+  const int T = qkv.size(0);
+  TORCH_CHECK(pos.numel() == T && slots.numel() == T, "positions/slots length");
+  TORCH_CHECK(q_out.is_contiguous() && q_out.numel() == (int64_t)T * nq * d, "q_out shape");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == d, "cos_sin must be [max_pos, d]");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.size(1) == nkv && kc.size(2) == 16 &&
+                  kc.size(3) == d && vc.size(2) == d && vc.size(3) == 16,
+              "cache layout: K [blocks, nkv, 16, d], V [blocks, nkv, d, 16]");
+  if (T == 0) return;
+  ok(dllm_rope_kv(qkv.data_ptr(), qkv.stride(0), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                  slots.data_ptr<int>(), q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(), T, nq, nkv, d, 16, stream()),
+     "rope_kv");
+}
+
+void kv_write(torch::Tensor k, torch::Tensor v, torch::Tensor slots, torch::Tensor kc, torch::Tensor vc) {
+  check_bf16(k, "k");
+  check_bf16(v, "v");
+  check_i32(slots, "slots");
+  TORCH_CHECK(k.dim() == 3 && k.is_contiguous() && v.is_contiguous() && v.sizes() == k.sizes(), "k/v [T, nkv, d]");
+  const int T = k.size(0), nkv = k.size(1), d = k.size(2);
+  TORCH_CHECK(kc.size(1) == nkv && kc.size(3) == d, "cache shape");
+  if (T == 0) return;
+  ok(dllm_kv_write(k.data_ptr(), v.data_ptr(), (long)nkv * d, slots.data_ptr<int>(), kc.data_ptr(), vc.data_ptr(), T,
+                   nkv, d, 16, stream()),
+     "kv_write");
+}
+
+void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
+                     torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
+                     torch::Tensor tile_tok0, torch::Tensor out, c10::optional<torch::Tensor> part_o,
+                     c10::optional<torch::Tensor> part_ml, int64_t splits, bool causal, double scale) {
+  check_bf16(q, "q");
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  check_bf16(out, "out");
+  for (auto* t : {&block_tables, &qstart, &qlen, &ctx, &tile_seq, &tile_tok0}) check_i32(*t, "attention metadata");
+  TORCH_CHECK(q.dim() == 3 && q.is_contiguous() && out.is_contiguous() && out.sizes() == q.sizes(), "q/out [T, nq, d]");
+  const int nq = q.size(1), d = q.size(2);
+  TORCH_CHECK(kc.dim() == 4 && kc.size(2) == 16 && kc.size(3) == d && vc.size(2) == d && vc.size(3) == 16,
+              "cache layout");
+  const int nkv = kc.size(1);
+  TORCH_CHECK(nq % nkv == 0 && 16 % (nq / nkv) == 0, "GQA group must divide 16");
+  TORCH_CHECK(d == 64 || d == 96 || d == 128, "head_dim must be 64, 96 or 128");
+  TORCH_CHECK(block_tables.dim() == 2, "block_tables [num_seqs, max_blocks]");
+  const int num_seqs = block_tables.size(0);
+  TORCH_CHECK(qstart.numel() == num_seqs && qlen.numel() == num_seqs && ctx.numel() == num_seqs, "seq metadata len");
+  const int num_tiles = tile_seq.numel();
+  TORCH_CHECK(tile_tok0.numel() == num_tiles, "tile metadata len");
+  float* po = nullptr;
+  float* pml = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "split-K needs workspaces");
+    check_f32(*part_o, "part_o");
+    check_f32(*part_ml, "part_ml");
+    TORCH_CHECK(part_o->numel() >= (int64_t)num_tiles * nkv * splits * 16 * d &&
+                    part_ml->numel() >= (int64_t)num_tiles * nkv * splits * 16 * 2,
+                "workspace too small");
+    po = part_o->data_ptr<float>();
+    pml = part_ml->data_ptr<float>();
+  }
+  ok(dllm_paged_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
+                          qstart.data_ptr<int>(), qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(),
+                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, num_tiles, nq, nkv, d,
+                          block_tables.size(1), splits, causal ? 1 : 0, (float)scale, stream()),
+     "paged_attention");
+}
+
+void silu_mul(torch::Tensor gu, torch::Tensor out) {
+  check_bf16(gu, "gate_up");
+  check_bf16(out, "out");
+  TORCH_CHECK(gu.dim() == 2 && gu.stride(1) == 1 && out.is_contiguous(), "2-D row-major");
+  const long T = gu.size(0);
+  const int I = gu.size(1) / 2;
+  TORCH_CHECK(out.size(0) == T && out.size(1) == I, "out shape");
+  ok(dllm_silu_mul(gu.data_ptr(), out.data_ptr(), T, I, gu.stride(0), stream()), "silu_mul");
+}
+
+void gelu(torch::Tensor x, torch::Tensor y) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "contiguous same-size");
+  ok(dllm_gelu(x.data_ptr(), y.data_ptr(), x.numel(), stream()), "gelu");
+}
+
+void mean_pool_l2(torch::Tensor x, torch::Tensor lens, torch::Tensor out) {
+  check_bf16(x, "x");
+  check_i32(lens, "lens");
+  check_f32(out, "out");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "x [B, S, H]");
+  const int B = x.size(0), S = x.size(1), H = x.size(2);
+  TORCH_CHECK(lens.numel() == B && out.size(0) == B && out.size(1) == H, "shapes");
+  ok(dllm_mean_pool_l2(x.data_ptr(), lens.data_ptr<int>(), out.data_ptr<float>(), B, S, H, stream()), "mean_pool_l2");
+}
+
+void moe_gate(torch::Tensor logits, int64_t k, torch::Tensor ids, torch::Tensor w) {
+  check_f32(logits, "router_logits");
+  check_i32(ids, "ids");
+  check_f32(w, "weights");
+  const int T = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(ids.numel() == (int64_t)T * k && w.numel() == (int64_t)T * k, "out shapes");
+  ok(dllm_moe_gate(logits.data_ptr<float>(), T, E, k, ids.data_ptr<int>(), w.data_ptr<float>(), stream()), "moe_gate");
+}
+
+void argmax(torch::Tensor logits, torch::Tensor out) {
+  check_dev(logits, "logits");
+  check_i32(out, "out");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] row-major");
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "logits bf16 or f32");
+  TORCH_CHECK(logits.stride(0) % (bf ? 8 : 4) == 0, "row stride must keep 16-B alignment");
+  TORCH_CHECK(out.numel() == logits.size(0), "out len");
+  ok(dllm_argmax(logits.data_ptr(), logits.stride(0), logits.size(0), logits.size(1), bf ? 1 : 0,
+                 out.data_ptr<int>(), stream()),
+     "argmax");
+}
+
+void sample_topp(torch::Tensor vals, torch::Tensor idx, torch::Tensor temp, torch::Tensor top_p, torch::Tensor u,
+                 torch::Tensor out) {
+  check_f32(vals, "vals");
+  check_dev(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == torch::kInt64 && idx.is_contiguous(), "idx int64");
+  check_f32(temp, "temperature");
+  check_f32(top_p, "top_p");
+  check_f32(u, "uniform");
+  check_i32(out, "out");
+  const int B = vals.size(0), K = vals.size(1);
+  TORCH_CHECK(idx.size(0) == B && idx.size(1) == K && temp.numel() == B && top_p.numel() == B && u.numel() == B &&
+                  out.numel() == B,
+              "shapes");
+  ok(dllm_sample_topp(vals.data_ptr<float>(), (const long*)idx.data_ptr<int64_t>(), B, K, temp.data_ptr<float>(),
+                      top_p.data_ptr<float>(), u.data_ptr<float>(), out.data_ptr<int>(), stream()),
+     "sample_topp");
+}
+
+void cosine_scores(torch::Tensor q, torch::Tensor c, torch::Tensor s) {
+  check_f32(q, "q");
+  check_f32(c, "c");
+  check_f32(s, "s");
+  TORCH_CHECK(q.dim() == 2 && c.dim() == 2 && q.size(1) == c.size(1), "q [B,d], c [N,d]");
+  TORCH_CHECK(s.size(0) == q.size(0) && s.size(1) == c.size(0), "s [B,N]");
+  ok(dllm_cosine_scores(q.data_ptr<float>(), c.data_ptr<float>(), s.data_ptr<float>(), q.size(0), c.size(0),
+                        q.size(1), stream()),
+     "cosine_scores");
+}
+
+void masked_cosine_argmax(torch::Tensor q, torch::Tensor table, torch::Tensor norms, torch::Tensor ctx, int64_t cid,
+                          double thr, torch::Tensor best) {
+  check_f32(q, "q");
+  check_f32(table, "table");
+  check_f32(norms, "norms");
+  check_i32(ctx, "ctx");
+  check_dev(best, "best");
+  TORCH_CHECK(best.scalar_type() == torch::kInt64 && best.numel() >= 1, "best: int64[1]");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == q.numel(), "table [N, d]");
+  const int N = table.size(0);
+  TORCH_CHECK(norms.numel() >= N && ctx.numel() >= N, "norms/ctx len");
+  ok(dllm_masked_cosine_argmax(q.data_ptr<float>(), table.data_ptr<float>(), norms.data_ptr<float>(),
+                               ctx.data_ptr<int>(), N, table.size(1), (int)cid, (float)thr,
+                               (unsigned long long*)best.data_ptr<int64_t>(), stream()),
+     "masked_cosine_argmax");
+}
+}  // namespace
+
+PYBIND11_MODULE(_hip_kernels, m) {
+  m.doc() = "gfx950 HIP kernels for distributed_llm_amd";
+  m.def("norm", &norm);
+  m.def("rope_kv", &rope_kv);
+  m.def("kv_write", &kv_write);
+  m.def("paged_attention", &paged_attention);
+  m.def("silu_mul", &silu_mul);
+  m.def("gelu", &gelu);
+  m.def("mean_pool_l2", &mean_pool_l2);
+  m.def("moe_gate", &moe_gate);
+  m.def("argmax", &argmax);
+  m.def("sample_topp", &sample_topp);
+  m.def("cosine_scores", &cosine_scores);
+  m.def("masked_cosine_argmax", &masked_cosine_argmax);
+}

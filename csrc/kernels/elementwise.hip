@@ -1,0 +1,120 @@
+// Memory-bound elementwise / small-reduction kernels (all 16-B vectorised, f32 math):
+//   silu_mul     : out[t, i] = silu(gu[t, i]) * gu[t, I + i]        (SwiGLU, fused gate|up GEMM output)
+//   gelu         : y = 0.5 x (1 + erf(x / sqrt 2))                    (MiniLM FFN)
+//   mean_pool_l2 : out[b] = normalize(sum_s mask[b,s] x[b,s,:] / sum_s mask[b,s])   (sentence embedding)
+//   moe_gate_topk: softmax over E experts, top-k, renormalised weights (Mixtral routing)
+#include "common.h"
+
+namespace {
+
+__global__ void silu_mul_kernel(const u16* __restrict__ gu, u16* __restrict__ out, long T, int I, long in_stride) {
+  const long nvec = T * (I >> 3);
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
+    const long t = v / (I >> 3);
+    const int c = (int)(v % (I >> 3)) * 8;
+    float gf[8], uf[8], o[8];
+    unpack8(ld16(gu + t * in_stride + c), gf);
+    unpack8(ld16(gu + t * in_stride + I + c), uf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gf[j] / (1.f + __expf(-gf[j])) * uf[j];
+    st16(out + t * (long)I + c, pack8(o));
+  }
+}
+
+__global__ void gelu_kernel(const u16* __restrict__ x, u16* __restrict__ y, long n8) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(ld16(x + v * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.5f * f[j] * (1.f + erff(f[j] * 0.70710678118654752f));
+    st16(y + v * 8, pack8(f));
+  }
+}
+
+__global__ void __launch_bounds__(256) mean_pool_l2_kernel(const u16* __restrict__ x, const int* __restrict__ lens,
+                                                           float* __restrict__ out, int S, int H) {
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int n = lens[b];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // H <= 4 * blockDim
+  for (int s = 0; s < n; ++s) {
+    const u16* row = x + ((long)b * S + s) * H;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = threadIdx.x + i * blockDim.x;
+      if (h < H) acc[i] += bf2f(row[h]);
+    }
+  }
+  float ss = 0.f;
+  const float inv = n > 0 ? 1.f / n : 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { acc[i] *= inv; ss += acc[i] * acc[i]; }
+  const float nrm = sqrtf(block_sum(ss, red));
+  const float sc = 1.f / fmaxf(nrm, 1e-12f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = threadIdx.x + i * blockDim.x;
+    if (h < H) out[(long)b * H + h] = acc[i] * sc;
+  }
+}
+
+// one thread per token; E <= 64, k <= 8
+__global__ void moe_gate_kernel(const float* __restrict__ logits, int T, int E, int k, int* __restrict__ ids,
+                                float* __restrict__ w) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const float* l = logits + (long)t * E;
+  unsigned long long used = 0ull;
+  float sel[8];
+  int sid[8];
+  for (int i = 0; i < k; ++i) {
+    float best = -INFINITY;
+    int bi = 0;
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1ull) && l[e] > best) { best = l[e]; bi = e; }
+    used |= 1ull << bi;
+    sel[i] = best;
+    sid[i] = bi;
+  }
+  // softmax over all E then renormalise over the selected == softmax over the selected logits
+  float s = 0.f;
+  for (int i = 0; i < k; ++i) { sel[i] = __expf(sel[i] - sel[0]); s += sel[i]; }
+  for (int i = 0; i < k; ++i) { ids[(long)t * k + i] = sid[i]; w[(long)t * k + i] = sel[i] / s; }
+}
+}  // namespace
+
+static inline int grid_for(long n, int threads) {
+  long g = (n + threads - 1) / threads;
+  if (g > 65536) g = 65536;
+  return g < 1 ? 1 : (int)g;
+}
+
+extern "C" int dllm_silu_mul(const void* gu, void* out, long T, int I, long in_stride, hipStream_t stream) {
+  if (I % 8 != 0) return -1;
+  const long n = T * (I / 8);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u16*)gu, (u16*)out, T, I,
+                     in_stride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_gelu(const void* x, void* y, long n, hipStream_t stream) {
+  if (n % 8 != 0) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(gelu_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, stream, (const u16*)x, (u16*)y, n / 8);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_mean_pool_l2(const void* x, const int* lens, float* out, int B, int S, int H, hipStream_t stream) {
+  int threads = ((H + 3) / 4 + 63) / 64 * 64;
+  if (threads > 256 || threads * 4 < H) return -1;
+  hipLaunchKernelGGL(mean_pool_l2_kernel, dim3(B), dim3(threads), 0, stream, (const u16*)x, lens, out, S, H);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_moe_gate(const float* logits, int T, int E, int k, int* ids, float* w, hipStream_t stream) {
+  if (E > 64 || k > 8 || k > E) return -1;
+  if (T == 0) return 0;
+  hipLaunchKernelGGL(moe_gate_kernel, dim3((T + 127) / 128), dim3(128), 0, stream, logits, T, E, k, ids, w);
+  return (int)hipGetLastError();
+}

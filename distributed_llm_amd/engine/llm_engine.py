@@ -1,0 +1,463 @@
+"""LLM serving engine: paged KV cache, prefix caching, continuous batching, hipGraph decode.
+
+Replaces the reference's external Ollama/llama.cpp engine (the hot loop of
+§3.2).  Structure:
+  * ``BlockManager`` (native, csrc/runtime/block_manager.cpp) — 16-token KV blocks with
+    hash-chained prefix caching: a new turn of a conversation reuses the previous turn's KV;
+  * scheduler — FIFO admission, chunked prefill under a token budget, prefill-first, then
+    one decode step for every running sequence (continuous batching);
+  * decode runner — each running sequence owns a ROW of persistent per-row metadata
+    (block table row, context length) on the device; a decode step uploads ONE small packed
+    int32 buffer and replays a hipGraph captured for the batch-size bucket (model forward +
+    greedy arg-max), so the host cost per step is O(batch) numpy work + one memcpy + one
+    graph launch;
+  * prefill runner — eager (shapes vary), packed variable-length batch, attention over the
+    cached prefix + new tokens with the same paged kernel.
+KV memory is sized for 288 GB HBM3E parts: ``kv_cache_gb`` (default: 60 % of free memory).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.configs import ModelConfig, get_model_config
+from ..models.llama import AttnMeta, LlamaModel
+from ..parallel.comm import SINGLE, ParallelContext
+from .sampling import SamplingParams
+from .tokenizer import get_tokenizer
+
+try:
+    from . import _runtime  # type: ignore
+except ImportError as _e:  # pragma: no cover - build step missing
+    _runtime = None
+    _runtime_err = _e
+
+BS = ops.BLOCK_SIZE
+
+
+def _need_runtime():
+    if _runtime is None:
+        raise RuntimeError(f"native runtime not built ({_runtime_err}); run `python -m distributed_llm_amd._build`")
+    return _runtime
+
+
+@dataclass
+class RequestOutput:
+    request_id: int
+    text: str
+    token_ids: List[int]
+    num_prompt: int
+    num_cached: int
+    num_generated: int
+    latency_ms: float
+    ttft_ms: float
+    queue_ms: float
+    decode_tok_s: float
+    error: Optional[str] = None
+
+    @property
+    def num_prefill(self) -> int:
+        return self.num_prompt - self.num_cached
+
+
+@dataclass
+class _Seq:
+    id: int
+    prompt: List[int]
+    params: SamplingParams
+    arrival: float
+    out: List[int] = field(default_factory=list)
+    fill: List[int] = field(default_factory=list)   # tokens to (re)compute on admission: prompt + out
+    num_cached: int = 0
+    num_computed: int = 0
+    row: int = -1
+    admitted: Optional[float] = None
+    first_tok: Optional[float] = None
+    finished: Optional[float] = None
+    error: Optional[str] = None
+
+    @property
+    def length(self) -> int:
+        return len(self.prompt) + len(self.out)
+
+
+class LLMEngine:
+    def __init__(self, model: Union[str, ModelConfig], device: str = "cuda", par: ParallelContext = SINGLE,
+                 kv_cache_gb: Optional[float] = None, max_num_seqs: int = 256, max_model_len: Optional[int] = None,
+                 max_prefill_tokens: int = 16384, prefix_cache: bool = True, use_graphs: bool = True,
+                 seed: int = 0, weights: Optional[str] = None, tokenizer: Optional[str] = None):
+        self.cfg = get_model_config(model) if isinstance(model, str) else model
+        self.device = torch.device(device)
+        self.par = par
+        self.model = LlamaModel(self.cfg, device=self.device, par=par, seed=seed, weights=weights)
+        self.tok = get_tokenizer(self.cfg.vocab, self.cfg.bos_id, self.cfg.eos_id, tokenizer)
+        self.max_model_len = min(max_model_len or self.cfg.max_position, self.cfg.max_position)
+        self.max_num_seqs = max_num_seqs
+        self.max_prefill_tokens = max_prefill_tokens
+        self.max_blocks = (self.max_model_len + BS - 1) // BS
+        self._alloc_kv(kv_cache_gb)
+        self.bm = _need_runtime().BlockManager(self.num_blocks, BS, prefix_cache)
+        self._ids = itertools.count()
+        self._lock = threading.Lock()
+        self.on_gpu = self.device.type == "cuda"
+        self.use_graphs = use_graphs and self.on_gpu
+        self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
+        self._gen.manual_seed(seed + 1)
+        self._init_rows()
+        self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self._graph_pool = None
+        self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
+
+    # ------------------------------------------------------------------ setup
+    def _alloc_kv(self, kv_cache_gb: Optional[float]) -> None:
+        m, L = self.model, self.cfg.n_layers
+        per_block = L * 2 * m.nkv * BS * m.d * 2
+        if kv_cache_gb is None:
+            if self.device.type == "cuda":
+                free, _ = torch.cuda.mem_get_info(self.device)
+                kv_cache_gb = 0.6 * free / 2**30
+            else:
+                kv_cache_gb = 0.25
+        self.num_blocks = max(int(kv_cache_gb * 2**30) // per_block, self.max_blocks + 8)
+        self.k_cache = torch.empty((L, self.num_blocks, m.nkv, BS, m.d), dtype=m.dtype, device=self.device)
+        self.v_cache = torch.empty((L, self.num_blocks, m.nkv, m.d, BS), dtype=m.dtype, device=self.device)
+        self.kv_caches = [(self.k_cache[i], self.v_cache[i]) for i in range(L)]
+
+    def _init_rows(self) -> None:
+        R = self.max_num_seqs
+        self.R = R
+        self._free_rows = list(range(R - 1, -1, -1))
+        self.bt_host = np.zeros((R + 1, self.max_blocks), dtype=np.int32)  # row R: dummy (padding)
+        self.bt_dev = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, device=self.device)
+        self._bt_dirty = True
+        self.buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if b < R] + [R]
+        mb = self.buckets[-1]
+        # packed decode buffer: ids | pos | slots | tile_seq  (mb each) | qstart | qlen | ctx (R+1 each)
+        self._dec_n = 4 * mb + 3 * (R + 1)
+        self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
+        pin = self.on_gpu
+        self.dec_host_t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
+        self.dec_host = self.dec_host_t.numpy()
+        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1)]
+        self._off = o
+        d = self.dec_dev
+        self.d_ids, self.d_pos, self.d_slots, self.d_tseq = (d[o[0]:o[1]], d[o[1]:o[2]], d[o[2]:o[3]], d[o[3]:o[4]])
+        self.d_qstart, self.d_qlen, self.d_ctx = d[o[4]:o[5]], d[o[5]:o[6]], d[o[6]:o[6] + R + 1]
+        self.d_tok0 = torch.zeros(mb, dtype=torch.int32, device=self.device)
+        self.d_last = torch.arange(mb, dtype=torch.int64, device=self.device)
+        self.d_out = torch.zeros(mb, dtype=torch.int32, device=self.device)
+        self.d_hidden = torch.zeros((mb, self.cfg.hidden), dtype=self.model.dtype, device=self.device)
+        nkv, dh = self.model.nkv, self.model.d
+        self.max_splits = 16
+        ws = mb * nkv * self.max_splits * 16
+        self.dec_ws = (torch.empty(ws * dh, dtype=torch.float32, device=self.device),
+                       torch.empty(ws * 2, dtype=torch.float32, device=self.device))
+
+    def _splits_for(self, tiles: int) -> int:
+        return int(max(1, min(self.max_splits, math.ceil(1024 / max(1, tiles * self.model.nkv)))))
+
+    # ------------------------------------------------------------------ public API
+    def encode(self, text: str) -> List[int]:
+        ids = self.tok.encode(text)
+        return ids
+
+    def generate(self, prompts: Sequence[Union[str, List[int]]],
+                 params: Union[SamplingParams, Sequence[SamplingParams], None] = None) -> List[RequestOutput]:
+        """Run a batch of requests to completion with continuous batching."""
+        if params is None:
+            params = SamplingParams()
+        plist = list(params) if isinstance(params, (list, tuple)) else [params] * len(prompts)
+        now = time.perf_counter()
+        seqs: List[_Seq] = []
+        for p, sp in zip(prompts, plist):
+            ids = self.encode(p) if isinstance(p, str) else list(p)
+            s = _Seq(next(self._ids), ids, sp, now)
+            limit = self.max_model_len - max(1, sp.max_new_tokens)
+            if len(ids) > limit:  # keep the most recent context (left truncation)
+                s.prompt = ids[:1] + ids[len(ids) - limit + 1:]
+            if len(s.prompt) == 0 or limit <= 1:
+                s.error = "prompt too long for max_model_len"
+            seqs.append(s)
+        with self._lock:
+            self._run(seqs)
+        return [self._output(s) for s in seqs]
+
+    def stats(self) -> Dict[str, object]:
+        st = dict(self.bm.stats())
+        st.update(self.steps)
+        st["model"] = self.cfg.name
+        st["kv_blocks"] = self.num_blocks
+        return st
+
+    # ------------------------------------------------------------------ scheduling
+    def _run(self, seqs: List[_Seq]) -> None:
+        waiting = [s for s in seqs if s.error is None]
+        prefilling: List[_Seq] = []
+        running: List[_Seq] = []
+        while waiting or prefilling or running:
+            # admit
+            while waiting and len(prefilling) + len(running) < self.R:
+                s = waiting[0]
+                s.fill = s.prompt + s.out
+                if not self.bm.can_allocate(len(s.fill) + 1):
+                    break
+                table, cached = self.bm.allocate(s.id, s.fill)
+                if not table:
+                    break
+                waiting.pop(0)
+                s.num_cached = s.num_computed = cached
+                s.admitted = time.perf_counter()
+                s.row = self._free_rows.pop()
+                self._set_row_blocks(s)
+                prefilling.append(s)
+            if not (prefilling or running):
+                if waiting:  # nothing fits even alone -> fail the head request
+                    s = waiting.pop(0)
+                    s.error = "insufficient KV cache for request"
+                continue
+            if prefilling:
+                done = self._prefill_step(prefilling)
+                for s in done:
+                    prefilling.remove(s)
+                    if self._finished(s):
+                        self._release(s)
+                    else:
+                        running.append(s)
+                continue
+            self._decode_step(running)
+            for s in [s for s in running if self._finished(s)]:
+                running.remove(s)
+                self._release(s)
+            # out of KV blocks for a running sequence: preempt the youngest and re-queue it
+            for s in [s for s in running if s.error == "__preempt__"]:
+                running.remove(s)
+                self._release(s, keep=False)
+                s.error = None
+                waiting.insert(0, s)  # re-admitted with fill = prompt + out (recompute)
+
+    def _finished(self, s: _Seq) -> bool:
+        if s.error is not None and s.error != "__preempt__":
+            return True
+        if not s.out:
+            return False
+        if len(s.out) >= s.params.max_new_tokens:
+            return True
+        if not s.params.ignore_eos and s.out[-1] == self.tok.eos_id:
+            return True
+        return s.length >= self.max_model_len
+
+    def _release(self, s: _Seq, keep: bool = True) -> None:
+        if keep:
+            s.finished = time.perf_counter()
+        self.bm.free(s.id)
+        if s.row >= 0:
+            self.bt_host[s.row].fill(0)
+            self._free_rows.append(s.row)
+            s.row = -1
+
+    def _set_row_blocks(self, s: _Seq) -> None:
+        t = self.bm.block_table(s.id)
+        self.bt_host[s.row, :len(t)] = t
+        self._bt_dirty = True
+
+    def _sync_bt(self) -> None:
+        if self._bt_dirty:
+            self.bt_dev.copy_(torch.from_numpy(self.bt_host), non_blocking=False)
+            self._bt_dirty = False
+
+    # ------------------------------------------------------------------ sampling
+    def _sample(self, hidden: torch.Tensor, seqs: List[_Seq], greedy_ids: Optional[torch.Tensor]) -> List[int]:
+        n = len(seqs)
+        if all(s.params.greedy for s in seqs):
+            ids = greedy_ids[:n] if greedy_ids is not None else self.model.greedy(hidden[:n])
+            return ids.tolist()
+        k = max(s.params.k for s in seqs)
+        vals, idx = self.model.topk_candidates(hidden[:n], k)
+        temp = torch.tensor([s.params.temperature if not s.params.greedy else 1e-5 for s in seqs],
+                            dtype=torch.float32, device=hidden.device)
+        top_p = torch.tensor([s.params.top_p if not s.params.greedy else 0.0 for s in seqs],
+                             dtype=torch.float32, device=hidden.device)
+        # per-row top-k: mask candidates beyond each row's k
+        ks = torch.tensor([s.params.k for s in seqs], device=hidden.device)
+        cols = torch.arange(vals.shape[1], device=hidden.device)[None, :]
+        vals = torch.where(cols < ks[:, None], vals, torch.full_like(vals, -float("inf")))
+        u = torch.rand(n, generator=self._gen, device=hidden.device)
+        if self.par.tp_size > 1:  # every TP rank must draw the same token
+            self.par.all_reduce(u)
+            u /= self.par.tp_size
+        return ops.sample_top_p(vals, idx, temp, top_p, u).tolist()
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill_step(self, prefilling: List[_Seq]) -> List[_Seq]:
+        budget = self.max_prefill_tokens
+        chunk: List[tuple] = []
+        for s in prefilling:
+            if budget <= 0:
+                break
+            n = min(len(s.fill) - s.num_computed, budget)
+            chunk.append((s, s.num_computed, s.num_computed + n))
+            budget -= n
+        ids, pos, slots, qstart, qlen, ctx, last = [], [], [], [], [], [], []
+        G = self.model.nq // self.model.nkv
+        tseq, ttok = [], []
+        t = 0
+        for i, (s, a, b) in enumerate(chunk):
+            ids.extend(s.fill[a:b])
+            pos.extend(range(a, b))
+            slots.extend(self.bm.slots(s.id, a, b))
+            qstart.append(t)
+            qlen.append(b - a)
+            ctx.append(b)
+            t += b - a
+            last.append(t - 1)
+            ts, tt = ops.build_tiles([b - a], G)
+            tseq.extend([i] * len(ts))
+            ttok.extend(tt)
+        nb = max((ctx_i + BS - 1) // BS for ctx_i in ctx)
+        bt = np.zeros((len(chunk), nb), dtype=np.int32)
+        for i, (s, _, _) in enumerate(chunk):
+            row = self.bt_host[s.row, :nb]
+            bt[i] = row
+        dev = self.device
+        T = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt, device=dev)
+        splits = self._splits_for(len(tseq))
+        meta = AttnMeta(slots=T(slots), block_tables=torch.from_numpy(bt).to(dev), qstart=T(qstart), qlen=T(qlen),
+                        ctx=T(ctx), tile_seq=T(tseq), tile_tok0=T(ttok), last_idx=T(last, torch.int64),
+                        splits=splits)
+        hidden = self.model.hidden_states(T(ids), T(pos), meta, self.kv_caches)
+        self.steps["prefill"] += 1
+        self.steps["prefill_tokens"] += t
+        done_seqs = [s for (s, a, b) in chunk if b == len(s.fill)]
+        for s, a, b in chunk:
+            s.num_computed = b
+            self.bm.commit(s.id, b)
+        if not done_seqs:
+            return []
+        sel = [i for i, (s, a, b) in enumerate(chunk) if b == len(s.fill)]
+        h = hidden if len(sel) == len(chunk) else hidden.index_select(0, T(sel, torch.int64))
+        toks = self._sample(h, done_seqs, None)
+        now = time.perf_counter()
+        for s, tok in zip(done_seqs, toks):
+            if s.first_tok is None:
+                s.first_tok = now
+            self._append(s, tok)
+        return done_seqs
+
+    def _append(self, s: _Seq, tok: int) -> None:
+        s.out.append(int(tok))
+        if self._finished(s):
+            return
+        slot = self.bm.append_token(s.id, int(tok))
+        if slot < 0:
+            s.error = "__preempt__"
+            return
+        nblk = (s.length + BS - 1) // BS
+        if self.bt_host[s.row, nblk - 1] != slot // BS:
+            self.bt_host[s.row, nblk - 1] = slot // BS
+            self._bt_dirty = True
+
+    # ------------------------------------------------------------------ decode
+    def _bucket(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        raise ValueError(f"batch {n} exceeds max_num_seqs")
+
+    def _decode_step(self, running: List[_Seq]) -> None:
+        B = len(running)
+        bs = self._bucket(B)
+        o, h = self._off, self.dec_host
+        R = self.R
+        rows = np.fromiter((s.row for s in running), dtype=np.int64, count=B)
+        lens = np.fromiter((s.length for s in running), dtype=np.int64, count=B)
+        last = np.fromiter((s.out[-1] for s in running), dtype=np.int64, count=B)
+        pos = lens - 1
+        blocks = self.bt_host[rows, pos // BS].astype(np.int64)
+        h[o[0]:o[0] + bs] = 0
+        h[o[0]:o[0] + B] = last
+        h[o[1]:o[1] + bs] = 0
+        h[o[1]:o[1] + B] = pos
+        h[o[2]:o[2] + bs] = -1
+        h[o[2]:o[2] + B] = blocks * BS + pos % BS
+        h[o[3]:o[3] + bs] = R            # padding tiles -> dummy row (qlen 0)
+        h[o[3]:o[3] + B] = rows
+        h[o[4]:o[6] + R + 1] = 0
+        h[o[4] + rows] = np.arange(B)
+        h[o[5] + rows] = 1
+        h[o[6] + rows] = lens
+        self._sync_bt()
+        self.dec_dev.copy_(self.dec_host_t, non_blocking=True)
+        if self.use_graphs:
+            g = self._graphs.get(bs)
+            if g is None:
+                g = self._capture(bs)
+            g.replay()
+        else:
+            self._decode_forward(bs)
+        self.steps["decode"] += 1
+        self.steps["decode_tokens"] += B
+        toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
+        for s, t in zip(running, toks):
+            self.bm.commit(s.id, s.length)
+            self._append(s, t)
+
+    def _decode_meta(self, bs: int) -> AttnMeta:
+        return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
+                        ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
+                        last_idx=self.d_last[:bs], splits=self._splits_for(bs), workspace=self.dec_ws)
+
+    def _decode_forward(self, bs: int) -> None:
+        hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches)
+        self.d_hidden[:bs].copy_(hid)
+        self.d_out[:bs].copy_(self.model.greedy(hid))
+
+    def _capture(self, bs: int) -> "torch.cuda.CUDAGraph":
+        # warm up (lazy library init must not happen inside capture), then capture
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._decode_forward(bs)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._graph_pool):
+            self._decode_forward(bs)
+        self._graphs[bs] = g
+        return g
+
+    def capture_all(self, max_bs: Optional[int] = None) -> None:
+        """Pre-capture decode graphs for every bucket up to ``max_bs`` (largest first)."""
+        if not self.use_graphs:
+            return
+        # a dummy decode state: all padding (qlen 0), so capture writes nothing to the KV cache
+        self.dec_host[:] = 0
+        self.dec_host[self._off[2]:self._off[3]] = -1
+        self.dec_host[self._off[3]:self._off[4]] = self.R
+        self.dec_dev.copy_(self.dec_host_t)
+        self._sync_bt()
+        for b in sorted((b for b in self.buckets if max_bs is None or b <= max_bs), reverse=True):
+            if b not in self._graphs:
+                self._capture(b)
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ outputs
+    def _output(self, s: _Seq) -> RequestOutput:
+        end = s.finished or time.perf_counter()
+        lat = (end - s.arrival) * 1000.0
+        ttft = ((s.first_tok or end) - s.arrival) * 1000.0
+        queue = ((s.admitted or end) - s.arrival) * 1000.0
+        n = len(s.out)
+        dec_t = (end - s.first_tok) if s.first_tok else 0.0
+        toks = [t for t in s.out if t != self.tok.eos_id] if not s.params.ignore_eos else s.out
+        return RequestOutput(s.id, self.tok.decode(toks), list(s.out), len(s.prompt), s.num_cached, n, lat, ttft,
+                             queue, (n - 1) / dec_t if n > 1 and dec_t > 0 else 0.0, s.error)

@@ -1,0 +1,251 @@
+"""Llama-family decoder (TinyLlama, Llama-3.x, Phi-3, Mixtral MoE) on the HIP op library.
+
+One module covers every BASELINE.json family: they differ only in shapes, RoPE parameters,
+tied embeddings and dense-vs-MoE MLP (models.configs).  MI355X-first layout decisions:
+  * fused QKV weight [(nq + 2 nkv) d, H] and fused gate|up weight [2 I, H] — one GEMM each
+    (hipBLASLt via F.linear, K-contiguous "TN" operands);
+  * RoPE + paged-KV write fused in one kernel reading the QKV GEMM output in place;
+  * RMSNorm fused with the residual add (the residual stream is read/written once per norm);
+  * the LM head runs only on the last position of each sequence;
+  * tensor parallel (Megatron column/row split): QKV / gate|up column-parallel, o_proj /
+    down_proj row-parallel + ONE all-reduce each, vocab-parallel embedding (masked lookup +
+    all-reduce) and LM head (distributed arg-max / top-k; parallel.comm).
+Weights: random init with a fixed seed (no checkpoints in this environment) or HF safetensors.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel.comm import SINGLE, ParallelContext, shard_range
+from .configs import ModelConfig
+
+
+@dataclass
+class AttnMeta:
+    """Per-forward attention metadata (all int32 device tensors)."""
+    slots: torch.Tensor        # [T] cache slot per new token (-1: skip)
+    block_tables: torch.Tensor  # [S, max_blocks]
+    qstart: torch.Tensor       # [S]
+    qlen: torch.Tensor         # [S]
+    ctx: torch.Tensor          # [S]
+    tile_seq: torch.Tensor     # [num_tiles]
+    tile_tok0: torch.Tensor    # [num_tiles]
+    last_idx: torch.Tensor     # [S] int64 index of each sequence's last new token in the packed batch
+    splits: int = 1
+    workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, par: ParallelContext = SINGLE,
+                 seed: int = 0, weights: Optional[str] = None, init_std: float = 0.02):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.par = par
+        tp, r = par.tp_size, par.tp_rank
+        if cfg.n_heads % tp or cfg.n_kv_heads % tp or cfg.intermediate % tp or cfg.vocab % tp:
+            raise ValueError(f"{cfg.name}: heads/kv_heads/intermediate/vocab must divide tp={tp}")
+        self.nq = cfg.n_heads // tp
+        self.nkv = cfg.n_kv_heads // tp
+        self.d = cfg.head_dim
+        self.I = cfg.intermediate // tp
+        self.vocab_shard = shard_range(cfg.vocab, r, tp)
+        self.scale = 1.0 / math.sqrt(self.d)
+        self.layers: List[Dict[str, torch.Tensor]] = []
+        self._init_random(seed, init_std)
+        if weights:
+            self.load_safetensors(weights)
+        self.cos_sin = ops.rope_cos_sin(cfg.max_position, self.d, cfg.rope_theta, self.device, cfg.rope_scaling)
+
+    # ------------------------------------------------------------------ weights
+    def _init_random(self, seed: int, std: float) -> None:
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev if dev.type == "cuda" else "cpu")
+        # every TP rank draws the SAME full tensor stream and keeps its shard -> TP == TP1 numerics
+        g.manual_seed(seed)
+
+        def rnd(*shape):
+            return (torch.randn(*shape, generator=g, device=dev, dtype=torch.float32) * std).to(dt)
+
+        H, d, nq, nkv = cfg.hidden, cfg.head_dim, cfg.n_heads, cfg.n_kv_heads
+        tp, r = self.par.tp_size, self.par.tp_rank
+        qs, ks = shard_range(nq * d, r, tp), shard_range(nkv * d, r, tp)
+        isl = shard_range(cfg.intermediate, r, tp)
+        emb_full = rnd(cfg.vocab, H)
+        self.embed = emb_full[self.vocab_shard].contiguous()
+        self.lm_head = self.embed if cfg.tie_embeddings else rnd(cfg.vocab, H)[self.vocab_shard].contiguous()
+        del emb_full
+        ones = torch.ones(H, device=dev, dtype=dt)
+        for _ in range(cfg.n_layers):
+            wq, wk, wv = rnd(nq * d, H), rnd(nkv * d, H), rnd(nkv * d, H)
+            wo = rnd(H, nq * d)
+            L = {"ln1": ones.clone(), "ln2": ones.clone(),
+                 "wqkv": torch.cat([wq[qs], wk[ks], wv[ks]], 0).contiguous(),
+                 "wo": wo[:, qs].contiguous()}
+            if cfg.is_moe:
+                E = cfg.n_experts
+                L["wgate"] = rnd(E, H)
+                w13 = []
+                w2 = []
+                for _e in range(E):
+                    gate, up, down = rnd(cfg.intermediate, H), rnd(cfg.intermediate, H), rnd(H, cfg.intermediate)
+                    w13.append(torch.cat([gate[isl], up[isl]], 0))
+                    w2.append(down[:, isl])
+                L["w13"] = torch.stack(w13).contiguous()   # [E, 2I, H]
+                L["w2"] = torch.stack(w2).contiguous()     # [E, H, I]
+            else:
+                gate, up, down = rnd(cfg.intermediate, H), rnd(cfg.intermediate, H), rnd(H, cfg.intermediate)
+                L["wgu"] = torch.cat([gate[isl], up[isl]], 0).contiguous()
+                L["wd"] = down[:, isl].contiguous()
+            self.layers.append(L)
+        self.final_norm = ones.clone()
+
+    def load_safetensors(self, path: str) -> None:
+        """Load HF-format weights (a file or a directory of shards); keeps this rank's shard."""
+        from safetensors import safe_open
+        files = [path] if os.path.isfile(path) else sorted(
+            os.path.join(path, f) for f in os.listdir(path) if f.endswith(".safetensors"))
+        tensors: Dict[str, torch.Tensor] = {}
+        for f in files:
+            with safe_open(f, framework="pt", device="cpu") as fh:
+                for k in fh.keys():
+                    tensors[k] = fh.get_tensor(k)
+        cfg, tp, r = self.cfg, self.par.tp_size, self.par.tp_rank
+        d, nq, nkv = cfg.head_dim, cfg.n_heads, cfg.n_kv_heads
+        qs, ks = shard_range(nq * d, r, tp), shard_range(nkv * d, r, tp)
+        isl = shard_range(cfg.intermediate, r, tp)
+        put = lambda t: t.to(self.device, self.dtype).contiguous()
+        self.embed = put(tensors["model.embed_tokens.weight"][self.vocab_shard])
+        self.lm_head = self.embed if cfg.tie_embeddings else put(tensors["lm_head.weight"][self.vocab_shard])
+        self.final_norm = put(tensors["model.norm.weight"])
+        for i, L in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            L["ln1"] = put(tensors[p + "input_layernorm.weight"])
+            L["ln2"] = put(tensors[p + "post_attention_layernorm.weight"])
+            if p + "self_attn.qkv_proj.weight" in tensors:  # phi-3 fused layout
+                w = tensors[p + "self_attn.qkv_proj.weight"]
+                wq, wk, wv = w[:nq * d], w[nq * d:(nq + nkv) * d], w[(nq + nkv) * d:]
+            else:
+                wq, wk, wv = (tensors[p + f"self_attn.{n}_proj.weight"] for n in "qkv")
+            L["wqkv"] = put(torch.cat([wq[qs], wk[ks], wv[ks]], 0))
+            L["wo"] = put(tensors[p + "self_attn.o_proj.weight"][:, qs])
+            if cfg.is_moe:
+                pm = p + "block_sparse_moe."
+                L["wgate"] = put(tensors[pm + "gate.weight"])
+                L["w13"] = put(torch.stack([torch.cat([tensors[pm + f"experts.{e}.w1.weight"][isl],
+                                                       tensors[pm + f"experts.{e}.w3.weight"][isl]], 0)
+                                            for e in range(cfg.n_experts)]))
+                L["w2"] = put(torch.stack([tensors[pm + f"experts.{e}.w2.weight"][:, isl]
+                                           for e in range(cfg.n_experts)]))
+            elif p + "mlp.gate_up_proj.weight" in tensors:
+                w = tensors[p + "mlp.gate_up_proj.weight"]
+                I = cfg.intermediate
+                L["wgu"] = put(torch.cat([w[:I][isl], w[I:][isl]], 0))
+                L["wd"] = put(tensors[p + "mlp.down_proj.weight"][:, isl])
+            else:
+                L["wgu"] = put(torch.cat([tensors[p + "mlp.gate_proj.weight"][isl],
+                                          tensors[p + "mlp.up_proj.weight"][isl]], 0))
+                L["wd"] = put(tensors[p + "mlp.down_proj.weight"][:, isl])
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + (0 if self.lm_head is self.embed else self.lm_head.numel()) + self.final_norm.numel()
+        for L in self.layers:
+            n += sum(t.numel() for t in L.values())
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------------ forward
+    def _embed(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.par.tp_size == 1:
+            return F.embedding(ids, self.embed)
+        lo = self.vocab_shard.start
+        local = ids - lo
+        ok = (local >= 0) & (local < self.embed.shape[0])
+        h = F.embedding(local.clamp(0, self.embed.shape[0] - 1), self.embed) * ok.unsqueeze(-1).to(self.dtype)
+        return self.par.all_reduce(h)
+
+    def _mlp(self, L, x: torch.Tensor) -> torch.Tensor:
+        if not self.cfg.is_moe:
+            return F.linear(ops.silu_mul(F.linear(x, L["wgu"])), L["wd"])
+        return self._moe(L, x)
+
+    def _moe(self, L, x: torch.Tensor) -> torch.Tensor:
+        """Top-k expert MLP: gate kernel -> token permutation by expert -> per-expert GEMMs ->
+        weighted un-permute (index_add).  Experts are TP-sharded along I."""
+        T = x.shape[0]
+        k = self.cfg.experts_per_token
+        ids, w = ops.moe_gate(F.linear(x, L["wgate"]).float(), k)
+        flat = ids.reshape(-1).long()
+        order = torch.argsort(flat, stable=True)
+        tok = order // k
+        counts = torch.bincount(flat, minlength=self.cfg.n_experts).tolist()
+        xs = x.index_select(0, tok)
+        ys = torch.empty_like(xs)
+        s = 0
+        for e, c in enumerate(counts):
+            if c == 0:
+                continue
+            seg = xs[s:s + c]
+            ys[s:s + c] = F.linear(ops.silu_mul(F.linear(seg, L["w13"][e])), L["w2"][e])
+            s += c
+        ys = ys * w.reshape(-1)[order].unsqueeze(-1).to(ys.dtype)
+        out = torch.zeros((T, x.shape[1]), dtype=torch.float32, device=x.device)
+        out.index_add_(0, tok, ys.float())
+        return out.to(x.dtype)
+
+    def hidden_states(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
+                      kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """Final-normed hidden states of each sequence's last new token: [S, H]."""
+        cfg = self.cfg
+        h = self._embed(input_ids)
+        residual = torch.zeros_like(h)
+        for li, L in enumerate(self.layers):
+            x = ops.rms_norm(h, L["ln1"], cfg.rms_eps, residual=residual)
+            qkv = F.linear(x, L["wqkv"])
+            kc, vc = kv_caches[li]
+            q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
+            o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
+                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
+                                    splits=meta.splits, workspace=meta.workspace)
+            h = self.par.all_reduce(F.linear(o.view(o.shape[0], -1), L["wo"]))
+            x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
+            h = self.par.all_reduce(self._mlp(L, x))
+        last_h = h.index_select(0, meta.last_idx)
+        last_r = residual.index_select(0, meta.last_idx)
+        return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)
+
+    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """This rank's vocab shard of the logits: [S, V / tp] (bf16)."""
+        return F.linear(hidden, self.lm_head)
+
+    def greedy(self, hidden: torch.Tensor) -> torch.Tensor:
+        """Distributed arg-max over the vocab-parallel LM head -> token ids [S] int32."""
+        lg = self.logits(hidden)
+        if self.par.tp_size == 1:
+            return ops.argmax(lg)
+        loc = ops.argmax(lg)
+        val = lg.gather(1, loc.long().unsqueeze(1)).float().squeeze(1)
+        pair = torch.stack([val, (loc + self.vocab_shard.start).float()], dim=1)  # ids < 2^24: exact in f32
+        allp = self.par.all_gather(pair)                    # [tp, S, 2]
+        best = allp[..., 0].argmax(dim=0)                   # first max -> lowest rank -> lowest id
+        return allp[..., 1].gather(0, best.unsqueeze(0)).squeeze(0).to(torch.int32)
+
+    def topk_candidates(self, hidden: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Global top-k (values desc, ids) from per-rank top-k of the vocab shards."""
+        lg = self.logits(hidden).float()
+        k_loc = min(k, lg.shape[1])
+        v, i = torch.topk(lg, k_loc, dim=-1)
+        i = i + self.vocab_shard.start
+        if self.par.tp_size > 1:
+            av, ai = self.par.all_gather(v), self.par.all_gather(i)   # [tp, S, k]
+            v = av.permute(1, 0, 2).reshape(v.shape[0], -1)
+            i = ai.permute(1, 0, 2).reshape(i.shape[0], -1)
+            v, j = torch.topk(v, min(k, v.shape[1]), dim=-1)
+            i = i.gather(1, j)
+        return v.contiguous(), i.contiguous()

@@ -1,0 +1,250 @@
+"""Op library: HIP/CDNA4 kernels (``_hip_kernels`` extension) with plain-PyTorch references.
+
+Dispatch rule: GPU tensors ALWAYS run the HIP kernel.  If the extension is missing on a GPU
+box the call raises (``NativeOpsMissing``) — there is no silent eager fallback
+(set ``DLLM_ALLOW_TORCH_FALLBACK=1`` only for debugging).  CPU tensors run the torch
+reference implementation (``ops.reference``), which is also what the kernel numerics tests
+compare against.
+
+KV-cache layout (per layer):  K [num_blocks, nkv, 16, d],  V [num_blocks, nkv, d, 16]
+(V transposed per block — see csrc/kernels/attention.hip).
+"""
+from __future__ import annotations
+
+import math
+import os
+import struct
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+
+BLOCK_SIZE = 16
+
+_ext = None
+_ext_err: Optional[BaseException] = None
+
+
+class NativeOpsMissing(RuntimeError):
+    pass
+
+
+def _load():
+    global _ext, _ext_err
+    if _ext is not None or _ext_err is not None:
+        return _ext
+    try:
+        from . import _hip_kernels  # type: ignore
+        _ext = _hip_kernels
+    except BaseException as e:  # ImportError or a loader error
+        _ext_err = e
+    return _ext
+
+
+def native_available() -> bool:
+    return _load() is not None
+
+
+def _native(t: torch.Tensor):
+    """Return the extension for a GPU tensor, None for CPU tensors; raise if missing on GPU."""
+    if not t.is_cuda:
+        return None
+    ext = _load()
+    if ext is None:
+        if os.environ.get("DLLM_ALLOW_TORCH_FALLBACK") == "1":
+            return None
+        raise NativeOpsMissing(
+            f"HIP kernel extension not built/loadable ({_ext_err}); run "
+            "`python -m distributed_llm_amd._build` (gfx950)")
+    return ext
+
+
+# ----------------------------------------------------------------------------- norms
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = rmsnorm(x + residual) * w;  ``residual`` is updated in place to ``x + residual``."""
+    ext = _native(x)
+    if ext is None:
+        return ref.rms_norm(x, w, eps, residual)
+    y = out if out is not None else torch.empty_like(x)
+    ext.norm(x, residual, w, None, y, eps, False)
+    return y
+
+
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
+               residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    ext = _native(x)
+    if ext is None:
+        return ref.layer_norm(x, w, b, eps, residual)
+    y = torch.empty_like(x)
+    ext.norm(x, residual, w, b, y, eps, True)
+    return y
+
+
+# ----------------------------------------------------------------------------- rope + kv
+
+def rope_cos_sin(max_pos: int, d: int, theta: float, device=None, scaling: Optional[dict] = None) -> torch.Tensor:
+    """Host-precomputed [max_pos, d] f32 table: cos in [:d/2], sin in [d/2:]."""
+    inv = 1.0 / (theta ** (torch.arange(0, d, 2, dtype=torch.float64) / d))
+    if scaling and scaling.get("rope_type") == "llama3":
+        inv = ref.llama3_scale_inv_freq(inv, scaling)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], dim=1).float().to(device)
+
+
+def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor,
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, nq: int, nkv: int, d: int,
+                   q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rotate q/k, write k and v into the paged caches, return q as [T, nq, d]."""
+    ext = _native(qkv)
+    if ext is None:
+        return ref.rope_and_cache(qkv, positions, cos_sin, slots, k_cache, v_cache, nq, nkv, d)
+    T = qkv.shape[0]
+    q = q_out if q_out is not None else torch.empty((T, nq, d), dtype=qkv.dtype, device=qkv.device)
+    ext.rope_kv(qkv, positions, cos_sin, slots, q, k_cache, v_cache, nq, nkv, d)
+    return q
+
+
+def kv_write(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
+             v_cache: torch.Tensor) -> None:
+    ext = _native(k)
+    if ext is None:
+        return ref.kv_write(k, v, slots, k_cache, v_cache)
+    ext.kv_write(k.contiguous(), v.contiguous(), slots, k_cache, v_cache)
+
+
+# ----------------------------------------------------------------------------- attention
+
+def build_tiles(q_lens, group: int) -> Tuple[list, list]:
+    """Host tile table: each 16-row tile covers 16/group tokens of one sequence."""
+    tpt = 16 // group
+    ts, tt = [], []
+    for s, n in enumerate(q_lens):
+        for t0 in range(0, int(n), tpt):
+            ts.append(s)
+            tt.append(t0)
+    return ts, tt
+
+
+def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                    seq_qstart: torch.Tensor, seq_qlen: torch.Tensor, seq_ctx: torch.Tensor,
+                    tile_seq: torch.Tensor, tile_tok0: torch.Tensor, scale: Optional[float] = None,
+                    causal: bool = True, splits: int = 1, out: Optional[torch.Tensor] = None,
+                    workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """Paged attention over new query tokens ``q [T, nq, d]`` (see csrc/kernels/attention.hip)."""
+    d = q.shape[-1]
+    scale = (1.0 / math.sqrt(d)) if scale is None else scale
+    ext = _native(q)
+    if ext is None:
+        return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, scale, causal)
+    o = out if out is not None else torch.empty_like(q)
+    po = pml = None
+    if splits > 1:
+        if workspace is None:
+            nt, nkv = tile_seq.numel(), k_cache.shape[1]
+            po = torch.empty(nt * nkv * splits * 16 * d, dtype=torch.float32, device=q.device)
+            pml = torch.empty(nt * nkv * splits * 16 * 2, dtype=torch.float32, device=q.device)
+        else:
+            po, pml = workspace
+    ext.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
+                        po, pml, splits, causal, scale)
+    return o
+
+
+# ----------------------------------------------------------------------------- activations
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    ext = _native(gu)
+    if ext is None:
+        return ref.silu_mul(gu)
+    T, I2 = gu.shape
+    o = out if out is not None else torch.empty((T, I2 // 2), dtype=gu.dtype, device=gu.device)
+    ext.silu_mul(gu, o)
+    return o
+
+
+def gelu(x: torch.Tensor) -> torch.Tensor:
+    ext = _native(x)
+    if ext is None:
+        return ref.gelu(x)
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    ext.gelu(x, y)
+    return y
+
+
+def mean_pool_l2(x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+    ext = _native(x)
+    if ext is None:
+        return ref.mean_pool_l2(x, lens)
+    out = torch.empty((x.shape[0], x.shape[2]), dtype=torch.float32, device=x.device)
+    ext.mean_pool_l2(x.contiguous(), lens.to(torch.int32).contiguous(), out)
+    return out
+
+
+def moe_gate(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    ext = _native(logits)
+    if ext is None:
+        return ref.moe_gate(logits, k)
+    T = logits.shape[0]
+    ids = torch.empty((T, k), dtype=torch.int32, device=logits.device)
+    w = torch.empty((T, k), dtype=torch.float32, device=logits.device)
+    ext.moe_gate(logits.float().contiguous(), k, ids, w)
+    return ids, w
+
+
+# ----------------------------------------------------------------------------- sampling
+
+def argmax(logits: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    ext = _native(logits)
+    if ext is None:
+        return torch.argmax(logits.float(), dim=-1).to(torch.int32)
+    o = out if out is not None else torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
+    ext.argmax(logits, o)
+    return o
+
+
+def sample_top_p(cand_vals: torch.Tensor, cand_idx: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
+                 uniform: torch.Tensor) -> torch.Tensor:
+    """Nucleus sampling over sorted top-k candidates (values descending)."""
+    ext = _native(cand_vals)
+    if ext is None:
+        return ref.sample_top_p(cand_vals, cand_idx, temperature, top_p, uniform)
+    o = torch.empty(cand_vals.shape[0], dtype=torch.int32, device=cand_vals.device)
+    ext.sample_topp(cand_vals.float().contiguous(), cand_idx.contiguous(), temperature.float().contiguous(),
+                    top_p.float().contiguous(), uniform.float().contiguous(), o)
+    return o
+
+
+# ----------------------------------------------------------------------------- router scorers
+
+def cosine_scores(q: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    ext = _native(q)
+    if ext is None:
+        return ref.cosine_scores(q, c)
+    q = q.float().contiguous()
+    c = c.float().contiguous()
+    s = torch.empty((q.shape[0], c.shape[0]), dtype=torch.float32, device=q.device)
+    ext.cosine_scores(q, c, s)
+    return s
+
+
+def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tensor, ctx: torch.Tensor, cid: int,
+                         thr: float) -> Tuple[int, float]:
+    """Best row of ``table`` with ctx id == cid and cosine >= thr -> (row, sim) or (-1, 0.0)."""
+    ext = _native(table)
+    if ext is None:
+        return ref.masked_cosine_argmax(q, table, norms, ctx, cid, thr)
+    best = torch.zeros(1, dtype=torch.int64, device=table.device)
+    ext.masked_cosine_argmax(q.float().contiguous(), table, norms, ctx, int(cid), float(thr), best)
+    key = int(best.item()) & 0xFFFFFFFFFFFFFFFF
+    if key == 0:
+        return -1, 0.0
+    row = 0xFFFFFFFF - (key & 0xFFFFFFFF)
+    bits = key >> 32
+    bits = (bits & 0x7FFFFFFF) if (bits & 0x80000000) else (~bits & 0xFFFFFFFF)
+    sim = struct.unpack("<f", struct.pack("<I", bits))[0]
+    return int(row), float(sim)

@@ -1,0 +1,175 @@
+"""Plain-PyTorch (f32 math) reference implementations of every kernel in csrc/kernels.
+
+Used (a) on CPU tensors (tests, CPU-only runs) and (b) as the numerics oracle the GPU kernel
+tests compare against.  Layout contracts are identical to the HIP kernels.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+BS = 16
+
+
+def rms_norm(x, w, eps, residual=None):
+    if residual is not None:
+        r = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(r)
+        x = r
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(x.dtype)
+
+
+def layer_norm(x, w, b, eps, residual=None):
+    if residual is not None:
+        r = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(r)
+        x = r
+    y = torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+    return y.to(x.dtype)
+
+
+def llama3_scale_inv_freq(inv: torch.Tensor, sc: dict) -> torch.Tensor:
+    factor = sc.get("factor", 8.0)
+    lo = sc.get("low_freq_factor", 1.0)
+    hi = sc.get("high_freq_factor", 4.0)
+    old = sc.get("original_max_position_embeddings", 8192)
+    wl = 2 * math.pi / inv
+    lo_wl, hi_wl = old / lo, old / hi
+    out = torch.where(wl > lo_wl, inv / factor, inv)
+    smooth = (old / wl - lo) / (hi - lo)
+    mid = (1 - smooth) * inv / factor + smooth * inv
+    is_mid = (wl <= lo_wl) & (wl >= hi_wl)
+    return torch.where(is_mid, mid, out)
+
+
+def _rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    # x [T, h, d] f32; cos/sin [T, d/2]
+    h = x.shape[-1] // 2
+    x1, x2 = x[..., :h], x[..., h:]
+    c, s = cos[:, None, :], sin[:, None, :]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def rope_and_cache(qkv, positions, cos_sin, slots, k_cache, v_cache, nq, nkv, d):
+    T = qkv.shape[0]
+    f = qkv[:, : (nq + 2 * nkv) * d].float()
+    q = f[:, : nq * d].view(T, nq, d)
+    k = f[:, nq * d:(nq + nkv) * d].view(T, nkv, d)
+    v = qkv[:, (nq + nkv) * d:(nq + 2 * nkv) * d].view(T, nkv, d)
+    cs = cos_sin[positions.long()].float()
+    cos, sin = cs[:, : d // 2], cs[:, d // 2:]
+    q = _rope(q, cos, sin).to(qkv.dtype)
+    k = _rope(k, cos, sin).to(qkv.dtype)
+    kv_write(k, v, slots, k_cache, v_cache)
+    return q.contiguous()
+
+
+def kv_write(k, v, slots, k_cache, v_cache):
+    sl = slots.long()
+    ok = sl >= 0
+    if not bool(ok.any()):
+        return
+    sl, k, v = sl[ok], k[ok], v[ok]
+    blk, off = sl // BS, sl % BS
+    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
+    v_cache[blk, :, :, off] = v.to(v_cache.dtype)
+
+
+def gather_kv(k_cache, v_cache, block_table, n):
+    """Dense K, V [n, nkv, d] of one sequence from the paged caches."""
+    nb = (n + BS - 1) // BS
+    blocks = block_table[:nb].long()
+    k = k_cache[blocks]                       # [nb, nkv, 16, d]
+    v = v_cache[blocks].transpose(2, 3)       # [nb, nkv, 16, d]
+    k = k.permute(0, 2, 1, 3).reshape(nb * BS, k.shape[1], k.shape[3])[:n]
+    v = v.permute(0, 2, 1, 3).reshape(nb * BS, v.shape[1], v.shape[3])[:n]
+    return k, v
+
+
+def paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, scale, causal=True):
+    out = torch.zeros_like(q)
+    nq, d = q.shape[1], q.shape[2]
+    nkv = k_cache.shape[1]
+    G = nq // nkv
+    for s in range(block_tables.shape[0]):
+        ql, ctx, qs = int(seq_qlen[s]), int(seq_ctx[s]), int(seq_qstart[s])
+        if ql == 0 or ctx == 0:
+            continue
+        k, v = gather_kv(k_cache, v_cache, block_tables[s], ctx)
+        k = k.float().repeat_interleave(G, dim=1)  # [ctx, nq, d]
+        v = v.float().repeat_interleave(G, dim=1)
+        qq = q[qs:qs + ql].float()                 # [ql, nq, d]
+        sc = torch.einsum("qhd,khd->hqk", qq, k) * scale
+        if causal:
+            pos = torch.arange(ctx - ql, ctx, device=q.device)[:, None]
+            keys = torch.arange(ctx, device=q.device)[None, :]
+            sc = sc.masked_fill((keys > pos)[None], float("-inf"))
+        p = torch.softmax(sc, dim=-1)
+        o = torch.einsum("hqk,khd->qhd", p, v)
+        out[qs:qs + ql] = o.to(q.dtype)
+    return out
+
+
+def silu_mul(gu):
+    I = gu.shape[1] // 2
+    g, u = gu[:, :I].float(), gu[:, I:].float()
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+def gelu(x):
+    return torch.nn.functional.gelu(x.float()).to(x.dtype)
+
+
+def mean_pool_l2(x, lens):
+    B, S, H = x.shape
+    m = (torch.arange(S)[None, :].to(x.device) < lens.to(x.device)[:, None]).float()
+    s = (x.float() * m[..., None]).sum(1) / m.sum(1, keepdim=True).clamp(min=1.0)
+    return torch.nn.functional.normalize(s, dim=-1, eps=1e-12)
+
+
+def moe_gate(logits, k):
+    lf = logits.float()
+    vals, ids = torch.topk(lf, k, dim=-1)
+    w = torch.softmax(vals, dim=-1)
+    return ids.to(torch.int32), w
+
+
+def sample_top_p(vals, idx, temperature, top_p, uniform):
+    t = temperature.float().clamp(min=1e-5)[:, None]
+    p = torch.softmax(vals.float() / t, dim=-1)
+    c = torch.cumsum(p, dim=-1)
+    # keep the smallest prefix whose mass reaches top_p
+    keep = (c - p) < top_p.float()[:, None]
+    keep[:, 0] = True
+    p = p * keep
+    p = p / p.sum(-1, keepdim=True)
+    cdf = torch.cumsum(p, dim=-1)
+    pick = torch.searchsorted(cdf, uniform.float()[:, None].clamp(max=0.999999), right=True).clamp(max=vals.shape[1] - 1)
+    return torch.gather(idx, 1, pick).view(-1).to(torch.int32)
+
+
+def cosine_scores(q, c):
+    qn = q.float()
+    cn = c.float()
+    num = qn @ cn.T
+    den = qn.norm(dim=-1, keepdim=True) * cn.norm(dim=-1)[None, :]
+    return torch.where(den < 1e-9, torch.zeros_like(num), num / den.clamp(min=1e-30))
+
+
+def masked_cosine_argmax(q, table, norms, ctx, cid, thr) -> Tuple[int, float]:
+    qf = q.float().reshape(-1)
+    nq = float(qf.norm())
+    if nq < 1e-9 or table.shape[0] == 0:
+        return -1, 0.0
+    mask = (ctx == cid) & (norms >= 1e-9)
+    if not bool(mask.any()):
+        return -1, 0.0
+    sims = (table.float() @ qf) / (norms.float().clamp(min=1e-30) * nq)
+    sims = torch.where(mask, sims, torch.full_like(sims, -float("inf")))
+    j = int(torch.argmax(sims))
+    s = float(sims[j])
+    return (j, s) if s >= thr else (-1, 0.0)

@@ -1,0 +1,283 @@
+"""Orchestrator — the ``Router.route_query`` contract (reference L5).
+
+Reference: ``src/router.py:13-319`` (ctor :14-59, ``set_threshold`` :65-67, ``_extract_text``
+:73-102, ``_history_to_query_and_context`` :104-147, ``_run_device`` :152-171, response
+cache :179-193, ``route_query`` :199-319).
+
+Same contract: ``route_query(history) -> (payload, response_tokens, device)`` with the same
+payload keys on a miss and on a response-cache hit.  MI355X-first additions:
+  * devices are *pools* (``pools.base.PoolClient``): an in-process GPU engine, an HTTP pool
+    worker, or the CPU echo backend; ``.nano`` / ``.orin`` attributes keep the reference
+    names for harness compatibility;
+  * ``route_batch(histories)`` routes many conversations at once and hands each pool its
+    whole group, so the engine batches prefill/decode (continuous batching) instead of
+    serving one request at a time;
+  * state (response store, perf feedback) is lock-protected;
+  * failover can optionally penalise the failed primary in the perf router
+    (``"penalise_failed_primary"``, default False = reference behaviour, quirk 3);
+  * per-request timing split (queue / prefill / decode / ttft) is surfaced under
+    ``payload["timing"]`` when the pool reports it.
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from .config import LARGE, PRODUCTION_CFG, BENCHMARK_CFG, SMALL, other_tier
+from .router.query_router import QueryRouter
+from .router.tokens import TokenCounter
+
+logger = logging.getLogger(__name__)
+
+
+def history_to_query_and_context(history: Sequence[Dict[str, Any]], last_k: int = 6
+                                 ) -> Tuple[str, Optional[str], str]:
+    """Split history into (latest user query, prior context text, context hash).
+
+    Context lines are ``"role: content"`` for non-empty messages; the hash is
+    sha256 over the last ``last_k`` prior messages, first 16 hex chars (reference
+    ``router.py:104-147``).
+    """
+    if not history:
+        return "", None, "nohist"
+    idx = None
+    for i in range(len(history) - 1, -1, -1):
+        m = history[i]
+        if isinstance(m, dict) and m.get("role") == "user":
+            idx = i
+            break
+    if idx is None:
+        query, prior = "", list(history)
+    else:
+        query, prior = (history[idx].get("content") or "").strip(), list(history[:idx])
+    lines = [f"{(m.get('role') or '').strip()}: {(m.get('content') or '').strip()}"
+             for m in prior if isinstance(m, dict) and (m.get("content") or "").strip()]
+    context = "\n".join(lines) if lines else None
+    tail = prior[-last_k:] if last_k > 0 else []
+    compact = [f"{m.get('role', '')}:{(m.get('content') or '').strip()}"
+               for m in tail if isinstance(m, dict)]
+    ctx_hash = hashlib.sha256("\n".join(compact).encode("utf-8")).hexdigest()[:16]
+    return query, context, ctx_hash
+
+
+def extract_text(resp: Any) -> Optional[str]:
+    """Normalise any pool response shape into text (reference ``router.py:73-102``)."""
+    if resp is None:
+        return None
+    if isinstance(resp, str):
+        return resp.strip() or None
+    if isinstance(resp, dict):
+        for key in ("response", "content", "message"):
+            v = resp.get(key)
+            if isinstance(v, str) and v.strip():
+                return v.strip()
+            if isinstance(v, dict):
+                inner = v.get("content")
+                if isinstance(inner, str) and inner.strip():
+                    return inner.strip()
+        if "error" in resp:
+            parts = [str(resp.get(k, "")).strip() for k in ("error", "detail", "body")]
+            joined = " ".join(p for p in parts if p)
+            return joined[:300] if joined else None
+    return None
+
+
+def is_error(raw: Any) -> bool:
+    return isinstance(raw, dict) and "error" in raw
+
+
+class Router:
+    def __init__(self, strategy: str = "hybrid", config: Optional[Dict[str, Any]] = None,
+                 threshold_fallback: int = 100, benchmark_mode: bool = False,
+                 pools: Optional[Dict[str, Any]] = None):
+        self.token_counter = TokenCounter()
+        self.threshold_fallback = threshold_fallback
+        self.benchmark_mode = benchmark_mode
+        if config is not None:
+            self.config = config
+        else:
+            self.config = BENCHMARK_CFG if benchmark_mode else PRODUCTION_CFG
+        self.query_router = QueryRouter(strategy=strategy, config=self.config)
+        self.enable_response_cache = (not benchmark_mode
+                                      and bool(self.config.get("enable_response_cache", False)))
+        self.cache_last_k = int(self.config.get("cache_last_k", 6))
+        self.enable_failover = bool(self.config.get("enable_failover", True))
+        self.penalise_failed_primary = bool(self.config.get("penalise_failed_primary", False))
+        self._responses: Dict[str, Dict[str, Any]] = {}
+        self._lock = threading.RLock()
+        if pools is None:
+            from .pools.base import default_pools
+            pools = default_pools(self.config)
+        self.pools = {SMALL: pools[SMALL], LARGE: pools[LARGE]}
+
+    # reference attribute names
+    @property
+    def nano(self):
+        return self.pools[SMALL]
+
+    @property
+    def orin(self):
+        return self.pools[LARGE]
+
+    def set_threshold(self, threshold: int) -> None:
+        self.threshold_fallback = threshold
+
+    # ------------------------------------------------------------------ helpers
+    def _split(self, history):
+        return history_to_query_and_context(history, self.cache_last_k)
+
+    def _response_key(self, query: str) -> str:
+        # Context-independent key, as in the reference (quirk 2); "response_cache_context": True
+        # opts into context-aware keys.
+        return f"{self.query_router.strategy}|{query.lower().strip()}"
+
+    def _decide(self, query: str, context: Optional[str], ctx_hash: str, history) -> Dict[str, Any]:
+        t0 = time.perf_counter()
+        try:
+            d = self.query_router.route_query(query=query, context=context, context_key=ctx_hash)
+            out = {"device": d.device, "method": d.method, "confidence": float(d.confidence),
+                   "reasoning": d.reasoning, "cache_hit": d.cache_hit}
+        except Exception as exc:
+            size = self.token_counter.get_context_size(history)
+            dev = LARGE if size > self.threshold_fallback else SMALL
+            out = {"device": dev, "method": "fallback_ctx_size", "confidence": 0.2,
+                   "reasoning": (f"router failed: {exc}; ctx_size={size}, "
+                                 f"threshold_fallback={self.threshold_fallback}"),
+                   "cache_hit": False}
+        out["overhead_ms"] = (time.perf_counter() - t0) * 1000.0
+        return out
+
+    def _cached_payload(self, query: str):
+        if not self.enable_response_cache:
+            return None
+        with self._lock:
+            c = self._responses.get(self._response_key(query))
+        if c is None:
+            return None
+        text, which = c.get("text", ""), c.get("device", SMALL)
+        toks = self.token_counter.count_tokens({"role": "assistant", "content": text})
+        return ({"response": text, "raw": c.get("raw"), "cache_hit": True,
+                 "routing_method": "response_cache", "routing_confidence": 1.0,
+                 "routing_reasoning": f"response cache hit -> {which}",
+                 "routing_overhead_ms": 0.0, "ok": True}, toks, which)
+
+    def _finish(self, query: str, dec: Dict[str, Any], raw: Any, which: str, lat_ms: float,
+                primary_failed: Optional[str] = None):
+        text = extract_text(raw) or "No response available"
+        ntok = raw.get("num_tokens") if isinstance(raw, dict) else None
+        toks = int(ntok) if ntok is not None else self.token_counter.count_tokens(
+            {"role": "assistant", "content": text})
+        ok = not is_error(raw)
+        try:
+            self.query_router.update_perf(which, lat_ms, toks, ok=ok)
+            if primary_failed and self.penalise_failed_primary:
+                self.query_router.update_perf(primary_failed, lat_ms, 0, ok=False)
+        except Exception:
+            pass
+        if self.enable_response_cache:
+            with self._lock:
+                self._responses[self._response_key(query)] = {
+                    "text": text, "raw": raw, "device": which,
+                    "routing_confidence": round(dec["confidence"], 4)}
+        payload = {"response": text, "raw": raw, "cache_hit": False,
+                   "benchmark_mode": self.benchmark_mode,
+                   "routing_overhead_ms": round(dec["overhead_ms"], 2),
+                   "routing_method": dec["method"],
+                   "routing_confidence": round(dec["confidence"], 4),
+                   "routing_reasoning": dec["reasoning"], "ok": ok}
+        if isinstance(raw, dict) and "timing" in raw:
+            payload["timing"] = raw["timing"]
+        return payload, toks, which
+
+    def _run(self, device: str, history) -> Tuple[Any, str, float]:
+        t0 = time.perf_counter()
+        try:
+            raw = self.pools[device].process(history)
+        except Exception as exc:  # a pool that raises is an error response, not a crash
+            raw = {"error": f"pool {device} failed: {exc}"}
+        return raw, device, (time.perf_counter() - t0) * 1000.0
+
+    # ------------------------------------------------------------------ public API
+    def route_query(self, conversation_history: List[Dict[str, Any]]):
+        query, context, ctx_hash = self._split(conversation_history)
+        hit = self._cached_payload(query)
+        if hit is not None:
+            return hit
+        dec = self._decide(query, context, ctx_hash, conversation_history)
+        raw, which, lat = self._run(dec["device"], conversation_history)
+        failed = None
+        if self.enable_failover and is_error(raw):
+            raw2, which2, lat2 = self._run(other_tier(which), conversation_history)
+            if not is_error(raw2):
+                failed = which
+                raw, which, lat = raw2, which2, lat2
+        return self._finish(query, dec, raw, which, lat, failed)
+
+    def route_batch(self, histories: Sequence[List[Dict[str, Any]]]):
+        """Route a batch of independent conversations; each pool serves its group batched.
+
+        Returns a list of ``(payload, response_tokens, device)`` in input order.  Latency per
+        request is the pool's per-request latency (queue + prefill + decode), as reported.
+        """
+        results: List[Any] = [None] * len(histories)
+        groups: Dict[str, List[int]] = {SMALL: [], LARGE: []}
+        meta: Dict[int, Tuple[str, Dict[str, Any]]] = {}
+        self._prefetch_embeddings([self._split(h)[0] for h in histories])
+        for i, h in enumerate(histories):
+            query, context, ctx_hash = self._split(h)
+            hit = self._cached_payload(query)
+            if hit is not None:
+                results[i] = hit
+                continue
+            dec = self._decide(query, context, ctx_hash, h)
+            meta[i] = (query, dec)
+            groups[dec["device"]].append(i)
+        retry: Dict[str, List[int]] = {SMALL: [], LARGE: []}
+        raws: Dict[int, Tuple[Any, str, float]] = {}
+        for dev, outs in self._process_groups(groups, histories).items():
+            for i, (raw, lat) in zip(groups[dev], outs):
+                raws[i] = (raw, dev, lat)
+                if self.enable_failover and is_error(raw):
+                    retry[other_tier(dev)].append(i)
+        failed: Dict[int, str] = {}
+        if any(retry.values()):
+            for dev, outs in self._process_groups(retry, histories).items():
+                for i, (raw, lat) in zip(retry[dev], outs):
+                    if not is_error(raw):
+                        failed[i] = raws[i][1]
+                        raws[i] = (raw, dev, lat)
+        for i, (query, dec) in meta.items():
+            raw, which, lat = raws[i]
+            results[i] = self._finish(query, dec, raw, which, lat, failed.get(i))
+        return results
+
+    def _prefetch_embeddings(self, queries: List[str]) -> None:
+        """One batched encoder forward for every query of a batch (fills the embedder's memo, so
+        the semantic router and the semantic cache do no per-query encoder launches)."""
+        emb = self.query_router.cache_embedder
+        needs = self.query_router.cache_enabled or self.query_router.strategy in ("semantic", "hybrid")
+        if emb is None or not needs or not queries:
+            return
+        enc = getattr(emb, "encode_tensor", None) or emb.encode
+        try:
+            enc(list(dict.fromkeys(queries)))
+        except Exception as exc:  # routing still works, just unbatched
+            logger.warning("batched embedding prefetch failed: %s", exc)
+
+    def _process_groups(self, groups: Dict[str, List[int]], histories) -> Dict[str, List[Tuple[Any, float]]]:
+        """Serve every tier's group (tiers sharing one engine run as ONE continuous batch)."""
+        from .pools.factory import dispatch_groups
+        hs = {dev: [histories[i] for i in idxs] for dev, idxs in groups.items() if idxs}
+        t0 = time.perf_counter()
+        try:
+            res = dispatch_groups(self.pools, hs)
+        except Exception as exc:
+            res = {dev: [{"error": f"pool {dev} failed: {exc}"}] * len(h) for dev, h in hs.items()}
+        wall = (time.perf_counter() - t0) * 1000.0
+        out: Dict[str, List[Tuple[Any, float]]] = {}
+        for dev, raws in res.items():
+            out[dev] = [(r, float(r.get("latency_ms", wall)) if isinstance(r, dict) else wall) for r in raws]
+        return out

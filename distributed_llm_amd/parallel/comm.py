@@ -1,0 +1,97 @@
+"""Process groups and collectives (RCCL over xGMI on MI355X; gloo on CPU for tests).
+
+One process per GPU (``torch.distributed``, backend "nccl" == RCCL on ROCm).  A node is
+partitioned into *pools*: each pool is a contiguous rank range with its own tensor-parallel
+group (e.g. 8 GPUs = small pool ranks 0-1 as two TP=1 replicas + large pool ranks 4-7 as one
+TP=4 group).  Collectives used on the serving path:
+  * TP all-reduce after o_proj / down_proj (decode messages are B x H bf16 = 8-16 KiB x B,
+    latency-bound — kept as ONE call per sub-layer, never split);
+  * vocab-parallel LM head: all-gather of per-rank (max, argmax) pairs or per-rank top-k
+    candidates instead of the full [B, V] logits;
+  * point-to-point send/recv between pools (failover hand-off, health probes) — parallel.p2p.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelContext:
+    tp_size: int = 1
+    tp_rank: int = 0
+    tp_group: Optional[object] = None   # torch ProcessGroup
+    global_rank: int = 0
+    world_size: int = 1
+
+    @property
+    def enabled(self) -> bool:
+        return self.tp_size > 1
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.tp_size > 1:
+            dist.all_reduce(t, group=self.tp_group)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate ``t`` from every TP rank along a new leading dim -> [tp, *t.shape]."""
+        if self.tp_size == 1:
+            return t.unsqueeze(0)
+        out = torch.empty((self.tp_size, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.tp_group)
+        return out
+
+
+SINGLE = ParallelContext()
+
+
+def init_distributed(backend: Optional[str] = None) -> ParallelContext:
+    """Initialise the default process group from torchrun env vars (idempotent)."""
+    if not dist.is_available():
+        return SINGLE
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and not dist.is_initialized():
+        return SINGLE
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group(backend=backend)
+    r, w = dist.get_rank(), dist.get_world_size()
+    return ParallelContext(tp_size=1, tp_rank=0, tp_group=None, global_rank=r, world_size=w)
+
+
+def make_tp_groups(tp: int, ranks: Optional[Sequence[int]] = None) -> ParallelContext:
+    """Split ``ranks`` (default: all) into consecutive TP groups of size ``tp``.
+
+    Every rank must call this with the same arguments (new_group is collective).
+    Returns this rank's context (tp_size 1 if the rank is not in ``ranks``).
+    """
+    if not dist.is_initialized():
+        if tp != 1:
+            raise RuntimeError("tensor parallelism needs torch.distributed initialised")
+        return SINGLE
+    world, me = dist.get_world_size(), dist.get_rank()
+    ranks = list(range(world)) if ranks is None else list(ranks)
+    if len(ranks) % tp != 0:
+        raise ValueError(f"{len(ranks)} ranks not divisible by tp={tp}")
+    mine = ParallelContext(1, 0, None, me, world)
+    for i in range(0, len(ranks), tp):
+        grp_ranks = ranks[i:i + tp]
+        g = dist.new_group(grp_ranks) if tp > 1 else None
+        if me in grp_ranks:
+            mine = ParallelContext(tp, grp_ranks.index(me), g, me, world)
+    return mine
+
+
+def shard_range(n: int, rank: int, size: int) -> slice:
+    if n % size != 0:
+        raise ValueError(f"dimension {n} not divisible by tp={size}")
+    k = n // size
+    return slice(rank * k, (rank + 1) * k)

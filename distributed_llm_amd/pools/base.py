@@ -1,0 +1,242 @@
+"""Pool clients — what the orchestrator dispatches to (reference L3 device clients).
+
+Reference: ``src/models/nano.py:10-40``, ``src/models/orin.py:12-29`` (HTTP via SSH tunnel,
+lazy server start), ``src/models/server_manager.py`` (SSH lifecycle) and the device shim
+prompt format ``src/devices/nano_api.py:49-52`` (``"role: content"`` lines).
+
+A pool is one model tier hosted on a set of GPUs of this node:
+  * ``EnginePool``  — in-process ``engine.LLMEngine`` (this process owns the pool's GPUs);
+  * ``HTTPPool``    — a pool-worker process (``pools.worker``) reached over loopback HTTP
+                      with the reference ``/query`` protocol, and a request timeout on BOTH
+                      tiers (the reference's Orin client has none, quirk 5);
+  * ``EchoPool``    — deterministic CPU backend for the plumbing config (BASELINE config 1);
+  * ``FaultInjectingPool`` — wraps any pool to drop / delay / fail requests (tests).
+Every pool exposes ``process(history) -> {"response": ...} | {"error": ...}``,
+optionally ``process_batch(histories)``, and a ``server_manager`` with the reference's
+``start_server / stop_server / is_server_running`` names.
+"""
+from __future__ import annotations
+
+import json
+import random
+import threading
+import time
+import urllib.error
+import urllib.request
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..config import LARGE, SMALL
+
+
+def format_prompt(query: Any) -> str:
+    """Reference device-shim formatting: ``"{role}: {content}"`` lines joined by newlines."""
+    if isinstance(query, list):
+        return "\n".join(f"{m.get('role', 'user')}: {m.get('content', '')}" for m in query).strip()
+    return str(query).strip()
+
+
+class NullServerManager:
+    """In-process pools are always 'running'; kept for harness API compatibility."""
+
+    def __init__(self):
+        self.running = True
+
+    def start_server(self):
+        self.running = True
+
+    def stop_server(self):
+        self.running = True  # in-process pools stay resident (weights stay in HBM)
+
+    def is_server_running(self) -> bool:
+        return self.running
+
+
+class PoolClient:
+    name: str = SMALL
+
+    def __init__(self):
+        self.server_manager = NullServerManager()
+
+    def process(self, history: Any) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def process_batch(self, histories: Sequence[Any]) -> List[Dict[str, Any]]:
+        return [self.process(h) for h in histories]
+
+    def health(self) -> Dict[str, Any]:
+        return {"ok": True}
+
+
+class EchoPool(PoolClient):
+    """Deterministic CPU backend: echoes the last user turn, ``tokens_per_reply`` words long."""
+
+    def __init__(self, name: str = SMALL, tokens_per_reply: int = 16, delay_s: float = 0.0):
+        super().__init__()
+        self.name = name
+        self.tokens_per_reply = tokens_per_reply
+        self.delay_s = delay_s
+        self.calls = 0
+        self._lock = threading.Lock()
+
+    def process(self, history: Any) -> Dict[str, Any]:
+        prompt = format_prompt(history)
+        if not prompt:
+            return {"error": "No query provided"}
+        with self._lock:
+            self.calls += 1
+        if self.delay_s:
+            time.sleep(self.delay_s)
+        last = prompt.rsplit("\n", 1)[-1]
+        words = (f"[{self.name}] " + last).split()
+        reply = " ".join((words * (self.tokens_per_reply // max(len(words), 1) + 1))[:self.tokens_per_reply])
+        return {"response": reply, "num_tokens": self.tokens_per_reply}
+
+
+class FaultInjectingPool(PoolClient):
+    """Wraps a pool; ``mode`` in {"ok", "error", "timeout", "flaky"}."""
+
+    def __init__(self, inner: PoolClient, mode: str = "error", p: float = 0.5, seed: int = 0,
+                 timeout_s: float = 0.0):
+        super().__init__()
+        self.inner, self.mode, self.p, self.timeout_s = inner, mode, p, timeout_s
+        self.name = inner.name
+        self.server_manager = inner.server_manager
+        self._rng = random.Random(seed)
+
+    def process(self, history: Any) -> Dict[str, Any]:
+        if self.mode == "error" or (self.mode == "flaky" and self._rng.random() < self.p):
+            return {"error": f"injected fault on {self.name}"}
+        if self.mode == "timeout":
+            time.sleep(self.timeout_s)
+            return {"error": f"Request timed out on {self.name}"}
+        return self.inner.process(history)
+
+    def process_batch(self, histories):
+        return [self.process(h) for h in histories]
+
+
+class HTTPServerManager:
+    """Liveness/readiness of a pool-worker process (local; no SSH on one node)."""
+
+    def __init__(self, url: str, supervisor=None, pool_name: str = SMALL):
+        self.url = url.rstrip("/")
+        self.supervisor = supervisor
+        self.pool_name = pool_name
+
+    def is_server_running(self) -> bool:
+        try:
+            with urllib.request.urlopen(self.url + "/health", timeout=1.0) as r:
+                return json.loads(r.read().decode()).get("ok", False) is True
+        except Exception:
+            return False
+
+    def start_server(self):
+        if self.supervisor is not None and not self.is_server_running():
+            self.supervisor.start(self.pool_name)
+
+    def stop_server(self):
+        if self.supervisor is not None:
+            self.supervisor.stop(self.pool_name)
+
+
+class HTTPPool(PoolClient):
+    def __init__(self, name: str, url: str, timeout_s: float = 180.0, connect_timeout_s: float = 5.0,
+                 supervisor=None, options: Optional[Dict[str, Any]] = None):
+        super().__init__()
+        self.name = name
+        self.url = url.rstrip("/")
+        self.timeout_s = timeout_s
+        self.options = dict(options or {})
+        self.server_manager = HTTPServerManager(url, supervisor, name)
+
+    def _post(self, payload: Dict[str, Any]) -> Dict[str, Any]:
+        req = urllib.request.Request(self.url + "/query", data=json.dumps(payload).encode(),
+                                     headers={"Content-Type": "application/json"}, method="POST")
+        try:
+            with urllib.request.urlopen(req, timeout=self.timeout_s) as r:
+                ct = (r.headers.get("Content-Type") or "").lower()
+                body = r.read().decode("utf-8", "replace")
+                if "application/json" not in ct:
+                    return {"error": f"Non-JSON response ({r.status})", "body": body[:500]}
+                return json.loads(body) if body else {"error": "Empty response"}
+        except urllib.error.HTTPError as e:
+            try:
+                return json.loads(e.read().decode())
+            except Exception:
+                return {"error": f"HTTP {e.code}"}
+        except TimeoutError:
+            return {"error": f"Request timed out on {self.name}"}
+        except Exception as e:
+            return {"error": f"Request failed: {e}"}
+
+    def process(self, history: Any) -> Dict[str, Any]:
+        if not self.server_manager.is_server_running():
+            self.server_manager.start_server()
+        return self._post({"query": history, **self.options})
+
+    def process_batch(self, histories):
+        if not self.server_manager.is_server_running():
+            self.server_manager.start_server()
+        res = self._post({"queries": list(histories), **self.options})
+        if isinstance(res, dict) and "responses" in res:
+            return res["responses"]
+        return [res] * len(histories)
+
+    def health(self) -> Dict[str, Any]:
+        return {"ok": self.server_manager.is_server_running()}
+
+
+class EnginePool(PoolClient):
+    """A pool served by an in-process ``engine.LLMEngine``."""
+
+    def __init__(self, name: str, engine, max_new_tokens: int = 256, temperature: float = 0.0,
+                 top_k: int = 0, top_p: float = 1.0, session_prefix_cache: bool = True):
+        super().__init__()
+        self.name = name
+        self.engine = engine
+        self.max_new_tokens = max_new_tokens
+        self.temperature = temperature
+        self.top_k = top_k
+        self.top_p = top_p
+
+    def _params(self, overrides: Optional[Dict[str, Any]] = None):
+        from ..engine.sampling import SamplingParams
+        o = overrides or {}
+        n = int(o.get("num_predict", self.max_new_tokens))
+        return SamplingParams(max_new_tokens=self.max_new_tokens if n < 0 else n,
+                              temperature=float(o.get("temperature", self.temperature)),
+                              top_k=int(o.get("top_k", self.top_k)),
+                              top_p=float(o.get("top_p", self.top_p)))
+
+    def process(self, history: Any, overrides: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+        return self.process_batch([history], overrides)[0]
+
+    def process_batch(self, histories, overrides: Optional[Dict[str, Any]] = None):
+        prompts = [format_prompt(h) for h in histories]
+        return self.to_payloads(self.engine.generate(prompts, self._params(overrides)))
+
+    @staticmethod
+    def to_payloads(outs) -> List[Dict[str, Any]]:
+        res = []
+        for o in outs:
+            if o.error:
+                res.append({"error": o.error})
+            else:
+                res.append({"response": o.text, "num_tokens": o.num_generated,
+                            "latency_ms": o.latency_ms,
+                            "timing": {"queue_ms": o.queue_ms, "ttft_ms": o.ttft_ms,
+                                       "prefill_tokens": o.num_prefill, "cached_tokens": o.num_cached,
+                                       "decode_tok_s": o.decode_tok_s}})
+        return res
+
+    def health(self) -> Dict[str, Any]:
+        return {"ok": True, **self.engine.stats()}
+
+
+def default_pools(config: Dict[str, Any]) -> Dict[str, PoolClient]:
+    """Pools from ``config["pools"]`` or echo pools (plumbing config) when none given."""
+    spec = config.get("pools")
+    if not spec:
+        return {SMALL: EchoPool(SMALL), LARGE: EchoPool(LARGE, tokens_per_reply=48)}
+    from .factory import build_pools
+    return build_pools(spec)

@@ -1,0 +1,83 @@
+"""Build pool clients from a topology spec, and dispatch grouped requests.
+
+Topology spec (``config["pools"]``)::
+
+    {"nano": {"kind": "engine", "model": "tinyllama-1.1b", "device": "cuda:0",
+              "max_new_tokens": 128, "temperature": 0.0, "share": "main"},
+     "orin": {"kind": "engine", "model": "tinyllama-1.1b", "device": "cuda:0",
+              "max_new_tokens": 384, "temperature": 0.8, "top_k": 40, "top_p": 0.9, "share": "main"}}
+
+``share``: pools with the same share key and model use ONE engine (BASELINE config 2: one
+model serving both tiers on one GPU).  ``kind`` may also be ``"http"`` (``url``: a pool
+worker) or ``"echo"``.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Sequence, Tuple
+
+from ..config import LARGE, SMALL, canonical_tier
+from .base import EchoPool, EnginePool, HTTPPool, PoolClient, format_prompt
+
+
+def build_pools(spec: Dict[str, Dict[str, Any]]) -> Dict[str, PoolClient]:
+    engines: Dict[Tuple[str, str], Any] = {}
+    pools: Dict[str, PoolClient] = {}
+    for name, s in spec.items():
+        tier = canonical_tier(name)
+        kind = s.get("kind", "engine")
+        if kind == "echo":
+            pools[tier] = EchoPool(tier, tokens_per_reply=int(s.get("max_new_tokens", 16)))
+        elif kind == "http":
+            pools[tier] = HTTPPool(tier, s["url"], timeout_s=float(s.get("timeout_s", 180.0)))
+        elif kind == "engine":
+            key = (s.get("share", tier), s["model"])
+            eng = engines.get(key)
+            if eng is None:
+                from ..engine.llm_engine import LLMEngine
+                eng = LLMEngine(s["model"], device=s.get("device", "cuda"), kv_cache_gb=s.get("kv_cache_gb"),
+                                max_num_seqs=int(s.get("max_num_seqs", 256)),
+                                max_model_len=s.get("max_model_len"), weights=s.get("weights"),
+                                seed=int(s.get("seed", 0)), use_graphs=bool(s.get("graphs", True)))
+                engines[key] = eng
+            pools[tier] = EnginePool(tier, eng, max_new_tokens=int(s.get("max_new_tokens", 256)),
+                                     temperature=float(s.get("temperature", 0.0)), top_k=int(s.get("top_k", 0)),
+                                     top_p=float(s.get("top_p", 1.0)))
+        else:
+            raise ValueError(f"unknown pool kind {kind!r}")
+    for t in (SMALL, LARGE):
+        if t not in pools:
+            raise ValueError(f"pool spec must define tier {t!r}")
+    return pools
+
+
+def dispatch_groups(pools: Dict[str, PoolClient], groups: Dict[str, List[Any]]) -> Dict[str, List[Dict[str, Any]]]:
+    """Serve each tier's group; tiers that share one engine are served in ONE continuous batch."""
+    out: Dict[str, List[Dict[str, Any]]] = {}
+    eng_groups: Dict[int, List[str]] = {}
+    for dev, hs in groups.items():
+        p = pools[dev]
+        if hs and isinstance(p, EnginePool):
+            eng_groups.setdefault(id(p.engine), []).append(dev)
+    done = set()
+    for devs in eng_groups.values():
+        if len(devs) < 2:
+            continue
+        engine = pools[devs[0]].engine
+        prompts, params, owners = [], [], []
+        for dev in devs:
+            pp = pools[dev]._params()
+            for h in groups[dev]:
+                prompts.append(format_prompt(h))
+                params.append(pp)
+                owners.append(dev)
+        res = EnginePool.to_payloads(engine.generate(prompts, params))
+        for dev in devs:
+            out[dev] = []
+        for dev, r in zip(owners, res):
+            out[dev].append(r)
+        done.update(devs)
+    for dev, hs in groups.items():
+        if dev in done or not hs:
+            continue
+        out[dev] = pools[dev].process_batch(hs)
+    return out

@@ -1,0 +1,442 @@
+"""Predictive routing cache: exact + semantic lookup, recency-weighted device prediction.
+
+Behavioural spec: reference ``src/cache.py`` —
+  RoutingRecord :53-77, CacheEntry :79-176 (predict_device :106-140), CacheLookupResult
+  :179-192, QueryCache :199-554 (lookup :236-326, insert :328-370, invalidate :372-396,
+  warm_up :398-420, save/load :426-465, stats :471-500, clear :502-512, eviction :532-554).
+
+MI355X-first differences:
+  * The reference scans every entry in a Python loop per lookup (O(N) cosine in the
+    interpreter).  Here embeddings live in a slot-indexed ``EmbeddingIndex`` — a contiguous
+    [capacity, dim] table with per-slot norms and context-key ids.  On a GPU box the table is
+    an HBM tensor and lookup is ONE fused HIP kernel (mask by context id, cosine, arg-max over
+    ≥ threshold) — ``ops.masked_cosine_argmax``; on CPU it is a vectorised numpy GEMV.  A
+    288 GB device holds ~180M fp32 384-d entries, so ``cache_max_size`` is no longer a memory
+    concern.
+  * All counters are updated under the lock (the reference increments ``_attempts`` outside it,
+    SURVEY §2.11 quirk 8).
+JSON persistence format is identical to the reference's ``CacheEntry.to_dict``.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import logging
+import re
+import threading
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..config import LARGE, SMALL
+
+logger = logging.getLogger(__name__)
+
+PREDICTION_CONFIDENCE_THRESHOLD = 0.60
+RECENCY_DECAY = 0.85
+MAX_HISTORY = 20
+
+
+@dataclass
+class RoutingRecord:
+    device: str
+    confidence: float
+    method: str
+    timestamp: str
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {"device": self.device, "confidence": self.confidence,
+                "method": self.method, "timestamp": self.timestamp}
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "RoutingRecord":
+        return cls(device=d["device"], confidence=float(d["confidence"]),
+                   method=d.get("method", "unknown"),
+                   timestamp=d.get("timestamp", datetime.now().isoformat()))
+
+
+@dataclass
+class CacheEntry:
+    query: str
+    query_hash: str
+    context_key: str
+    embedding: Optional[np.ndarray]
+    timestamp: datetime
+    device_used: str
+    response_time: Optional[float] = None
+    hit_count: int = 0
+    routing_history: List[RoutingRecord] = field(default_factory=list)
+    slot: int = -1  # row in the EmbeddingIndex (-1: no embedding)
+
+    MAX_HISTORY = MAX_HISTORY
+
+    def record_routing(self, device: str, confidence: float, method: str) -> None:
+        self.routing_history.append(
+            RoutingRecord(device, confidence, method, datetime.now().isoformat()))
+        if len(self.routing_history) > MAX_HISTORY:
+            del self.routing_history[:-MAX_HISTORY]
+        self.device_used = device
+
+    def predict_device(self) -> Tuple[str, float]:
+        """Recency-decayed (0.85^i, newest first) confidence-weighted vote; large wins ties."""
+        if not self.routing_history:
+            return self.device_used, 0.5
+        small = large = 0.0
+        w = 1.0
+        for rec in reversed(self.routing_history):
+            v = w * rec.confidence
+            if rec.device == LARGE:
+                large += v
+            else:
+                small += v
+            w *= RECENCY_DECAY
+        total = small + large
+        if total < 1e-9:
+            return self.device_used, 0.5
+        if large >= small:
+            return LARGE, float(min(large / total, 1.0))
+        return SMALL, float(min(small / total, 1.0))
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {
+            "query": self.query,
+            "query_hash": self.query_hash,
+            "context_key": self.context_key,
+            "embedding": self.embedding.tolist() if self.embedding is not None else None,
+            "timestamp": self.timestamp.isoformat(),
+            "device_used": self.device_used,
+            "response_time": self.response_time,
+            "hit_count": self.hit_count,
+            "routing_history": [r.to_dict() for r in self.routing_history],
+        }
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "CacheEntry":
+        emb = d.get("embedding")
+        return cls(
+            query=d["query"], query_hash=d["query_hash"], context_key=d["context_key"],
+            embedding=np.asarray(emb, dtype=np.float32) if emb else None,
+            timestamp=datetime.fromisoformat(d["timestamp"]), device_used=d["device_used"],
+            response_time=d.get("response_time"), hit_count=d.get("hit_count", 0),
+            routing_history=[RoutingRecord.from_dict(r) for r in d.get("routing_history", [])])
+
+
+@dataclass
+class CacheLookupResult:
+    entry: CacheEntry
+    predicted_device: str
+    predicted_confidence: float
+    use_hybrid_fallback: bool
+
+
+class EmbeddingIndex:
+    """Slot-indexed embedding table for vectorised / on-GPU semantic lookup.
+
+    ``device=None`` keeps a numpy table on the host; a torch device string keeps an HBM table
+    and uses the fused HIP scorer.
+    """
+
+    def __init__(self, dim: int = 384, capacity: int = 1024, device: Optional[str] = None):
+        self.dim = dim
+        self.device = device
+        self._free: List[int] = []
+        self._next = 0
+        self._ctx_ids: Dict[str, int] = {}
+        self._alloc(capacity)
+
+    def _alloc(self, capacity: int) -> None:
+        self.capacity = capacity
+        if self.device is None:
+            self.table = np.zeros((capacity, self.dim), dtype=np.float32)
+            self.norms = np.zeros(capacity, dtype=np.float32)
+            self.ctx = np.full(capacity, -1, dtype=np.int32)
+        else:
+            import torch
+            self.table = torch.zeros((capacity, self.dim), dtype=torch.float32, device=self.device)
+            self.norms = torch.zeros(capacity, dtype=torch.float32, device=self.device)
+            self.ctx = torch.full((capacity,), -1, dtype=torch.int32, device=self.device)
+
+    def _grow(self) -> None:
+        old_t, old_n, old_c, old_cap = self.table, self.norms, self.ctx, self.capacity
+        self._alloc(old_cap * 2)
+        self.table[:old_cap] = old_t
+        self.norms[:old_cap] = old_n
+        self.ctx[:old_cap] = old_c
+
+    def ctx_id(self, key: str) -> int:
+        i = self._ctx_ids.get(key)
+        if i is None:
+            i = self._ctx_ids[key] = len(self._ctx_ids)
+        return i
+
+    def put(self, vec: np.ndarray, context_key: str, slot: int = -1) -> int:
+        if slot < 0:
+            if self._free:
+                slot = self._free.pop()
+            else:
+                if self._next >= self.capacity:
+                    self._grow()
+                slot = self._next
+                self._next += 1
+        v = np.asarray(vec, dtype=np.float32).reshape(-1)
+        n = float(np.linalg.norm(v))
+        cid = self.ctx_id(context_key)
+        if self.device is None:
+            self.table[slot] = v
+            self.norms[slot] = n
+            self.ctx[slot] = cid
+        else:
+            import torch
+            self.table[slot] = torch.from_numpy(v).to(self.device, non_blocking=True)
+            self.norms[slot] = n
+            self.ctx[slot] = cid
+        return slot
+
+    def remove(self, slot: int) -> None:
+        if slot < 0:
+            return
+        self.ctx[slot] = -1
+        self._free.append(slot)
+
+    def clear(self) -> None:
+        self._free.clear()
+        self._next = 0
+        self._ctx_ids.clear()
+        self.ctx[:] = -1
+
+    def best(self, q: Any, context_key: str, threshold: float) -> Tuple[int, float]:
+        """Best slot with cosine >= threshold among slots of ``context_key``; (-1, 0) if none."""
+        cid = self._ctx_ids.get(context_key)
+        if cid is None or self._next == 0:
+            return -1, 0.0
+        hi = self._next
+        if self.device is None:
+            qv = np.asarray(q, dtype=np.float32).reshape(-1)
+            nq = float(np.linalg.norm(qv))
+            if nq < 1e-9:
+                return -1, 0.0
+            mask = (self.ctx[:hi] == cid) & (self.norms[:hi] >= 1e-9)
+            if not mask.any():
+                return -1, 0.0
+            idx = np.nonzero(mask)[0]
+            sims = (self.table[idx] @ qv) / (self.norms[idx] * nq)
+            j = int(np.argmax(sims))
+            s = float(sims[j])
+            return (int(idx[j]), s) if s >= threshold else (-1, 0.0)
+        from .. import ops
+        import torch
+        qt = q if isinstance(q, torch.Tensor) else torch.from_numpy(np.asarray(q, np.float32))
+        qt = qt.to(self.device, torch.float32).reshape(-1)
+        slot, sim = ops.masked_cosine_argmax(qt, self.table[:hi], self.norms[:hi], self.ctx[:hi],
+                                             cid, threshold)
+        return slot, sim
+
+
+class QueryCache:
+    """Thread-safe LRU + TTL routing cache with semantic lookup and device prediction."""
+
+    def __init__(self, max_size: int = 100, ttl_seconds: int = 300, similarity_threshold: float = 0.85,
+                 use_semantic: bool = True,
+                 prediction_confidence_threshold: float = PREDICTION_CONFIDENCE_THRESHOLD,
+                 index_device: Optional[str] = None, dim: int = 384):
+        self.max_size = max_size
+        self.ttl_seconds = ttl_seconds
+        self.similarity_threshold = similarity_threshold
+        self.use_semantic = use_semantic
+        self.prediction_confidence_threshold = prediction_confidence_threshold
+        self._store: "OrderedDict[str, CacheEntry]" = OrderedDict()
+        self._lock = threading.RLock()
+        self._index = EmbeddingIndex(dim=dim, capacity=max(64, min(max_size, 1 << 20)),
+                                     device=index_device)
+        self._slot_to_hash: Dict[int, str] = {}
+        self._hits = 0
+        self._attempts = 0
+        self._evictions = 0
+        self._hybrid_fallbacks = 0
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _make_hash(query: str, context_key: str) -> str:
+        return hashlib.md5(f"{context_key}||{query.lower().strip()}".encode("utf-8")).hexdigest()
+
+    def _is_valid(self, entry: CacheEntry, now: Optional[datetime] = None) -> bool:
+        return ((now or datetime.now()) - entry.timestamp).total_seconds() <= self.ttl_seconds
+
+    def _delete_entry(self, h: str) -> None:
+        e = self._store.pop(h, None)
+        if e is not None and e.slot >= 0:
+            self._index.remove(e.slot)
+            self._slot_to_hash.pop(e.slot, None)
+            e.slot = -1
+
+    def _set_embedding(self, e: CacheEntry, emb: Optional[np.ndarray]) -> None:
+        if emb is None:
+            return
+        arr = np.asarray(emb.detach().float().cpu().numpy() if hasattr(emb, "detach") else emb,
+                         dtype=np.float32).reshape(-1)
+        e.embedding = arr.copy()
+        if e.slot < 0 or self._slot_to_hash.get(e.slot) != e.query_hash:
+            e.slot = self._index.put(arr, e.context_key)
+            self._slot_to_hash[e.slot] = e.query_hash
+        else:
+            self._index.put(arr, e.context_key, slot=e.slot)
+
+    def _evict_expired(self) -> None:
+        now = datetime.now()
+        with self._lock:
+            for h in [h for h, e in self._store.items() if not self._is_valid(e, now)]:
+                self._delete_entry(h)
+                self._evictions += 1
+
+    def _evict_one(self) -> None:
+        now = datetime.now()
+        for h, e in self._store.items():
+            if not self._is_valid(e, now):
+                self._delete_entry(h)
+                self._evictions += 1
+                return
+        if self._store:
+            self._delete_entry(next(iter(self._store)))
+            self._evictions += 1
+
+    def _result(self, entry: CacheEntry) -> CacheLookupResult:
+        dev, conf = entry.predict_device()
+        low = conf < self.prediction_confidence_threshold
+        if low:
+            self._hybrid_fallbacks += 1
+        return CacheLookupResult(entry, dev, conf, low)
+
+    # ------------------------------------------------------------------ API
+    def lookup(self, query: str, context_key: str, q_emb: Any = None) -> Optional[CacheLookupResult]:
+        with self._lock:
+            self._attempts += 1
+        self._evict_expired()
+        h = self._make_hash(query, context_key)
+        with self._lock:
+            cand = self._store.get(h)
+            if cand is not None and cand.context_key == context_key:
+                if self._is_valid(cand):
+                    cand.hit_count += 1
+                    self._store.move_to_end(h)
+                    self._hits += 1
+                    return self._result(cand)
+                self._delete_entry(h)
+            if not self.use_semantic or q_emb is None:
+                return None
+            slot, _sim = self._index.best(q_emb, context_key, self.similarity_threshold)
+            if slot < 0:
+                return None
+            bh = self._slot_to_hash.get(slot)
+            cand = self._store.get(bh) if bh else None
+            if cand is None or not self._is_valid(cand):
+                return None
+            cand.hit_count += 1
+            self._store.move_to_end(bh)
+            self._hits += 1
+            return self._result(cand)
+
+    def insert(self, query: str, context_key: str, device: str, confidence: float = 1.0,
+               method: str = "unknown", q_emb: Any = None, response_time: Optional[float] = None) -> None:
+        h = self._make_hash(query, context_key)
+        with self._lock:
+            e = self._store.get(h)
+            if e is not None:
+                e.timestamp = datetime.now()
+                e.record_routing(device, confidence, method)
+                self._set_embedding(e, q_emb)
+                if response_time is not None:
+                    e.response_time = response_time
+                self._store.move_to_end(h)
+                return
+            if len(self._store) >= self.max_size:
+                self._evict_one()
+            e = CacheEntry(query=query, query_hash=h, context_key=context_key, embedding=None,
+                           timestamp=datetime.now(), device_used=device, response_time=response_time)
+            self._set_embedding(e, q_emb)
+            e.record_routing(device, confidence, method)
+            self._store[h] = e
+
+    def invalidate(self, context_key: Optional[str] = None, query_pattern: Optional[str] = None) -> int:
+        pat = re.compile(query_pattern, re.IGNORECASE) if query_pattern else None
+        with self._lock:
+            doomed = [h for h, e in self._store.items()
+                      if (context_key is None or e.context_key == context_key)
+                      and (pat is None or pat.search(e.query))]
+            for h in doomed:
+                self._delete_entry(h)
+        return len(doomed)
+
+    def warm_up(self, pairs: List[Tuple[str, str, str]], embedder: Any = None) -> None:
+        vecs: List[Optional[np.ndarray]] = [None] * len(pairs)
+        if embedder is not None and pairs:
+            try:
+                vecs = list(embedder.encode([q for q, _, _ in pairs]))
+            except Exception as exc:  # embedding is optional for warm-up
+                logger.warning("warm_up: embedding failed, skipping vectors: %s", exc)
+        for (q, ck, dev), v in zip(pairs, vecs):
+            self.insert(q, ck, dev, q_emb=v)
+
+    def save(self, path: str) -> None:
+        self._evict_expired()
+        with self._lock:
+            data = [e.to_dict() for e in self._store.values()]
+        Path(path).write_text(json.dumps(data, indent=2), encoding="utf-8")
+
+    def load(self, path: str) -> int:
+        p = Path(path)
+        if not p.exists():
+            return 0
+        try:
+            raw = json.loads(p.read_text(encoding="utf-8"))
+        except json.JSONDecodeError as exc:
+            logger.error("Cache load: JSON parse error: %s", exc)
+            return 0
+        n = 0
+        with self._lock:
+            for d in raw:
+                try:
+                    e = CacheEntry.from_dict(d)
+                except Exception as exc:
+                    logger.warning("Cache load: skipping malformed entry: %s", exc)
+                    continue
+                if not self._is_valid(e):
+                    continue
+                if e.query_hash in self._store:
+                    self._delete_entry(e.query_hash)
+                emb, e.embedding = e.embedding, None
+                self._set_embedding(e, emb)
+                self._store[e.query_hash] = e
+                n += 1
+        return n
+
+    def stats(self) -> Dict[str, Any]:
+        with self._lock:
+            now = datetime.now()
+            valid = sum(1 for e in self._store.values() if self._is_valid(e, now))
+            size = len(self._store)
+            hot = sorted(self._store.values(), key=lambda e: e.hit_count, reverse=True)[:5]
+            top = []
+            for e in hot:
+                dev, conf = e.predict_device()
+                top.append({"query": e.query[:60], "hits": e.hit_count, "predicted_device": dev,
+                            "predicted_confidence": round(conf, 3),
+                            "history_len": len(e.routing_history)})
+            return {"size": size, "max_size": self.max_size, "valid": valid, "stale": size - valid,
+                    "hits": self._hits, "attempts": self._attempts,
+                    "hit_rate": round(self._hits / max(self._attempts, 1), 4),
+                    "evictions": self._evictions, "hybrid_fallbacks": self._hybrid_fallbacks,
+                    "top_queries": top}
+
+    def clear(self) -> None:
+        with self._lock:
+            self._store.clear()
+            self._slot_to_hash.clear()
+            self._index.clear()
+            self._hits = self._attempts = self._evictions = self._hybrid_fallbacks = 0
+
+    def __len__(self) -> int:
+        return len(self._store)

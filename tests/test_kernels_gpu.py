@@ -1,0 +1,186 @@
+"""Numerics of every HIP kernel vs the plain-PyTorch f32 reference (ops.reference)."""
+import math
+
+import pytest
+import torch
+
+from distributed_llm_amd import ops
+from distributed_llm_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native():
+    assert ops.native_available(), "HIP extension must be built for GPU tests"
+
+
+def bf(*s, scale=1.0):
+    return (torch.randn(*s, device=DEV) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("H", [384, 2048, 3072, 4096, 8192])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rms_norm(H, with_res):
+    torch.manual_seed(0)
+    x, w = bf(37, H), bf(H)
+    r1 = bf(37, H) if with_res else None
+    r2 = r1.clone() if with_res else None
+    y = ops.rms_norm(x, w, 1e-5, residual=r1)
+    yr = ref.rms_norm(x, w, 1e-5, residual=r2)
+    torch.testing.assert_close(y.float(), yr.float(), atol=3e-2, rtol=2e-2)
+    if with_res:
+        torch.testing.assert_close(r1, r2, atol=0, rtol=0)
+
+
+def test_layer_norm():
+    torch.manual_seed(1)
+    x, w, b, r = bf(50, 384), bf(384), bf(384), bf(50, 384)
+    r2 = r.clone()
+    y = ops.layer_norm(x, w, b, 1e-12, residual=r)
+    yr = ref.layer_norm(x, w, b, 1e-12, residual=r2)
+    torch.testing.assert_close(y.float(), yr.float(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 4, 64), (32, 8, 128), (32, 32, 96)])
+def test_rope_and_cache(nq, nkv, d):
+    torch.manual_seed(2)
+    T, NB = 29, 8
+    qkv = bf(T, (nq + 2 * nkv) * d)
+    pos = torch.randint(0, 500, (T,), device=DEV, dtype=torch.int32)
+    perm = torch.randperm(NB * 16, device=DEV)[:T].to(torch.int32)
+    perm[3] = -1
+    cs = ops.rope_cos_sin(1024, d, 10000.0, DEV)
+    kc, vc = torch.zeros(NB, nkv, 16, d, dtype=torch.bfloat16, device=DEV), torch.zeros(NB, nkv, d, 16, dtype=torch.bfloat16, device=DEV)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = ops.rope_and_cache(qkv, pos, cs, perm, kc, vc, nq, nkv, d)
+    q2 = ref.rope_and_cache(qkv, pos, cs, perm, kc2, vc2, nq, nkv, d)
+    torch.testing.assert_close(q.float(), q2.float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(kc.float(), kc2.float(), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(vc, vc2, atol=0, rtol=0)
+
+
+def _attn_case(nq, nkv, d, seqs, NB=64, spike=False, seed=3):
+    torch.manual_seed(seed)
+    kc, vc = bf(NB, nkv, 16, d), bf(NB, nkv, d, 16)
+    S = len(seqs)
+    maxb = max((c + 15) // 16 for _, c in seqs)
+    bt = torch.zeros(S, maxb, dtype=torch.int32)
+    perm = torch.randperm(NB)
+    k = 0
+    for s, (_, c) in enumerate(seqs):
+        nb = (c + 15) // 16
+        bt[s, :nb] = perm[k:k + nb]
+        k += nb
+    assert k <= NB
+    T = sum(q for q, _ in seqs)
+    q = bf(T, nq, d)
+    if spike:  # force online-softmax rescales: one huge key late in each sequence
+        for s, (_, c) in enumerate(seqs):
+            key = c - 3
+            blk, off = int(bt[s, key // 16]), key % 16
+            kc[blk, :, off, :] = 8.0
+        q = q.abs()
+    qstart, qlen, ctx = [], [], []
+    t = 0
+    for ql, c in seqs:
+        qstart.append(t); qlen.append(ql); ctx.append(c); t += ql
+    ts, tt = ops.build_tiles(qlen, nq // nkv)
+    I = lambda x: torch.tensor(x, dtype=torch.int32, device=DEV)
+    return q, kc, vc, bt.to(DEV), I(qstart), I(qlen), I(ctx), I(ts), I(tt)
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 4, 64), (32, 8, 64), (32, 8, 128), (32, 32, 96), (64, 8, 128), (16, 16, 64)])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_paged_attention_mixed(nq, nkv, d, splits):
+    # decode rows (qlen 1), prefix-cached prefill (qlen < ctx), fresh prefill (qlen == ctx), ragged sizes
+    seqs = [(1, 1), (1, 17), (1, 300), (5, 40), (33, 33), (7, 129), (1, 64), (16, 16)]
+    q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(nq, nkv, d, seqs, NB=96)
+    scale = 1 / math.sqrt(d)
+    o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, scale=scale, splits=splits)
+    o2 = ref.paged_attention(q, kc, vc, bt, qs, ql, cx, scale)
+    torch.testing.assert_close(o.float(), o2.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_paged_attention_rescale_branch(splits):
+    seqs = [(1, 200), (9, 150), (1, 1000)]
+    q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(32, 8, 128, seqs, NB=96, spike=True)
+    o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=splits)
+    o2 = ref.paged_attention(q, kc, vc, bt, qs, ql, cx, 1 / math.sqrt(128))
+    torch.testing.assert_close(o.float(), o2.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_paged_attention_bidirectional():
+    seqs = [(20, 20), (7, 7)]
+    q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(16, 16, 64, seqs)
+    o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, causal=False)
+    o2 = ref.paged_attention(q, kc, vc, bt, qs, ql, cx, 1 / 8.0, causal=False)
+    torch.testing.assert_close(o.float(), o2.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_silu_mul_gelu():
+    torch.manual_seed(4)
+    gu = bf(19, 2 * 5632)
+    torch.testing.assert_close(ops.silu_mul(gu).float(), ref.silu_mul(gu).float(), atol=2e-2, rtol=2e-2)
+    x = bf(7, 1536)
+    torch.testing.assert_close(ops.gelu(x).float(), ref.gelu(x).float(), atol=2e-2, rtol=2e-2)
+
+
+def test_mean_pool_l2():
+    torch.manual_seed(5)
+    x = bf(6, 33, 384)
+    lens = torch.tensor([1, 5, 33, 2, 17, 33], dtype=torch.int32, device=DEV)
+    torch.testing.assert_close(ops.mean_pool_l2(x, lens), ref.mean_pool_l2(x, lens), atol=1e-3, rtol=1e-3)
+
+
+def test_moe_gate():
+    torch.manual_seed(6)
+    lg = torch.randn(300, 8, device=DEV)
+    ids, w = ops.moe_gate(lg, 2)
+    ids2, w2 = ref.moe_gate(lg, 2)
+    assert torch.equal(ids.long(), ids2.long())
+    torch.testing.assert_close(w, w2, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("V", [32000, 32064, 128256, 1001])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_argmax(V, dtype):
+    torch.manual_seed(7)
+    Vp = (V + 15) // 8 * 8  # strided rows, row stride kept 16-B aligned
+    lg = torch.randn(9, Vp, device=DEV).to(dtype)[:, :V]
+    lg[3, 17] = 100.0
+    a = ops.argmax(lg)
+    assert torch.equal(a.long(), torch.argmax(lg.float(), -1))
+
+
+def test_sample_top_p():
+    torch.manual_seed(8)
+    B, K = 64, 40
+    vals = torch.sort(torch.randn(B, K, device=DEV) * 3, dim=-1, descending=True).values
+    idx = torch.randint(0, 32000, (B, K), device=DEV)
+    temp = torch.rand(B, device=DEV) + 0.3
+    top_p = torch.rand(B, device=DEV) * 0.9 + 0.1
+    u = torch.rand(B, device=DEV)
+    a = ops.sample_top_p(vals, idx, temp, top_p, u)
+    b = ref.sample_top_p(vals, idx, temp, top_p, u)
+    # identical except for float ties at CDF boundaries
+    assert (a.long() == b.long()).float().mean() > 0.95
+
+
+def test_cosine_kernels():
+    torch.manual_seed(9)
+    q, c = torch.randn(5, 384, device=DEV), torch.randn(7, 384, device=DEV)
+    torch.testing.assert_close(ops.cosine_scores(q, c), ref.cosine_scores(q, c), atol=1e-5, rtol=1e-4)
+    N = 5000
+    table = torch.randn(N, 384, device=DEV)
+    qv = table[1234] + 0.05 * torch.randn(384, device=DEV)
+    norms = table.norm(dim=-1)
+    ctx = torch.randint(0, 3, (N,), device=DEV, dtype=torch.int32)
+    ctx[1234] = 2
+    r, s = ops.masked_cosine_argmax(qv, table, norms, ctx, 2, 0.85)
+    r2, s2 = ref.masked_cosine_argmax(qv, table, norms, ctx, 2, 0.85)
+    assert r == r2 == 1234 and abs(s - s2) < 1e-4
+    r, s = ops.masked_cosine_argmax(qv, table, norms, ctx, 1, 0.85)
+    assert r == -1
