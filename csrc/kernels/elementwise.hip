@@ -77,8 +77,9 @@ __global__ void moe_gate_kernel(const float* __restrict__ logits, int T, int E, 
     sid[i] = bi;
   }
   // softmax over all E then renormalise over the selected == softmax over the selected logits
+  const float m = sel[0];
   float s = 0.f;
-  for (int i = 0; i < k; ++i) { sel[i] = __expf(sel[i] - sel[0]); s += sel[i]; }
+  for (int i = 0; i < k; ++i) { sel[i] = __expf(sel[i] - m); s += sel[i]; }
   for (int i = 0; i < k; ++i) { ids[(long)t * k + i] = sid[i]; w[(long)t * k + i] = sel[i] / s; }
 }
 }  // namespace

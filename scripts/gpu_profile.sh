@@ -1,0 +1,14 @@
+#!/bin/bash
+# Kernel-level profile of the flagship bench (rocprofv3 kernel trace + stats, no PMC).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+STEPS=${STEPS:-3}
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
+  python3 bench.py --steps $STEPS --warmup 1 ${BENCH_ARGS} > gpurun_out/prof_bench.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof_bench.log
+f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
+[ -n "$f" ] && python3 scripts/prof_summary.py "$f" 40 > gpurun_out/prof/summary.md && head -50 gpurun_out/prof/summary.md
+find gpurun_out/prof -name "*trace*" -delete
+exit $rc

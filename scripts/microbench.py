@@ -1,0 +1,137 @@
+"""Engine/kernel micro-benchmarks on one GPU (prints JSON lines).
+
+  decode  : one hipGraph decode step of the flagship model at batch B, context C
+            (weight bytes + KV bytes per step -> effective HBM bandwidth)
+  attn    : paged decode attention kernel alone (KV bytes / time)
+  prefill : packed prefill throughput (tokens/s) for a batch of prompts
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from distributed_llm_amd import ops
+from distributed_llm_amd.engine.llm_engine import LLMEngine
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def bench_attn(B, C, nq, nkv, d, splits):
+    NB = B * ((C + 15) // 16) + 8
+    kc = torch.randn(NB, nkv, 16, d, device="cuda").to(torch.bfloat16)
+    vc = torch.randn(NB, nkv, d, 16, device="cuda").to(torch.bfloat16)
+    nb = (C + 15) // 16
+    bt = torch.randperm(NB - 8, device="cuda")[:B * nb].view(B, nb).to(torch.int32)
+    q = torch.randn(B, nq, d, device="cuda").to(torch.bfloat16)
+    I = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    qs, ql, cx = I(list(range(B))), I([1] * B), I([C] * B)
+    ts, tt = ops.build_tiles([1] * B, nq // nkv)
+    ts, tt = I(ts), I(tt)
+    ms = timeit(lambda: ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=splits))
+    kv_bytes = B * C * nkv * d * 2 * 2
+    return {"bench": "attn_decode", "B": B, "C": C, "nq": nq, "nkv": nkv, "d": d, "splits": splits,
+            "us": round(ms * 1000, 1), "GBps": round(kv_bytes / ms / 1e6, 1)}
+
+
+def bench_decode(eng, B, C):
+    # fabricate B running sequences of context C (tokens are irrelevant for timing)
+    bm = eng.bm
+    seqs = []
+    for i in range(B):
+        sid = 10_000_000 + i
+        bm.allocate(sid, [5] * C)
+        row = eng._free_rows.pop()
+        t = bm.block_table(sid)
+        eng.bt_host[row, :len(t)] = t
+        seqs.append((sid, row))
+    eng._bt_dirty = True
+
+    class S:  # minimal stand-in for engine._Seq
+        pass
+    run = []
+    for sid, row in seqs:
+        s = S()
+        s.id, s.row, s.out = sid, row, [7]
+        s.length = C
+        run.append(s)
+    bs = eng._bucket(B)
+    o, h, R = eng._off, eng.dec_host, eng.R
+    import numpy as np
+    rows = np.array([s.row for s in run])
+    pos = np.full(B, C - 1)
+    blocks = eng.bt_host[rows, pos // 16]
+    h[:] = 0
+    h[o[0]:o[0] + B] = 7
+    h[o[1]:o[1] + B] = pos
+    h[o[2]:o[2] + bs] = -1
+    h[o[2]:o[2] + B] = blocks * 16 + pos % 16
+    h[o[3]:o[3] + bs] = R
+    h[o[3]:o[3] + B] = rows
+    h[o[4] + rows] = np.arange(B)
+    h[o[5] + rows] = 1
+    h[o[6] + rows] = C
+    eng._sync_bt()
+    eng.dec_dev.copy_(eng.dec_host_t)
+    g = eng._graphs.get(bs) or eng._capture(bs)
+    ms = timeit(g.replay)
+    wbytes = eng.model.weight_bytes()
+    kv = B * C * eng.cfg.n_layers * eng.model.nkv * eng.model.d * 2 * 2
+    for sid, row in seqs:
+        bm.free(sid)
+        eng.bt_host[row] = 0
+        eng._free_rows.append(row)
+    return {"bench": "decode_step", "model": eng.cfg.name, "B": B, "bucket": bs, "C": C, "ms": round(ms, 3),
+            "tok_s": round(B / ms * 1000, 1), "weight_GB": round(wbytes / 1e9, 2),
+            "eff_GBps": round((wbytes + kv) / ms / 1e6, 1)}
+
+
+def bench_prefill(eng, B, L):
+    from distributed_llm_amd.engine.sampling import SamplingParams
+    import random
+    prompts = [[random.randint(3, 250) for _ in range(L)] for _ in range(B)]
+    eng.bm.reset()
+    t = time.perf_counter()
+    eng.generate(prompts, SamplingParams(max_new_tokens=1))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    return {"bench": "prefill", "B": B, "L": L, "s": round(dt, 4), "tok_s": round(B * L / dt, 1)}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="tinyllama-1.1b")
+    ap.add_argument("--what", default="attn,decode,prefill")
+    a = ap.parse_args()
+    what = a.what.split(",")
+    if "attn" in what:
+        for (B, C) in [(1, 2048), (16, 2048), (64, 2048), (64, 8192), (256, 1024)]:
+            for (nq, nkv, d) in [(32, 4, 64), (32, 8, 128)]:
+                tiles = B
+                splits = max(1, min(16, math.ceil(1024 / (tiles * nkv))))
+                print(json.dumps(bench_attn(B, C, nq, nkv, d, splits)), flush=True)
+    if "decode" in what or "prefill" in what:
+        eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
+        if "decode" in what:
+            for B in (1, 8, 32, 64, 128, 256):
+                for C in (512, 2048):
+                    print(json.dumps(bench_decode(eng, B, C)), flush=True)
+        if "prefill" in what:
+            for B, L in ((1, 512), (8, 1024), (32, 2048)):
+                print(json.dumps(bench_prefill(eng, B, L)), flush=True)
