@@ -13,7 +13,7 @@ int dllm_rope_kv(const void*, long, const int*, const float*, const int*, void*,
                  hipStream_t);
 int dllm_kv_write(const void*, const void*, long, const int*, void*, void*, int, int, int, int, hipStream_t);
 int dllm_paged_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*,
-                         const int*, const int*, void*, float*, float*, int, int, int, int, int, int, int, float,
+                         const int*, const int*, void*, float*, float*, int*, int, int, int, int, int, int, int, float,
                          hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
@@ -22,6 +22,10 @@ int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
 int dllm_argmax(const void*, long, int, int, int, int*, hipStream_t);
 int dllm_sample_topp(const float*, const long*, int, int, const float*, const float*, const float*, int*, hipStream_t);
 int dllm_cosine_scores(const float*, const float*, float*, int, int, int, hipStream_t);
+int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
+                     hipStream_t);
+int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
+                         hipStream_t);
 int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
                               unsigned long long*, hipStream_t);
 }
@@ -111,7 +115,8 @@ void kv_write(torch::Tensor k, torch::Tensor v, torch::Tensor slots, torch::Tens
 void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
                      torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
                      torch::Tensor tile_tok0, torch::Tensor out, c10::optional<torch::Tensor> part_o,
-                     c10::optional<torch::Tensor> part_ml, int64_t splits, bool causal, double scale) {
+                     c10::optional<torch::Tensor> part_ml, c10::optional<torch::Tensor> counters, int64_t splits,
+                     bool causal, double scale) {
   check_bf16(q, "q");
   check_bf16(kc, "k_cache");
   check_bf16(vc, "v_cache");
@@ -131,7 +136,12 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
   TORCH_CHECK(tile_tok0.numel() == num_tiles, "tile metadata len");
   float* po = nullptr;
   float* pml = nullptr;
+  int* cnt = nullptr;
   if (splits > 1) {
+    TORCH_CHECK(counters.has_value(), "split-K needs a zeroed counter buffer");
+    check_i32(*counters, "counters");
+    TORCH_CHECK(counters->numel() >= (int64_t)num_tiles * nkv, "counter buffer too small");
+    cnt = counters->data_ptr<int>();
     TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "split-K needs workspaces");
     check_f32(*part_o, "part_o");
     check_f32(*part_ml, "part_ml");
@@ -143,7 +153,7 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
   }
   ok(dllm_paged_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                           qstart.data_ptr<int>(), qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(),
-                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, num_tiles, nq, nkv, d,
+                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, num_tiles, nq, nkv, d,
                           block_tables.size(1), splits, causal ? 1 : 0, (float)scale, stream()),
      "paged_attention");
 }
@@ -242,6 +252,34 @@ void masked_cosine_argmax(torch::Tensor q, torch::Tensor table, torch::Tensor no
                                (unsigned long long*)best.data_ptr<int64_t>(), stream()),
      "masked_cosine_argmax");
 }
+// y[M, N] = x[M, K] . w[N, K]^T   (swiglu: x is [M, 2K] gate|up, silu(gate)*up computed on load)
+void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw, int64_t splits, bool swiglu,
+                 torch::Tensor part, torch::Tensor counters, int64_t variant) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  check_f32(part, "part");
+  check_i32(counters, "counters");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous() && y.dim() == 2 &&
+                  y.stride(1) == 1,
+              "2-D row-major operands");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == (swiglu ? 2 * K : K), "x inner dim");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N, "y shape");
+  TORCH_CHECK(M >= 1 && M <= 128 && K % 32 == 0, "M in [1,128], K % 32 == 0");
+  TORCH_CHECK(ntw == 1 || ntw == 2 || ntw == 4, "ntw in {1,2,4}");
+  TORCH_CHECK(variant == 0 || ntw <= 2, "LDS variant: ntw in {1,2}");
+  TORCH_CHECK(variant == 0 || M <= 64 || ntw == 1, "LDS variant: M > 64 needs ntw 1");
+  const int nc = (variant == 0 ? 16 : 64) * ntw, tiles = (N + nc - 1) / nc, mp = ((M + 15) / 16) * 16;
+  if (splits > 1) {
+    TORCH_CHECK(part.numel() >= (int64_t)splits * tiles * nc * mp, "split-K workspace too small");
+    TORCH_CHECK(counters.numel() >= tiles, "counter buffer too small");
+  }
+  auto fn = variant == 0 ? dllm_skinny_gemm : dllm_skinny_lds_gemm;
+  ok(fn(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, ntw, splits, swiglu ? 1 : 0,
+        part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
+     "skinny_gemm");
+}
 }  // namespace
 
 PYBIND11_MODULE(_hip_kernels, m) {
@@ -258,4 +296,5 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("sample_topp", &sample_topp);
   m.def("cosine_scores", &cosine_scores);
   m.def("masked_cosine_argmax", &masked_cosine_argmax);
+  m.def("skinny_gemm", &skinny_gemm);
 }

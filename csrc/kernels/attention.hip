@@ -17,7 +17,8 @@
 //
 // Split-K: grid.z splits the key range of every tile; 4 waves of a workgroup interleave 32-key
 // chunks of the split and are combined through LDS.  With grid.z == 1 the workgroup writes the
-// normalised bf16 output; otherwise it writes (m, l, O) partials and attn_combine_kernel reduces.
+// normalised bf16 output; otherwise it writes (m, l, O) partials, takes a ticket, and the LAST
+// workgroup of the tile combines all splits in the same launch (no second kernel).
 #include "common.h"
 
 namespace {
@@ -38,6 +39,7 @@ struct AttnArgs {
   u16* out;              // [Tq, nq, d]
   float* part_o;         // [num_tiles, nkv, splits, 16, d]
   float* part_ml;        // [num_tiles, nkv, splits, 16, 2]
+  int* counters;         // [num_tiles * nkv] zeroed; re-armed by the reducing workgroup
   int nq, nkv, G, max_blocks, causal;
   float scale_log2;
 };
@@ -49,6 +51,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
   __shared__ float s_o[WAVES][16][D + 1];
   __shared__ float s_m[WAVES][16];
   __shared__ float s_l[WAVES][16];
+  __shared__ int s_last;
 
   const int tile = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z, splits = gridDim.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -88,40 +91,45 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
 
   const int* bt = a.block_tables + (long)(seq >= 0 ? seq : 0) * a.max_blocks;
   const long head_stride = (long)BS * D;  // elements per (block, head) in either cache
-  for (int kb = k_begin + 32 * wave; kb < k_end; kb += 32 * WAVES) {
+  // One register stage per 32-key chunk (a 2-stage prefetch pipeline measured SLOWER on MI355X:
+  // +30 VGPRs cost a wave per SIMD, and occupancy hides the K/V latency better than ILP here).
+  struct KV {
+    uint4 k0[KSTEPS], k1[KSTEPS];
+    uint2 v0[NT], v1[NT];
+  };
+  auto load = [&](KV& r, int kb) {
     const int b0 = bt[kb >> 4];
     const int b1 = (kb + 16 < k_end) ? bt[(kb >> 4) + 1] : b0;
     const u16* k0 = a.kc + ((long)b0 * a.nkv + kvh) * head_stride;
     const u16* k1 = a.kc + ((long)b1 * a.nkv + kvh) * head_stride;
     const u16* v0 = a.vc + ((long)b0 * a.nkv + kvh) * head_stride;
     const u16* v1 = a.vc + ((long)b1 * a.nkv + kvh) * head_stride;
-    // issue all K and V loads up-front (latency overlap)
-    uint4 kf0[KSTEPS], kf1[KSTEPS];
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
-      kf0[s] = ld16(k0 + rl * D + 8 * g + 32 * s);
-      kf1[s] = ld16(k1 + rl * D + 8 * g + 32 * s);
+      r.k0[s] = ld16(k0 + rl * D + 8 * g + 32 * s);
+      r.k1[s] = ld16(k1 + rl * D + 8 * g + 32 * s);
     }
-    uint2 vf0[NT], vf1[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
-      vf0[n] = *reinterpret_cast<const uint2*>(v0 + (16 * n + rl) * BS + 4 * g);
-      vf1[n] = *reinterpret_cast<const uint2*>(v1 + (16 * n + rl) * BS + 4 * g);
+      r.v0[n] = *reinterpret_cast<const uint2*>(v0 + (16 * n + rl) * BS + 4 * g);
+      r.v1[n] = *reinterpret_cast<const uint2*>(v1 + (16 * n + rl) * BS + 4 * g);
     }
+  };
+  auto compute = [&](const KV& r, int kb) {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
-      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf0[s]), qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf1[s]), qf[s], s1, 0, 0, 0);
+      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.k0[s]), qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.k1[s]), qf[s], s1, 0, 0, 0);
     }
     // scores for row rl: keys kb + 4g + r (s0) and kb + 16 + 4g + r (s1)
     float p[8];
     float mloc = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key0 = kb + 4 * g + r, key1 = kb + 16 + 4 * g + r;
-      p[r] = (key0 < row_lim && key0 < k_end) ? s0[r] * a.scale_log2 : -INFINITY;
-      p[4 + r] = (key1 < row_lim && key1 < k_end) ? s1[r] * a.scale_log2 : -INFINITY;
+    for (int q = 0; q < 4; ++q) {
+      const int key0 = kb + 4 * g + q, key1 = kb + 16 + 4 * g + q;
+      p[q] = (key0 < row_lim && key0 < k_end) ? s0[q] * a.scale_log2 : -INFINITY;
+      p[4 + q] = (key1 < row_lim && key1 < k_end) ? s1[q] * a.scale_log2 : -INFINITY;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) mloc = fmaxf(mloc, p[j]);
@@ -141,9 +149,14 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       acc[n] *= alpha;
-      const uint4 vv = make_uint4(vf0[n].x, vf0[n].y, vf1[n].x, vf1[n].y);
+      const uint4 vv = make_uint4(r.v0[n].x, r.v0[n].y, r.v1[n].x, r.v1[n].y);
       acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, acc[n], 0, 0, 0);
     }
+  };
+  for (int kb = k_begin + 32 * wave; kb < k_end; kb += 32 * WAVES) {
+    KV r;
+    load(r, kb);
+    compute(r, kb);
   }
 
   // ---- combine the 4 waves through LDS.  acc[n][r] = O^T[dim 16n + 4g + r][row rl]
@@ -154,68 +167,117 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
     for (int r = 0; r < 4; ++r) s_o[wave][rl][16 * n + 4 * g + r] = acc[n][r];
   __syncthreads();
 
-  for (int e = threadIdx.x; e < 16 * D; e += blockDim.x) {
+  const int G_ = G;
+  if (splits == 1) {
+    for (int e = threadIdx.x; e < 16 * D; e += blockDim.x) {
+      const int row = e / D, col = e % D;
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) M = fmaxf(M, s_m[w][row]);
+      const float Ms = (M == -INFINITY) ? 0.f : M;
+      float L = 0.f, O = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) {
+        const float f = exp2f(s_m[w][row] - Ms);
+        L += s_l[w][row] * f;
+        O += s_o[w][row][col] * f;
+      }
+      const int tok = tok0 + row / G_, head = kvh * G_ + row % G_;
+      if (seq >= 0 && tok < qlen)
+        a.out[((long)(qstart + tok) * a.nq + head) * D + col] = f2bf(L > 0.f ? O / L : 0.f);
+    }
+    return;
+  }
+  // ---- split-K: write-through partials (O unnormalised in the workgroup's max frame, and per-row
+  // (m, l)), ticket per (tile, kv head); the last arriver combines with sc1 loads (R1 recipe).
+  const long pbase = (((long)tile * a.nkv + kvh) * splits + split) * 16;  // first row of this partial
+  const unsigned obytes = (unsigned)min((long)gridDim.x * a.nkv * splits * 16 * D * 4, 0x7fffffffL);
+  const unsigned mlbytes = (unsigned)min((long)gridDim.x * a.nkv * splits * 16 * 2 * 4, 0x7fffffffL);
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.part_o, obytes), rml = make_rsrc(a.part_ml, mlbytes);
+  for (int e = threadIdx.x * 4; e < 16 * D; e += blockDim.x * 4) {
     const int row = e / D, col = e % D;
     float M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) M = fmaxf(M, s_m[w][row]);
     const float Ms = (M == -INFINITY) ? 0.f : M;
-    float L = 0.f, O = 0.f;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) {
       const float f = exp2f(s_m[w][row] - Ms);
-      L += s_l[w][row] * f;
-      O += s_o[w][row][col] * f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += s_o[w][row][col + j] * f;
     }
-    const int tok = tok0 + row / G, head = kvh * G + row % G;
-    if (splits == 1) {
-      if (seq >= 0 && tok < qlen)
-        a.out[((long)(qstart + tok) * a.nq + head) * D + col] = f2bf(L > 0.f ? O / L : 0.f);
-    } else {
-      const long pidx = (((long)tile * a.nkv + kvh) * splits + split) * 16 + row;
-      a.part_o[pidx * D + col] = O;
-      if (col == 0) { a.part_ml[pidx * 2] = M; a.part_ml[pidx * 2 + 1] = L; }
+    st_wt16(ro, (unsigned)(((pbase + row) * D + col) * 4), make_float4(o[0], o[1], o[2], o[3]));
+  }
+  if (threadIdx.x < 8) {  // rows 2t, 2t+1: (m, l, m, l)
+    float ml[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 2 * threadIdx.x + h;
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) M = fmaxf(M, s_m[w][row]);
+      const float Ms = (M == -INFINITY) ? 0.f : M;
+      float L = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) L += s_l[w][row] * exp2f(s_m[w][row] - Ms);
+      ml[2 * h] = M;
+      ml[2 * h + 1] = L;
     }
+    st_wt16(rml, (unsigned)((pbase + 2 * threadIdx.x) * 2 * 4), make_float4(ml[0], ml[1], ml[2], ml[3]));
+  }
+  if (!ticket_last(&a.counters[tile * a.nkv + kvh], splits, &s_last)) return;
+  const long tbase = (((long)tile * a.nkv + kvh) * splits) * 16;
+  if (threadIdx.x < 16) {
+    const int row = threadIdx.x;
+    float M = -INFINITY;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 q = ld_wt16(rml, (unsigned)((tbase + sp * 16 + (row & ~1)) * 2 * 4));
+      M = fmaxf(M, (row & 1) ? q.z : q.x);
+    }
+    const float Ms = (M == -INFINITY) ? 0.f : M;
+    float L = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 q = ld_wt16(rml, (unsigned)((tbase + sp * 16 + (row & ~1)) * 2 * 4));
+      const float m = (row & 1) ? q.z : q.x, l = (row & 1) ? q.w : q.y;
+      L += l * exp2f(m - Ms);
+    }
+    s_m[0][row] = Ms;
+    s_l[0][row] = L;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x * 4; e < 16 * D; e += blockDim.x * 4) {
+    const int row = e / D, col = e % D;
+    const int tok = tok0 + row / G_, head = kvh * G_ + row % G_;
+    if (seq < 0 || tok >= qlen) continue;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 mq = ld_wt16(rml, (unsigned)((tbase + sp * 16 + (row & ~1)) * 2 * 4));
+      const float f = exp2f(((row & 1) ? mq.z : mq.x) - s_m[0][row]);
+      const float4 q = ld_wt16(ro, (unsigned)(((tbase + sp * 16 + row) * D + col) * 4));
+      o[0] += q.x * f; o[1] += q.y * f; o[2] += q.z * f; o[3] += q.w * f;
+    }
+    const float L = s_l[0][row], inv = L > 0.f ? 1.f / L : 0.f;
+    u16* dst = a.out + ((long)(qstart + tok) * a.nq + head) * D + col;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = f2bf(o[j] * inv);
   }
 }
 
-__global__ void attn_combine_kernel(AttnArgs a, int D, int splits) {
-  const int tile = blockIdx.x, kvh = blockIdx.y;
-  const int seq = a.tile_seq[tile];
-  if (seq < 0) return;
-  const int qlen = a.seq_qlen[seq], qstart = a.seq_qstart[seq], tok0 = a.tile_tok0[tile];
-  for (int e = threadIdx.x; e < 16 * D; e += blockDim.x) {
-    const int row = e / D, col = e % D;
-    const int tok = tok0 + row / a.G, head = kvh * a.G + row % a.G;
-    if (tok >= qlen) continue;
-    const long base = ((long)tile * a.nkv + kvh) * splits * 16 + row;
-    float M = -INFINITY;
-    for (int s = 0; s < splits; ++s) M = fmaxf(M, a.part_ml[(base + s * 16) * 2]);
-    const float Ms = (M == -INFINITY) ? 0.f : M;
-    float L = 0.f, O = 0.f;
-    for (int s = 0; s < splits; ++s) {
-      const long pi = base + s * 16;
-      const float f = exp2f(a.part_ml[pi * 2] - Ms);
-      L += a.part_ml[pi * 2 + 1] * f;
-      O += a.part_o[pi * D + col] * f;
-    }
-    a.out[((long)(qstart + tok) * a.nq + head) * D + col] = f2bf(L > 0.f ? O / L : 0.f);
-  }
-}
 }  // namespace
 
 extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* vc, const int* block_tables,
                                     const int* seq_qstart, const int* seq_qlen, const int* seq_ctx,
                                     const int* tile_seq, const int* tile_tok0, void* out, float* part_o,
-                                    float* part_ml, int num_tiles, int nq, int nkv, int d, int max_blocks,
+                                    float* part_ml, int* counters, int num_tiles, int nq, int nkv, int d, int max_blocks,
                                     int splits, int causal, float scale, hipStream_t stream) {
   if (nq % nkv != 0) return -1;
   const int G = nq / nkv;
   if (16 % G != 0) return -2;
-  if (splits < 1 || (splits > 1 && (!part_o || !part_ml))) return -3;
+  if (splits < 1 || (splits > 1 && (!part_o || !part_ml || !counters))) return -3;
   if (num_tiles <= 0) return 0;
   AttnArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
-             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, nq, nkv, G, max_blocks, causal, scale * LOG2E};
+             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, nq, nkv, G, max_blocks, causal, scale * LOG2E};
   dim3 grid(num_tiles, nkv, splits), block(64 * WAVES);
   switch (d) {
     case 64: hipLaunchKernelGGL(paged_attn_kernel<64>, grid, block, 0, stream, a); break;
@@ -223,7 +285,5 @@ extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* v
     case 128: hipLaunchKernelGGL(paged_attn_kernel<128>, grid, block, 0, stream, a); break;
     default: return -4;
   }
-  if (splits > 1)
-    hipLaunchKernelGGL(attn_combine_kernel, dim3(num_tiles, nkv), dim3(256), 0, stream, a, d, splits);
   return (int)hipGetLastError();
 }

@@ -27,8 +27,45 @@ static __device__ __forceinline__ u16 f2bf(float f) {
   return (u16)(u >> 16);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 static __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+// non-temporal 16-B load (streamed-once operands: decode weights) -> bf16x8 operand
+static __device__ __forceinline__ bf16x8 ldnt_bf16x8(const void* p) {
+  return __builtin_bit_cast(bf16x8, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
+}
 static __device__ __forceinline__ void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+// ---- in-launch hand-off helpers (cdna_hip_programming.md Guideline 16, recipe R1):
+// payload stored WRITE-THROUGH (sc1, 16 B) so no release fence (which writes back the whole XCD
+// L2) is needed; every storing wave drains with s_waitcnt vmcnt(0) before the workgroup barrier;
+// one lane takes the ticket with a relaxed agent-scope atomic; the consumer reads the payload
+// ONLY with sc1 loads (bypass its L1), so it needs no acquire fence either.
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+static __device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float4 v) {
+  const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, byte_off, 0, 16 /* sc1 */);
+}
+static __device__ __forceinline__ float4 ld_wt16(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */);
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
+// Drain this wave's stores, barrier, one ticket per workgroup; returns true in the LAST arriver.
+// `flag` must be a __shared__ int.  The counter is re-armed (0) by the last arriver.
+static __device__ __forceinline__ bool ticket_last(int* counter, int expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = (old == expected - 1);
+    if (last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
 
 // unpack 8 bf16 (one uint4) to f32
 static __device__ __forceinline__ void unpack8(uint4 v, float* f) {

@@ -22,6 +22,7 @@ import math
 import os
 import threading
 import time
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -80,6 +81,7 @@ class _Seq:
     num_cached: int = 0
     num_computed: int = 0
     row: int = -1
+    text: Optional[str] = None
     admitted: Optional[float] = None
     first_tok: Optional[float] = None
     finished: Optional[float] = None
@@ -108,11 +110,15 @@ class LLMEngine:
         self.bm = _need_runtime().BlockManager(self.num_blocks, BS, prefix_cache)
         self._ids = itertools.count()
         self._lock = threading.Lock()
+        self._memo: "OrderedDict[str, List[int]]" = OrderedDict()
+        self._memo_cap = 200_000
         self.on_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.on_gpu
         self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
         self._gen.manual_seed(seed + 1)
         self._init_rows()
+        if self.on_gpu:
+            self._autotune()
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
@@ -160,15 +166,55 @@ class LLMEngine:
         self.max_splits = 16
         ws = mb * nkv * self.max_splits * 16
         self.dec_ws = (torch.empty(ws * dh, dtype=torch.float32, device=self.device),
-                       torch.empty(ws * 2, dtype=torch.float32, device=self.device))
+                       torch.empty(ws * 2, dtype=torch.float32, device=self.device),
+                       torch.zeros(mb * nkv, dtype=torch.int32, device=self.device))
+
+    def _autotune(self) -> None:
+        """Pick the fastest GEMM plan for every decode bucket and weight shape (before capture)."""
+        m = self.model
+        shapes = set()
+        L = m.layers[0]
+        for name in ("wqkv", "wo", "wgu"):
+            if name in L:
+                shapes.add((L[name].shape[0], L[name].shape[1], False))
+        if "wd" in L:
+            shapes.add((L["wd"].shape[0], L["wd"].shape[1], True))
+        shapes.add((m.lm_head.shape[0], m.lm_head.shape[1], False))
+        ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= 128], self.device,
+                          verbose=os.environ.get("DLLM_VERBOSE") == "1")
 
     def _splits_for(self, tiles: int) -> int:
-        return int(max(1, min(self.max_splits, math.ceil(1024 / max(1, tiles * self.model.nkv)))))
+        # measured on MI355X (scripts/microbench.py attn): split-K pays only while tiles x kv-heads
+        # leaves CUs idle; at >= 256 work units one split is fastest.
+        return int(max(1, min(8, math.ceil(256 / max(1, tiles * self.model.nkv)))))
 
     # ------------------------------------------------------------------ public API
     def encode(self, text: str) -> List[int]:
-        ids = self.tok.encode(text)
-        return ids
+        """Tokenise a prompt, re-using the exact token ids of the longest previously served
+        prompt+response text that prefixes it (session memo).
+
+        A chat turn's prompt is the previous turn's prompt + the model's reply + the new user
+        message.  Re-tokenising the reply text does not, in general, give back the token ids the
+        model generated (and whose KV blocks are cached); re-using the generated ids makes the
+        whole previous turn a prefix-cache hit, so only the new user message is prefilled.
+        """
+        memo = self._memo
+        if memo:
+            pos = len(text)
+            for _ in range(64):  # message boundaries, newest first
+                pos = text.rfind("\n", 0, pos)
+                if pos <= 0:
+                    break
+                ids = memo.get(text[:pos])
+                if ids is not None:
+                    memo.move_to_end(text[:pos])
+                    return list(ids) + self.tok.encode(text[pos:], add_bos=False)
+        return self.tok.encode(text)
+
+    def _remember(self, text: str, ids: List[int]) -> None:
+        self._memo[text] = ids
+        while len(self._memo) > self._memo_cap:
+            self._memo.popitem(last=False)
 
     def generate(self, prompts: Sequence[Union[str, List[int]]],
                  params: Union[SamplingParams, Sequence[SamplingParams], None] = None) -> List[RequestOutput]:
@@ -181,6 +227,7 @@ class LLMEngine:
         for p, sp in zip(prompts, plist):
             ids = self.encode(p) if isinstance(p, str) else list(p)
             s = _Seq(next(self._ids), ids, sp, now)
+            s.text = p if isinstance(p, str) else None
             limit = self.max_model_len - max(1, sp.max_new_tokens)
             if len(ids) > limit:  # keep the most recent context (left truncation)
                 s.prompt = ids[:1] + ids[len(ids) - limit + 1:]
@@ -458,6 +505,14 @@ class LLMEngine:
         queue = ((s.admitted or end) - s.arrival) * 1000.0
         n = len(s.out)
         dec_t = (end - s.first_tok) if s.first_tok else 0.0
-        toks = [t for t in s.out if t != self.tok.eos_id] if not s.params.ignore_eos else s.out
-        return RequestOutput(s.id, self.tok.decode(toks), list(s.out), len(s.prompt), s.num_cached, n, lat, ttft,
+        toks = [t for t in s.out if t != self.tok.eos_id] if not s.params.ignore_eos else list(s.out)
+        # strip whitespace-only tokens at both ends so that text == decode(ids) exactly (pools strip)
+        while toks and not self.tok.decode(toks[:1]).strip():
+            toks.pop(0)
+        while toks and not self.tok.decode(toks[-1:]).strip():
+            toks.pop()
+        text = self.tok.decode(toks)
+        if s.text is not None and s.error is None and text:
+            self._remember(s.text + text, s.prompt + toks)
+        return RequestOutput(s.id, text, list(s.out), len(s.prompt), s.num_cached, n, lat, ttft,
                              queue, (n - 1) / dec_t if n > 1 and dec_t > 0 else 0.0, s.error)

@@ -172,7 +172,7 @@ class LlamaModel:
 
     def _mlp(self, L, x: torch.Tensor) -> torch.Tensor:
         if not self.cfg.is_moe:
-            return F.linear(ops.silu_mul(F.linear(x, L["wgu"])), L["wd"])
+            return ops.linear_swiglu(ops.linear(x, L["wgu"]), L["wd"])
         return self._moe(L, x)
 
     def _moe(self, L, x: torch.Tensor) -> torch.Tensor:
@@ -207,13 +207,13 @@ class LlamaModel:
         residual = torch.zeros_like(h)
         for li, L in enumerate(self.layers):
             x = ops.rms_norm(h, L["ln1"], cfg.rms_eps, residual=residual)
-            qkv = F.linear(x, L["wqkv"])
+            qkv = ops.linear(x, L["wqkv"])
             kc, vc = kv_caches[li]
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
             o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                     meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
                                     splits=meta.splits, workspace=meta.workspace)
-            h = self.par.all_reduce(F.linear(o.view(o.shape[0], -1), L["wo"]))
+            h = self.par.all_reduce(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
             h = self.par.all_reduce(self._mlp(L, x))
         last_h = h.index_select(0, meta.last_idx)
@@ -222,7 +222,7 @@ class LlamaModel:
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """This rank's vocab shard of the logits: [S, V / tp] (bf16)."""
-        return F.linear(hidden, self.lm_head)
+        return ops.linear(hidden, self.lm_head)
 
     def greedy(self, hidden: torch.Tensor) -> torch.Tensor:
         """Distributed arg-max over the vocab-parallel LM head -> token ids [S] int32."""

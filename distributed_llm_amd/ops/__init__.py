@@ -133,7 +133,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                     seq_qstart: torch.Tensor, seq_qlen: torch.Tensor, seq_ctx: torch.Tensor,
                     tile_seq: torch.Tensor, tile_tok0: torch.Tensor, scale: Optional[float] = None,
                     causal: bool = True, splits: int = 1, out: Optional[torch.Tensor] = None,
-                    workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+                    workspace: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Paged attention over new query tokens ``q [T, nq, d]`` (see csrc/kernels/attention.hip)."""
     d = q.shape[-1]
     scale = (1.0 / math.sqrt(d)) if scale is None else scale
@@ -141,16 +141,17 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     if ext is None:
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, scale, causal)
     o = out if out is not None else torch.empty_like(q)
-    po = pml = None
+    po = pml = cnt = None
     if splits > 1:
         if workspace is None:
             nt, nkv = tile_seq.numel(), k_cache.shape[1]
             po = torch.empty(nt * nkv * splits * 16 * d, dtype=torch.float32, device=q.device)
             pml = torch.empty(nt * nkv * splits * 16 * 2, dtype=torch.float32, device=q.device)
+            cnt = torch.zeros(nt * nkv, dtype=torch.int32, device=q.device)
         else:
-            po, pml = workspace
+            po, pml, cnt = workspace
     ext.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
-                        po, pml, splits, causal, scale)
+                        po, pml, cnt, splits, causal, scale)
     return o
 
 
@@ -248,3 +249,6 @@ def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tens
     bits = (bits & 0x7FFFFFFF) if (bits & 0x80000000) else (~bits & 0xFFFFFFFF)
     sim = struct.unpack("<f", struct.pack("<I", bits))[0]
     return int(row), float(sim)
+
+
+from .gemm import autotune as gemm_autotune, linear, linear_swiglu  # noqa: E402

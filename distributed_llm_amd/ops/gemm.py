@@ -1,0 +1,182 @@
+"""Linear layers: decode-shaped GEMMs on the hand-written MFMA skinny kernel, autotuned.
+
+``linear(x, w)`` computes ``x @ w.T`` (w stored [N, K], K contiguous).
+``linear_swiglu(gu, w)`` computes ``silu(gu[:, :K]) * gu[:, K:] @ w.T`` — the SwiGLU activation is
+fused into the down projection's operand load, so decode runs no separate activation kernel.
+
+Dispatch (GPU): M <= 128 -> ``csrc/kernels/skinny_gemm.hip`` with the (ntw, split-K) plan that the
+autotuner measured fastest for this (M, N, K, swiglu) — including "blas" (hipBLASLt via
+``F.linear``) as a candidate, so the custom kernel is only used where it wins; M > 128 (prefill)
+-> hipBLASLt.  Plans are tuned once per shape OUTSIDE graph capture (``autotune`` is called by the
+engine for every decode bucket before capturing); an unseen shape during capture falls back to
+a heuristic plan.  CPU tensors -> plain torch.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Dict, Iterable, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _native, reference as ref
+
+MAX_M = 128
+_SPLITS = (1, 2, 4, 8, 16)
+_NTWS = (1, 2, 4)
+
+
+class _Planner:
+    def __init__(self):
+        self.plans: Dict[Tuple[int, int, int, bool], Tuple] = {}
+        self.part: Dict[torch.device, torch.Tensor] = {}
+        self.counters: Dict[torch.device, torch.Tensor] = {}
+        self.timings: Dict[Tuple[int, int, int, bool], Dict[str, float]] = {}
+
+    def workspace(self, dev: torch.device, floats: int, tiles: int):
+        p = self.part.get(dev)
+        if p is None or p.numel() < floats:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("skinny_gemm workspace growth during graph capture")
+            p = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=dev)
+            self.part[dev] = p
+        c = self.counters.get(dev)
+        if c is None or c.numel() < tiles:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("skinny_gemm counter growth during graph capture")
+            c = torch.zeros(max(tiles, 4096), dtype=torch.int32, device=dev)
+            self.counters[dev] = c
+        return p, c
+
+
+_P = _Planner()
+
+
+def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tuple[int, int]:
+    nc = (16 if variant == 0 else 64) * ntw
+    tiles = (N + nc - 1) // nc
+    kchunk = ((K + splits - 1) // splits + 31) // 32 * 32
+    S = (K + kchunk - 1) // kchunk
+    mp = (M + 15) // 16 * 16
+    return (S * tiles * nc * mp if S > 1 else 0), tiles
+
+
+def _heuristic(M: int, N: int, K: int) -> Tuple:
+    ntw = 1 if M > 64 else 2
+    tiles = (N + 16 * ntw - 1) // (16 * ntw)
+    splits = max(1, min(16, math.ceil(512 / tiles), K // 256))
+    return ("skinny", ntw, splits)
+
+
+def _run_plan(plan, x, w, swiglu, out):
+    if plan[0] == "blas":
+        if swiglu:
+            x = ref_silu_mul(x)
+        return torch.matmul(x, w.t(), out=out) if out is not None else F.linear(x, w)
+    kind, ntw, splits = plan
+    variant = 0 if kind == "skinny" else 1
+    ext = _native(x)
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
+    floats, tiles = _need(M, N, K, ntw, splits, variant)
+    part, cnt = _P.workspace(x.device, floats, tiles)
+    ext.skinny_gemm(x, w, y, ntw, splits, swiglu, part, cnt, variant)
+    return y
+
+
+def ref_silu_mul(gu):
+    from . import silu_mul
+    return silu_mul(gu)
+
+
+def _key(x, w, swiglu):
+    return (x.shape[0], w.shape[0], w.shape[1], bool(swiglu))
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not x.is_cuda or x.shape[0] > MAX_M or os.environ.get("DLLM_GEMM") == "blas":
+        return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
+    plan = _P.plans.get(_key(x, w, False)) or _heuristic(x.shape[0], w.shape[0], w.shape[1])
+    return _run_plan(plan, x, w, False, out)
+
+
+def linear_swiglu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``silu(gate) * up @ w.T`` with gu = [gate | up] of width 2K."""
+    if not gu.is_cuda:
+        return F.linear(ref.silu_mul(gu), w)
+    if gu.shape[0] > MAX_M or os.environ.get("DLLM_GEMM") == "blas":
+        from . import silu_mul
+        return F.linear(silu_mul(gu), w)
+    plan = _P.plans.get(_key(gu, w, True)) or _heuristic(gu.shape[0], w.shape[0], w.shape[1])
+    return _run_plan(plan, gu, w, True, None)
+
+
+def _time(fn, iters=24) -> float:
+    """GPU time per call of fn(i) in us, measured as a hipGraph replay of ``iters`` calls (the
+    decode step is a graph replay too, so host launch cost is excluded exactly as in serving).
+    Callers rotate operands over i so weights come from HBM, not the 256 MiB Infinity Cache
+    (a decode step streams the whole model: its weights are cold)."""
+    fn(0)  # eager warm-up: allocates workspaces / initialises libraries outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            for i in range(iters):
+                fn(i)
+    torch.cuda.current_stream().wait_stream(st)
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
+
+
+def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False) -> None:
+    """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest."""
+    dev = torch.device(device)
+    if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
+        return
+    for (N, K, sw) in shapes:
+        copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
+        ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        for M in ms:
+            if M > MAX_M:
+                continue
+            key = (M, N, K, sw)
+            if key in _P.plans:
+                continue
+            x = torch.randn(M, 2 * K if sw else K, device=dev).to(torch.bfloat16)
+            cands = [("blas",)]
+            for kind, ntws in (("skinny", _NTWS), ("lds", (1, 2))):
+                for ntw in ntws:
+                    if M > 64 and (ntw == 4 or (kind == "lds" and ntw == 2)):
+                        continue
+                    for s in _SPLITS:
+                        if s > 1 and K // s < 128:
+                            continue
+                        floats, _ = _need(M, N, K, ntw, s, 0 if kind == "skinny" else 1)
+                        if floats * 4 > 256 << 20:
+                            continue
+                        cands.append((kind, ntw, s))
+            res = {}
+            for c in cands:
+                res[c] = _time(lambda i: _run_plan(c, x, ws[i % copies], sw, None))
+            best = min(res, key=res.get)
+            _P.plans[key] = best
+            _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
+            if verbose:
+                bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None) for k in ("skinny", "lds")}
+                extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
+                print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
+                      f"({N * K * 2 / res[best] / 1e3:.0f} GB/s; blas {res[('blas',)]:.1f}us; {extra})", flush=True)
+        del ws
+
+
+def plans() -> Dict:
+    return {str(k): v for k, v in _P.plans.items()}

@@ -189,15 +189,24 @@ class HTTPPool(PoolClient):
 class EnginePool(PoolClient):
     """A pool served by an in-process ``engine.LLMEngine``."""
 
+    # Generation prompt appended after the reference's "role: content" lines (a minimal chat
+    # template): the reply then continues the prompt text exactly, so the next turn's prompt
+    # extends prompt + reply and the engine's session memo / prefix cache reuse the whole turn.
+    GENERATION_PROMPT = "\nassistant: "
+
     def __init__(self, name: str, engine, max_new_tokens: int = 256, temperature: float = 0.0,
-                 top_k: int = 0, top_p: float = 1.0, session_prefix_cache: bool = True):
+                 top_k: int = 0, top_p: float = 1.0, generation_prompt: Optional[str] = None):
         super().__init__()
         self.name = name
+        self.generation_prompt = self.GENERATION_PROMPT if generation_prompt is None else generation_prompt
         self.engine = engine
         self.max_new_tokens = max_new_tokens
         self.temperature = temperature
         self.top_k = top_k
         self.top_p = top_p
+
+    def prompt_for(self, history: Any) -> str:
+        return format_prompt(history) + self.generation_prompt
 
     def _params(self, overrides: Optional[Dict[str, Any]] = None):
         from ..engine.sampling import SamplingParams
@@ -212,7 +221,7 @@ class EnginePool(PoolClient):
         return self.process_batch([history], overrides)[0]
 
     def process_batch(self, histories, overrides: Optional[Dict[str, Any]] = None):
-        prompts = [format_prompt(h) for h in histories]
+        prompts = [self.prompt_for(h) for h in histories]
         return self.to_payloads(self.engine.generate(prompts, self._params(overrides)))
 
     @staticmethod

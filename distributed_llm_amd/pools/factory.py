@@ -67,7 +67,7 @@ def dispatch_groups(pools: Dict[str, PoolClient], groups: Dict[str, List[Any]]) 
         for dev in devs:
             pp = pools[dev]._params()
             for h in groups[dev]:
-                prompts.append(format_prompt(h))
+                prompts.append(pools[dev].prompt_for(h))
                 params.append(pp)
                 owners.append(dev)
         res = EnginePool.to_payloads(engine.generate(prompts, params))

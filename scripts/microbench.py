@@ -114,18 +114,34 @@ def bench_prefill(eng, B, L):
     return {"bench": "prefill", "B": B, "L": L, "s": round(dt, 4), "tok_s": round(B * L / dt, 1)}
 
 
+def bench_gemm(M, N, K):
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    ms = timeit(lambda: torch.nn.functional.linear(x, w), iters=50)
+    return {"bench": "gemm_hipblaslt", "M": M, "N": N, "K": K, "us": round(ms * 1000, 1),
+            "weight_GBps": round(N * K * 2 / ms / 1e6, 1), "TFLOPs": round(2 * M * N * K / ms / 1e9, 1)}
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="tinyllama-1.1b")
-    ap.add_argument("--what", default="attn,decode,prefill")
+    ap.add_argument("--what", default="gemm,attn,decode,prefill")
     a = ap.parse_args()
     what = a.what.split(",")
+    if "tune" in what:
+        from distributed_llm_amd.ops import gemm as G
+        shapes = [(2560, 2048, False), (2048, 2048, False), (11264, 2048, False), (2048, 5632, True),
+                  (32000, 2048, False), (6144, 4096, False), (4096, 4096, False), (28672, 4096, False), (4096, 14336, True)]
+        G.autotune(shapes, [1, 8, 32, 64, 128], "cuda", verbose=True)
+    if "gemm" in what:
+        for M in (1, 16, 64, 128, 256):
+            for (N, K) in [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632), (32000, 2048), (6144, 4096), (28672, 4096), (4096, 14336)]:
+                print(json.dumps(bench_gemm(M, N, K)), flush=True)
     if "attn" in what:
-        for (B, C) in [(1, 2048), (16, 2048), (64, 2048), (64, 8192), (256, 1024)]:
+        for (B, C) in [(1, 2048), (16, 2048), (64, 512), (64, 2048), (64, 8192), (256, 1024)]:
             for (nq, nkv, d) in [(32, 4, 64), (32, 8, 128)]:
-                tiles = B
-                splits = max(1, min(16, math.ceil(1024 / (tiles * nkv))))
-                print(json.dumps(bench_attn(B, C, nq, nkv, d, splits)), flush=True)
+                for splits in (1, 2, 4, 8, 16):
+                    print(json.dumps(bench_attn(B, C, nq, nkv, d, splits)), flush=True)
     if "decode" in what or "prefill" in what:
         eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
         if "decode" in what:

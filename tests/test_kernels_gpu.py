@@ -184,3 +184,33 @@ def test_cosine_kernels():
     assert r == r2 == 1234 and abs(s - s2) < 1e-4
     r, s = ops.masked_cosine_argmax(qv, table, norms, ctx, 1, 0.85)
     assert r == -1
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 100, 128])
+@pytest.mark.parametrize("N,K", [(2560, 2048), (2048, 5632), (200, 96)])
+@pytest.mark.parametrize("ntw,splits", [(1, 1), (2, 4), (4, 8), (1, 16)])
+@pytest.mark.parametrize("kind", ["skinny", "lds"])
+def test_skinny_gemm(M, N, K, ntw, splits, kind):
+    from distributed_llm_amd.ops import gemm
+    if (M > 64 and ntw == 4) or (kind == "lds" and (ntw == 4 or (M > 64 and ntw == 2))):
+        pytest.skip("unsupported tile")
+    torch.manual_seed(10)
+    x, w = bf(M, K, scale=0.5), bf(N, K, scale=0.05)
+    y = gemm._run_plan((kind, ntw, splits), x, w, False, None)
+    yr = (x.float() @ w.float().T)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+    # repeated launches reuse the re-armed counters
+    y2 = gemm._run_plan((kind, ntw, splits), x, w, False, None)
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("M", [1, 64, 128])
+@pytest.mark.parametrize("kind", ["skinny", "lds"])
+def test_skinny_gemm_swiglu(M, kind):
+    from distributed_llm_amd.ops import gemm
+    torch.manual_seed(11)
+    I, H = 1024, 512
+    gu, w = bf(M, 2 * I), bf(H, I, scale=0.05)
+    y = gemm._run_plan((kind, 2 if M <= 64 else 1, 4), gu, w, True, None)
+    yr = ref.silu_mul(gu).float() @ w.float().T
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
