@@ -41,9 +41,14 @@ class ParallelContext:
         """Concatenate ``t`` from every TP rank along a new leading dim -> [tp, *t.shape]."""
         if self.tp_size == 1:
             return t.unsqueeze(0)
-        out = torch.empty((self.tp_size, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.tp_group)
-        return out
+        t = t.contiguous()
+        if t.is_cuda:  # RCCL: one fused all-gather into a preallocated tensor
+            out = torch.empty((self.tp_size, *t.shape), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t, group=self.tp_group)
+            return out
+        parts = [torch.empty_like(t) for _ in range(self.tp_size)]  # gloo (CPU tests)
+        dist.all_gather(parts, t, group=self.tp_group)
+        return torch.stack(parts)
 
 
 SINGLE = ParallelContext()

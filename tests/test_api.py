@@ -1,0 +1,87 @@
+"""HTTP API contract: /chat, /history (reference src/app.py) and the pool worker /, /health,
+/query (reference src/devices/*_api.py), on echo pools."""
+import pytest
+
+from distributed_llm_amd.config import LARGE, SMALL
+from distributed_llm_amd.orchestrator import Router
+from distributed_llm_amd.pools.base import EchoPool, FaultInjectingPool
+from distributed_llm_amd.pools.worker import create_worker_app
+from distributed_llm_amd.server.app import BASE_CONFIG, HISTORY_LIMIT, create_app
+
+CHAT_KEYS = {"reply", "device", "reasoning", "method", "confidence", "cache_hit", "tokens"}
+
+
+@pytest.fixture()
+def client():
+    app = create_app(config=dict(BASE_CONFIG), pools={SMALL: EchoPool(SMALL, 6), LARGE: EchoPool(LARGE, 20)})
+    return app.test_client()
+
+
+def test_chat_contract(client):
+    r = client.post("/chat", json={"message": "Thank you!", "strategy": "heuristic", "session_id": "s1"})
+    assert r.status_code == 200
+    d = r.get_json()
+    assert set(d) == CHAT_KEYS and d["device"] == SMALL and d["tokens"] == 6
+    assert r.headers["Access-Control-Allow-Origin"] == "*"
+    h = client.get("/history?session_id=s1").get_json()
+    assert [m["role"] for m in h] == ["user", "assistant"] and h[1]["content"] == d["reply"]
+
+
+def test_blank_message_400(client):
+    r = client.post("/chat", json={"message": "   "})
+    assert r.status_code == 400 and r.get_json() == {"error": "No message provided"}
+
+
+def test_token_counting_alias_and_bad_strategy(client):
+    assert client.post("/chat", json={"message": "hi", "strategy": "token-counting"}).status_code == 200
+    r = client.post("/chat", json={"message": "hi", "strategy": "nonsense"})
+    assert r.status_code == 500 and r.get_json()["error"].startswith("Failed to switch strategy")
+
+
+def test_history_cap_and_clear(client):
+    for i in range(8):
+        client.post("/chat", json={"message": f"question {i}?", "strategy": "token", "session_id": "cap"})
+    h = client.get("/history?session_id=cap").get_json()
+    assert len(h) == HISTORY_LIMIT
+    assert client.delete("/history?session_id=cap").get_json() == {"cleared": "cap"}
+    assert client.get("/history?session_id=cap").get_json() == []
+
+
+def test_error_rolls_back_history():
+    class Boom(EchoPool):
+        def process(self, h):
+            raise RuntimeError("dead")
+
+    router = Router("token", config={"cache_enabled": False, "enable_failover": False},
+                    pools={SMALL: EchoPool(SMALL), LARGE: EchoPool(LARGE)})
+
+    def broken(history):
+        raise RuntimeError("kaboom")
+    router.route_query = broken
+    c = create_app(router=router).test_client()
+    r = c.post("/chat", json={"message": "hi", "strategy": "token", "session_id": "e"})
+    assert r.status_code == 500
+    d = r.get_json()
+    assert set(d) == CHAT_KEYS and d["device"] == "error" and d["reasoning"] == "kaboom"
+    assert c.get("/history?session_id=e").get_json() == []
+
+
+def test_metrics(client):
+    client.post("/chat", json={"message": "hello"})
+    m = client.get("/metrics").get_json()
+    assert m["strategy"] == "hybrid" and "cache" in m and set(m["pools"]) == {SMALL, LARGE}
+
+
+def test_worker_endpoints():
+    c = create_worker_app(EchoPool(SMALL, 4)).test_client()
+    assert c.get("/").data == b"Test again: Server is running!\n"
+    assert c.get("/health").get_json() == {"ok": True}
+    r = c.post("/query", json={"query": [{"role": "user", "content": "hello"}]})
+    assert r.status_code == 200 and "response" in r.get_json()
+    assert c.post("/query", json={}).status_code == 400
+    assert c.post("/query", json={"query": 5}).status_code == 400
+    rb = c.post("/query", json={"queries": [[{"role": "user", "content": "a"}], "b"]})
+    assert len(rb.get_json()["responses"]) == 2
+    err = create_worker_app(FaultInjectingPool(EchoPool(SMALL), mode="error")).test_client()
+    r = err.post("/query", json={"query": "x"})
+    assert r.status_code == 500 and "error" in r.get_json()

@@ -1,0 +1,109 @@
+"""Benchmark harness: reference CSV schemas (column names and order), experiment sweep semantics,
+resume, legacy final_results.csv, power-log parsing, CLI REPL — on echo pools (BASELINE config 1)."""
+import csv
+import io
+import os
+from datetime import datetime, timedelta
+
+from distributed_llm_amd.bench import harness, legacy_harness, power
+from distributed_llm_amd.config import LARGE, SMALL
+from distributed_llm_amd.pools.base import EchoPool
+
+REF_SUMMARY = ["query_set", "strategy", "cache_mode", "token_threshold", "routing_accuracy",
+               "nano_total_latency_ms", "nano_total_energy_mJ", "nano_avg_power_mW", "nano_total_tokens",
+               "nano_latency_per_token_ms", "nano_energy_per_token_mJ",
+               "orin_total_latency_ms", "orin_total_energy_mJ", "orin_avg_power_mW", "orin_total_tokens",
+               "orin_latency_per_token_ms", "orin_energy_per_token_mJ",
+               "overall_total_latency_ms", "overall_total_energy_mJ", "overall_total_tokens",
+               "overall_latency_per_token_ms", "overall_energy_per_token_mJ"]
+REF_PER_QUERY = ["query_set", "strategy", "cache_mode", "token_threshold", "query_index", "query_text",
+                 "expected_device", "device_used", "cache_hit", "routing_method", "routing_confidence",
+                 "routing_reasoning", "routing_overhead_ms", "start_time", "end_time", "latency_ms",
+                 "response_tokens", "energy_mJ", "latency_per_token_ms", "energy_per_token_mJ"]
+
+
+def test_harness_schema_and_sweep(tmp_path):
+    out, pq = str(tmp_path / "s.csv"), str(tmp_path / "q.csv")
+    harness.main(["--query-set", "general_knowledge", "--thresholds", "100", "1000",
+                  "--strategies", "token", "heuristic", "--cache-modes", "off", "on",
+                  "--output-csv", out, "--output-per-query-csv", pq, "--pools", "echo", "--no-power"])
+    with open(out) as f:
+        rows = list(csv.reader(f))
+    assert rows[0][:len(REF_SUMMARY)] == REF_SUMMARY
+    assert rows[0][len(REF_SUMMARY):] == harness.SUMMARY_EXTRA
+    # token sweeps 2 thresholds x 2 cache modes; heuristic runs once per cache mode at the last threshold
+    keys = [(r[1], r[2], r[3]) for r in rows[1:]]
+    assert keys == [("token", "off", "100"), ("token", "off", "1000"), ("token", "on", "100"),
+                    ("token", "on", "1000"), ("heuristic", "off", "1000"), ("heuristic", "on", "1000")]
+    with open(pq) as f:
+        q = list(csv.DictReader(f))
+    assert list(q[0].keys())[:len(REF_PER_QUERY)] == REF_PER_QUERY
+    assert len(q) == 6 * 12
+    heur = [r for r in q if r["strategy"] == "heuristic" and r["cache_mode"] == "off"]
+    assert heur[0]["device_used"] == "nano" and heur[0]["routing_method"] == "heuristic"
+    acc = [r for r in rows[1:] if r[1] == "heuristic" and r[2] == "off"][0][4]
+    assert 0.0 <= float(acc) <= 1.0
+
+
+def test_heuristic_accuracy_goldens():
+    """SURVEY §2.9 probe goldens: per-query heuristic accuracy 0.75 / 0.80 / 1.00."""
+    from distributed_llm_amd.bench.query_sets import normalize_query_set, query_sets
+    from distributed_llm_amd.config import BENCHMARK_CFG
+    from distributed_llm_amd.router.query_router import QueryRouter
+    qr = QueryRouter("heuristic", dict(BENCHMARK_CFG))
+    for name, want in (("general_knowledge", 0.75), ("technical_coding", 0.80), ("personal_health", 1.00)):
+        items = normalize_query_set(query_sets[name])
+        acc = sum(qr.route_query(i.text).device == i.expected_device for i in items) / len(items)
+        assert abs(acc - want) < 1e-9, name
+
+
+def test_harness_resume(tmp_path):
+    out, pq = str(tmp_path / "s.csv"), str(tmp_path / "q.csv")
+    args = ["--query-set", "technical_coding", "--strategies", "heuristic", "--output-csv", out,
+            "--output-per-query-csv", pq, "--pools", "echo", "--no-power"]
+    harness.main(args)
+    harness.main(args + ["--strategies", "heuristic", "token", "--resume"])
+    with open(out) as f:
+        rows = list(csv.reader(f))
+    assert [r[1] for r in rows[1:]] == ["heuristic", "token"]
+
+
+def test_legacy_final_results(tmp_path):
+    out = str(tmp_path / "final_results.csv")
+    pools = {SMALL: EchoPool(SMALL, 5), LARGE: EchoPool(LARGE, 50)}
+    res = legacy_harness.run_legacy("personal_health", [100, 4000], pools, {}, None, threshold_routing=True,
+                                    output_file=out)
+    with open(out) as f:
+        rows = list(csv.reader(f))
+    assert rows[0] == legacy_harness.LEGACY_HEADER
+    assert len(rows) == 3 and rows[1][0] == "personal_health" and rows[1][1] == "100"
+    # a higher token threshold sends more turns to the small tier (the published table's trend)
+    assert res[4000][SMALL][3] >= res[100][SMALL][3]
+
+
+def test_power_log_roundtrip(tmp_path):
+    p = tmp_path / "power.log"
+    t0 = datetime(2026, 1, 1, 12, 0, 0)
+    lines = [f"{(t0 + timedelta(seconds=i)).strftime(power.TS_FMT)}: {1000 * (i + 1)}" for i in range(5)]
+    p.write_text("\n".join(lines + ["garbage line", "2026-01-01 12:00:09: notanumber"]) + "\n")
+    data = power.parse_power_log(str(p))
+    assert len(data) == 5
+    # left Riemann over [0, 4] s: 1000 + 2000 + 3000 + 4000 mW*s
+    assert power.energy_for_window(data, t0, t0 + timedelta(seconds=4)) == 10000.0
+    assert power.energy_sum_1hz(data, t0, t0 + timedelta(seconds=4)) == 15000.0
+
+
+def test_power_sampler_degrades_without_gpu():
+    s = power.PowerSampler(gpus=[0], hz=5).start()
+    s.stop()
+    assert s.energy_mj([0], datetime.now(), datetime.now()) == 0.0
+
+
+def test_cli_repl():
+    from distributed_llm_amd.server.cli import Chatbot
+    bot = Chatbot(strategy="heuristic", config={"cache_enabled": False}, pools={SMALL: EchoPool(SMALL, 3),
+                                                                                LARGE: EchoPool(LARGE, 9)})
+    out = io.StringIO()
+    bot.chat(stdin=io.StringIO("Thank you!\nquit\n"), stdout=out)
+    assert "Assistant:" in out.getvalue() and out.getvalue().strip().endswith("3\nYou:") or "3" in out.getvalue()
+    assert len(bot.conversation_history) == 2

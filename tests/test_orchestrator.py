@@ -1,0 +1,127 @@
+"""Orchestrator contract (reference src/router.py) on echo pools: payload keys, response cache,
+failover, context hashing, batch routing, fallback on routing exceptions."""
+import hashlib
+
+import pytest
+
+from distributed_llm_amd.config import BENCHMARK_CFG, LARGE, PRODUCTION_CFG, SMALL
+from distributed_llm_amd.orchestrator import Router, extract_text, history_to_query_and_context
+from distributed_llm_amd.pools.base import EchoPool, FaultInjectingPool
+
+MISS_KEYS = {"response", "raw", "cache_hit", "benchmark_mode", "routing_overhead_ms", "routing_method",
+             "routing_confidence", "routing_reasoning", "ok"}
+HIT_KEYS = {"response", "raw", "cache_hit", "routing_method", "routing_confidence", "routing_reasoning",
+            "routing_overhead_ms", "ok"}
+
+
+def pools():
+    return {SMALL: EchoPool(SMALL, 8), LARGE: EchoPool(LARGE, 32)}
+
+
+def test_history_split_and_hash():
+    h = [{"role": "user", "content": " hi "}, {"role": "assistant", "content": "hello"},
+         {"role": "user", "content": "  what is 2+2? "}]
+    q, ctx, k = history_to_query_and_context(h, 6)
+    assert q == "what is 2+2?"
+    assert ctx == "user: hi\nassistant: hello"
+    expect = hashlib.sha256("user:hi\nassistant:hello".encode()).hexdigest()[:16]
+    assert k == expect
+    assert history_to_query_and_context([], 6) == ("", None, "nohist")
+    # no user message: whole history is context
+    q, ctx, _ = history_to_query_and_context([{"role": "assistant", "content": "x"}], 6)
+    assert q == "" and ctx == "assistant: x"
+
+
+def test_extract_text_shapes():
+    assert extract_text({"response": " a "}) == "a"
+    assert extract_text({"message": {"content": "b"}}) == "b"
+    assert extract_text({"error": "boom", "detail": "d"}) == "boom d"
+    assert extract_text("  ") is None and extract_text(None) is None
+
+
+def test_route_query_payload_keys_and_tokens():
+    r = Router("heuristic", config=dict(BENCHMARK_CFG), benchmark_mode=True, pools=pools())
+    payload, ntok, dev = r.route_query([{"role": "user", "content": "Thank you!"}])
+    assert set(payload) == MISS_KEYS
+    assert dev == SMALL and payload["routing_method"] == "heuristic" and payload["ok"] is True
+    assert ntok == 8  # echo pool reports its generated token count
+    payload, ntok, dev = r.route_query([{"role": "user", "content": "Write a Python script that parses CSV"}])
+    assert dev == LARGE and ntok == 32
+
+
+def test_response_cache_is_context_independent_like_reference():
+    cfg = dict(PRODUCTION_CFG)
+    r = Router("heuristic", config=cfg, pools=pools())
+    a, _, _ = r.route_query([{"role": "user", "content": "hello"}])
+    b, ntok, dev = r.route_query([{"role": "user", "content": "x"}, {"role": "assistant", "content": "y"},
+                                  {"role": "user", "content": "  HELLO "}])
+    assert a["cache_hit"] is False
+    assert set(b) == HIT_KEYS and b["cache_hit"] is True and b["routing_method"] == "response_cache"
+    assert b["response"] == a["response"] and dev == SMALL
+
+
+def test_benchmark_mode_disables_response_cache():
+    r = Router("token", config=dict(PRODUCTION_CFG), benchmark_mode=True, pools=pools())
+    assert not r.enable_response_cache
+
+
+def test_failover_to_other_tier():
+    p = pools()
+    p[SMALL] = FaultInjectingPool(p[SMALL], mode="error")
+    r = Router("heuristic", config={"enable_failover": True, "cache_enabled": False}, pools=p)
+    payload, ntok, dev = r.route_query([{"role": "user", "content": "Thank you!"}])
+    assert dev == LARGE and payload["ok"] is True and payload["routing_method"] == "heuristic"
+
+
+def test_failover_disabled_returns_error_payload():
+    p = pools()
+    p[SMALL] = FaultInjectingPool(p[SMALL], mode="error")
+    r = Router("heuristic", config={"enable_failover": False, "cache_enabled": False}, pools=p)
+    payload, ntok, dev = r.route_query([{"role": "user", "content": "Thank you!"}])
+    assert dev == SMALL and payload["ok"] is False and "injected fault" in payload["response"]
+
+
+def test_perf_feedback_reaches_perf_router():
+    r = Router("perf", config={"cache_enabled": False}, pools=pools())
+    for _ in range(3):
+        r.route_query([{"role": "user", "content": "q"}])
+    snap = r.query_router.router.snapshot()
+    assert snap[SMALL]["n"] == 3
+
+
+def test_routing_exception_falls_back_to_context_size():
+    r = Router("token", config={"cache_enabled": False}, threshold_fallback=5, pools=pools())
+
+    def boom(**kw):
+        raise RuntimeError("router down")
+    r.query_router.route_query = boom
+    payload, _, dev = r.route_query([{"role": "user", "content": "a long enough message to exceed five tokens"}])
+    assert payload["routing_method"] == "fallback_ctx_size" and payload["routing_confidence"] == 0.2
+    assert dev == LARGE
+
+
+def test_route_batch_matches_sequential_decisions():
+    hs = [[{"role": "user", "content": q}] for q in ("Thank you!", "Write code for a web api", "hello there")]
+    r1 = Router("heuristic", config={"cache_enabled": False}, pools=pools())
+    r2 = Router("heuristic", config={"cache_enabled": False}, pools=pools())
+    seq = [r1.route_query(h) for h in hs]
+    bat = r2.route_batch(hs)
+    assert [s[2] for s in seq] == [b[2] for b in bat]
+    assert [s[0]["routing_method"] for s in seq] == [b[0]["routing_method"] for b in bat]
+
+
+def test_route_batch_failover():
+    p = pools()
+    p[LARGE] = FaultInjectingPool(p[LARGE], mode="error")
+    r = Router("heuristic", config={"cache_enabled": False}, pools=p)
+    out = r.route_batch([[{"role": "user", "content": "Write a Python function"}]])
+    assert out[0][2] == SMALL and out[0][0]["ok"]
+
+
+def test_penalise_failed_primary_option():
+    p = pools()
+    p[SMALL] = FaultInjectingPool(p[SMALL], mode="error")
+    r = Router("perf", config={"cache_enabled": False, "penalise_failed_primary": True}, pools=p)
+    r.route_query([{"role": "user", "content": "q"}])
+    snap = r.query_router.router.snapshot()
+    assert snap[SMALL]["n"] == 1 and snap[LARGE]["n"] == 1
