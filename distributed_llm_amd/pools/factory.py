@@ -13,6 +13,7 @@ worker) or ``"echo"``.
 """
 from __future__ import annotations
 
+from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Dict, List, Sequence, Tuple
 
 from ..config import LARGE, SMALL, canonical_tier
@@ -76,8 +77,12 @@ def dispatch_groups(pools: Dict[str, PoolClient], groups: Dict[str, List[Any]]) 
         for dev, r in zip(owners, res):
             out[dev].append(r)
         done.update(devs)
-    for dev, hs in groups.items():
-        if dev in done or not hs:
-            continue
-        out[dev] = pools[dev].process_batch(hs)
+    rest = [dev for dev, hs in groups.items() if dev not in done and hs]
+    if len(rest) == 1:
+        out[rest[0]] = pools[rest[0]].process_batch(groups[rest[0]])
+    elif rest:  # different pools (other GPUs / other ranks) serve their groups concurrently
+        with ThreadPoolExecutor(max_workers=len(rest)) as ex:
+            futs = {dev: ex.submit(pools[dev].process_batch, groups[dev]) for dev in rest}
+            for dev, f in futs.items():
+                out[dev] = f.result()
     return out
