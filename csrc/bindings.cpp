@@ -19,6 +19,7 @@ int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
 int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
+int dllm_scatter_pairs(int*, const int*, int, hipStream_t);
 int dllm_argmax(const void*, long, int, int, int, int*, hipStream_t);
 int dllm_sample_topp(const float*, const long*, int, int, const float*, const float*, const float*, int*, hipStream_t);
 int dllm_cosine_scores(const float*, const float*, float*, int, int, int, hipStream_t);
@@ -194,6 +195,15 @@ void moe_gate(torch::Tensor logits, int64_t k, torch::Tensor ids, torch::Tensor 
   ok(dllm_moe_gate(logits.data_ptr<float>(), T, E, k, ids.data_ptr<int>(), w.data_ptr<float>(), stream()), "moe_gate");
 }
 
+// dst (int32, any shape, contiguous) flat[idx_i] = val_i for buf = [n, idx0, val0, ...]
+void scatter_pairs(torch::Tensor dst, torch::Tensor buf) {
+  check_i32(dst, "dst");
+  check_i32(buf, "buf");
+  TORCH_CHECK(buf.numel() >= 1 && buf.numel() % 2 == 1, "buf = [n, (idx, val)*]");
+  ok(dllm_scatter_pairs(dst.data_ptr<int>(), buf.data_ptr<int>(), (int)(buf.numel() - 1) / 2, stream()),
+     "scatter_pairs");
+}
+
 void argmax(torch::Tensor logits, torch::Tensor out) {
   check_dev(logits, "logits");
   check_i32(out, "out");
@@ -293,6 +303,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("moe_gate", &moe_gate);
   m.def("argmax", &argmax);
+  m.def("scatter_pairs", &scatter_pairs);
   m.def("sample_topp", &sample_topp);
   m.def("cosine_scores", &cosine_scores);
   m.def("masked_cosine_argmax", &masked_cosine_argmax);

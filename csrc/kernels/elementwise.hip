@@ -82,6 +82,12 @@ __global__ void moe_gate_kernel(const float* __restrict__ logits, int T, int E, 
   for (int i = 0; i < k; ++i) { sel[i] = __expf(sel[i] - m); s += sel[i]; }
   for (int i = 0; i < k; ++i) { ids[(long)t * k + i] = sid[i]; w[(long)t * k + i] = sel[i] / s; }
 }
+// buf = [n, idx0, val0, idx1, val1, ...]: dst[idx_i] = val_i.  n is read on the device, so a
+// captured decode graph applies a different number of block-table updates on every replay.
+__global__ void scatter_pairs_kernel(int* __restrict__ dst, const int* __restrict__ buf, int cap) {
+  const int n = min(buf[0], cap);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[buf[1 + 2 * i]] = buf[2 + 2 * i];
+}
 }  // namespace
 
 static inline int grid_for(long n, int threads) {
@@ -110,6 +116,11 @@ extern "C" int dllm_mean_pool_l2(const void* x, const int* lens, float* out, int
   int threads = ((H + 3) / 4 + 63) / 64 * 64;
   if (threads > 256 || threads * 4 < H) return -1;
   hipLaunchKernelGGL(mean_pool_l2_kernel, dim3(B), dim3(threads), 0, stream, (const u16*)x, lens, out, S, H);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_scatter_pairs(int* dst, const int* buf, int cap, hipStream_t stream) {
+  hipLaunchKernelGGL(scatter_pairs_kernel, dim3(1), dim3(256), 0, stream, dst, buf, cap);
   return (int)hipGetLastError();
 }
 

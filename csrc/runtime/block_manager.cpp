@@ -113,6 +113,19 @@ class BlockManager {
     return s.blocks[pos / bs_] * bs_ + pos % bs_;
   }
 
+  // One decode step for a batch: commit the K/V of every sequence's current length, then append
+  // its new token.  Returns the new token's slot per sequence (-1: finished/skip or out of blocks).
+  std::vector<int> commit_append(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks,
+                                 const std::vector<uint8_t>& append) {
+    std::vector<int> out(ids.size(), -1);
+    for (size_t i = 0; i < ids.size(); ++i) {
+      Seq& s = get(ids[i]);
+      commit(ids[i], (int)s.tokens.size());
+      if (append[i]) out[i] = append_token(ids[i], toks[i]);
+    }
+    return out;
+  }
+
   // Slots of token positions [start, end) of a sequence.
   std::vector<int> slots(int64_t id, int start, int end) {
     Seq& s = get(id);
@@ -256,6 +269,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def("allocate", &BlockManager::allocate)
       .def("append_token", &BlockManager::append_token)
       .def("slots", &BlockManager::slots)
+      .def("commit_append", &BlockManager::commit_append)
       .def("commit", &BlockManager::commit)
       .def("block_table", &BlockManager::block_table)
       .def("seq_len", &BlockManager::seq_len)

@@ -142,19 +142,24 @@ class LLMEngine:
         R = self.max_num_seqs
         self.R = R
         self._free_rows = list(range(R - 1, -1, -1))
-        self.bt_host = np.zeros((R + 1, self.max_blocks), dtype=np.int32)  # row R: dummy (padding)
+        pin = self.on_gpu
+        # host mirror of the device block table (pinned); row R is the dummy row of padding tiles.
+        self.bt_host_t = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, pin_memory=pin)
+        self.bt_host = self.bt_host_t.numpy()
         self.bt_dev = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, device=self.device)
-        self._bt_dirty = True
+        self._bt_dirty = True          # whole-table copy needed (admissions / releases)
+        self._bt_upd: List[int] = []   # (flat index, block) pairs applied inside the decode graph
         self.buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if b < R] + [R]
         mb = self.buckets[-1]
         # packed decode buffer: ids | pos | slots | tile_seq  (mb each) | qstart | qlen | ctx (R+1 each)
-        self._dec_n = 4 * mb + 3 * (R + 1)
+        #                       | block-table updates [n, (flat idx, block) * R]
+        self._dec_n = 4 * mb + 3 * (R + 1) + 1 + 2 * R
         self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
-        pin = self.on_gpu
         self.dec_host_t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
         self.dec_host = self.dec_host_t.numpy()
-        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1)]
+        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1), 4 * mb + 3 * (R + 1)]
         self._off = o
+        self.d_upd = self.dec_dev[o[7]:]
         d = self.dec_dev
         self.d_ids, self.d_pos, self.d_slots, self.d_tseq = (d[o[0]:o[1]], d[o[1]:o[2]], d[o[2]:o[3]], d[o[3]:o[4]])
         self.d_qstart, self.d_qlen, self.d_ctx = d[o[4]:o[5]], d[o[5]:o[6]], d[o[6]:o[6] + R + 1]
@@ -317,31 +322,36 @@ class LLMEngine:
         self._bt_dirty = True
 
     def _sync_bt(self) -> None:
-        if self._bt_dirty:
-            self.bt_dev.copy_(torch.from_numpy(self.bt_host), non_blocking=False)
+        if self._bt_dirty:  # rare (admission / release): synchronous whole-table copy
+            self.bt_dev.copy_(self.bt_host_t, non_blocking=False)
             self._bt_dirty = False
+            self._bt_upd.clear()
 
     # ------------------------------------------------------------------ sampling
     def _sample(self, hidden: torch.Tensor, seqs: List[_Seq], greedy_ids: Optional[torch.Tensor]) -> List[int]:
         n = len(seqs)
-        if all(s.params.greedy for s in seqs):
-            ids = greedy_ids[:n] if greedy_ids is not None else self.model.greedy(hidden[:n])
+        dev = hidden.device
+        ids = greedy_ids[:n] if greedy_ids is not None else self.model.greedy(hidden[:n])
+        sampled = [i for i, s in enumerate(seqs) if not s.params.greedy]
+        if not sampled:
             return ids.tolist()
-        k = max(s.params.k for s in seqs)
-        vals, idx = self.model.topk_candidates(hidden[:n], k)
-        temp = torch.tensor([s.params.temperature if not s.params.greedy else 1e-5 for s in seqs],
-                            dtype=torch.float32, device=hidden.device)
-        top_p = torch.tensor([s.params.top_p if not s.params.greedy else 0.0 for s in seqs],
-                             dtype=torch.float32, device=hidden.device)
-        # per-row top-k: mask candidates beyond each row's k
-        ks = torch.tensor([s.params.k for s in seqs], device=hidden.device)
-        cols = torch.arange(vals.shape[1], device=hidden.device)[None, :]
-        vals = torch.where(cols < ks[:, None], vals, torch.full_like(vals, -float("inf")))
-        u = torch.rand(n, generator=self._gen, device=hidden.device)
+        # only the sampled rows go through top-k + nucleus sampling; greedy rows keep the arg-max
+        sel = torch.tensor(sampled, dtype=torch.int64, device=dev)
+        k = max(seqs[i].params.k for i in sampled)
+        vals, idx = self.model.topk_candidates(hidden.index_select(0, sel), k)
+        prm = torch.tensor([[seqs[i].params.temperature, seqs[i].params.top_p, float(seqs[i].params.k)]
+                            for i in sampled], dtype=torch.float32).to(dev, non_blocking=True)
+        if any(seqs[i].params.k < vals.shape[1] for i in sampled):  # per-row top-k cut
+            cols = torch.arange(vals.shape[1], device=dev, dtype=torch.float32)[None, :]
+            vals = torch.where(cols < prm[:, 2:3], vals, torch.full_like(vals, -float("inf")))
+        u = torch.rand(len(sampled), generator=self._gen, device=dev)
         if self.par.tp_size > 1:  # every TP rank must draw the same token
             self.par.all_reduce(u)
             u /= self.par.tp_size
-        return ops.sample_top_p(vals, idx, temp, top_p, u).tolist()
+        picks = ops.sample_top_p(vals, idx, prm[:, 0].contiguous(), prm[:, 1].contiguous(), u)
+        out = ids.clone()
+        out.index_copy_(0, sel, picks.to(out.dtype))
+        return out.tolist()
 
     # ------------------------------------------------------------------ prefill
     def _prefill_step(self, prefilling: List[_Seq]) -> List[_Seq]:
@@ -408,9 +418,10 @@ class LLMEngine:
             s.error = "__preempt__"
             return
         nblk = (s.length + BS - 1) // BS
-        if self.bt_host[s.row, nblk - 1] != slot // BS:
-            self.bt_host[s.row, nblk - 1] = slot // BS
-            self._bt_dirty = True
+        blk = slot // BS
+        if self.bt_host[s.row, nblk - 1] != blk:
+            self.bt_host[s.row, nblk - 1] = blk
+            self._bt_upd.extend((s.row * self.max_blocks + nblk - 1, blk))
 
     # ------------------------------------------------------------------ decode
     def _bucket(self, n: int) -> int:
@@ -442,7 +453,12 @@ class LLMEngine:
         h[o[5] + rows] = 1
         h[o[6] + rows] = lens
         self._sync_bt()
-        self.dec_dev.copy_(self.dec_host_t, non_blocking=True)
+        nu = len(self._bt_upd) // 2
+        h[o[7]] = nu
+        if nu:
+            h[o[7] + 1:o[7] + 1 + 2 * nu] = self._bt_upd
+            self._bt_upd.clear()
+        self.dec_dev[:o[7] + 1 + 2 * nu].copy_(self.dec_host_t[:o[7] + 1 + 2 * nu], non_blocking=True)
         if self.use_graphs:
             g = self._graphs.get(bs)
             if g is None:
@@ -453,9 +469,28 @@ class LLMEngine:
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
         toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
+        # stop checks in Python, then ONE native call commits every sequence's K/V and appends
+        # the new tokens of those that continue
+        eos, mml = self.tok.eos_id, self.max_model_len
+        cont = []
         for s, t in zip(running, toks):
-            self.bm.commit(s.id, s.length)
-            self._append(s, t)
+            s.out.append(int(t))
+            p = s.params
+            cont.append(not (len(s.out) >= p.max_new_tokens or (not p.ignore_eos and t == eos)
+                             or s.length >= mml))
+        slots = self.bm.commit_append([s.id for s in running], toks, cont)
+        mb_ = self.max_blocks
+        for s, c, slot in zip(running, cont, slots):
+            if not c:
+                continue
+            if slot < 0:
+                s.error = "__preempt__"
+                continue
+            nblk = (s.length + BS - 1) // BS
+            blk = slot // BS
+            if self.bt_host[s.row, nblk - 1] != blk:
+                self.bt_host[s.row, nblk - 1] = blk
+                self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
 
     def _decode_meta(self, bs: int) -> AttnMeta:
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
@@ -463,6 +498,7 @@ class LLMEngine:
                         last_idx=self.d_last[:bs], splits=self._splits_for(bs), workspace=self.dec_ws)
 
     def _decode_forward(self, bs: int) -> None:
+        ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)
         hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches)
         self.d_hidden[:bs].copy_(hid)
         self.d_out[:bs].copy_(self.model.greedy(hid))

@@ -252,3 +252,15 @@ def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tens
 
 
 from .gemm import autotune as gemm_autotune, linear, linear_swiglu  # noqa: E402
+
+
+def scatter_pairs(dst: torch.Tensor, buf: torch.Tensor) -> None:
+    """dst.view(-1)[idx_i] = val_i for buf = [n, idx0, val0, idx1, val1, ...] (int32)."""
+    ext = _native(dst)
+    if ext is None:
+        n = int(buf[0])
+        if n:
+            pairs = buf[1:1 + 2 * n].view(-1, 2).long()
+            dst.view(-1)[pairs[:, 0]] = pairs[:, 1].to(dst.dtype)
+        return
+    ext.scatter_pairs(dst, buf)
