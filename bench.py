@@ -173,14 +173,14 @@ def main() -> int:
         convs = Conversations(n_convs, rank)
         for _ in range(a.warmup):
             convs.step(router)
-        st0 = [dict(e.bm.stats()) for e in engines]
+        st0 = [dict(e.stats()) for e in engines]
         sync()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             convs.step(router, records)
         sync()
         elapsed = time.perf_counter() - t0
-        st1 = [dict(e.bm.stats()) for e in engines]
+        st1 = [dict(e.stats()) for e in engines]
         if cluster is not None:
             cluster.shutdown()
         tokens = sum(r["tok"] for r in records)
@@ -227,6 +227,9 @@ def main() -> int:
             "routing_overhead_ms_mean": round(statistics.mean(r["ovh"] for r in records), 3) if records else None,
             "ttft_ms_p50": round(statistics.median(r["ttft"] for r in records), 1) if records else None,
             "prefix_cache_hit_rate": round(hits / max(1, prompt), 3),
+            "engine_time_split_s": {k: round(sum(b_.get(k, 0.0) - a_.get(k, 0.0) for a_, b_ in zip(st0, st1)), 3)
+                                    for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
+                                              "t_decode_host_post_s")},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -122,6 +122,7 @@ class LLMEngine:
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
+        self.timers = {"prefill": 0.0, "decode_host_pre": 0.0, "decode_gpu_wait": 0.0, "decode_host_post": 0.0}
 
     # ------------------------------------------------------------------ setup
     def _alloc_kv(self, kv_cache_gb: Optional[float]) -> None:
@@ -246,6 +247,7 @@ class LLMEngine:
     def stats(self) -> Dict[str, object]:
         st = dict(self.bm.stats())
         st.update(self.steps)
+        st.update({f"t_{k}_s": round(v, 4) for k, v in self.timers.items()})
         st["model"] = self.cfg.name
         st["kv_blocks"] = self.num_blocks
         return st
@@ -277,7 +279,9 @@ class LLMEngine:
                     s.error = "insufficient KV cache for request"
                 continue
             if prefilling:
+                _t = time.perf_counter()
                 done = self._prefill_step(prefilling)
+                self.timers["prefill"] += time.perf_counter() - _t
                 for s in done:
                     prefilling.remove(s)
                     if self._finished(s):
@@ -286,6 +290,7 @@ class LLMEngine:
                         running.append(s)
                 continue
             self._decode_step(running)
+            _t = time.perf_counter()
             for s in [s for s in running if self._finished(s)]:
                 running.remove(s)
                 self._release(s)
@@ -295,6 +300,7 @@ class LLMEngine:
                 self._release(s, keep=False)
                 s.error = None
                 waiting.insert(0, s)  # re-admitted with fill = prompt + out (recompute)
+            self.timers["decode_host_post"] += time.perf_counter() - _t
 
     def _finished(self, s: _Seq) -> bool:
         if s.error is not None and s.error != "__preempt__":
@@ -431,6 +437,7 @@ class LLMEngine:
         raise ValueError(f"batch {n} exceeds max_num_seqs")
 
     def _decode_step(self, running: List[_Seq]) -> None:
+        _t0 = time.perf_counter()
         B = len(running)
         bs = self._bucket(B)
         o, h = self._off, self.dec_host
@@ -459,6 +466,7 @@ class LLMEngine:
             h[o[7] + 1:o[7] + 1 + 2 * nu] = self._bt_upd
             self._bt_upd.clear()
         self.dec_dev[:o[7] + 1 + 2 * nu].copy_(self.dec_host_t[:o[7] + 1 + 2 * nu], non_blocking=True)
+        _t1 = time.perf_counter()
         if self.use_graphs:
             g = self._graphs.get(bs)
             if g is None:
@@ -469,6 +477,9 @@ class LLMEngine:
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
         toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
+        _t2 = time.perf_counter()
+        self.timers["decode_host_pre"] += _t1 - _t0
+        self.timers["decode_gpu_wait"] += _t2 - _t1
         # stop checks in Python, then ONE native call commits every sequence's K/V and appends
         # the new tokens of those that continue
         eos, mml = self.tok.eos_id, self.max_model_len
@@ -491,6 +502,7 @@ class LLMEngine:
             if self.bt_host[s.row, nblk - 1] != blk:
                 self.bt_host[s.row, nblk - 1] = blk
                 self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
+        self.timers["decode_host_post"] += time.perf_counter() - _t2
 
     def _decode_meta(self, bs: int) -> AttnMeta:
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
