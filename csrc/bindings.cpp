@@ -27,6 +27,13 @@ int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int,
                      hipStream_t);
 int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                          hipStream_t);
+int dllm_car_alloc(long, void**);
+int dllm_car_get_handle(void*, char*);
+int dllm_car_handle_size();
+int dllm_car_open_handle(const char*, void**);
+int dllm_car_close_handle(void*);
+int dllm_car_free(void*);
+int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
 int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
                               unsigned long long*, hipStream_t);
 }
@@ -290,9 +297,52 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
         part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
      "skinny_gemm");
 }
+// ---- one-shot all-reduce over IPC-mapped peer buffers (csrc/kernels/custom_ar.hip)
+int64_t car_alloc(int64_t data_bytes) {
+  void* p = nullptr;
+  ok(dllm_car_alloc(data_bytes, &p), "car_alloc");
+  return (int64_t)p;
+}
+py::bytes car_handle(int64_t base) {
+  char buf[64] = {0};
+  ok(dllm_car_get_handle((void*)base, buf), "hipIpcGetMemHandle");
+  return py::bytes(buf, dllm_car_handle_size());
+}
+int64_t car_open(py::bytes h) {
+  std::string s = h;
+  TORCH_CHECK((int)s.size() == dllm_car_handle_size(), "bad IPC handle size");
+  void* p = nullptr;
+  ok(dllm_car_open_handle(s.data(), &p), "hipIpcOpenMemHandle");
+  return (int64_t)p;
+}
+void car_close(int64_t base) { ok(dllm_car_close_handle((void*)base), "hipIpcCloseMemHandle"); }
+void car_free(int64_t base) { ok(dllm_car_free((void*)base), "hipFree"); }
+void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> bases, int64_t rank, int64_t data_bytes,
+                   torch::Tensor counters, torch::Tensor err, int64_t spin_limit) {
+  check_bf16(x, "x");
+  check_bf16(out, "out");
+  check_i32(counters, "counters");
+  check_i32(err, "err");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel(), "contiguous, same size");
+  TORCH_CHECK(counters.numel() >= 2 && err.numel() >= 1, "counters[2], err[1]");
+  const int64_t nbytes = x.numel() * 2;
+  TORCH_CHECK(nbytes % 16 == 0 && nbytes <= data_bytes, "message must be a multiple of 16 B and fit the buffer");
+  TORCH_CHECK(!bases.empty() && bases.size() <= 8 && rank >= 0 && rank < (int64_t)bases.size(), "bad ranks");
+  void* b[8];
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = (void*)bases[i];
+  ok(dllm_car_allreduce(x.data_ptr(), out.data_ptr(), nbytes, b, (int)bases.size(), (int)rank, data_bytes,
+                        (unsigned*)counters.data_ptr<int>(), err.data_ptr<int>(), spin_limit, stream()),
+     "car_allreduce");
+}
 }  // namespace
 
 PYBIND11_MODULE(_hip_kernels, m) {
+  m.def("car_alloc", &car_alloc);
+  m.def("car_handle", &car_handle);
+  m.def("car_open", &car_open);
+  m.def("car_close", &car_close);
+  m.def("car_free", &car_free);
+  m.def("car_allreduce", &car_allreduce);
   m.doc() = "gfx950 HIP kernels for distributed_llm_amd";
   m.def("norm", &norm);
   m.def("rope_kv", &rope_kv);

@@ -23,7 +23,7 @@
 
 namespace {
 constexpr int BS = 16;     // tokens per KV block
-constexpr int WAVES = 4;
+constexpr int WAVES = 4;   // LDS combine slots; a workgroup runs W = 4 or 8 waves
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct AttnArgs {
@@ -44,8 +44,8 @@ struct AttnArgs {
   float scale_log2;
 };
 
-template <int D>
-__global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
+template <int D, int W>
+__global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   constexpr int KSTEPS = D / 32;
   constexpr int NT = D / 16;
   __shared__ float s_o[WAVES][16][D + 1];
@@ -93,44 +93,44 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
   const long head_stride = (long)BS * D;  // elements per (block, head) in either cache
   // One register stage per 32-key chunk (a 2-stage prefetch pipeline measured SLOWER on MI355X:
   // +30 VGPRs cost a wave per SIMD, and occupancy hides the K/V latency better than ILP here).
-  struct KV {
-    uint4 k0[KSTEPS], k1[KSTEPS];
-    uint2 v0[NT], v1[NT];
-  };
-  auto load = [&](KV& r, int kb) {
-    const int b0 = bt[kb >> 4];
-    const int b1 = (kb + 16 < k_end) ? bt[(kb >> 4) + 1] : b0;
-    const u16* k0 = a.kc + ((long)b0 * a.nkv + kvh) * head_stride;
-    const u16* k1 = a.kc + ((long)b1 * a.nkv + kvh) * head_stride;
-    const u16* v0 = a.vc + ((long)b0 * a.nkv + kvh) * head_stride;
-    const u16* v1 = a.vc + ((long)b1 * a.nkv + kvh) * head_stride;
+  // (Plain local arrays in the loop body: an earlier lambda + struct form made hipcc keep part
+  // of the K/V registers in scratch for some instantiations — 48-80 B/lane of scratch traffic.)
+  for (int kb = k_begin + 32 * wave; kb < k_end; kb += 32 * W) {
+    uint4 k0r[KSTEPS], k1r[KSTEPS];
+    uint2 v0r[NT], v1r[NT];
+    {
+      const int b0 = bt[kb >> 4];
+      const int b1 = (kb + 16 < k_end) ? bt[(kb >> 4) + 1] : b0;
+      const u16* k0 = a.kc + ((long)b0 * a.nkv + kvh) * head_stride + rl * D + 8 * g;
+      const u16* k1 = a.kc + ((long)b1 * a.nkv + kvh) * head_stride + rl * D + 8 * g;
+      const u16* v0 = a.vc + ((long)b0 * a.nkv + kvh) * head_stride + rl * BS + 4 * g;
+      const u16* v1 = a.vc + ((long)b1 * a.nkv + kvh) * head_stride + rl * BS + 4 * g;
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-      r.k0[s] = ld16(k0 + rl * D + 8 * g + 32 * s);
-      r.k1[s] = ld16(k1 + rl * D + 8 * g + 32 * s);
-    }
+      for (int s = 0; s < KSTEPS; ++s) {
+        k0r[s] = ld16(k0 + 32 * s);
+        k1r[s] = ld16(k1 + 32 * s);
+      }
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      r.v0[n] = *reinterpret_cast<const uint2*>(v0 + (16 * n + rl) * BS + 4 * g);
-      r.v1[n] = *reinterpret_cast<const uint2*>(v1 + (16 * n + rl) * BS + 4 * g);
+      for (int n = 0; n < NT; ++n) {
+        v0r[n] = *reinterpret_cast<const uint2*>(v0 + 16 * n * BS);
+        v1r[n] = *reinterpret_cast<const uint2*>(v1 + 16 * n * BS);
+      }
     }
-  };
-  auto compute = [&](const KV& r, int kb) {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
-      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.k0[s]), qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.k1[s]), qf[s], s1, 0, 0, 0);
+      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0r[s]), qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1r[s]), qf[s], s1, 0, 0, 0);
     }
     // scores for row rl: keys kb + 4g + r (s0) and kb + 16 + 4g + r (s1)
     float p[8];
-    float mloc = -INFINITY;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int key0 = kb + 4 * g + q, key1 = kb + 16 + 4 * g + q;
       p[q] = (key0 < row_lim && key0 < k_end) ? s0[q] * a.scale_log2 : -INFINITY;
       p[4 + q] = (key1 < row_lim && key1 < k_end) ? s1[q] * a.scale_log2 : -INFINITY;
     }
+    float mloc = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) mloc = fmaxf(mloc, p[j]);
     mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
@@ -149,22 +149,41 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       acc[n] *= alpha;
-      const uint4 vv = make_uint4(r.v0[n].x, r.v0[n].y, r.v1[n].x, r.v1[n].y);
+      const uint4 vv = make_uint4(v0r[n].x, v0r[n].y, v1r[n].x, v1r[n].y);
       acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, acc[n], 0, 0, 0);
     }
-  };
-  for (int kb = k_begin + 32 * wave; kb < k_end; kb += 32 * WAVES) {
-    KV r;
-    load(r, kb);
-    compute(r, kb);
   }
 
-  // ---- combine the 4 waves through LDS.  acc[n][r] = O^T[dim 16n + 4g + r][row rl]
-  if (g == 0) { s_m[wave][rl] = m_run; s_l[wave][rl] = l_run; }
+  // ---- combine the waves through LDS.  acc[n][r] = O^T[dim 16n + 4g + r][row rl]
+  if constexpr (W == 8) {  // waves 4..7 fold into waves 0..3 first (keeps LDS at 4 slots)
+    if (wave >= WAVES) {
+      if (g == 0) { s_m[wave - WAVES][rl] = m_run; s_l[wave - WAVES][rl] = l_run; }
 #pragma unroll
-  for (int n = 0; n < NT; ++n)
+      for (int n = 0; n < NT; ++n)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s_o[wave][rl][16 * n + 4 * g + r] = acc[n][r];
+        for (int r = 0; r < 4; ++r) s_o[wave - WAVES][rl][16 * n + 4 * g + r] = acc[n][r];
+    }
+    __syncthreads();
+    if (wave < WAVES) {
+      const float mo = s_m[wave][rl], lo = s_l[wave][rl];
+      const float mn = fmaxf(m_run, mo), ms = (mn == -INFINITY) ? 0.f : mn;
+      const float fa = exp2f(m_run - ms), fb = exp2f(mo - ms);
+      l_run = l_run * fa + lo * fb;
+      m_run = mn;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[n][r] = acc[n][r] * fa + s_o[wave][rl][16 * n + 4 * g + r] * fb;
+    }
+    __syncthreads();
+  }
+  if (wave < WAVES) {
+    if (g == 0) { s_m[wave][rl] = m_run; s_l[wave][rl] = l_run; }
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_o[wave][rl][16 * n + 4 * g + r] = acc[n][r];
+  }
   __syncthreads();
 
   const int G_ = G;
@@ -264,6 +283,10 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(AttnArgs a) {
   }
 }
 
+template <int D, int W>
+void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL((paged_attn_kernel<D, W>), grid, dim3(64 * W), 0, stream, a);
+}
 }  // namespace
 
 extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* vc, const int* block_tables,
@@ -278,11 +301,16 @@ extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* v
   if (num_tiles <= 0) return 0;
   AttnArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
              tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, nq, nkv, G, max_blocks, causal, scale * LOG2E};
-  dim3 grid(num_tiles, nkv, splits), block(64 * WAVES);
-  switch (d) {
-    case 64: hipLaunchKernelGGL(paged_attn_kernel<64>, grid, block, 0, stream, a); break;
-    case 96: hipLaunchKernelGGL(paged_attn_kernel<96>, grid, block, 0, stream, a); break;
-    case 128: hipLaunchKernelGGL(paged_attn_kernel<128>, grid, block, 0, stream, a); break;
+  // 8 waves per workgroup when the grid alone cannot fill the CUs with memory requests
+  // (decode at moderate batch: tiles x kv-heads x splits workgroups are all resident at once).
+  static const int env_w = [] { const char* e = getenv("DLLM_ATTN_WAVES"); return e ? atoi(e) : 0; }();
+  const long wgs = (long)num_tiles * nkv * splits;
+  const int W = env_w == 4 || env_w == 8 ? env_w : (wgs <= 2048 ? 8 : 4);
+  dim3 grid(num_tiles, nkv, splits);
+switch (d) {
+    case 64: W == 8 ? launch_attn<64, 8>(grid, a, stream) : launch_attn<64, 4>(grid, a, stream); break;
+    case 96: W == 8 ? launch_attn<96, 8>(grid, a, stream) : launch_attn<96, 4>(grid, a, stream); break;
+    case 128: W == 8 ? launch_attn<128, 8>(grid, a, stream) : launch_attn<128, 4>(grid, a, stream); break;
     default: return -4;
   }
   return (int)hipGetLastError();

@@ -90,6 +90,8 @@ class Cluster:
                 continue
             par = ParallelContext(len(ranks), ranks.index(self.rank), self.tp_groups.get(tuple(ranks)),
                                   self.rank, self.world)
+            if str(self.device).startswith("cuda"):
+                par.enable_custom_all_reduce(self.device)  # collective over this TP group
             self.engines[key] = LLMEngine(spec.model, device=self.device, par=par, kv_cache_gb=spec.kv_cache_gb,
                                           max_num_seqs=spec.max_num_seqs)
 

@@ -27,15 +27,37 @@ class ParallelContext:
     tp_group: Optional[object] = None   # torch ProcessGroup
     global_rank: int = 0
     world_size: int = 1
+    custom_ar: Optional[object] = None  # parallel.custom_ar.CustomAllReduce (GPU TP groups)
 
     @property
     def enabled(self) -> bool:
         return self.tp_size > 1
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the TP group: one-shot xGMI kernel for decode-size bf16 messages,
+        RCCL for everything else (prefill activations, f32, CPU/gloo)."""
         if self.tp_size > 1:
-            dist.all_reduce(t, group=self.tp_group)
+            car = self.custom_ar
+            if car is not None and car.eligible(t):
+                car.all_reduce(t)
+            else:
+                dist.all_reduce(t, group=self.tp_group)
         return t
+
+    def enable_custom_all_reduce(self, device, max_bytes: Optional[int] = None) -> bool:
+        """Collective over the TP group.  Returns False (RCCL only) when not applicable."""
+        if self.tp_size <= 1 or self.tp_size > 8 or torch.device(device).type != "cuda":
+            return False
+        if os.environ.get("DLLM_CUSTOM_AR", "1") == "0":
+            return False
+        from .custom_ar import DEFAULT_MAX_BYTES, CustomAllReduce, CustomAllReduceUnavailable
+        try:
+            self.custom_ar = CustomAllReduce(self.tp_group, torch.device(device), max_bytes or DEFAULT_MAX_BYTES)
+        except CustomAllReduceUnavailable as e:  # agreed by every rank: all stay on RCCL
+            import logging
+            logging.getLogger(__name__).warning("custom all-reduce disabled: %s", e)
+            return False
+        return True
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate ``t`` from every TP rank along a new leading dim -> [tp, *t.shape]."""

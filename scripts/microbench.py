@@ -33,7 +33,11 @@ def timeit(fn, iters=20, warm=3):
     return s.elapsed_time(e) / iters
 
 
-def bench_attn(B, C, nq, nkv, d, splits):
+def bench_attn(B, C, nq, nkv, d, splits, var=False):
+    """var=True: contexts uniform in [C/4, 7C/4] (mean C) like a serving batch, else all C."""
+    g = torch.Generator().manual_seed(0)
+    ctxs = (torch.randint(C // 4, 7 * C // 4 + 1, (B,), generator=g).tolist() if var else [C] * B)
+    C = max(ctxs)
     NB = B * ((C + 15) // 16) + 8
     kc = torch.randn(NB, nkv, 16, d, device="cuda").to(torch.bfloat16)
     vc = torch.randn(NB, nkv, d, 16, device="cuda").to(torch.bfloat16)
@@ -41,12 +45,13 @@ def bench_attn(B, C, nq, nkv, d, splits):
     bt = torch.randperm(NB - 8, device="cuda")[:B * nb].view(B, nb).to(torch.int32)
     q = torch.randn(B, nq, d, device="cuda").to(torch.bfloat16)
     I = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
-    qs, ql, cx = I(list(range(B))), I([1] * B), I([C] * B)
+    qs, ql, cx = I(list(range(B))), I([1] * B), I(ctxs)
     ts, tt = ops.build_tiles([1] * B, nq // nkv)
     ts, tt = I(ts), I(tt)
     ms = timeit(lambda: ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=splits))
-    kv_bytes = B * C * nkv * d * 2 * 2
-    return {"bench": "attn_decode", "B": B, "C": C, "nq": nq, "nkv": nkv, "d": d, "splits": splits,
+    kv_bytes = sum(ctxs) * nkv * d * 2 * 2
+    return {"bench": "attn_decode", "B": B, "C": sum(ctxs) // B, "var": var, "nq": nq, "nkv": nkv, "d": d,
+            "splits": splits, "waves": os.environ.get("DLLM_ATTN_WAVES", "auto"),
             "us": round(ms * 1000, 1), "GBps": round(kv_bytes / ms / 1e6, 1)}
 
 
@@ -138,10 +143,11 @@ if __name__ == "__main__":
             for (N, K) in [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632), (32000, 2048), (6144, 4096), (28672, 4096), (4096, 14336)]:
                 print(json.dumps(bench_gemm(M, N, K)), flush=True)
     if "attn" in what:
-        for (B, C) in [(1, 2048), (16, 2048), (64, 512), (64, 2048), (64, 8192), (256, 1024)]:
+        for (B, C, var) in [(1, 2048, False), (16, 2048, False), (64, 512, False), (64, 2048, False),
+                            (64, 8192, False), (256, 1024, False), (256, 2048, True), (128, 2048, True)]:
             for (nq, nkv, d) in [(32, 4, 64), (32, 8, 128)]:
-                for splits in (1, 2, 4, 8, 16):
-                    print(json.dumps(bench_attn(B, C, nq, nkv, d, splits)), flush=True)
+                for splits in (1, 2, 4, 8):
+                    print(json.dumps(bench_attn(B, C, nq, nkv, d, splits, var)), flush=True)
     if "decode" in what or "prefill" in what:
         eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
         if "decode" in what:
