@@ -86,6 +86,7 @@ class _Seq:
     first_tok: Optional[float] = None
     finished: Optional[float] = None
     error: Optional[str] = None
+    done: threading.Event = field(default_factory=threading.Event)
 
     @property
     def length(self) -> int:
@@ -109,9 +110,14 @@ class LLMEngine:
         self._alloc_kv(kv_cache_gb)
         self.bm = _need_runtime().BlockManager(self.num_blocks, BS, prefix_cache)
         self._ids = itertools.count()
-        self._lock = threading.Lock()
+        self._lock = threading.Lock()          # held by the thread currently driving the step loop
+        self._inbox: List[_Seq] = []            # submitted, not yet seen by the driver
+        self._inbox_lock = threading.Lock()
+        self._driving = False
+        self._active: List[_Seq] = []
         self._memo: "OrderedDict[str, List[int]]" = OrderedDict()
         self._memo_cap = 200_000
+        self._memo_lock = threading.Lock()
         self.on_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.on_gpu
         self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
@@ -211,16 +217,19 @@ class LLMEngine:
                 pos = text.rfind("\n", 0, pos)
                 if pos <= 0:
                     break
-                ids = memo.get(text[:pos])
+                with self._memo_lock:
+                    ids = memo.get(text[:pos])
+                    if ids is not None:
+                        memo.move_to_end(text[:pos])
                 if ids is not None:
-                    memo.move_to_end(text[:pos])
                     return list(ids) + self.tok.encode(text[pos:], add_bos=False)
         return self.tok.encode(text)
 
     def _remember(self, text: str, ids: List[int]) -> None:
-        self._memo[text] = ids
-        while len(self._memo) > self._memo_cap:
-            self._memo.popitem(last=False)
+        with self._memo_lock:
+            self._memo[text] = ids
+            while len(self._memo) > self._memo_cap:
+                self._memo.popitem(last=False)
 
     def generate(self, prompts: Sequence[Union[str, List[int]]],
                  params: Union[SamplingParams, Sequence[SamplingParams], None] = None) -> List[RequestOutput]:
@@ -239,10 +248,63 @@ class LLMEngine:
                 s.prompt = ids[:1] + ids[len(ids) - limit + 1:]
             if len(s.prompt) == 0 or limit <= 1:
                 s.error = "prompt too long for max_model_len"
+                s.done.set()
             seqs.append(s)
-        with self._lock:
-            self._run(seqs)
+        self._submit_and_wait([s for s in seqs if s.error is None])
         return [self._output(s) for s in seqs]
+
+    def _submit_and_wait(self, seqs: List[_Seq]) -> None:
+        """Continuous batching across callers (leader/follower): requests from concurrent threads
+        (HTTP handlers, pool dispatchers) join ONE running batch.  The first caller to find the
+        engine idle drives the step loop until every submitted sequence is done; later callers
+        only enqueue and wait — their sequences are admitted at the driver's next step."""
+        if self.par.enabled:
+            # TP ranks must run IDENTICAL batches in lockstep: no cross-caller merging (the TP
+            # leader serialises requests and broadcasts each one to the members).
+            with self._lock:
+                self._run(seqs)
+            return
+        with self._inbox_lock:
+            self._inbox.extend(seqs)
+            lead = not self._driving
+            if lead:
+                self._driving = True
+        if lead:
+            with self._lock:
+                try:
+                    self._run([])
+                except BaseException as e:
+                    self._abort_all(f"engine step failed: {e!r}")
+                    raise
+        for s in seqs:
+            s.done.wait()
+
+    def _abort_all(self, why: str) -> None:
+        """A failed step must not strand followers: fail every admitted/queued sequence."""
+        with self._inbox_lock:
+            pending, self._inbox = self._inbox, []
+            self._driving = False
+        for s in pending + list(self._active):
+            if not s.done.is_set():
+                s.error = s.error or why
+                try:
+                    self.bm.free(s.id)
+                except Exception:  # noqa: BLE001 - best effort cleanup
+                    pass
+                if s.row >= 0:
+                    self.bt_host[s.row].fill(0)
+                    self._free_rows.append(s.row)
+                    s.row = -1
+                s.done.set()
+        self._active = []
+        self._bt_dirty = True
+
+    def _take_inbox(self, final: bool) -> List[_Seq]:
+        with self._inbox_lock:
+            new, self._inbox = self._inbox, []
+            if final and not new:
+                self._driving = False   # atomically with the empty check: no submission is lost
+        return new
 
     def stats(self) -> Dict[str, object]:
         st = dict(self.bm.stats())
@@ -257,7 +319,11 @@ class LLMEngine:
         waiting = [s for s in seqs if s.error is None]
         prefilling: List[_Seq] = []
         running: List[_Seq] = []
-        while waiting or prefilling or running:
+        while True:
+            waiting.extend(self._take_inbox(final=not (waiting or prefilling or running)))
+            self._active = waiting + prefilling + running
+            if not (waiting or prefilling or running):
+                break
             # admit
             while waiting and len(prefilling) + len(running) < self.R:
                 s = waiting[0]
@@ -277,6 +343,7 @@ class LLMEngine:
                 if waiting:  # nothing fits even alone -> fail the head request
                     s = waiting.pop(0)
                     s.error = "insufficient KV cache for request"
+                    s.done.set()
                 continue
             if prefilling:
                 _t = time.perf_counter()
@@ -317,6 +384,8 @@ class LLMEngine:
         if keep:
             s.finished = time.perf_counter()
         self.bm.free(s.id)
+        if keep:
+            s.done.set()
         if s.row >= 0:
             self.bt_host[s.row].fill(0)
             self._free_rows.append(s.row)

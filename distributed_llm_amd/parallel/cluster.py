@@ -15,6 +15,8 @@ Default layouts (``default_topology``): 1 GPU â€” both tiers on one engine; 2 â€
 """
 from __future__ import annotations
 
+import threading
+
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
@@ -169,16 +171,27 @@ class _LeaderPool:
     """Rank 0 leads a TP group: fan the request out to the members, then run it locally."""
 
     def __new__(cls, tier, engine, tp_group, **kw):
-        from ..pools.base import EnginePool
+        from ..pools.base import Coalescer, EnginePool
 
         class LeaderPool(EnginePool):
+            """Concurrent callers are coalesced into ONE broadcast + generate, so the members see
+            requests in exactly the leader's order and batch as the leader does."""
+
+            def __init__(self, *a, **k):
+                super().__init__(*a, **k)
+                self._coalesce = Coalescer(self._run_items)
+
             def process_batch(self, histories, overrides=None):
-                from . import p2p
                 params = self._params(overrides)
-                prompts = [self.prompt_for(h) for h in histories]
+                return self._coalesce.submit([(self.prompt_for(h), params) for h in histories])
+
+            def _run_items(self, items):
+                from . import p2p
+                prompts = [q for q, _ in items]
+                plist = [p for _, p in items]
                 p2p.bcast_obj({"op": "generate", "id": 0, "prompts": prompts,
-                               "params": {"max_new_tokens": params.max_new_tokens, "temperature": params.temperature,
-                                          "top_k": params.top_k, "top_p": params.top_p}}, 0, tp_group)
-                return self.to_payloads(self.engine.generate(prompts, params))
+                               "params_list": [{"max_new_tokens": p.max_new_tokens, "temperature": p.temperature,
+                                                "top_k": p.top_k, "top_p": p.top_p} for p in plist]}, 0, tp_group)
+                return self.to_payloads(self.engine.generate(prompts, plist))
 
         return LeaderPool(tier, engine, **kw)

@@ -35,6 +35,59 @@ def format_prompt(query: Any) -> str:
     return str(query).strip()
 
 
+class Coalescer:
+    """Merge concurrent submissions into one downstream batch call (leader/follower).
+
+    ``fn(items) -> results`` is called with the items of every caller that arrived while the
+    previous call was in flight, so N concurrent HTTP requests to a remote / tensor-parallel pool
+    become one batched exchange instead of N serialised ones.  The caller that finds the pool
+    idle drives; the others wait for their slice of the results.
+    """
+
+    def __init__(self, fn):
+        self.fn = fn
+        self._lock = threading.Lock()
+        self._queue: List[Dict[str, Any]] = []
+        self._busy = False
+        self.calls = 0
+        self.items = 0
+
+    def submit(self, items: Sequence[Any]) -> List[Any]:
+        job = {"items": list(items), "done": threading.Event(), "out": None, "err": None}
+        with self._lock:
+            self._queue.append(job)
+            lead = not self._busy
+            if lead:
+                self._busy = True
+        if lead:
+            while True:
+                with self._lock:
+                    jobs, self._queue = self._queue, []
+                    if not jobs:
+                        self._busy = False
+                        break
+                flat = [it for j in jobs for it in j["items"]]
+                try:
+                    res = list(self.fn(flat))
+                    if len(res) != len(flat):
+                        raise RuntimeError(f"batch returned {len(res)} results for {len(flat)} items")
+                    err = None
+                except Exception as e:  # every waiter sees the failure
+                    res, err = [None] * len(flat), e
+                self.calls += 1
+                self.items += len(flat)
+                k = 0
+                for j in jobs:
+                    n = len(j["items"])
+                    j["out"], j["err"] = res[k:k + n], err
+                    k += n
+                    j["done"].set()
+        job["done"].wait()
+        if job["err"] is not None:
+            raise job["err"]
+        return job["out"]
+
+
 class NullServerManager:
     """In-process pools are always 'running'; kept for harness API compatibility."""
 

@@ -18,7 +18,7 @@ from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Dict, List, Optional, Sequence
 
 from ..parallel import p2p
-from .base import EnginePool, NullServerManager, PoolClient, format_prompt
+from .base import Coalescer, EnginePool, NullServerManager, PoolClient, format_prompt
 
 
 class RemoteServerManager(NullServerManager):
@@ -44,6 +44,7 @@ class RemotePool(PoolClient):
         self._lock = threading.Lock()  # one outstanding exchange per pair group
         self._ids = itertools.count()
         self.last_rtt_us: Optional[float] = None
+        self._coalesce = Coalescer(self._generate_items)  # concurrent callers -> one exchange
 
     def prompt_for(self, history: Any) -> str:
         return format_prompt(history) + self.generation_prompt
@@ -66,14 +67,24 @@ class RemotePool(PoolClient):
         if not self.alive:
             return [{"error": f"pool {self.name} unavailable"}] * len(histories)
         params = dict(self.params, **(overrides or {}))
-        msg = {"op": "generate", "id": next(self._ids), "prompts": [self.prompt_for(h) for h in histories],
-               "params": params}
+        return self._coalesce.submit([(self.prompt_for(h), params) for h in histories])
+
+    def _generate_items(self, items: List[tuple]) -> List[Dict[str, Any]]:
+        plist = [p for _, p in items]
+        msg = {"op": "generate", "id": next(self._ids), "prompts": [q for q, _ in items]}
+        if all(p == plist[0] for p in plist):
+            msg["params"] = plist[0]
+        else:
+            msg["params_list"] = plist
         try:
             rep = self._exchange(msg)
         except Exception as e:  # transport failure -> error payloads (router fails over)
             self.alive = False
-            return [{"error": f"pool {self.name} transport failed: {e}"}] * len(histories)
-        return rep.get("results") or [{"error": rep.get("error", "empty reply")}] * len(histories)
+            return [{"error": f"pool {self.name} transport failed: {e}"}] * len(items)
+        res = rep.get("results")
+        if not res or len(res) != len(items):
+            return [{"error": rep.get("error", "empty reply")}] * len(items)
+        return res
 
     def probe(self) -> Dict[str, Any]:
         """Health probe: round trip + the pool's engine statistics."""
@@ -126,7 +137,10 @@ def serve_pool(engine, router_rank: int, leader: int, pair_group, tp_group=None,
             continue
         if op == "generate":
             try:
-                sp = SamplingParams(**msg["params"])
+                if "params_list" in msg:
+                    sp = [SamplingParams(**p) for p in msg["params_list"]]
+                else:
+                    sp = SamplingParams(**msg["params"])
                 outs = engine.generate(msg["prompts"], sp)
                 res = EnginePool.to_payloads(outs)
                 rep = {"id": msg["id"], "results": res}
