@@ -144,3 +144,43 @@ class QueryRouter:
         with self._lock:
             self.router = self._build(strategy)
             self.strategy_name = strategy
+
+
+def smoke(cache_path: str = "/tmp/qr_cache.json", strategy: str = "hybrid") -> Dict[str, Any]:
+    """Routing-engine smoke run (reference query_router_engine.py:734-764): warm the cache with two
+    labelled pairs, route three queries, route them again (predictive hits from the routing
+    history), print cache statistics and persist the cache as JSON.
+
+    The reference runs this on BENCHMARK_CFG, whose ``cache_enabled`` is False — so its second
+    pass never hits; here the cache is switched on so the predictive path is what gets exercised.
+    """
+    from ..config import BENCHMARK_CFG
+    qr = QueryRouter(strategy=strategy, config=dict(BENCHMARK_CFG, cache_enabled=True))
+    qr.warm_up_cache([("hello", "demo", "nano"), ("what is 2+2", "demo", "nano")])
+    tests = ["hello", "what is 2+2", "Explain quantum computing and its implications for cryptography"]
+    first = []
+    for t in tests:
+        d = qr.route_query(t, context_key="demo")
+        first.append(d)
+        print(f"{t!r:55} => {d.device:4}  [{d.method}]  {d.reasoning}")
+    stats = qr.get_cache_stats()
+    print("\nCache stats:", stats)
+    print("\n--- Second pass (predictive routing from history) ---")
+    second = []
+    for t in tests:
+        d = qr.route_query(t, context_key="demo")
+        second.append(d)
+        print(f"{t!r:55} => {d.device:4}  [{d.method}]  cache_hit={d.cache_hit}")
+    qr.save_cache(cache_path)
+    print(f"\nCache saved to {cache_path}")
+    return {"first": first, "second": second, "stats": qr.get_cache_stats()}
+
+
+if __name__ == "__main__":
+    import argparse
+    logging.basicConfig(level=logging.INFO)
+    _ap = argparse.ArgumentParser()
+    _ap.add_argument("--cache-path", default="/tmp/qr_cache.json")
+    _ap.add_argument("--strategy", default="hybrid")
+    _a = _ap.parse_args()
+    smoke(_a.cache_path, _a.strategy)

@@ -5,7 +5,8 @@ Reference: POST /chat :27-106, GET /history :109-113, DELETE /history :116-121, 
 (user turn appended before routing and rolled back on error; last 10 messages kept).
 Differences: state is lock-protected (the reference mutates module globals from Flask's threaded
 server), CORS headers are set without flask-cors, and ``GET /metrics`` exposes cache statistics,
-pool health and engine counters.
+pool health and engine counters; ``GET /`` serves a no-build browser chat client with the same
+request/metadata contract as the reference React app (server/static/index.html).
 
 Run:  ``python -m distributed_llm_amd.server.app --pools echo|gpu [--port 8000]``
 """
@@ -15,11 +16,14 @@ import argparse
 import threading
 from typing import Any, Dict, List, Optional
 
-from flask import Flask, jsonify, request
+import os
+
+from flask import Flask, jsonify, request, send_from_directory
 
 from ..config import CLASS_DEFAULTS
 
 HISTORY_LIMIT = 10
+_STATIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "static")
 
 BASE_CONFIG: Dict[str, Any] = {
     "cache_enabled": True,
@@ -95,6 +99,11 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
             return jsonify({"reply": "System Error: The router encountered an issue.", "device": "error",
                             "reasoning": str(e), "method": strategy, "confidence": 0.0, "cache_hit": False,
                             "tokens": 0}), 500
+
+    @app.route("/", methods=["GET"])
+    def ui():
+        """Browser chat client (server/static/index.html; reference fyp-chat-frontend App.tsx)."""
+        return send_from_directory(_STATIC, "index.html")
 
     @app.route("/history", methods=["GET"])
     def get_history():

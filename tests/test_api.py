@@ -85,3 +85,11 @@ def test_worker_endpoints():
     err = create_worker_app(FaultInjectingPool(EchoPool(SMALL), mode="error")).test_client()
     r = err.post("/query", json={"query": "x"})
     assert r.status_code == 500 and "error" in r.get_json()
+
+
+def test_browser_client_served(client):
+    r = client.get("/")
+    assert r.status_code == 200
+    body = r.get_data(as_text=True)
+    # same request contract as the reference React client (App.tsx:101-109)
+    assert "/chat" in body and "session_id" in body and "token-counting" in body

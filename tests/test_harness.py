@@ -107,3 +107,29 @@ def test_cli_repl():
     bot.chat(stdin=io.StringIO("Thank you!\nquit\n"), stdout=out)
     assert "Assistant:" in out.getvalue() and out.getvalue().strip().endswith("3\nYou:") or "3" in out.getvalue()
     assert len(bot.conversation_history) == 2
+
+
+def test_analysis_derived_metrics_and_compare(tmp_path):
+    """bench.analysis (reference results_analysis.ipynb): published table re-derives BASELINE.md's
+    headline numbers, and our CSVs (legacy + summary) load and compare."""
+    from distributed_llm_amd.bench import analysis
+    pub = analysis.derive_metrics(analysis.published_rows())
+    gk200 = [r for r in pub if r["query_set"] == "general_knowledge" and r["threshold"] == 200][0]
+    assert abs(gk200["routed_tok_s"] - 10.57) < 0.01          # BASELINE.md best routed tok/s
+    assert abs(gk200["mean_s_per_query"] - 39.6) < 0.05        # BASELINE.md best mean s/query
+    best = analysis.best_by_set(analysis.published_rows())
+    assert best["technical_coding"]["threshold"] == 400 and best["personal_health"]["threshold"] == 400
+
+    legacy = str(tmp_path / "final_results.csv")
+    pools = {SMALL: EchoPool(SMALL, 5), LARGE: EchoPool(LARGE, 50)}
+    legacy_harness.run_legacy("personal_health", [100, 4000], pools, {}, None, threshold_routing=True,
+                              output_file=legacy)
+    summ, pq = str(tmp_path / "s.csv"), str(tmp_path / "q.csv")
+    harness.main(["--query-set", "general_knowledge", "--strategies", "token", "heuristic",
+                  "--output-csv", summ, "--output-per-query-csv", pq, "--pools", "echo", "--no-power"])
+    md = str(tmp_path / "report.md")
+    text = analysis.main([legacy, "--summary", summ, "--markdown", md])
+    assert "personal_health" in text and "general_knowledge" in text and "pub_tok_s" in text
+    assert os.path.exists(md)
+    rows = analysis.derive_metrics(analysis.load_legacy(legacy))
+    assert len(rows) == 2 and all(r["total_tokens"] > 0 for r in rows)

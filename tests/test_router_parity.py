@@ -148,3 +148,20 @@ def test_cache_prediction_and_persistence(refmod, tmp_path):
     mine.save(str(p2))
     # file formats are interchangeable
     assert QueryCache(ttl_seconds=100).load(str(p1)) == cache_mod.QueryCache(ttl_seconds=100).load(str(p2)) == 3
+
+
+def test_router_smoke_entry(tmp_path, monkeypatch):
+    """Routing-engine smoke (reference query_router_engine.py:734-764): warm-up, two passes, save."""
+    import json as _json
+    monkeypatch.setenv("DLLM_EMBEDDER", "hash")
+    from distributed_llm_amd.router.embedder import clear_registry
+    from distributed_llm_amd.router.query_router import smoke
+    clear_registry()
+    path = str(tmp_path / "qr_cache.json")
+    res = smoke(path)
+    assert [d.device for d in res["first"][:2]] == ["nano", "nano"]
+    assert all(d.cache_hit for d in res["second"])
+    with open(path) as f:
+        entries = _json.load(f)
+    assert {e["query"] for e in entries} >= {"hello", "what is 2+2"}
+    clear_registry()
