@@ -27,6 +27,9 @@ int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int,
                      hipStream_t);
 int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                          hipStream_t);
+int dllm_moe_max_tiles(int, int);
+int dllm_moe_ffn(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int, int*,
+                 int*, void*, float*, void*, hipStream_t);
 int dllm_car_alloc(long, void**);
 int dllm_car_get_handle(void*, char*);
 int dllm_car_handle_size();
@@ -297,6 +300,36 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
         part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
      "skinny_gemm");
 }
+// Mixtral-style MoE FFN: x [T, H] bf16, ids [T, k] int32, wts [T, k] f32, w13 [E, 2I, H], w2 [E, H, I]
+// -> out [T, H] bf16 (partial sum over this rank's I shard under TP).  Workspace from torch's
+// caching allocator, so the call is graph-capturable.
+void moe_ffn(torch::Tensor x, torch::Tensor ids, torch::Tensor wts, torch::Tensor w13, torch::Tensor w2,
+             torch::Tensor out) {
+  check_bf16(x, "x");
+  check_i32(ids, "ids");
+  check_f32(wts, "wts");
+  check_bf16(w13, "w13");
+  check_bf16(w2, "w2");
+  check_bf16(out, "out");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && out.is_contiguous(), "x 2-D row-major, out contiguous");
+  TORCH_CHECK(w13.dim() == 3 && w2.dim() == 3 && w13.is_contiguous() && w2.is_contiguous(), "w13/w2 [E, N, K]");
+  const int64_t T = x.size(0), H = x.size(1), E = w13.size(0), I = w13.size(1) / 2;
+  TORCH_CHECK(w13.size(2) == H && w2.size(0) == E && w2.size(1) == H && w2.size(2) == I, "expert weight shapes");
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) == T && wts.sizes() == ids.sizes(), "ids/wts [T, k]");
+  TORCH_CHECK(out.size(0) == T && out.size(1) == H, "out shape");
+  const int k = ids.size(1);
+  auto iopt = ids.options();
+  const int P = (int)(T * k), mt = dllm_moe_max_tiles(P, (int)E);
+  auto perm = torch::empty({std::max(P, 1)}, iopt);
+  auto tiles = torch::empty({4 * mt}, iopt);
+  auto act = torch::empty({std::max(P, 1), I}, x.options());
+  auto y = torch::empty({std::max(P, 1), H}, wts.options());
+  ok(dllm_moe_ffn(x.data_ptr(), x.stride(0), T, (int)H, ids.data_ptr<int>(), wts.data_ptr<float>(), k, (int)E,
+                  w13.data_ptr(), w2.data_ptr(), (int)I, perm.data_ptr<int>(), tiles.data_ptr<int>(), act.data_ptr(),
+                  y.data_ptr<float>(), out.data_ptr(), stream()),
+     "moe_ffn");
+}
+
 // ---- one-shot all-reduce over IPC-mapped peer buffers (csrc/kernels/custom_ar.hip)
 int64_t car_alloc(int64_t data_bytes) {
   void* p = nullptr;
@@ -337,6 +370,7 @@ void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
 }  // namespace
 
 PYBIND11_MODULE(_hip_kernels, m) {
+  m.def("moe_ffn", &moe_ffn);
   m.def("car_alloc", &car_alloc);
   m.def("car_handle", &car_handle);
   m.def("car_open", &car_open);

@@ -176,28 +176,11 @@ class LlamaModel:
         return self._moe(L, x)
 
     def _moe(self, L, x: torch.Tensor) -> torch.Tensor:
-        """Top-k expert MLP: gate kernel -> token permutation by expert -> per-expert GEMMs ->
-        weighted un-permute (index_add).  Experts are TP-sharded along I."""
-        T = x.shape[0]
-        k = self.cfg.experts_per_token
-        ids, w = ops.moe_gate(F.linear(x, L["wgate"]).float(), k)
-        flat = ids.reshape(-1).long()
-        order = torch.argsort(flat, stable=True)
-        tok = order // k
-        counts = torch.bincount(flat, minlength=self.cfg.n_experts).tolist()
-        xs = x.index_select(0, tok)
-        ys = torch.empty_like(xs)
-        s = 0
-        for e, c in enumerate(counts):
-            if c == 0:
-                continue
-            seg = xs[s:s + c]
-            ys[s:s + c] = F.linear(ops.silu_mul(F.linear(seg, L["w13"][e])), L["w2"][e])
-            s += c
-        ys = ys * w.reshape(-1)[order].unsqueeze(-1).to(ys.dtype)
-        out = torch.zeros((T, x.shape[1]), dtype=torch.float32, device=x.device)
-        out.index_add_(0, tok, ys.float())
-        return out.to(x.dtype)
+        """Top-k expert FFN: HIP gate kernel (softmax top-k) -> ops.moe_ffn (device-side token
+        permutation + grouped expert GEMMs, no host sync, so decode steps stay graph-captured).
+        Experts are TP-sharded along I; the caller all-reduces the partial sums."""
+        ids, w = ops.moe_gate(F.linear(x, L["wgate"]).float(), self.cfg.experts_per_token)
+        return ops.moe_ffn(x, ids, w, L["w13"], L["w2"])
 
     def hidden_states(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:

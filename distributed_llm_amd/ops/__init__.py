@@ -197,6 +197,19 @@ def moe_gate(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     return ids, w
 
 
+def moe_ffn(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13: torch.Tensor,
+            w2: torch.Tensor) -> torch.Tensor:
+    """Top-k expert FFN (csrc/kernels/moe.hip): device-side routing + grouped MFMA GEMMs with the
+    SwiGLU in the first GEMM's epilogue; graph-capturable.  x [T, H], ids [T, k] int32,
+    wts [T, k] f32, w13 [E, 2I, H], w2 [E, H, I] -> [T, H]."""
+    ext = _native(x)
+    if ext is None:
+        return ref.moe_ffn(x, ids, wts, w13, w2)
+    out = torch.empty((x.shape[0], x.shape[1]), dtype=x.dtype, device=x.device)
+    ext.moe_ffn(x, ids.to(torch.int32).contiguous(), wts.float().contiguous(), w13, w2, out)
+    return out
+
+
 # ----------------------------------------------------------------------------- sampling
 
 def argmax(logits: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

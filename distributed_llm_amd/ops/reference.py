@@ -138,6 +138,22 @@ def moe_gate(logits, k):
     return ids.to(torch.int32), w
 
 
+def moe_ffn(x, ids, wts, w13, w2):
+    """sum_j wts[t, j] * (silu(x w13_e[:I]^T) * (x w13_e[I:]^T)) w2_e^T  with e = ids[t, j] (f32 math,
+    bf16 rounding of the activation like the kernel)."""
+    T, H = x.shape
+    I = w13.shape[1] // 2
+    out = torch.zeros((T, H), dtype=torch.float32, device=x.device)
+    xf = x.float()
+    for j in range(ids.shape[1]):
+        for e in ids[:, j].unique().tolist():
+            sel = (ids[:, j] == e).nonzero().flatten()
+            gu = xf[sel] @ w13[e].float().t()
+            act = (torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]).to(x.dtype).float()
+            out[sel] += wts[sel, j:j + 1].float() * (act @ w2[e].float().t())
+    return out.to(x.dtype)
+
+
 def sample_top_p(vals, idx, temperature, top_p, uniform):
     t = temperature.float().clamp(min=1e-5)[:, None]
     p = torch.softmax(vals.float() / t, dim=-1)

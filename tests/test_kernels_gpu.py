@@ -214,3 +214,47 @@ def test_skinny_gemm_swiglu(M, kind):
     y = gemm._run_plan((kind, 2 if M <= 64 else 1, 4), gu, w, True, None)
     yr = ref.silu_mul(gu).float() @ w.float().T
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("T,H,I,E,k", [(1, 128, 64, 4, 2), (7, 256, 96, 8, 2), (64, 512, 256, 8, 2),
+                                       (300, 256, 128, 8, 2), (33, 128, 160, 4, 1), (16, 4096, 1792, 8, 2)])
+def test_moe_ffn(T, H, I, E, k):
+    """Grouped MoE FFN (routing + gathered GEMMs + SwiGLU + combine) vs the torch fp32 reference."""
+    g = torch.Generator(device="cuda").manual_seed(T * 31 + E)
+    x = (torch.randn(T, H, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    w13 = (torch.randn(E, 2 * I, H, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(E, H, I, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    logits = torch.randn(T, E, device="cuda", generator=g)
+    ids, w = ops.moe_gate(logits, k)
+    got = ops.moe_ffn(x, ids, w, w13, w2).float()
+    want = ref.moe_ffn(x, ids, w, w13, w2).float()
+    err = (got - want).abs().max().item()
+    assert err <= 2e-2 * max(1.0, want.abs().max().item()), err
+
+
+def test_moe_ffn_graph_capture():
+    """The MoE path has no host sync: capture once, replay with different routing."""
+    T, H, I, E, k = 32, 256, 128, 8, 2
+    g = torch.Generator(device="cuda").manual_seed(5)
+    w13 = (torch.randn(E, 2 * I, H, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(E, H, I, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    x = torch.zeros(T, H, device="cuda", dtype=torch.bfloat16)
+    logits = torch.zeros(T, E, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ids, w = ops.moe_gate(logits, k)
+        ops.moe_ffn(x, ids, w, w13, w2)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ids, w = ops.moe_gate(logits, k)
+        out = ops.moe_ffn(x, ids, w, w13, w2)
+    for it in range(3):
+        x.copy_((torch.randn(T, H, device="cuda", generator=g) * 0.5).to(torch.bfloat16))
+        logits.copy_(torch.randn(T, E, device="cuda", generator=g))
+        graph.replay()
+        torch.cuda.synchronize()
+        i2, w2_ = ref.moe_gate(logits, k)
+        want = ref.moe_ffn(x, i2, w2_, w13, w2).float()
+        assert (out.float() - want).abs().max().item() < 2e-2
