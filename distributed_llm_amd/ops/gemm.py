@@ -142,6 +142,22 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
     dev = torch.device(device)
     if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
         return
+    cache = os.environ.get("DLLM_GEMM_PLANS")  # JSON plan cache: re-use a previous run's choices
+    if cache and os.path.exists(cache):
+        import json
+        with open(cache) as f:
+            for k, v in json.load(f).items():
+                M, N, K, sw = k.split(",")
+                _P.plans[(int(M), int(N), int(K), sw == "1")] = tuple(v)
+    shapes = list(shapes)
+    _autotune(shapes, list(ms), dev, verbose)
+    if cache:
+        import json
+        with open(cache, "w") as f:
+            json.dump({f"{M},{N},{K},{int(sw)}": list(v) for (M, N, K, sw), v in _P.plans.items()}, f)
+
+
+def _autotune(shapes, ms, dev, verbose: bool) -> None:
     for (N, K, sw) in shapes:
         copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
         ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]

@@ -5,6 +5,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 STEPS=${STEPS:-3}
+# first a plain run that autotunes and saves the GEMM plans, so the profiled run below does not
+# include the tuning sweeps (its kernel statistics then cover warm-up + timed steps only)
+export DLLM_GEMM_PLANS=gpurun_out/prof/gemm_plans.json
+timeout -k 10 600 python3 bench.py --steps 1 --warmup 0 ${BENCH_ARGS} > gpurun_out/prof_tune.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
   python3 bench.py --steps $STEPS --warmup 1 ${BENCH_ARGS} > gpurun_out/prof_bench.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof_bench.log
