@@ -1,0 +1,80 @@
+"""Failure detection and recovery on real worker processes (echo pools, CPU):
+supervisor bring-up / health, crash detection + restart, lazy restart from the pool client,
+watchdog restart, and orchestrator failover when a pool process is killed."""
+import os
+import signal
+import socket
+import time
+
+import pytest
+
+from distributed_llm_amd.config import LARGE, SMALL
+from distributed_llm_amd.pools.base import HTTPPool
+from distributed_llm_amd.pools.supervisor import PoolSpec, Supervisor
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture()
+def sup(tmp_path):
+    s = Supervisor([PoolSpec(SMALL, _port(), kind="echo", max_new_tokens=8),
+                    PoolSpec(LARGE, _port(), kind="echo", max_new_tokens=16)],
+                   log_dir=str(tmp_path / "logs"), startup_timeout_s=120)
+    yield s
+    s.stop_all()
+
+
+def _crash(sup, name):
+    p = sup.procs[name]
+    os.killpg(p.pid, signal.SIGKILL)  # the process group the supervisor created for this worker
+    p.wait(timeout=30)
+    assert not sup.alive(name)
+
+
+HIST = [{"role": "user", "content": "hello there"}]
+
+
+def test_start_health_crash_restart(sup):
+    assert sup.start_all() == {SMALL: True, LARGE: True}
+    assert sup.is_running(SMALL) and sup.is_running(LARGE)
+    pool = HTTPPool(SMALL, sup.specs[SMALL].url)
+    assert "response" in pool.process(HIST)
+    _crash(sup, SMALL)
+    assert "error" in pool.process(HIST)           # detection: the client sees an error dict
+    assert sup.ensure(SMALL) and sup.restarts[SMALL] == 1
+    assert "response" in pool.process(HIST)
+
+
+def test_lazy_restart_from_client(sup):
+    sup.start_all()
+    pool = HTTPPool(SMALL, sup.specs[SMALL].url, supervisor=sup)
+    _crash(sup, SMALL)
+    # reference nano.py:19-21: the client restarts a server whose port is closed before posting
+    assert "response" in pool.process(HIST)
+
+
+def test_watchdog_restarts_dead_worker(sup):
+    sup.start_all()
+    sup.watch(interval_s=0.2)
+    _crash(sup, LARGE)
+    t0 = time.time()
+    while time.time() - t0 < 60 and not sup.is_running(LARGE):
+        time.sleep(0.2)
+    assert sup.is_running(LARGE) and sup.restarts[LARGE] >= 1
+
+
+def test_router_fails_over_when_pool_process_dies(sup):
+    from distributed_llm_amd.config import BENCHMARK_CFG
+    from distributed_llm_amd.orchestrator import Router
+    sup.start_all()
+    pools = {SMALL: HTTPPool(SMALL, sup.specs[SMALL].url), LARGE: HTTPPool(LARGE, sup.specs[LARGE].url)}
+    r = Router(strategy="token", config=dict(BENCHMARK_CFG, enable_failover=True), pools=pools)
+    _, _, dev = r.route_query(HIST)
+    assert dev == SMALL                               # short query -> small tier
+    _crash(sup, SMALL)
+    payload, tokens, dev = r.route_query(HIST)
+    assert dev == LARGE and payload.get("ok") and tokens > 0   # failover served it
