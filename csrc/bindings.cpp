@@ -13,8 +13,8 @@ int dllm_rope_kv(const void*, long, const int*, const float*, const int*, void*,
                  hipStream_t);
 int dllm_kv_write(const void*, const void*, long, const int*, void*, void*, int, int, int, int, hipStream_t);
 int dllm_paged_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*,
-                         const int*, const int*, void*, float*, float*, int*, int, int, int, int, int, int, int, float,
-                         hipStream_t);
+                         const int*, const int*, void*, float*, float*, int*, const int*, int, int, int, int, int, int,
+                         int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
@@ -127,7 +127,7 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
                      torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
                      torch::Tensor tile_tok0, torch::Tensor out, c10::optional<torch::Tensor> part_o,
                      c10::optional<torch::Tensor> part_ml, c10::optional<torch::Tensor> counters, int64_t splits,
-                     bool causal, double scale) {
+                     bool causal, double scale, c10::optional<torch::Tensor> split_len) {
   check_bf16(q, "q");
   check_bf16(kc, "k_cache");
   check_bf16(vc, "v_cache");
@@ -162,9 +162,15 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
     po = part_o->data_ptr<float>();
     pml = part_ml->data_ptr<float>();
   }
+  const int* sl = nullptr;
+  if (split_len.has_value()) {
+    check_i32(*split_len, "split_len");
+    TORCH_CHECK(split_len->numel() >= 1, "split_len: device scalar");
+    sl = split_len->data_ptr<int>();
+  }
   ok(dllm_paged_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                           qstart.data_ptr<int>(), qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(),
-                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, num_tiles, nq, nkv, d,
+                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, sl, num_tiles, nq, nkv, d,
                           block_tables.size(1), splits, causal ? 1 : 0, (float)scale, stream()),
      "paged_attention");
 }

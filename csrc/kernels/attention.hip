@@ -40,6 +40,7 @@ struct AttnArgs {
   float* part_o;         // [num_tiles, nkv, splits, 16, d]
   float* part_ml;        // [num_tiles, nkv, splits, 16, 2]
   int* counters;         // [num_tiles * nkv] zeroed; re-armed by the reducing workgroup
+  const int* split_len;  // optional device scalar: keys per split (dynamic per-tile split count)
   int nq, nkv, G, max_blocks, causal;
   float scale_log2;
 };
@@ -68,7 +69,17 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   const int row_lim = !row_ok ? 0 : (a.causal ? ctx - qlen + my_tok + 1 : ctx);
   int last_tok = min(tok0 + tpt, qlen) - 1;
   int kmax = (seq < 0 || last_tok < tok0) ? 0 : (a.causal ? ctx - qlen + last_tok + 1 : ctx);
-  int chunk = (kmax + splits - 1) / splits;
+  // Dynamic split-K: with a device-side split length every tile takes only as many of the
+  // gridDim.z splits as its own key range needs (long contexts split, short ones run whole), so
+  // one launch is balanced across a batch of very different context lengths; surplus blocks
+  // leave immediately (uniform per block: split is blockIdx.z).
+  int nsplit = splits;
+  if (a.split_len != nullptr) {
+    const int sl = max(*a.split_len, 32);
+    nsplit = min(splits, max(1, (kmax + sl - 1) / sl));
+    if (split >= nsplit) return;
+  }
+  int chunk = (kmax + nsplit - 1) / nsplit;
   chunk = (chunk + 31) & ~31;
   const int k_begin = split * chunk;
   const int k_end = min(kmax, k_begin + chunk);
@@ -187,7 +198,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   __syncthreads();
 
   const int G_ = G;
-  if (splits == 1) {
+  if (nsplit == 1) {
     for (int e = threadIdx.x; e < 16 * D; e += blockDim.x) {
       const int row = e / D, col = e % D;
       float M = -INFINITY;
@@ -245,18 +256,18 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     }
     st_wt16(rml, (unsigned)((pbase + 2 * threadIdx.x) * 2 * 4), make_float4(ml[0], ml[1], ml[2], ml[3]));
   }
-  if (!ticket_last(&a.counters[tile * a.nkv + kvh], splits, &s_last)) return;
+  if (!ticket_last(&a.counters[tile * a.nkv + kvh], nsplit, &s_last)) return;
   const long tbase = (((long)tile * a.nkv + kvh) * splits) * 16;
   if (threadIdx.x < 16) {
     const int row = threadIdx.x;
     float M = -INFINITY;
-    for (int sp = 0; sp < splits; ++sp) {
+    for (int sp = 0; sp < nsplit; ++sp) {
       const float4 q = ld_wt16(rml, (unsigned)((tbase + sp * 16 + (row & ~1)) * 2 * 4));
       M = fmaxf(M, (row & 1) ? q.z : q.x);
     }
     const float Ms = (M == -INFINITY) ? 0.f : M;
     float L = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
+    for (int sp = 0; sp < nsplit; ++sp) {
       const float4 q = ld_wt16(rml, (unsigned)((tbase + sp * 16 + (row & ~1)) * 2 * 4));
       const float m = (row & 1) ? q.z : q.x, l = (row & 1) ? q.w : q.y;
       L += l * exp2f(m - Ms);
@@ -270,7 +281,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     const int tok = tok0 + row / G_, head = kvh * G_ + row % G_;
     if (seq < 0 || tok >= qlen) continue;
     float o[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < splits; ++sp) {
+    for (int sp = 0; sp < nsplit; ++sp) {
       const float4 mq = ld_wt16(rml, (unsigned)((tbase + sp * 16 + (row & ~1)) * 2 * 4));
       const float f = exp2f(((row & 1) ? mq.z : mq.x) - s_m[0][row]);
       const float4 q = ld_wt16(ro, (unsigned)(((tbase + sp * 16 + row) * D + col) * 4));
@@ -292,20 +303,22 @@ void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
 extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* vc, const int* block_tables,
                                     const int* seq_qstart, const int* seq_qlen, const int* seq_ctx,
                                     const int* tile_seq, const int* tile_tok0, void* out, float* part_o,
-                                    float* part_ml, int* counters, int num_tiles, int nq, int nkv, int d, int max_blocks,
-                                    int splits, int causal, float scale, hipStream_t stream) {
+                                    float* part_ml, int* counters, const int* split_len, int num_tiles, int nq, int nkv,
+                                    int d, int max_blocks, int splits, int causal, float scale, hipStream_t stream) {
   if (nq % nkv != 0) return -1;
   const int G = nq / nkv;
   if (16 % G != 0) return -2;
   if (splits < 1 || (splits > 1 && (!part_o || !part_ml || !counters))) return -3;
   if (num_tiles <= 0) return 0;
   AttnArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
-             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, nq, nkv, G, max_blocks, causal, scale * LOG2E};
+             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, split_len, nq, nkv, G, max_blocks, causal,
+             scale * LOG2E};
   // 8 waves per workgroup when the grid alone cannot fill the CUs with memory requests
   // (decode at moderate batch: tiles x kv-heads x splits workgroups are all resident at once).
   static const int env_w = [] { const char* e = getenv("DLLM_ATTN_WAVES"); return e ? atoi(e) : 0; }();
   const long wgs = (long)num_tiles * nkv * splits;
-  const int W = env_w == 4 || env_w == 8 ? env_w : (wgs <= 2048 ? 8 : 4);
+  // (dynamic splitting bounds every block's key range, where 8 waves measured best)
+  const int W = env_w == 4 || env_w == 8 ? env_w : ((split_len != nullptr || wgs <= 2048) ? 8 : 4);
   dim3 grid(num_tiles, nkv, splits);
 switch (d) {
     case 64: W == 8 ? launch_attn<64, 8>(grid, a, stream) : launch_attn<64, 4>(grid, a, stream); break;

@@ -159,14 +159,16 @@ class LLMEngine:
         self.buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if b < R] + [R]
         mb = self.buckets[-1]
         # packed decode buffer: ids | pos | slots | tile_seq  (mb each) | qstart | qlen | ctx (R+1 each)
-        #                       | block-table updates [n, (flat idx, block) * R]
-        self._dec_n = 4 * mb + 3 * (R + 1) + 1 + 2 * R
+        #                       | attention split length | block-table updates [n, (flat idx, block) * R]
+        self._dec_n = 4 * mb + 3 * (R + 1) + 1 + 1 + 2 * R
         self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
         self.dec_host_t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
         self.dec_host = self.dec_host_t.numpy()
-        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1), 4 * mb + 3 * (R + 1)]
+        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1), 4 * mb + 3 * (R + 1),
+             4 * mb + 3 * (R + 1) + 1]
         self._off = o
-        self.d_upd = self.dec_dev[o[7]:]
+        self.d_split = self.dec_dev[o[7]:o[7] + 1]
+        self.d_upd = self.dec_dev[o[8]:]
         d = self.dec_dev
         self.d_ids, self.d_pos, self.d_slots, self.d_tseq = (d[o[0]:o[1]], d[o[1]:o[2]], d[o[2]:o[3]], d[o[3]:o[4]])
         self.d_qstart, self.d_qlen, self.d_ctx = d[o[4]:o[5]], d[o[5]:o[6]], d[o[6]:o[6] + R + 1]
@@ -194,6 +196,18 @@ class LLMEngine:
         shapes.add((m.lm_head.shape[0], m.lm_head.shape[1], False))
         ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= 128], self.device,
                           verbose=os.environ.get("DLLM_VERBOSE") == "1")
+
+    # Decode attention: the graph is captured with a fixed split-K depth; each step the host writes
+    # the split length so that the whole batch yields ~ATTN_TARGET_WGS workgroups, and every tile
+    # takes ceil(its context / split length) splits (long conversations split, short ones don't).
+    ATTN_TARGET_WGS = int(os.environ.get("DLLM_ATTN_TARGET_WGS", "2048"))
+
+    def _decode_splits(self, bs: int) -> int:
+        return 8 if bs <= 64 else 4
+
+    def _split_len(self, total_ctx: int) -> int:
+        per = total_ctx * self.model.nkv / max(1, self.ATTN_TARGET_WGS)
+        return int(max(256, math.ceil(per / 256) * 256))
 
     def _splits_for(self, tiles: int) -> int:
         # measured on MI355X (scripts/microbench.py attn): split-K pays only while tiles x kv-heads
@@ -529,12 +543,13 @@ class LLMEngine:
         h[o[5] + rows] = 1
         h[o[6] + rows] = lens
         self._sync_bt()
+        h[o[7]] = self._split_len(int(lens.sum()))
         nu = len(self._bt_upd) // 2
-        h[o[7]] = nu
+        h[o[8]] = nu
         if nu:
-            h[o[7] + 1:o[7] + 1 + 2 * nu] = self._bt_upd
+            h[o[8] + 1:o[8] + 1 + 2 * nu] = self._bt_upd
             self._bt_upd.clear()
-        self.dec_dev[:o[7] + 1 + 2 * nu].copy_(self.dec_host_t[:o[7] + 1 + 2 * nu], non_blocking=True)
+        self.dec_dev[:o[8] + 1 + 2 * nu].copy_(self.dec_host_t[:o[8] + 1 + 2 * nu], non_blocking=True)
         _t1 = time.perf_counter()
         if self.use_graphs:
             g = self._graphs.get(bs)
@@ -576,7 +591,8 @@ class LLMEngine:
     def _decode_meta(self, bs: int) -> AttnMeta:
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
                         ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
-                        last_idx=self.d_last[:bs], splits=self._splits_for(bs), workspace=self.dec_ws)
+                        last_idx=self.d_last[:bs], splits=self._decode_splits(bs), workspace=self.dec_ws,
+                        split_len=self.d_split)
 
     def _decode_forward(self, bs: int) -> None:
         ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)

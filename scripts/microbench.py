@@ -33,6 +33,34 @@ def timeit(fn, iters=20, warm=3):
     return s.elapsed_time(e) / iters
 
 
+def bench_attn_dyn(B, C, nq, nkv, d, z, target, var=True):
+    """Dynamic split-K (engine decode path): split length from the batch's total context."""
+    g = torch.Generator().manual_seed(0)
+    ctxs = (torch.randint(C // 4, 7 * C // 4 + 1, (B,), generator=g).tolist() if var else [C] * B)
+    Cm = max(ctxs)
+    NB = B * ((Cm + 15) // 16) + 8
+    kc = torch.randn(NB, nkv, 16, d, device="cuda").to(torch.bfloat16)
+    vc = torch.randn(NB, nkv, d, 16, device="cuda").to(torch.bfloat16)
+    nb = (Cm + 15) // 16
+    bt = torch.randperm(NB - 8, device="cuda")[:B * nb].view(B, nb).to(torch.int32)
+    q = torch.randn(B, nq, d, device="cuda").to(torch.bfloat16)
+    I = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    qs, ql, cx = I(list(range(B))), I([1] * B), I(ctxs)
+    ts, tt = ops.build_tiles([1] * B, nq // nkv)
+    ts, tt = I(ts), I(tt)
+    sl = int(max(256, math.ceil(sum(ctxs) * nkv / target / 256) * 256))
+    slt = I([sl])
+    ms = timeit(lambda: ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, split_len=slt))
+    # correctness against the single-split kernel
+    ref_o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=1)
+    got = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, split_len=slt)
+    err = (ref_o.float() - got.float()).abs().max().item()
+    kv_bytes = sum(ctxs) * nkv * d * 2 * 2
+    return {"bench": "attn_decode_dyn", "B": B, "C": sum(ctxs) // B, "var": var, "nq": nq, "nkv": nkv, "d": d,
+            "z": z, "target": target, "split_len": sl, "us": round(ms * 1000, 1),
+            "GBps": round(kv_bytes / ms / 1e6, 1), "max_err_vs_1split": err}
+
+
 def bench_attn(B, C, nq, nkv, d, splits, var=False):
     """var=True: contexts uniform in [C/4, 7C/4] (mean C) like a serving batch, else all C."""
     g = torch.Generator().manual_seed(0)
@@ -148,6 +176,14 @@ if __name__ == "__main__":
             for (nq, nkv, d) in [(32, 4, 64), (32, 8, 128)]:
                 for splits in (1, 2, 4, 8):
                     print(json.dumps(bench_attn(B, C, nq, nkv, d, splits, var)), flush=True)
+    if "attn_dyn" in what:
+        for (B, C, var) in [(1, 2048, False), (16, 2048, False), (64, 2048, True), (128, 2021, True),
+                            (256, 1024, False), (256, 2034, True), (256, 4000, True)]:
+            for (nq, nkv, d) in [(32, 4, 64), (32, 8, 128)]:
+                print(json.dumps(bench_attn(B, C, nq, nkv, d, 1, var)), flush=True)
+                for z in (4, 8):
+                    for target in (1024, 2048, 4096):
+                        print(json.dumps(bench_attn_dyn(B, C, nq, nkv, d, z, target, var)), flush=True)
     if "decode" in what or "prefill" in what:
         eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
         if "decode" in what:

@@ -112,6 +112,25 @@ def test_paged_attention_rescale_branch(splits):
     torch.testing.assert_close(o.float(), o2.float(), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("split_len,z", [(32, 8), (64, 4), (256, 8), (4096, 4)])
+def test_paged_attention_dynamic_split(split_len, z):
+    """Dynamic split-K: each tile takes ceil(keys / split_len) of the z splits (decode path), mixed
+    with prefill tiles and an empty padding tile; repeated launches re-use the ticket counters."""
+    seqs = [(1, 1), (1, 17), (1, 300), (1, 1000), (5, 40), (1, 64), (9, 150)]
+    q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(32, 8, 128, seqs, NB=128, spike=True)
+    ts = torch.cat([ts, torch.tensor([-1], dtype=torch.int32, device=DEV)])   # padding tile
+    tt = torch.cat([tt, torch.tensor([0], dtype=torch.int32, device=DEV)])
+    nt, nkv, d = ts.numel(), kc.shape[1], 128
+    ws = (torch.empty(nt * nkv * z * 16 * d, device=DEV), torch.empty(nt * nkv * z * 16 * 2, device=DEV),
+          torch.zeros(nt * nkv, dtype=torch.int32, device=DEV))
+    sl = torch.tensor([split_len], dtype=torch.int32, device=DEV)
+    o2 = ref.paged_attention(q, kc, vc, bt, qs, ql, cx, 1 / math.sqrt(d))
+    for _ in range(3):
+        o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, workspace=ws, split_len=sl)
+        torch.testing.assert_close(o.float(), o2.float(), atol=3e-2, rtol=3e-2)
+    assert int(ws[2].abs().sum()) == 0   # every ticket counter re-armed
+
+
 def test_paged_attention_bidirectional():
     seqs = [(20, 20), (7, 7)]
     q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(16, 16, 64, seqs)
