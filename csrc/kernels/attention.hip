@@ -54,7 +54,23 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   __shared__ float s_l[WAVES][16];
   __shared__ int s_last;
 
-  const int tile = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z, splits = gridDim.z;
+  // XCD-aware block order (bijective; cdna_hip_programming.md T1): blocks b, b+8, ... share an
+  // XCD (and its L2), so give each XCD a CONTIGUOUS range of (split, tile, head) work: prefill
+  // tiles of one sequence/head then re-read the same K/V from that XCD's L2 instead of from HBM,
+  // and a decode tile's split-K partials are combined on the XCD that wrote them.
+  int tile, kvh, split;
+  const int splits = gridDim.z;
+  {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const long n = (long)nx * ny * splits;
+    const long lin = blockIdx.x + (long)nx * (blockIdx.y + (long)ny * blockIdx.z);
+    const long q8 = n / 8, r8 = n % 8, xcd = lin % 8;
+    const long logical = xcd * q8 + (xcd < r8 ? xcd : r8) + lin / 8;
+    split = (int)(logical % splits);
+    const long rest = logical / splits;
+    tile = (int)(rest % nx);
+    kvh = (int)(rest / nx);
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, rl = lane & 15;
   const int seq = a.tile_seq[tile];
@@ -72,7 +88,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   // Dynamic split-K: with a device-side split length every tile takes only as many of the
   // gridDim.z splits as its own key range needs (long contexts split, short ones run whole), so
   // one launch is balanced across a batch of very different context lengths; surplus blocks
-  // leave immediately (uniform per block: split is blockIdx.z).
+  // leave immediately (uniform per block: split is a per-block index).
   int nsplit = splits;
   if (a.split_len != nullptr) {
     const int sl = max(*a.split_len, 32);
