@@ -296,7 +296,9 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
   TORCH_CHECK(ntw == 1 || ntw == 2 || ntw == 4, "ntw in {1,2,4}");
   TORCH_CHECK(variant == 0 || ntw <= 2, "LDS variant: ntw in {1,2}");
   TORCH_CHECK(variant == 0 || M <= 64 || ntw == 1, "LDS variant: M > 64 needs ntw 1");
-  const int nc = (variant == 0 ? 16 : 64) * ntw, tiles = (N + nc - 1) / nc, mp = ((M + 15) / 16) * 16;
+  // slab rows = the kernel's row-tile height (MT x 16, MT in {1, 2, 4, 8}), not ceil(M / 16) x 16
+  const int nc = (variant == 0 ? 16 : 64) * ntw, tiles = (N + nc - 1) / nc,
+            mp = 16 * (M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : 8);
   if (splits > 1) {
     TORCH_CHECK(part.numel() >= (int64_t)splits * tiles * nc * mp, "split-K workspace too small");
     TORCH_CHECK(counters.numel() >= tiles, "counter buffer too small");

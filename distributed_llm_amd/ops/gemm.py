@@ -58,7 +58,9 @@ def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tu
     tiles = (N + nc - 1) // nc
     kchunk = ((K + splits - 1) // splits + 31) // 32 * 32
     S = (K + kchunk - 1) // kchunk
-    mp = (M + 15) // 16 * 16
+    # split-K slabs are laid out with the kernel's row-tile height (MT x 16 rows, MT in 1/2/4/8),
+    # not ceil(M/16) x 16: e.g. M = 100 runs the MT = 8 kernel and needs 128-row slabs
+    mp = 16 * (1 if M <= 16 else 2 if M <= 32 else 4 if M <= 64 else 8)
     return (S * tiles * nc * mp if S > 1 else 0), tiles
 
 
