@@ -14,7 +14,7 @@ int dllm_rope_kv(const void*, long, const int*, const float*, const int*, void*,
 int dllm_kv_write(const void*, const void*, long, const int*, void*, void*, int, int, int, int, hipStream_t);
 int dllm_paged_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*,
                          const int*, const int*, void*, float*, float*, int*, const int*, int, int, int, int, int, int,
-                         int, float, hipStream_t);
+                         int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
@@ -127,7 +127,7 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
                      torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
                      torch::Tensor tile_tok0, torch::Tensor out, c10::optional<torch::Tensor> part_o,
                      c10::optional<torch::Tensor> part_ml, c10::optional<torch::Tensor> counters, int64_t splits,
-                     bool causal, double scale, c10::optional<torch::Tensor> split_len) {
+                     bool causal, double scale, c10::optional<torch::Tensor> split_len, bool xcd_remap) {
   check_bf16(q, "q");
   check_bf16(kc, "k_cache");
   check_bf16(vc, "v_cache");
@@ -170,7 +170,7 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
   }
   ok(dllm_paged_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                           qstart.data_ptr<int>(), qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(),
-                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, sl, num_tiles, nq, nkv, d,
+                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, sl, xcd_remap ? 1 : 0, num_tiles, nq, nkv, d,
                           block_tables.size(1), splits, causal ? 1 : 0, (float)scale, stream()),
      "paged_attention");
 }

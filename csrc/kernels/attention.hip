@@ -41,9 +41,13 @@ struct AttnArgs {
   float* part_ml;        // [num_tiles, nkv, splits, 16, 2]
   int* counters;         // [num_tiles * nkv] zeroed; re-armed by the reducing workgroup
   const int* split_len;  // optional device scalar: keys per split (dynamic per-tile split count)
+  int xcd_remap;         // 1: XCD-contiguous block order (prefill K/V reuse in L2)
   int nq, nkv, G, max_blocks, causal;
   float scale_log2;
 };
+// NOTE (measured, MI355X): surplus blocks are not free — a grid whose z-splits are mostly empty
+// for short contexts ran 1.5-4.7x slower than the same work with z = 1, so the engine uses static
+// split counts sized to the batch and keeps the dynamic split for explicit opt-in.
 
 template <int D, int W>
 __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
@@ -54,22 +58,23 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   __shared__ float s_l[WAVES][16];
   __shared__ int s_last;
 
-  // XCD-aware block order (bijective; cdna_hip_programming.md T1): blocks b, b+8, ... share an
-  // XCD (and its L2), so give each XCD a CONTIGUOUS range of (split, tile, head) work: prefill
-  // tiles of one sequence/head then re-read the same K/V from that XCD's L2 instead of from HBM,
-  // and a decode tile's split-K partials are combined on the XCD that wrote them.
-  int tile, kvh, split;
+  // Prefill: XCD-aware block order (bijective; cdna_hip_programming.md T1): blocks b, b+8, ...
+  // share an XCD (and its L2), so each XCD gets a CONTIGUOUS range of (tile, head, split) work
+  // and the tiles of one sequence/head re-read the same K/V from that XCD's L2, not from HBM.
+  // Decode (xcd_remap = 0): tiles carry no shared K/V; the host orders them longest context
+  // first so the dispatcher starts the longest chains first and spreads them over all XCDs.
+  int tile = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
   const int splits = gridDim.z;
-  {
+  if (a.xcd_remap) {
     const int nx = gridDim.x, ny = gridDim.y;
     const long n = (long)nx * ny * splits;
     const long lin = blockIdx.x + (long)nx * (blockIdx.y + (long)ny * blockIdx.z);
     const long q8 = n / 8, r8 = n % 8, xcd = lin % 8;
     const long logical = xcd * q8 + (xcd < r8 ? xcd : r8) + lin / 8;
-    split = (int)(logical % splits);
-    const long rest = logical / splits;
-    tile = (int)(rest % nx);
-    kvh = (int)(rest / nx);
+    tile = (int)(logical % nx);
+    const long rest = logical / nx;
+    kvh = (int)(rest % ny);
+    split = (int)(rest / ny);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, rl = lane & 15;
@@ -319,16 +324,17 @@ void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
 extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* vc, const int* block_tables,
                                     const int* seq_qstart, const int* seq_qlen, const int* seq_ctx,
                                     const int* tile_seq, const int* tile_tok0, void* out, float* part_o,
-                                    float* part_ml, int* counters, const int* split_len, int num_tiles, int nq, int nkv,
-                                    int d, int max_blocks, int splits, int causal, float scale, hipStream_t stream) {
+                                    float* part_ml, int* counters, const int* split_len, int xcd_remap, int num_tiles,
+                                    int nq, int nkv, int d, int max_blocks, int splits, int causal, float scale,
+                                    hipStream_t stream) {
   if (nq % nkv != 0) return -1;
   const int G = nq / nkv;
   if (16 % G != 0) return -2;
   if (splits < 1 || (splits > 1 && (!part_o || !part_ml || !counters))) return -3;
   if (num_tiles <= 0) return 0;
   AttnArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
-             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, split_len, nq, nkv, G, max_blocks, causal,
-             scale * LOG2E};
+             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, split_len, xcd_remap, nq, nkv, G, max_blocks,
+             causal, scale * LOG2E};
   // 8 waves per workgroup when the grid alone cannot fill the CUs with memory requests
   // (decode at moderate batch: tiles x kv-heads x splits workgroups are all resident at once).
   static const int env_w = [] { const char* e = getenv("DLLM_ATTN_WAVES"); return e ? atoi(e) : 0; }();

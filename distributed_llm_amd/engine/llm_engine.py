@@ -197,13 +197,18 @@ class LLMEngine:
         ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= 128], self.device,
                           verbose=os.environ.get("DLLM_VERBOSE") == "1")
 
-    # Decode attention: the graph is captured with a fixed split-K depth; each step the host writes
-    # the split length so that the whole batch yields ~ATTN_TARGET_WGS workgroups, and every tile
-    # takes ceil(its context / split length) splits (long conversations split, short ones don't).
+    # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),
+    # tiles ordered longest context first (the dispatcher then starts the longest chains first).
+    # Opt-in (DLLM_ATTN_DYNAMIC=1): fixed grid depth, and each step the host writes a split length
+    # so the batch yields ~ATTN_TARGET_WGS workgroups; measured slower on MI355X because surplus
+    # early-exit blocks cost dispatch slots (csrc/kernels/attention.hip note).
+    ATTN_DYNAMIC = os.environ.get("DLLM_ATTN_DYNAMIC") == "1"
     ATTN_TARGET_WGS = int(os.environ.get("DLLM_ATTN_TARGET_WGS", "2048"))
 
     def _decode_splits(self, bs: int) -> int:
-        return 8 if bs <= 64 else 4
+        if self.ATTN_DYNAMIC:
+            return 8 if bs <= 64 else 4
+        return self._splits_for(bs)
 
     def _split_len(self, total_ctx: int) -> int:
         per = total_ctx * self.model.nkv / max(1, self.ATTN_TARGET_WGS)
@@ -478,7 +483,7 @@ class LLMEngine:
         splits = self._splits_for(len(tseq))
         meta = AttnMeta(slots=T(slots), block_tables=torch.from_numpy(bt).to(dev), qstart=T(qstart), qlen=T(qlen),
                         ctx=T(ctx), tile_seq=T(tseq), tile_tok0=T(ttok), last_idx=T(last, torch.int64),
-                        splits=splits)
+                        splits=splits, xcd_remap=True)
         hidden = self.model.hidden_states(T(ids), T(pos), meta, self.kv_caches)
         self.steps["prefill"] += 1
         self.steps["prefill_tokens"] += t
@@ -537,7 +542,7 @@ class LLMEngine:
         h[o[2]:o[2] + bs] = -1
         h[o[2]:o[2] + B] = blocks * BS + pos % BS
         h[o[3]:o[3] + bs] = R            # padding tiles -> dummy row (qlen 0)
-        h[o[3]:o[3] + B] = rows
+        h[o[3]:o[3] + B] = rows[np.argsort(-lens, kind="stable")]   # longest context first
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)
         h[o[5] + rows] = 1
@@ -592,7 +597,7 @@ class LLMEngine:
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
                         ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
                         last_idx=self.d_last[:bs], splits=self._decode_splits(bs), workspace=self.dec_ws,
-                        split_len=self.d_split)
+                        split_len=self.d_split if self.ATTN_DYNAMIC else None)
 
     def _decode_forward(self, bs: int) -> None:
         ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)

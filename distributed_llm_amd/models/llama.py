@@ -40,7 +40,8 @@ class AttnMeta:
     last_idx: torch.Tensor     # [S] int64 index of each sequence's last new token in the packed batch
     splits: int = 1
     workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
-    split_len: Optional[torch.Tensor] = None  # int32 device scalar: dynamic split-K (decode)
+    split_len: Optional[torch.Tensor] = None  # int32 device scalar: dynamic split-K (opt-in)
+    xcd_remap: bool = False                    # prefill: XCD-contiguous attention block order
 
 
 class LlamaModel:
@@ -196,7 +197,8 @@ class LlamaModel:
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
             o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                     meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
-                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len)
+                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
+                                    xcd_remap=meta.xcd_remap)
             h = self.par.all_reduce(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
             h = self.par.all_reduce(self._mlp(L, x))

@@ -134,11 +134,13 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                     tile_seq: torch.Tensor, tile_tok0: torch.Tensor, scale: Optional[float] = None,
                     causal: bool = True, splits: int = 1, out: Optional[torch.Tensor] = None,
                     workspace: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                    split_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    split_len: Optional[torch.Tensor] = None, xcd_remap: bool = False) -> torch.Tensor:
     """Paged attention over new query tokens ``q [T, nq, d]`` (see csrc/kernels/attention.hip).
 
     ``splits`` is the split-K grid depth; with ``split_len`` (int32 device scalar, keys per split)
-    each tile uses only ceil(its keys / split_len) of them (dynamic, balanced split-K)."""
+    each tile uses only ceil(its keys / split_len) of them (dynamic, balanced split-K).
+    ``xcd_remap``: XCD-contiguous block order, for prefill (K/V re-read by a sequence's tiles hits
+    one XCD's L2)."""
     d = q.shape[-1]
     scale = (1.0 / math.sqrt(d)) if scale is None else scale
     ext = _native(q)
@@ -155,7 +157,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         else:
             po, pml, cnt = workspace
     ext.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
-                        po, pml, cnt, splits, causal, scale, split_len if splits > 1 else None)
+                        po, pml, cnt, splits, causal, scale, split_len if splits > 1 else None, xcd_remap)
     return o
 
 
