@@ -203,6 +203,7 @@ class LLMEngine:
     # so the batch yields ~ATTN_TARGET_WGS workgroups; measured slower on MI355X because surplus
     # early-exit blocks cost dispatch slots (csrc/kernels/attention.hip note).
     ATTN_DYNAMIC = os.environ.get("DLLM_ATTN_DYNAMIC") == "1"
+    SORT_TILES = os.environ.get("DLLM_DECODE_SORT", "1") == "1"   # decode tiles longest context first
     ATTN_TARGET_WGS = int(os.environ.get("DLLM_ATTN_TARGET_WGS", "2048"))
 
     def _decode_splits(self, bs: int) -> int:
@@ -542,7 +543,7 @@ class LLMEngine:
         h[o[2]:o[2] + bs] = -1
         h[o[2]:o[2] + B] = blocks * BS + pos % BS
         h[o[3]:o[3] + bs] = R            # padding tiles -> dummy row (qlen 0)
-        h[o[3]:o[3] + B] = rows[np.argsort(-lens, kind="stable")]   # longest context first
+        h[o[3]:o[3] + B] = rows[np.argsort(-lens, kind="stable")] if self.SORT_TILES else rows
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)
         h[o[5] + rows] = 1
