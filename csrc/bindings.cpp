@@ -27,6 +27,8 @@ int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int,
                      hipStream_t);
 int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                          hipStream_t);
+int dllm_mm_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
+                 hipStream_t);
 int dllm_moe_max_tiles(int, int);
 int dllm_moe_ffn(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int, int*,
                  int*, void*, float*, void*, hipStream_t);
@@ -308,6 +310,32 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
         part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
      "skinny_gemm");
 }
+// Mid-size decode GEMM (64 < M <= 256; csrc/kernels/mm_gemm.hip): y = x . w^T (x = silu(g)*u if swiglu).
+void mm_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t nt, int64_t splits, bool swiglu,
+             torch::Tensor part, torch::Tensor counters) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  check_f32(part, "part");
+  check_i32(counters, "counters");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous() && y.dim() == 2 &&
+                  y.stride(1) == 1 && y.stride(0) % 8 == 0,
+              "2-D row-major operands");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == (swiglu ? 2 * K : K), "x inner dim");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N, "y shape");
+  TORCH_CHECK(M >= 1 && M <= 256 && K % 64 == 0 && N % 8 == 0, "M in [1,256], K % 64 == 0, N % 8 == 0");
+  TORCH_CHECK(nt == 2 || nt == 4, "nt in {2,4}");
+  const int bn = 16 * nt, tiles = (N + bn - 1) / bn, bm = M <= 64 ? 64 : M <= 128 ? 128 : 256;
+  if (splits > 1) {
+    TORCH_CHECK(part.numel() >= (int64_t)splits * tiles * bn * bm, "split-K workspace too small");
+    TORCH_CHECK(counters.numel() >= tiles, "counter buffer too small");
+  }
+  ok(dllm_mm_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, (int)nt, (int)splits,
+                  swiglu ? 1 : 0, part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
+     "mm_gemm");
+}
+
 // Mixtral-style MoE FFN: x [T, H] bf16, ids [T, k] int32, wts [T, k] f32, w13 [E, 2I, H], w2 [E, H, I]
 // -> out [T, H] bf16 (partial sum over this rank's I shard under TP).  Workspace from torch's
 // caching allocator, so the call is graph-capturable.
@@ -379,6 +407,7 @@ void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
 
 PYBIND11_MODULE(_hip_kernels, m) {
   m.def("moe_ffn", &moe_ffn);
+  m.def("mm_gemm", &mm_gemm);
   m.def("car_alloc", &car_alloc);
   m.def("car_handle", &car_handle);
   m.def("car_open", &car_open);

@@ -194,7 +194,7 @@ class LLMEngine:
         if "wd" in L:
             shapes.add((L["wd"].shape[0], L["wd"].shape[1], True))
         shapes.add((m.lm_head.shape[0], m.lm_head.shape[1], False))
-        ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= 128], self.device,
+        ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= ops.gemm.MAX_M], self.device,
                           verbose=os.environ.get("DLLM_VERBOSE") == "1")
 
     # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),

@@ -22,9 +22,12 @@ import torch.nn.functional as F
 
 from . import _native, reference as ref
 
-MAX_M = 128
+MAX_M = 256        # custom kernels cover decode buckets up to 256 rows
+SKINNY_MAX_M = 128
 _SPLITS = (1, 2, 4, 8, 16)
 _NTWS = (1, 2, 4)
+_MM_NTS = (2, 4)
+_MM_SPLITS = (1, 2, 4, 8)
 
 
 class _Planner:
@@ -53,6 +56,15 @@ class _Planner:
 _P = _Planner()
 
 
+def _need_mm(M: int, N: int, K: int, nt: int, splits: int) -> Tuple[int, int]:
+    bn = 16 * nt
+    tiles = (N + bn - 1) // bn
+    kchunk = ((K + splits - 1) // splits + 63) // 64 * 64
+    S = (K + kchunk - 1) // kchunk
+    bm = 64 if M <= 64 else 128 if M <= 128 else 256
+    return (S * tiles * bn * bm if S > 1 else 0), tiles
+
+
 def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tuple[int, int]:
     nc = (16 if variant == 0 else 64) * ntw
     tiles = (N + nc - 1) // nc
@@ -65,6 +77,8 @@ def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tu
 
 
 def _heuristic(M: int, N: int, K: int) -> Tuple:
+    if M > SKINNY_MAX_M:
+        return ("blas",)
     ntw = 1 if M > 64 else 2
     tiles = (N + 16 * ntw - 1) // (16 * ntw)
     splits = max(1, min(16, math.ceil(512 / tiles), K // 256))
@@ -77,10 +91,15 @@ def _run_plan(plan, x, w, swiglu, out):
             x = ref_silu_mul(x)
         return torch.matmul(x, w.t(), out=out) if out is not None else F.linear(x, w)
     kind, ntw, splits = plan
-    variant = 0 if kind == "skinny" else 1
     ext = _native(x)
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if kind == "mm":
+        floats, tiles = _need_mm(M, N, K, ntw, splits)
+        part, cnt = _P.workspace(x.device, floats, tiles)
+        ext.mm_gemm(x, w, y, ntw, splits, swiglu, part, cnt)
+        return y
+    variant = 0 if kind == "skinny" else 1
     floats, tiles = _need(M, N, K, ntw, splits, variant)
     part, cnt = _P.workspace(x.device, floats, tiles)
     ext.skinny_gemm(x, w, y, ntw, splits, swiglu, part, cnt, variant)
@@ -171,7 +190,16 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 continue
             x = torch.randn(M, 2 * K if sw else K, device=dev).to(torch.bfloat16)
             cands = [("blas",)]
-            for kind, ntws in (("skinny", _NTWS), ("lds", (1, 2))):
+            if M > 16 and K % 64 == 0 and N % 8 == 0 and os.environ.get("DLLM_GEMM_NO_MM") != "1":
+                for nt in _MM_NTS:
+                    for s in _MM_SPLITS:
+                        if s > 1 and K // s < 256:
+                            continue
+                        floats, _ = _need_mm(M, N, K, nt, s)
+                        if floats * 4 > 256 << 20:
+                            continue
+                        cands.append(("mm", nt, s))
+            for kind, ntws in ((("skinny", _NTWS), ("lds", (1, 2))) if M <= SKINNY_MAX_M else ()):
                 for ntw in ntws:
                     if M > 64 and (ntw == 4 or (kind == "lds" and ntw == 2)):
                         continue
@@ -189,7 +217,8 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
             _P.plans[key] = best
             _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
             if verbose:
-                bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None) for k in ("skinny", "lds")}
+                bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
+                      for k in ("skinny", "lds", "mm")}
                 extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
                       f"({N * K * 2 / res[best] / 1e3:.0f} GB/s; blas {res[('blas',)]:.1f}us; {extra})", flush=True)

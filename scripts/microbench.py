@@ -165,7 +165,7 @@ if __name__ == "__main__":
         from distributed_llm_amd.ops import gemm as G
         shapes = [(2560, 2048, False), (2048, 2048, False), (11264, 2048, False), (2048, 5632, True),
                   (32000, 2048, False), (6144, 4096, False), (4096, 4096, False), (28672, 4096, False), (4096, 14336, True)]
-        G.autotune(shapes, [1, 8, 32, 64, 128], "cuda", verbose=True)
+        G.autotune(shapes, [1, 8, 32, 64, 128, 256], "cuda", verbose=True)
     if "gemm" in what:
         for M in (1, 16, 64, 128, 256):
             for (N, K) in [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632), (32000, 2048), (6144, 4096), (28672, 4096), (4096, 14336)]:
