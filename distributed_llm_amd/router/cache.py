@@ -20,6 +20,8 @@ JSON persistence format is identical to the reference's ``CacheEntry.to_dict``.
 from __future__ import annotations
 
 import hashlib
+import heapq
+import itertools
 import json
 import logging
 import re
@@ -253,6 +255,11 @@ class QueryCache:
         self._index = EmbeddingIndex(dim=dim, capacity=max(64, min(max_size, 1 << 20)),
                                      device=index_device)
         self._slot_to_hash: Dict[int, str] = {}
+        # expiry heap (timestamp, seq, hash) with lazy deletion: TTL eviction pops only expired
+        # records instead of scanning every entry on every lookup (the reference's O(N) sweep,
+        # cache.py:250,532-538, was ~0.25 s per 256-conversation step at 1e4 entries)
+        self._expiry: List[Tuple[datetime, int, str]] = []
+        self._seq = itertools.count()
         self._hits = 0
         self._attempts = 0
         self._evictions = 0
@@ -285,20 +292,33 @@ class QueryCache:
         else:
             self._index.put(arr, e.context_key, slot=e.slot)
 
-    def _evict_expired(self) -> None:
-        now = datetime.now()
-        with self._lock:
-            for h in [h for h, e in self._store.items() if not self._is_valid(e, now)]:
+    def _stamp(self, e: CacheEntry, ts: Optional[datetime] = None) -> None:
+        e.timestamp = ts or datetime.now()
+        heapq.heappush(self._expiry, (e.timestamp, next(self._seq), e.query_hash))
+
+    def _pop_expired(self, now: datetime, limit: Optional[int] = None) -> int:
+        """Delete expired entries in expiry order (stale heap records are skipped)."""
+        n = 0
+        while self._expiry and (limit is None or n < limit):
+            ts, _, h = self._expiry[0]
+            if (now - ts).total_seconds() <= self.ttl_seconds:
+                break
+            heapq.heappop(self._expiry)
+            e = self._store.get(h)
+            if e is not None and e.timestamp == ts:
                 self._delete_entry(h)
                 self._evictions += 1
+                n += 1
+        return n
+
+    def _evict_expired(self) -> None:
+        with self._lock:
+            self._pop_expired(datetime.now())
 
     def _evict_one(self) -> None:
-        now = datetime.now()
-        for h, e in self._store.items():
-            if not self._is_valid(e, now):
-                self._delete_entry(h)
-                self._evictions += 1
-                return
+        # stale first (reference cache.py:540-554), then least recently used
+        if self._pop_expired(datetime.now(), limit=1):
+            return
         if self._store:
             self._delete_entry(next(iter(self._store)))
             self._evictions += 1
@@ -345,7 +365,7 @@ class QueryCache:
         with self._lock:
             e = self._store.get(h)
             if e is not None:
-                e.timestamp = datetime.now()
+                self._stamp(e)
                 e.record_routing(device, confidence, method)
                 self._set_embedding(e, q_emb)
                 if response_time is not None:
@@ -356,6 +376,7 @@ class QueryCache:
                 self._evict_one()
             e = CacheEntry(query=query, query_hash=h, context_key=context_key, embedding=None,
                            timestamp=datetime.now(), device_used=device, response_time=response_time)
+            self._stamp(e, e.timestamp)
             self._set_embedding(e, q_emb)
             e.record_routing(device, confidence, method)
             self._store[h] = e
@@ -410,6 +431,7 @@ class QueryCache:
                 emb, e.embedding = e.embedding, None
                 self._set_embedding(e, emb)
                 self._store[e.query_hash] = e
+                self._stamp(e, e.timestamp)
                 n += 1
         return n
 
@@ -436,6 +458,7 @@ class QueryCache:
             self._store.clear()
             self._slot_to_hash.clear()
             self._index.clear()
+            self._expiry.clear()
             self._hits = self._attempts = self._evictions = self._hybrid_fallbacks = 0
 
     def __len__(self) -> int:

@@ -150,6 +150,34 @@ def test_cache_prediction_and_persistence(refmod, tmp_path):
     assert QueryCache(ttl_seconds=100).load(str(p1)) == cache_mod.QueryCache(ttl_seconds=100).load(str(p2)) == 3
 
 
+def test_cache_ttl_expiry_parity(refmod):
+    """TTL eviction (reference cache.py:250,523-538): entries older than ttl are evicted on lookup
+    and preferred as the victim when full; refreshed entries survive.  Ours uses an expiry heap."""
+    import time
+    cache_mod = sys.modules["cache"]
+    from distributed_llm_amd.router.cache import QueryCache
+    ref, mine = cache_mod.QueryCache(max_size=3, ttl_seconds=0.3), QueryCache(max_size=3, ttl_seconds=0.3)
+    for c in (ref, mine):
+        c.insert("a", "k", "nano", 0.9, "m")
+        c.insert("b", "k", "orin", 0.9, "m")
+    time.sleep(0.2)
+    for c in (ref, mine):
+        c.insert("b", "k", "orin", 0.8, "m")      # refresh b
+        c.insert("c", "k", "nano", 0.8, "m")
+    time.sleep(0.15)                               # a expired, b and c alive
+    for c in (ref, mine):
+        c.insert("d", "k", "orin", 0.7, "m")      # full: the stale entry (a) is the victim
+    for q in ("a", "b", "c", "d"):
+        assert (ref.lookup(q, "k") is None) == (mine.lookup(q, "k") is None), q
+    sa, sb = ref.stats(), mine.stats()
+    for k in ("size", "valid", "stale", "hits", "attempts", "evictions"):
+        assert sa[k] == sb[k], k
+    time.sleep(0.35)                               # everything expires
+    assert ref.lookup("d", "k") is None and mine.lookup("d", "k") is None
+    assert ref.stats()["size"] == mine.stats()["size"] == 0
+    assert ref.stats()["evictions"] == mine.stats()["evictions"]
+
+
 def test_router_smoke_entry(tmp_path, monkeypatch):
     """Routing-engine smoke (reference query_router_engine.py:734-764): warm-up, two passes, save."""
     import json as _json
