@@ -49,7 +49,7 @@ struct AttnArgs {
 // for short contexts ran 1.5-4.7x slower than the same work with z = 1, so the engine uses static
 // split counts sized to the batch and keeps the dynamic split for explicit opt-in.
 
-template <int D, int W>
+template <int D, int W, int CH>
 __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   constexpr int KSTEPS = D / 32;
   constexpr int NT = D / 16;
@@ -127,62 +127,72 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   // +30 VGPRs cost a wave per SIMD, and occupancy hides the K/V latency better than ILP here).
   // (Plain local arrays in the loop body: an earlier lambda + struct form made hipcc keep part
   // of the K/V registers in scratch for some instantiations — 48-80 B/lane of scratch traffic.)
-  for (int kb = k_begin + 32 * wave; kb < k_end; kb += 32 * W) {
-    uint4 k0r[KSTEPS], k1r[KSTEPS];
-    uint2 v0r[NT], v1r[NT];
-    {
-      const int b0 = bt[kb >> 4];
-      const int b1 = (kb + 16 < k_end) ? bt[(kb >> 4) + 1] : b0;
+  // CH 32-key chunks per wave trip: all CH chunks' K/V loads are issued before the first chunk's
+  // MFMAs, so a wave keeps CH x 8 KB (d = 64) in flight (CH = 2 for decode: more bytes in flight
+  // per CU at the cost of VGPRs).
+  for (int kb = k_begin + 32 * CH * wave; kb < k_end; kb += 32 * CH * W) {
+    uint4 kr[CH][2][KSTEPS];
+    uint2 vr[CH][2][NT];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int kc = kb + 32 * c;
+      const int b0 = kc < k_end ? bt[kc >> 4] : bt[kb >> 4];
+      const int b1 = (kc + 16 < k_end) ? bt[(kc >> 4) + 1] : b0;
       const u16* k0 = a.kc + ((long)b0 * a.nkv + kvh) * head_stride + rl * D + 8 * g;
       const u16* k1 = a.kc + ((long)b1 * a.nkv + kvh) * head_stride + rl * D + 8 * g;
       const u16* v0 = a.vc + ((long)b0 * a.nkv + kvh) * head_stride + rl * BS + 4 * g;
       const u16* v1 = a.vc + ((long)b1 * a.nkv + kvh) * head_stride + rl * BS + 4 * g;
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
-        k0r[s] = ld16(k0 + 32 * s);
-        k1r[s] = ld16(k1 + 32 * s);
+        kr[c][0][s] = ld16(k0 + 32 * s);
+        kr[c][1][s] = ld16(k1 + 32 * s);
       }
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        v0r[n] = *reinterpret_cast<const uint2*>(v0 + 16 * n * BS);
-        v1r[n] = *reinterpret_cast<const uint2*>(v1 + 16 * n * BS);
+        vr[c][0][n] = *reinterpret_cast<const uint2*>(v0 + 16 * n * BS);
+        vr[c][1][n] = *reinterpret_cast<const uint2*>(v1 + 16 * n * BS);
       }
     }
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0r[s]), qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1r[s]), qf[s], s1, 0, 0, 0);
-    }
-    // scores for row rl: keys kb + 4g + r (s0) and kb + 16 + 4g + r (s1)
-    float p[8];
+    for (int c = 0; c < CH; ++c) {
+      const int kc = kb + 32 * c;
+      if (kc >= k_end) break;  // wave-uniform
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int key0 = kb + 4 * g + q, key1 = kb + 16 + 4 * g + q;
-      p[q] = (key0 < row_lim && key0 < k_end) ? s0[q] * a.scale_log2 : -INFINITY;
-      p[4 + q] = (key1 < row_lim && key1 < k_end) ? s1[q] * a.scale_log2 : -INFINITY;
-    }
-    float mloc = -INFINITY;
+      for (int s = 0; s < KSTEPS; ++s) {
+        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kr[c][0][s]), qf[s], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kr[c][1][s]), qf[s], s1, 0, 0, 0);
+      }
+      // scores for row rl: keys kc + 4g + r (s0) and kc + 16 + 4g + r (s1)
+      float p[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mloc = fmaxf(mloc, p[j]);
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m_run, mloc);
-    const float m_safe = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_safe);
-    float lsum = 0.f;
+      for (int q = 0; q < 4; ++q) {
+        const int key0 = kc + 4 * g + q, key1 = kc + 16 + 4 * g + q;
+        p[q] = (key0 < row_lim && key0 < k_end) ? s0[q] * a.scale_log2 : -INFINITY;
+        p[4 + q] = (key1 < row_lim && key1 < k_end) ? s1[q] * a.scale_log2 : -INFINITY;
+      }
+      float mloc = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { p[j] = exp2f(p[j] - m_safe); lsum += p[j]; }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    l_run = l_run * alpha + lsum;
-    m_run = m_new;
-    const bf16x8 pf = __builtin_bit_cast(bf16x8, pack8(p));
+      for (int j = 0; j < 8; ++j) mloc = fmaxf(mloc, p[j]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run, mloc);
+      const float m_safe = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_safe);
+      float lsum = 0.f;
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      acc[n] *= alpha;
-      const uint4 vv = make_uint4(v0r[n].x, v0r[n].y, v1r[n].x, v1r[n].y);
-      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, acc[n], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) { p[j] = exp2f(p[j] - m_safe); lsum += p[j]; }
+      lsum += __shfl_xor(lsum, 16, 64);
+      lsum += __shfl_xor(lsum, 32, 64);
+      l_run = l_run * alpha + lsum;
+      m_run = m_new;
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, pack8(p));
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        acc[n] *= alpha;
+        const uint4 vv = make_uint4(vr[c][0][n].x, vr[c][0][n].y, vr[c][1][n].x, vr[c][1][n].y);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, acc[n], 0, 0, 0);
+      }
     }
   }
 
@@ -317,7 +327,11 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
 
 template <int D, int W>
 void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
-  hipLaunchKernelGGL((paged_attn_kernel<D, W>), grid, dim3(64 * W), 0, stream, a);
+  static const int ch = [] { const char* e = getenv("DLLM_ATTN_CH"); return e ? atoi(e) : 1; }();
+  if (ch == 2)
+    hipLaunchKernelGGL((paged_attn_kernel<D, W, 2>), grid, dim3(64 * W), 0, stream, a);
+  else
+    hipLaunchKernelGGL((paged_attn_kernel<D, W, 1>), grid, dim3(64 * W), 0, stream, a);
 }
 }  // namespace
 
