@@ -26,6 +26,7 @@ answers = skipped work); small tier greedy (reference Nano), large tier Ollama-d
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
 import statistics
@@ -54,6 +55,8 @@ def parse():
     ap.add_argument("--kv-gb", type=float, default=64.0)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (tiny model)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: turn pipelining (replicated topology): conversations advance independently")
     return ap.parse_args()
 
 
@@ -62,12 +65,11 @@ class Conversations:
         from distributed_llm_amd.bench.query_sets import normalize_query_set, query_sets
         self.sets = [normalize_query_set(query_sets[k]) for k in ("general_knowledge", "technical_coding",
                                                                   "personal_health")]
-        self.rank, self.sessions = rank, 0
+        self.rank, self._ids = rank, itertools.count(1)   # next() is atomic: safe from worker threads
         self.convs = [self._new(i) for i in range(n)]
 
     def _new(self, i):
-        self.sessions += 1
-        return {"set": self.sets[i % 3], "turn": 0, "hist": [], "tag": f"[session r{self.rank}-{self.sessions}] "}
+        return {"set": self.sets[i % 3], "turn": 0, "hist": [], "tag": f"[session r{self.rank}-{next(self._ids)}] "}
 
     def step(self, router, records=None):
         hs = []
@@ -90,6 +92,75 @@ class Conversations:
             c["turn"] += 1
             if c["turn"] >= len(c["set"]):
                 self.convs[i] = self._new(i)
+
+
+class PipelinedConversations(Conversations):
+    """Turn pipelining: one thread per conversation runs route -> serve -> next turn on its own.
+
+    Each conversation stays strictly sequential (turn t+1 is built from turn t's answer, as in
+    the reference harness, routing_chatbot_tester.py:405-486), but conversations no longer wait
+    for each other: a conversation whose small-tier answer (<= 128 tokens) is done submits its
+    next turn while large-tier answers (<= 384 tokens) are still decoding, so the engine's decode
+    batch stays full instead of draining to the large-tier share at the end of every step.
+
+    Steady-state accounting: with no per-step barrier a *step* is ``n_convs`` completed turns
+    (one turn per conversation on average).  ``start()`` launches the workers; ``wait_turns(n)``
+    blocks until ``n`` turns in total have completed.  Only turns that complete inside the timed
+    window are recorded and counted (a turn in flight at the window's end is not counted; one in
+    flight at its start is counted whole), so no work is skipped or double counted."""
+
+    def start(self, router) -> None:
+        import threading
+        self._cv = threading.Condition()
+        self.completed = 0
+        self.records = None
+        self._stop = False
+        self.errors = []
+
+        def worker(i):
+            try:
+                while not self._stop:
+                    c = self.convs[i]
+                    q = c["set"][c["turn"]].text
+                    if c["turn"] == 0:
+                        q = c["tag"] + q
+                    c["hist"].append({"role": "user", "content": q})
+                    payload, ntok, device = router.route_concurrent(c["hist"])
+                    c["hist"].append({"role": "assistant", "content": payload["response"]})
+                    raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
+                    rec = {"lat": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
+                           "ovh": float(payload.get("routing_overhead_ms", 0.0)),
+                           "ttft": float((raw.get("timing") or {}).get("ttft_ms", 0.0))}
+                    c["turn"] += 1
+                    if c["turn"] >= len(c["set"]):
+                        self.convs[i] = self._new(i)
+                    with self._cv:
+                        if self.records is not None:
+                            self.records.append(rec)
+                        self.completed += 1
+                        self._cv.notify_all()
+            except BaseException as e:  # surfaced by wait_turns
+                with self._cv:
+                    self.errors.append(e)
+                    self._cv.notify_all()
+
+        self._threads = [threading.Thread(target=worker, args=(i,), daemon=True) for i in range(len(self.convs))]
+        for t in self._threads:
+            t.start()
+
+    def wait_turns(self, n: int, records=None) -> None:
+        """Block until ``n`` turns have completed in total; from then on record into ``records``."""
+        with self._cv:
+            while self.completed < n and not self.errors:
+                self._cv.wait()
+            if self.errors:
+                raise self.errors[0]
+            self.records = records
+
+    def stop(self) -> None:
+        self._stop = True            # workers exit after their in-flight turn
+        for t in self._threads:
+            t.join()
 
 
 def main() -> int:
@@ -170,19 +241,48 @@ def main() -> int:
         pools_for_router = cluster.router_pools() if cluster is not None else pools
         router = Router(strategy=a.strategy, config=cfg, threshold_fallback=a.threshold, benchmark_mode=False,
                         pools=pools_for_router)
-        convs = Conversations(n_convs, rank)
-        for _ in range(a.warmup):
-            convs.step(router)
-        st0 = [dict(e.stats()) for e in engines]
-        sync()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            convs.step(router, records)
-        sync()
-        elapsed = time.perf_counter() - t0
-        st1 = [dict(e.stats()) for e in engines]
+        pipelined = bool(a.pipeline) and cluster is None
+        if pipelined:
+            for e in engines:
+                e.start()              # background step loop: callers only enqueue and wait
+            convs = PipelinedConversations(n_convs, rank)
+            convs.start(router)
+            convs.wait_turns(a.warmup * n_convs)
+        else:
+            convs = Conversations(n_convs, rank)
+            for _ in range(a.warmup):
+                convs.step(router)
+        if pipelined:
+            # steady-state window: the turns completing from here on are the timed ones
+            if world > 1:
+                dist.barrier()         # replicas open their windows together
+            with convs._cv:
+                st0 = [dict(e.stats()) for e in engines]
+                if on_gpu:
+                    torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                convs.records = records
+            convs.wait_turns((a.warmup + a.steps) * n_convs)
+            with convs._cv:
+                convs.records = None
+                if on_gpu:
+                    torch.cuda.synchronize()
+                elapsed = time.perf_counter() - t0
+                st1 = [dict(e.stats()) for e in engines]
+            convs.stop()
+        else:
+            st0 = [dict(e.stats()) for e in engines]
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                convs.step(router, records)
+            sync()
+            elapsed = time.perf_counter() - t0
+            st1 = [dict(e.stats()) for e in engines]
         if cluster is not None:
             cluster.shutdown()
+        for e in engines:
+            e.stop()
         tokens = sum(r["tok"] for r in records)
     lats = sorted(r["lat"] for r in records)
     if world > 1:
@@ -217,6 +317,7 @@ def main() -> int:
             "config": {"model": model_desc, "global_batch": a.convs * world,
                        "seq_len": "growing conversation (<=16384)", "parallelism": parallelism,
                        "strategy": a.strategy, "semantic_cache": True, "response_cache": False,
+                       "turn_pipelining": bool(a.pipeline) and topology == "replicated",
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
             "p50_latency_ms": round(statistics.median(lats), 1) if lats else None,
             "p90_latency_ms": round(pct(0.9), 1),
@@ -227,6 +328,10 @@ def main() -> int:
             "routing_overhead_ms_mean": round(statistics.mean(r["ovh"] for r in records), 3) if records else None,
             "ttft_ms_p50": round(statistics.median(r["ttft"] for r in records), 1) if records else None,
             "prefix_cache_hit_rate": round(hits / max(1, prompt), 3),
+            "engine_decode_tok_s": round(sum(b["decode_tokens"] - a_["decode_tokens"] for a_, b in zip(st0, st1))
+                                         / max(elapsed_max, 1e-9), 1),
+            "avg_decode_batch": round(sum(b["decode_tokens"] - a_["decode_tokens"] for a_, b in zip(st0, st1))
+                                      / max(1, sum(b["decode"] - a_["decode"] for a_, b in zip(st0, st1))), 1),
             "engine_time_split_s": {k: round(sum(b_.get(k, 0.0) - a_.get(k, 0.0) for a_, b_ in zip(st0, st1)), 3)
                                     for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
                                               "t_decode_host_post_s")},

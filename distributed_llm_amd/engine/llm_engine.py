@@ -113,7 +113,10 @@ class LLMEngine:
         self._lock = threading.Lock()          # held by the thread currently driving the step loop
         self._inbox: List[_Seq] = []            # submitted, not yet seen by the driver
         self._inbox_lock = threading.Lock()
+        self._inbox_cv = threading.Condition(self._inbox_lock)
         self._driving = False
+        self._bg: Optional[threading.Thread] = None   # background step-loop thread (start())
+        self._bg_stop = False
         self._active: List[_Seq] = []
         self._memo: "OrderedDict[str, List[int]]" = OrderedDict()
         self._memo_cap = 200_000
@@ -286,9 +289,10 @@ class LLMEngine:
             return
         with self._inbox_lock:
             self._inbox.extend(seqs)
-            lead = not self._driving
+            lead = not self._driving    # always False while a background loop owns the driver role
             if lead:
                 self._driving = True
+            self._inbox_cv.notify()
         if lead:
             with self._lock:
                 try:
@@ -303,7 +307,7 @@ class LLMEngine:
         """A failed step must not strand followers: fail every admitted/queued sequence."""
         with self._inbox_lock:
             pending, self._inbox = self._inbox, []
-            self._driving = False
+            self._driving = self._bg is not None
         for s in pending + list(self._active):
             if not s.done.is_set():
                 s.error = s.error or why
@@ -322,9 +326,60 @@ class LLMEngine:
     def _take_inbox(self, final: bool) -> List[_Seq]:
         with self._inbox_lock:
             new, self._inbox = self._inbox, []
-            if final and not new:
+            if final and not new and self._bg is None:
                 self._driving = False   # atomically with the empty check: no submission is lost
         return new
+
+    # ------------------------------------------------------------------ background serving loop
+    def start(self) -> "LLMEngine":
+        """Serve from a dedicated step-loop thread (server mode).
+
+        Leader/follower driving (``_submit_and_wait``) makes the first caller run the loop until
+        the engine drains, so under a continuous stream of requests that caller's own request is
+        held back until every other caller is done.  With a background loop callers only enqueue
+        and wait for THEIR sequences: a conversation can submit its next turn while the rest of
+        the batch is still decoding (turn pipelining, bench.py --pipeline)."""
+        if self.par.enabled:
+            return self   # TP ranks run the leader's batches in lockstep (parallel.cluster)
+        with self._inbox_lock:
+            if self._bg is not None:
+                return self
+            if self._driving:
+                raise RuntimeError("start() while a caller is driving the step loop")
+            self._bg_stop = False
+            self._driving = True          # the loop thread owns the driver role from now on
+            self._bg = threading.Thread(target=self._bg_loop, name=f"dllm-engine-{self.cfg.name}",
+                                        daemon=True)
+            self._bg.start()
+        return self
+
+    def stop(self, timeout: float = 60.0) -> None:
+        """Finish queued work, then end the background loop (callers drive again afterwards)."""
+        with self._inbox_lock:
+            t = self._bg
+            if t is None:
+                return
+            self._bg_stop = True
+            self._inbox_cv.notify_all()
+        t.join(timeout)
+        with self._inbox_lock:
+            self._bg = None
+            self._driving = False
+
+    def _bg_loop(self) -> None:
+        if self.on_gpu:
+            torch.cuda.set_device(self.device)
+        while True:
+            with self._inbox_lock:
+                while not self._inbox and not self._bg_stop:
+                    self._inbox_cv.wait()
+                if not self._inbox and self._bg_stop:
+                    return
+            with self._lock:
+                try:
+                    self._run([])
+                except BaseException as e:  # fail the affected requests, keep serving
+                    self._abort_all(f"engine step failed: {e!r}")
 
     def stats(self) -> Dict[str, object]:
         st = dict(self.bm.stats())

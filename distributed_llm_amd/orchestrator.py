@@ -254,6 +254,50 @@ class Router:
             results[i] = self._finish(query, dec, raw, which, lat, failed.get(i))
         return results
 
+    # ------------------------------------------------------------------ turn pipelining
+    def _decide_batch(self, histories: Sequence[List[Dict[str, Any]]]) -> List[Tuple[str, Any, Any]]:
+        """Routing half of ``route_batch``: ("hit", payload, None) for a response-cache hit,
+        else ("route", query, decision)."""
+        self._prefetch_embeddings([self._split(h)[0] for h in histories])
+        out: List[Tuple[str, Any, Any]] = []
+        for h in histories:
+            query, context, ctx_hash = self._split(h)
+            hit = self._cached_payload(query)
+            if hit is not None:
+                out.append(("hit", hit, None))
+            else:
+                out.append(("route", query, self._decide(query, context, ctx_hash, h)))
+        return out
+
+    def route_concurrent(self, conversation_history: List[Dict[str, Any]]):
+        """``route_query`` for many concurrent callers (one thread per conversation).
+
+        Routing decisions of callers that arrive while a decision batch is in flight are made
+        together (one batched encoder forward, ``pools.base.Coalescer``); each request is then
+        served on its own, so with an engine running its background loop (``LLMEngine.start``)
+        it joins the running continuous batch and its caller resumes as soon as ITS answer is
+        done — no conversation waits for another conversation's generation (unlike
+        ``route_batch``, whose callers all wait for the slowest member of the batch)."""
+        with self._lock:
+            dc = getattr(self, "_decider", None)
+            if dc is None:
+                from .pools.base import Coalescer
+                dc = self._decider = Coalescer(self._decide_batch)
+        kind, a, dec = dc.submit([conversation_history])[0]
+        if kind == "hit":
+            return a
+        query = a
+        raw, which, lat = self._run(dec["device"], conversation_history)
+        failed = None
+        if self.enable_failover and is_error(raw):
+            raw2, which2, lat2 = self._run(other_tier(which), conversation_history)
+            if not is_error(raw2):
+                failed = which
+                raw, which, lat = raw2, which2, lat2
+        if isinstance(raw, dict) and "latency_ms" in raw:
+            lat = float(raw["latency_ms"])
+        return self._finish(query, dec, raw, which, lat, failed)
+
     def _prefetch_embeddings(self, queries: List[str]) -> None:
         """One batched encoder forward for every query of a batch (fills the embedder's memo, so
         the semantic router and the semantic cache do no per-query encoder launches)."""

@@ -87,3 +87,60 @@ def test_coalescer_propagates_errors():
 
     with pytest.raises(ValueError):
         Coalescer(fn).submit([1])
+
+
+def test_background_loop_serves_staggered_callers():
+    """Server mode (LLMEngine.start): a caller returns as soon as ITS request is done, while a
+    longer request keeps decoding; results equal the leader-driven engine's."""
+    eng = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=16, seed=0)
+    short = SamplingParams(max_new_tokens=4, temperature=0.0, ignore_eos=True)
+    long_ = SamplingParams(max_new_tokens=40, temperature=0.0, ignore_eos=True)
+    p_short, p_long = "user: short one\nassistant: ", "user: a long answer please\nassistant: "
+    ref_short = eng.generate([p_short], short)[0].token_ids
+    ref_long = eng.generate([p_long], long_)[0].token_ids
+    eng.start()
+    try:
+        out, done_at = {}, {}
+
+        def call(name, p, sp):
+            out[name] = eng.generate([p], sp)[0]
+            done_at[name] = time.perf_counter()
+
+        tl = threading.Thread(target=call, args=("long", p_long, long_))
+        tl.start()
+        time.sleep(0.05)
+        ts = threading.Thread(target=call, args=("short", p_short, short))
+        ts.start()
+        ts.join(timeout=120)
+        tl.join(timeout=120)
+        assert out["short"].token_ids == ref_short and out["long"].token_ids == ref_long
+        assert done_at["short"] < done_at["long"]     # the short caller was not held by the long one
+        assert eng._driving and eng._bg is not None
+    finally:
+        eng.stop()
+    assert not eng._driving and eng._bg is None
+    assert eng.generate([p_short], short)[0].token_ids == ref_short   # leader mode again
+
+
+def test_route_concurrent_matches_route_query():
+    from distributed_llm_amd.config import BENCHMARK_CFG, LARGE, SMALL
+    from distributed_llm_amd.orchestrator import Router
+    from distributed_llm_amd.pools.base import EchoPool
+    pools = {SMALL: EchoPool(SMALL), LARGE: EchoPool(LARGE, tokens_per_reply=48)}
+    a = Router("heuristic", config=dict(BENCHMARK_CFG), pools=pools)
+    b = Router("heuristic", config=dict(BENCHMARK_CFG), pools=pools)
+    hs = [[{"role": "user", "content": q}] for q in ("Thank you!", "Write a Python function for knapsack",
+                                                      "what is 2+2", "Compare TCP versus UDP")]
+    ref = [a.route_query(h) for h in hs]
+    got = [None] * len(hs)
+
+    def call(i):
+        got[i] = b.route_concurrent(hs[i])
+
+    th = [threading.Thread(target=call, args=(i,)) for i in range(len(hs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    for (p1, t1, d1), (p2, t2, d2) in zip(ref, got):
+        assert (p1["response"], t1, d1, p1["routing_method"]) == (p2["response"], t2, d2, p2["routing_method"])
