@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--small-model", default="llama-3.2-1b")
     ap.add_argument("--large-model", default="llama-3-8b")
     ap.add_argument("--large-tp", type=int, default=None)
-    ap.add_argument("--convs", type=int, default=256, help="concurrent conversations per GPU")
+    ap.add_argument("--convs", type=int, default=512, help="concurrent conversations per GPU")
     ap.add_argument("--strategy", default="hybrid")
     ap.add_argument("--threshold", type=int, default=1000)
     ap.add_argument("--small-new", type=int, default=128)
