@@ -23,6 +23,8 @@ int dllm_scatter_pairs(int*, const int*, int, hipStream_t);
 int dllm_argmax(const void*, long, int, int, int, int*, hipStream_t);
 int dllm_sample_topp(const float*, const long*, int, int, const float*, const float*, const float*, int*, hipStream_t);
 int dllm_cosine_scores(const float*, const float*, float*, int, int, int, hipStream_t);
+int dllm_sample_rows(const void*, long, int, int, const float*, const float*, const int*, const unsigned*, int*,
+                     hipStream_t);
 int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                      hipStream_t);
 int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
@@ -253,6 +255,28 @@ void sample_topp(torch::Tensor vals, torch::Tensor idx, torch::Tensor temp, torc
      "sample_topp");
 }
 
+// Fused per-row sampler: temp <= 0 -> arg-max; else exact top-k (k <= 256; 0 -> 256), temperature,
+// top-p and an inverse-CDF draw with u = hash(seed, row).  seed: int32 device scalar.
+void sample_rows(torch::Tensor logits, torch::Tensor temp, torch::Tensor top_p, torch::Tensor top_k,
+                 torch::Tensor seed, torch::Tensor out) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0,
+              "logits [B, V] row-major, 16-B aligned rows");
+  check_f32(temp, "temperature");
+  check_f32(top_p, "top_p");
+  check_i32(top_k, "top_k");
+  check_i32(seed, "seed");
+  check_i32(out, "out");
+  const int B = logits.size(0);
+  TORCH_CHECK(temp.numel() >= B && top_p.numel() >= B && top_k.numel() >= B && out.numel() >= B &&
+                  seed.numel() >= 1,
+              "per-row parameter lengths");
+  ok(dllm_sample_rows(logits.data_ptr(), logits.stride(0), B, logits.size(1), temp.data_ptr<float>(),
+                      top_p.data_ptr<float>(), top_k.data_ptr<int>(), (const unsigned*)seed.data_ptr<int>(),
+                      out.data_ptr<int>(), stream()),
+     "sample_rows");
+}
+
 void cosine_scores(torch::Tensor q, torch::Tensor c, torch::Tensor s) {
   check_f32(q, "q");
   check_f32(c, "c");
@@ -426,6 +450,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("argmax", &argmax);
   m.def("scatter_pairs", &scatter_pairs);
   m.def("sample_topp", &sample_topp);
+  m.def("sample_rows", &sample_rows);
   m.def("cosine_scores", &cosine_scores);
   m.def("masked_cosine_argmax", &masked_cosine_argmax);
   m.def("skinny_gemm", &skinny_gemm);

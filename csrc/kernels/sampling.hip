@@ -4,6 +4,10 @@
 //   sample_topp_kernel : temperature + top-p (nucleus) sampling over the row's top-K candidates
 //                        (values sorted descending, from a top-k pass), one wave per row,
 //                        inverse-CDF draw with a per-row uniform u in [0,1).
+//   sample_rows_kernel : the whole sampler for one decode step in ONE launch (graph-captured):
+//                        per row, greedy -> arg-max, else exact top-k of the bf16 logits, then
+//                        temperature, nucleus cut and inverse-CDF draw — no torch.topk kernel
+//                        chain, no second LM-head GEMM, no host round trip for sampled rows.
 #include "common.h"
 
 namespace {
@@ -88,7 +92,246 @@ __global__ void sample_topp_kernel(const float* __restrict__ vals, const long* _
     out[row] = (int)idx[(long)row * K + pick];
   }
 }
+// ---------------------------------------------------------------------------- fused row sampler
+// Exact top-k (k <= 256) without sorting 32 K logits:
+//   1. histogram of the 12 high bits of a monotonic 16-bit key of each bf16 logit (LDS atomics;
+//      3 mantissa bits per bin keep same-address conflicts low), a block-wide scan from the top
+//      finds the bin holding the k-th largest; if that bin is crowded (> SR_MAXN candidates) a
+//      second 16-bin pass over its low 4 bits pins the exact threshold key;
+//   2. every logit at or above the threshold is appended to an LDS candidate list;
+//   3. rank of each candidate = #candidates strictly better (value desc, index asc: the same tie
+//      rule as torch.argmax), an O(n^2) LDS-broadcast pass — no sort; ranks < k are the top-k,
+//      written in rank order;
+//   4. wave 0: softmax weights at temperature t, inclusive prefix sums in rank order (wave scan),
+//      nucleus = shortest prefix with mass >= top_p, inverse-CDF pick with u = hash(seed, row).
+constexpr int SR_THREADS = 256;
+constexpr int SR_CAP = 1024;   // candidate list capacity (ties beyond it at the threshold are dropped)
+constexpr int SR_MAXN = 512;   // above this many candidates the exact-threshold pass runs
+constexpr int SR_KMAX = 256;
+
+static __device__ __forceinline__ unsigned bf_key(u16 b) {
+  if ((b & 0x7f80) == 0x7f80 && (b & 0x7f)) return 0u;  // NaN: never selected
+  return (b & 0x8000) ? (unsigned)(~b & 0xffff) : (unsigned)(b | 0x8000);
+}
+
+static __device__ __forceinline__ float key_f(unsigned k) {
+  return bf2f((k & 0x8000) ? (u16)(k & 0x7fff) : (u16)(~k & 0xffff));
+}
+
+// counter-based uniform in [0, 1): identical on host (ops.reference.row_uniform)
+static __device__ __forceinline__ float row_uniform(unsigned seed, unsigned row) {
+  unsigned h = seed + row * 0x9E3779B9u;
+  h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+__global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __restrict__ logits, long stride, int V,
+                                                                 const float* __restrict__ temp,
+                                                                 const float* __restrict__ top_p,
+                                                                 const int* __restrict__ top_k,
+                                                                 const unsigned* __restrict__ seed,
+                                                                 int* __restrict__ out) {
+  __shared__ unsigned hist[4096];
+  __shared__ float2 cand[SR_CAP];          // (value, index bits)
+  __shared__ float w_r[SR_KMAX];           // softmax weight by rank
+  __shared__ int i_r[SR_KMAX];             // token id by rank
+  __shared__ unsigned wsum[SR_THREADS / 64];
+  __shared__ float sv[SR_THREADS / 64];
+  __shared__ int si[SR_THREADS / 64];
+  __shared__ int s_bin, s_above, s_n, s_lo;
+  __shared__ float s_m;
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const u16* l = logits + (long)row * stride;
+  const int nv = V >> 3;
+  const float t = temp[row];
+
+  if (!(t > 0.f)) {  // greedy row: arg-max, ties -> lowest index
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = tid; c < nv; c += SR_THREADS) {
+      float f[8];
+      unpack8(ld16(l + c * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) better(bv, bi, f[j], c * 8 + j);
+    }
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) better(bv, bi, bf2f(l[i]), i);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      better(bv, bi, ov, oi);
+    }
+    if (lane == 0) { sv[wid] = bv; si[wid] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < SR_THREADS / 64; ++w) better(bv, bi, sv[w], si[w]);
+      out[row] = (bi == 0x7fffffff) ? 0 : bi;
+    }
+    return;
+  }
+  int k = top_k[row];
+  if (k <= 0 || k > SR_KMAX) k = SR_KMAX;
+  if (k > V) k = V;
+
+  // ---- 1. coarse histogram (12-bit bins) and the bin of the k-th largest
+  for (int i = tid; i < 4096; i += SR_THREADS) hist[i] = 0u;
+  __syncthreads();
+  for (int c = tid; c < nv; c += SR_THREADS) {
+    const uint4 v = ld16(l + c * 8);
+    const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&hist[bf_key(e[j]) >> 4], 1u);
+  }
+  for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) atomicAdd(&hist[bf_key(l[i]) >> 4], 1u);
+  __syncthreads();
+  unsigned mine = 0;  // thread t owns bins 4095-16t .. 4080-16t (descending key order)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) mine += hist[4095 - 16 * tid - j];
+  unsigned x = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  unsigned base = 0;
+  for (int w = 0; w < wid; ++w) base += wsum[w];
+  const unsigned incl = base + x, excl = incl - mine;
+  if (excl < (unsigned)k && incl >= (unsigned)k) {  // exactly one thread
+    unsigned acc = excl;
+    for (int j = 0; j < 16; ++j) {
+      const int b = 4095 - 16 * tid - j;
+      if (acc + hist[b] >= (unsigned)k) { s_bin = b; s_above = (int)acc; break; }
+      acc += hist[b];
+    }
+  }
+  __syncthreads();
+  const int bin = s_bin;
+  if (s_above + (int)hist[bin] > SR_MAXN) {  // crowded bin: exact threshold from its low 4 bits
+    __syncthreads();
+    if (tid < 16) hist[tid] = 0u;            // hist[0..15] re-used as the 16 fine bins (the coarse
+    __syncthreads();                         // counts are no longer needed past this point)
+    for (int c = tid; c < nv; c += SR_THREADS) {
+      const uint4 v = ld16(l + c * 8);
+      const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned key = bf_key(e[j]);
+        if ((int)(key >> 4) == bin) atomicAdd(&hist[key & 15], 1u);
+      }
+    }
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
+      const unsigned key = bf_key(l[i]);
+      if ((int)(key >> 4) == bin) atomicAdd(&hist[key & 15], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned acc = (unsigned)s_above;
+      int lo = bin << 4;
+      for (int b = 15; b >= 0; --b) {
+        if (acc + hist[b] >= (unsigned)k) { lo = (bin << 4) | b; break; }
+        acc += hist[b];
+      }
+      s_lo = lo;
+    }
+  } else if (tid == 0) {
+    s_lo = bin << 4;
+  }
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+
+  // ---- 2. candidates: every logit at or above the threshold key
+  const unsigned lo = (unsigned)s_lo;
+  for (int c = tid; c < nv; c += SR_THREADS) {
+    const uint4 v = ld16(l + c * 8);
+    const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned key = bf_key(e[j]);
+      if (key >= lo) {
+        const int p = atomicAdd(&s_n, 1);
+        if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+      }
+    }
+  }
+  for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
+    const unsigned key = bf_key(l[i]);
+    if (key >= lo) {
+      const int p = atomicAdd(&s_n, 1);
+      if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(i));
+    }
+  }
+  __syncthreads();
+  const int n = min(s_n, SR_CAP);
+
+  // ---- 3. rank = #strictly better candidates; ranks < k are the top-k
+  for (int j = tid; j < n; j += SR_THREADS) {
+    const float2 cj = cand[j];
+    const int ij = __float_as_int(cj.y);
+    int r = 0;
+    for (int i = 0; i < n; ++i) {
+      const float2 ci = cand[i];
+      r += (ci.x > cj.x || (ci.x == cj.x && __float_as_int(ci.y) < ij)) ? 1 : 0;
+    }
+    if (r < k) { i_r[r] = ij; w_r[r] = cj.x; }
+    if (r == 0) s_m = cj.x;
+  }
+  __syncthreads();
+
+  // ---- 4. temperature, nucleus, draw (wave 0; rank r = 4 * lane + q)
+  if (wid == 0) {
+    const int kk = min(k, n);
+    const float m = s_m, it = 1.f / fmaxf(t, 1e-5f);
+    float c4[4];
+    float run = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 4 * lane + q;
+      run += r < kk ? __expf((w_r[r] - m) * it) : 0.f;
+      c4[q] = run;                                  // lane-local inclusive prefix
+    }
+    float pre = run;                                // wave exclusive scan of lane totals
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float y = __shfl_up(pre, o, 64);
+      if (lane >= o) pre += y;
+    }
+    pre -= run;
+    const float s = __shfl(pre + run, 63, 64);      // total mass of the top-k
+    const float tp = top_p[row] * s;
+    int cut = kk;                                   // nucleus size = first rank with cum >= top_p, + 1
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 4 * lane + q;
+      if (r < kk && pre + c4[q] >= tp) cut = min(cut, r + 1);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cut = min(cut, __shfl_xor(cut, o, 64));
+    const int last = cut - 1;
+    const float mass = __shfl(pre + c4[last & 3], last >> 2, 64);
+    const float target = row_uniform(*seed, (unsigned)row) * mass;
+    int pick = last;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 4 * lane + q;
+      if (r < cut && pre + c4[q] > target) pick = min(pick, r);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pick = min(pick, __shfl_xor(pick, o, 64));
+    if (lane == 0) out[row] = i_r[pick];
+  }
+}
 }  // namespace
+
+extern "C" int dllm_sample_rows(const void* logits, long stride, int B, int V, const float* temp, const float* top_p,
+                                const int* top_k, const unsigned* seed, int* out, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (V <= 0 || stride % 8 != 0) return -1;
+  hipLaunchKernelGGL(sample_rows_kernel, dim3(B), dim3(SR_THREADS), 0, stream, (const u16*)logits, stride, V, temp,
+                     top_p, top_k, seed, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dllm_argmax(const void* logits, long stride, int B, int V, int is_bf16, int* out, hipStream_t stream) {
   if (B <= 0) return 0;

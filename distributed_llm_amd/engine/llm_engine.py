@@ -9,8 +9,8 @@ Replaces the reference's external Ollama/llama.cpp engine (the hot
   * decode runner — each running sequence owns a ROW of persistent per-row metadata
     (block table row, context length) on the device; a decode step uploads ONE small packed
     int32 buffer and replays a hipGraph captured for the batch-size bucket (model forward +
-    greedy arg-max), so the host cost per step is O(batch) numpy work + one memcpy + one
-    graph launch;
+    LM head + the fused per-row sampler: arg-max or top-k/top-p, ops.sample_rows), so the host
+    cost per step is O(batch) numpy work + one memcpy + one graph launch + one token read-back;
   * prefill runner — eager (shapes vary), packed variable-length batch, attention over the
     cached prefix + new tokens with the same paged kernel.
 KV memory is sized for 288 GB HBM3E parts: ``kv_cache_gb`` (default: 60 % of free memory).
@@ -125,6 +125,7 @@ class LLMEngine:
         self.use_graphs = use_graphs and self.on_gpu
         self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
         self._gen.manual_seed(seed + 1)
+        self._seed_base = (seed * 0x9E3779B1 + 0x5851F42D) & 0x7FFFFFFF
         self._init_rows()
         if self.on_gpu:
             self._autotune()
@@ -162,14 +163,28 @@ class LLMEngine:
         self.buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if b < R] + [R]
         mb = self.buckets[-1]
         # packed decode buffer: ids | pos | slots | tile_seq  (mb each) | qstart | qlen | ctx (R+1 each)
-        #                       | attention split length | block-table updates [n, (flat idx, block) * R]
-        self._dec_n = 4 * mb + 3 * (R + 1) + 1 + 1 + 2 * R
+        #                       | attention split length
+        #                       | sampler: temperature, top_p (f32 bits), top_k (mb each) | seed
+        #                       | block-table updates [n, (flat idx, block) * R]
+        s0 = 4 * mb + 3 * (R + 1) + 1
+        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1), 4 * mb + 3 * (R + 1),
+             s0 + 3 * mb + 1]
+        self._dec_n = o[8] + 1 + 2 * R
         self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
         self.dec_host_t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
         self.dec_host = self.dec_host_t.numpy()
-        o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1), 4 * mb + 3 * (R + 1),
-             4 * mb + 3 * (R + 1) + 1]
+        self.dec_host_f = self.dec_host.view(np.float32)
         self._off = o
+        self._so = s0
+        # the whole sampler runs inside the decode graph (ops.sample_rows) unless the vocab is
+        # tensor-parallel (then the distributed arg-max / top-k of LlamaModel is used)
+        self.fused_sampler = self.par.tp_size == 1 and os.environ.get("DLLM_FUSED_SAMPLER", "1") == "1"
+        self._seed_ctr = 0
+        dv = self.dec_dev
+        self.d_temp = dv[s0:s0 + mb].view(torch.float32)
+        self.d_topp = dv[s0 + mb:s0 + 2 * mb].view(torch.float32)
+        self.d_topk = dv[s0 + 2 * mb:s0 + 3 * mb]
+        self.d_seed = dv[s0 + 3 * mb:s0 + 3 * mb + 1]
         self.d_split = self.dec_dev[o[7]:o[7] + 1]
         self.d_upd = self.dec_dev[o[8]:]
         d = self.dec_dev
@@ -478,9 +493,31 @@ class LLMEngine:
             self._bt_upd.clear()
 
     # ------------------------------------------------------------------ sampling
+    def _next_seed(self) -> int:
+        self._seed_ctr += 1
+        return (self._seed_ctr * 0x2545F491 + self._seed_base) & 0x7FFFFFFF
+
+    def _fill_sampler(self, h: np.ndarray, hf: np.ndarray, base: int, stride: int, seqs: List[_Seq], pad: int) -> None:
+        """Per-row sampler parameters into a packed int32 buffer: temperature | top_p | top_k
+        (``stride`` apart) and the step seed; rows [len(seqs), pad) are greedy padding."""
+        n = len(seqs)
+        ps = [s.params for s in seqs]
+        hf[base:base + n] = np.fromiter((p.temperature for p in ps), dtype=np.float32, count=n)
+        hf[base + stride:base + stride + n] = np.fromiter((p.top_p for p in ps), dtype=np.float32, count=n)
+        h[base + 2 * stride:base + 2 * stride + n] = np.fromiter((p.top_k for p in ps), dtype=np.int32, count=n)
+        if pad > n:
+            hf[base + n:base + pad] = 0.0
+        h[base + 3 * stride] = self._next_seed()
+
     def _sample(self, hidden: torch.Tensor, seqs: List[_Seq], greedy_ids: Optional[torch.Tensor]) -> List[int]:
         n = len(seqs)
         dev = hidden.device
+        if self.fused_sampler:   # one launch: arg-max / top-k / top-p per row
+            buf = np.zeros(3 * n + 1, dtype=np.int32)
+            self._fill_sampler(buf, buf.view(np.float32), 0, n, seqs, n)
+            t = torch.from_numpy(buf).to(dev, non_blocking=True)
+            return ops.sample_rows(self.model.logits(hidden[:n]), t[:n].view(torch.float32),
+                                   t[n:2 * n].view(torch.float32), t[2 * n:3 * n], t[3 * n:]).tolist()
         ids = greedy_ids[:n] if greedy_ids is not None else self.model.greedy(hidden[:n])
         sampled = [i for i, s in enumerate(seqs) if not s.params.greedy]
         if not sampled:
@@ -605,6 +642,8 @@ class LLMEngine:
         h[o[6] + rows] = lens
         self._sync_bt()
         h[o[7]] = self._split_len(int(lens.sum()))
+        if self.fused_sampler:
+            self._fill_sampler(h, self.dec_host_f, self._so, self.buckets[-1], running, bs)
         nu = len(self._bt_upd) // 2
         h[o[8]] = nu
         if nu:
@@ -621,7 +660,10 @@ class LLMEngine:
             self._decode_forward(bs)
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
-        toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
+        if self.fused_sampler:
+            toks = self.d_out[:B].tolist()
+        else:
+            toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
         _t2 = time.perf_counter()
         self.timers["decode_host_pre"] += _t1 - _t0
         self.timers["decode_gpu_wait"] += _t2 - _t1
@@ -658,6 +700,10 @@ class LLMEngine:
     def _decode_forward(self, bs: int) -> None:
         ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)
         hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches)
+        if self.fused_sampler:
+            ops.sample_rows(self.model.logits(hid), self.d_temp[:bs], self.d_topp[:bs], self.d_topk[:bs],
+                            self.d_seed, out=self.d_out[:bs])
+            return
         self.d_hidden[:bs].copy_(hid)
         self.d_out[:bs].copy_(self.model.greedy(hid))
 

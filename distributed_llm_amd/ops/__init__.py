@@ -239,6 +239,24 @@ def sample_top_p(cand_vals: torch.Tensor, cand_idx: torch.Tensor, temperature: t
     return o
 
 
+def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
+                seed: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One-launch sampler over bf16 logits [B, V] (csrc/kernels/sampling.hip sample_rows_kernel):
+    per row, temperature <= 0 -> arg-max, else exact top-k (top_k <= 0 -> 256 candidates),
+    temperature, top-p and an inverse-CDF draw with u = hash(seed, row).  All parameters are
+    device tensors (f32 / int32, ``seed`` an int32 scalar), so the call is graph-capturable."""
+    ext = _native(logits)
+    if ext is None:
+        r = ref.sample_rows(logits, temperature.cpu(), top_p.cpu(), top_k.cpu(), int(seed.reshape(-1)[0]))
+        if out is not None:
+            out[:r.numel()].copy_(r)
+            return out
+        return r
+    o = out if out is not None else torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
+    ext.sample_rows(logits, temperature, top_p, top_k, seed, o)
+    return o
+
+
 # ----------------------------------------------------------------------------- router scorers
 
 def cosine_scores(q: torch.Tensor, c: torch.Tensor) -> torch.Tensor:

@@ -168,6 +168,56 @@ def sample_top_p(vals, idx, temperature, top_p, uniform):
     return torch.gather(idx, 1, pick).view(-1).to(torch.int32)
 
 
+def row_uniform(seed: int, rows: int) -> torch.Tensor:
+    """Counter-based uniforms u[row] in [0, 1) — the same hash as sample_rows_kernel."""
+    M = 0xFFFFFFFF
+    out = []
+    for r in range(rows):
+        h = (seed + r * 0x9E3779B9) & M
+        h ^= h >> 16
+        h = (h * 0x7FEB352D) & M
+        h ^= h >> 15
+        h = (h * 0x846CA68B) & M
+        h ^= h >> 16
+        out.append((h >> 8) / 16777216.0)
+    return torch.tensor(out, dtype=torch.float32)
+
+
+def sample_rows(logits, temperature, top_p, top_k, seed: int):
+    """Reference of the fused row sampler: greedy rows -> arg-max (lowest index on ties); sampled
+    rows -> top-k (value desc, index asc; k <= 0 -> 256) -> temperature -> nucleus -> draw."""
+    lg = logits.float()
+    B, V = lg.shape
+    u = row_uniform(int(seed) & 0xFFFFFFFF, B)
+    out = torch.empty(B, dtype=torch.int32)
+    for r in range(B):
+        t = float(temperature[r])
+        if not t > 0.0:
+            out[r] = int(torch.argmax(lg[r]))
+            continue
+        k = int(top_k[r])
+        k = 256 if k <= 0 or k > 256 else k
+        k = min(k, V)
+        order = sorted(range(V), key=lambda i: (-float(lg[r, i]), i))[:k]
+        vals = lg[r, order]
+        w = torch.exp((vals - vals[0]) / max(t, 1e-5))
+        c = torch.cumsum(w, 0)
+        s = float(c[-1])
+        cut = k
+        for i in range(k):
+            if float(c[i]) >= float(top_p[r]) * s:
+                cut = i + 1
+                break
+        target = float(u[r]) * float(c[cut - 1])
+        pick = cut - 1
+        for i in range(cut):
+            if float(c[i]) > target:
+                pick = i
+                break
+        out[r] = order[pick]
+    return out
+
+
 def cosine_scores(q, c):
     qn = q.float()
     cn = c.float()

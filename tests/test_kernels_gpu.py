@@ -188,6 +188,50 @@ def test_sample_top_p():
     assert (a.long() == b.long()).float().mean() > 0.95
 
 
+@pytest.mark.parametrize("V", [32000, 1000, 37])
+def test_sample_rows_matches_reference(V):
+    torch.manual_seed(9)
+    B = 48
+    Vp = (V + 7) // 8 * 8        # rows stay 16-B aligned; V = 37 exercises the scalar tail
+    lg = (torch.randn(B, Vp, device=DEV) * 2.0).to(torch.bfloat16)[:, :V]
+    temp = torch.where(torch.arange(B, device=DEV) % 4 == 0, torch.zeros(B, device=DEV),
+                       torch.rand(B, device=DEV) + 0.3)
+    top_p = torch.rand(B, device=DEV) * 0.9 + 0.1
+    top_k = torch.tensor([[0, 1, 5, 40][i % 4] if i % 3 else 256 for i in range(B)], dtype=torch.int32, device=DEV)
+    seed = torch.tensor([12345], dtype=torch.int32, device=DEV)
+    a = ops.sample_rows(lg, temp, top_p, top_k, seed).cpu()
+    b = ref.sample_rows(lg.cpu(), temp.cpu(), top_p.cpu(), top_k.cpu(), 12345)
+    greedy = (temp.cpu() <= 0)
+    assert torch.equal(a[greedy], b[greedy])
+    assert torch.equal(a[greedy].long(), lg.float().argmax(-1).cpu()[greedy])
+    # sampled rows: identical except for float rounding at CDF boundaries; always inside the top-k
+    assert (a == b).float().mean() > 0.95
+    for r in range(B):
+        k = int(top_k[r]) if 0 < int(top_k[r]) <= 256 else 256
+        kth = torch.topk(lg[r].float(), min(k, V)).values[-1]
+        assert lg[r, int(a[r])].float() >= kth
+
+
+def test_sample_rows_crowded_ties_and_distribution():
+    # heavy ties at the top (exercises the exact-threshold pass and candidate-list overflow)
+    B, V = 8, 32000
+    lg = torch.randint(0, 4, (B, V), device=DEV).to(torch.bfloat16)
+    p = lambda x: torch.full((B,), x, device=DEV)
+    a = ops.sample_rows(lg, p(1.0), p(0.9), torch.full((B,), 40, dtype=torch.int32, device=DEV),
+                        torch.tensor([3], dtype=torch.int32, device=DEV))
+    assert bool((lg.gather(1, a.long()[:, None]).float() == 3.0).all())
+    # many rows of the same small-vocab logits: empirical frequencies follow softmax(logits / t)
+    B, V, t = 8192, 8, 0.7
+    base = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5, -1.0, -3.0], device=DEV)
+    lg = base.to(torch.bfloat16).expand(B, V).contiguous()
+    pick = ops.sample_rows(lg, p(t)[:1].expand(B).contiguous(), torch.ones(B, device=DEV),
+                           torch.zeros(B, dtype=torch.int32, device=DEV),
+                           torch.tensor([99], dtype=torch.int32, device=DEV))
+    freq = torch.bincount(pick.long(), minlength=V).float() / B
+    want = torch.softmax(base.to(torch.bfloat16).float() / t, 0)
+    assert (freq - want).abs().max() < 0.02
+
+
 def test_cosine_kernels():
     torch.manual_seed(9)
     q, c = torch.randn(5, 384, device=DEV), torch.randn(7, 384, device=DEV)
