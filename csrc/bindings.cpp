@@ -13,8 +13,8 @@ int dllm_rope_kv(const void*, long, const int*, const float*, const int*, void*,
                  hipStream_t);
 int dllm_kv_write(const void*, const void*, long, const int*, void*, void*, int, int, int, int, hipStream_t);
 int dllm_paged_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*,
-                         const int*, const int*, void*, float*, float*, int*, const int*, int, int, int, int, int, int,
-                         int, int, float, hipStream_t);
+                         const int*, const int*, void*, float*, float*, int*, const int*, const int*, int, int, int,
+                         int, int, int, int, int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
@@ -131,7 +131,8 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
                      torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
                      torch::Tensor tile_tok0, torch::Tensor out, c10::optional<torch::Tensor> part_o,
                      c10::optional<torch::Tensor> part_ml, c10::optional<torch::Tensor> counters, int64_t splits,
-                     bool causal, double scale, c10::optional<torch::Tensor> split_len, bool xcd_remap) {
+                     bool causal, double scale, c10::optional<torch::Tensor> split_len, bool xcd_remap,
+                     c10::optional<torch::Tensor> items, int64_t grid_items) {
   check_bf16(q, "q");
   check_bf16(kc, "k_cache");
   check_bf16(vc, "v_cache");
@@ -172,10 +173,22 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
     TORCH_CHECK(split_len->numel() >= 1, "split_len: device scalar");
     sl = split_len->data_ptr<int>();
   }
+  const int* it = nullptr;
+  if (items.has_value()) {
+    // work list [1 + 2 * n]: units outside (num_tiles, nkv, splits) are skipped by the kernel; the
+    // two ints after the tile counters hold the dynamic-fetch cursor and exit count (kept zeroed)
+    check_i32(*items, "items");
+    TORCH_CHECK(splits > 1 && cnt != nullptr, "work-list attention needs split-K workspaces");
+    TORCH_CHECK(items->numel() >= 1, "work list [1 + 2n]");
+    TORCH_CHECK(counters->numel() >= (int64_t)num_tiles * nkv + 2, "work list: counters need 2 cursor slots");
+    TORCH_CHECK(grid_items >= 1 && !xcd_remap, "work-list attention: grid >= 1, no XCD remap");
+    it = items->data_ptr<int>();
+  }
   ok(dllm_paged_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                           qstart.data_ptr<int>(), qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(),
-                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, sl, xcd_remap ? 1 : 0, num_tiles, nq, nkv, d,
-                          block_tables.size(1), splits, causal ? 1 : 0, (float)scale, stream()),
+                          tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, sl, it, (int)grid_items,
+                          xcd_remap ? 1 : 0, num_tiles, nq, nkv, d, block_tables.size(1), splits, causal ? 1 : 0,
+                          (float)scale, stream()),
      "paged_attention");
 }
 

@@ -19,6 +19,9 @@
 // chunks of the split and are combined through LDS.  With grid.z == 1 the workgroup writes the
 // normalised bf16 output; otherwise it writes (m, l, O) partials, takes a ticket, and the LAST
 // workgroup of the tile combines all splits in the same launch (no second kernel).
+// Decode can instead pass a work list (persistent mode): a fixed grid loops over host-built
+// (tile, kv head, split, nsplit) units of ~equal key counts — balanced across ragged batches
+// while the launch geometry stays constant for hipGraph replay.
 #include "common.h"
 
 namespace {
@@ -41,41 +44,36 @@ struct AttnArgs {
   float* part_ml;        // [num_tiles, nkv, splits, 16, 2]
   int* counters;         // [num_tiles * nkv] zeroed; re-armed by the reducing workgroup
   const int* split_len;  // optional device scalar: keys per split (dynamic per-tile split count)
+  const int* items;      // optional work list: [0] = n, then n pairs (tile | kvh << 16, split | nsplit << 8)
   int xcd_remap;         // 1: XCD-contiguous block order (prefill K/V reuse in L2)
   int nq, nkv, G, max_blocks, causal;
+  int num_tiles, split_stride;  // partial-workspace geometry: [num_tiles, nkv, split_stride, 16, d]
+  int wl_dynamic;        // work list: 1 = units fetched with an atomic cursor (counters[num_tiles * nkv])
   float scale_log2;
 };
 // NOTE (measured, MI355X): surplus blocks are not free — a grid whose z-splits are mostly empty
 // for short contexts ran 1.5-4.7x slower than the same work with z = 1, so the engine uses static
 // split counts sized to the batch and keeps the dynamic split for explicit opt-in.
 
+template <int D>
+struct AttnSmem {
+  float o[WAVES][16][D + 1];
+  float m[WAVES][16];
+  float l[WAVES][16];
+  int last;
+};
+
+// One work unit: (16-row tile, kv head, split `split` of `nsplit`).  Returns with the LDS free
+// for reuse only after a __syncthreads by the caller.
 template <int D, int W, int CH>
-__global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
+__device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, const int tile, const int kvh,
+                                          const int split, int nsplit) {
   constexpr int KSTEPS = D / 32;
   constexpr int NT = D / 16;
-  __shared__ float s_o[WAVES][16][D + 1];
-  __shared__ float s_m[WAVES][16];
-  __shared__ float s_l[WAVES][16];
-  __shared__ int s_last;
-
-  // Prefill: XCD-aware block order (bijective; cdna_hip_programming.md T1): blocks b, b+8, ...
-  // share an XCD (and its L2), so each XCD gets a CONTIGUOUS range of (tile, head, split) work
-  // and the tiles of one sequence/head re-read the same K/V from that XCD's L2, not from HBM.
-  // Decode (xcd_remap = 0): tiles carry no shared K/V; the host orders them longest context
-  // first so the dispatcher starts the longest chains first and spreads them over all XCDs.
-  int tile = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
-  const int splits = gridDim.z;
-  if (a.xcd_remap) {
-    const int nx = gridDim.x, ny = gridDim.y;
-    const long n = (long)nx * ny * splits;
-    const long lin = blockIdx.x + (long)nx * (blockIdx.y + (long)ny * blockIdx.z);
-    const long q8 = n / 8, r8 = n % 8, xcd = lin % 8;
-    const long logical = xcd * q8 + (xcd < r8 ? xcd : r8) + lin / 8;
-    tile = (int)(logical % nx);
-    const long rest = logical / nx;
-    kvh = (int)(rest % ny);
-    split = (int)(rest / ny);
-  }
+  auto& s_o = sm.o;
+  auto& s_m = sm.m;
+  auto& s_l = sm.l;
+  const int splits = a.split_stride;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, rl = lane & 15;
   const int seq = a.tile_seq[tile];
@@ -94,8 +92,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   // gridDim.z splits as its own key range needs (long contexts split, short ones run whole), so
   // one launch is balanced across a batch of very different context lengths; surplus blocks
   // leave immediately (uniform per block: split is a per-block index).
-  int nsplit = splits;
-  if (a.split_len != nullptr) {
+  if (a.items == nullptr && a.split_len != nullptr) {
     const int sl = max(*a.split_len, 32);
     nsplit = min(splits, max(1, (kmax + sl - 1) / sl));
     if (split >= nsplit) return;
@@ -252,8 +249,8 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   // ---- split-K: write-through partials (O unnormalised in the workgroup's max frame, and per-row
   // (m, l)), ticket per (tile, kv head); the last arriver combines with sc1 loads (R1 recipe).
   const long pbase = (((long)tile * a.nkv + kvh) * splits + split) * 16;  // first row of this partial
-  const unsigned obytes = (unsigned)min((long)gridDim.x * a.nkv * splits * 16 * D * 4, 0x7fffffffL);
-  const unsigned mlbytes = (unsigned)min((long)gridDim.x * a.nkv * splits * 16 * 2 * 4, 0x7fffffffL);
+  const unsigned obytes = (unsigned)min((long)a.num_tiles * a.nkv * splits * 16 * D * 4, 0x7fffffffL);
+  const unsigned mlbytes = (unsigned)min((long)a.num_tiles * a.nkv * splits * 16 * 2 * 4, 0x7fffffffL);
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.part_o, obytes), rml = make_rsrc(a.part_ml, mlbytes);
   for (int e = threadIdx.x * 4; e < 16 * D; e += blockDim.x * 4) {
     const int row = e / D, col = e % D;
@@ -287,7 +284,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     }
     st_wt16(rml, (unsigned)((pbase + 2 * threadIdx.x) * 2 * 4), make_float4(ml[0], ml[1], ml[2], ml[3]));
   }
-  if (!ticket_last(&a.counters[tile * a.nkv + kvh], nsplit, &s_last)) return;
+  if (!ticket_last(&a.counters[tile * a.nkv + kvh], nsplit, &sm.last)) return;
   const long tbase = (((long)tile * a.nkv + kvh) * splits) * 16;
   if (threadIdx.x < 16) {
     const int row = threadIdx.x;
@@ -325,6 +322,68 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   }
 }
 
+template <int D, int W, int CH>
+__global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
+  __shared__ AttnSmem<D> sm;
+  if (a.items != nullptr) {
+    // Persistent decode: a fixed grid (graph-capturable) walks a host-built list of equal-sized
+    // key ranges, longest sequences first, so a batch of very different context lengths costs
+    // ~(total keys / grid) per workgroup instead of the longest sequence's keys (no surplus
+    // early-exit blocks, no tail of one long chain).
+    const int n = a.items[0];
+    auto run = [&](int it) {
+      const int w0 = a.items[1 + 2 * it], w1 = a.items[2 + 2 * it];
+      const int tile = w0 & 0xffff, kvh = w0 >> 16, split = w1 & 0xff, nsplit = w1 >> 8;
+      // a malformed unit is skipped rather than trusted (it would index past the workspaces)
+      if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.split_stride && split < nsplit)
+        attn_unit<D, W, CH>(a, sm, tile, kvh, split, nsplit);
+      __syncthreads();
+    };
+    if (!a.wl_dynamic) {
+      for (int it = blockIdx.x; it < n; it += gridDim.x) run(it);
+      return;
+    }
+    // dynamic: workgroups take the next unit from an atomic cursor (greedy longest-first
+    // scheduling of unequal units); the last workgroup to leave re-arms cursor and exit count
+    int* cur = a.counters + (long)a.num_tiles * a.nkv;
+    for (;;) {
+      if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int it = sm.last;
+      __syncthreads();
+      if (it >= n) break;
+      run(it);
+    }
+    if (threadIdx.x == 0) {
+      const int done = __hip_atomic_fetch_add(cur + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == (int)gridDim.x - 1) {
+        __hip_atomic_store(cur, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cur + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
+  // Prefill: XCD-aware block order (bijective; cdna_hip_programming.md T1): blocks b, b+8, ...
+  // share an XCD (and its L2), so each XCD gets a CONTIGUOUS range of (tile, head, split) work
+  // and the tiles of one sequence/head re-read the same K/V from that XCD's L2, not from HBM.
+  // Decode (xcd_remap = 0): tiles carry no shared K/V; the host orders them longest context
+  // first so the dispatcher starts the longest chains first and spreads them over all XCDs.
+  int tile = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  const int splits = gridDim.z;
+  if (a.xcd_remap) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const long n = (long)nx * ny * splits;
+    const long lin = blockIdx.x + (long)nx * (blockIdx.y + (long)ny * blockIdx.z);
+    const long q8 = n / 8, r8 = n % 8, xcd = lin % 8;
+    const long logical = xcd * q8 + (xcd < r8 ? xcd : r8) + lin / 8;
+    tile = (int)(logical % nx);
+    const long rest = logical / nx;
+    kvh = (int)(rest % ny);
+    split = (int)(rest / ny);
+  }
+  attn_unit<D, W, CH>(a, sm, tile, kvh, split, splits);
+}
+
 template <int D, int W>
 void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
   static const int ch = [] { const char* e = getenv("DLLM_ATTN_CH"); return e ? atoi(e) : 1; }();
@@ -338,24 +397,28 @@ void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
 extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* vc, const int* block_tables,
                                     const int* seq_qstart, const int* seq_qlen, const int* seq_ctx,
                                     const int* tile_seq, const int* tile_tok0, void* out, float* part_o,
-                                    float* part_ml, int* counters, const int* split_len, int xcd_remap, int num_tiles,
-                                    int nq, int nkv, int d, int max_blocks, int splits, int causal, float scale,
-                                    hipStream_t stream) {
+                                    float* part_ml, int* counters, const int* split_len, const int* items,
+                                    int grid_items, int xcd_remap, int num_tiles, int nq, int nkv, int d,
+                                    int max_blocks, int splits, int causal, float scale, hipStream_t stream) {
   if (nq % nkv != 0) return -1;
   const int G = nq / nkv;
   if (16 % G != 0) return -2;
   if (splits < 1 || (splits > 1 && (!part_o || !part_ml || !counters))) return -3;
+  if (items != nullptr && (grid_items < 1 || xcd_remap)) return -5;
   if (num_tiles <= 0) return 0;
   AttnArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
-             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, split_len, xcd_remap, nq, nkv, G, max_blocks,
-             causal, scale * LOG2E};
+             tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, split_len, items, xcd_remap, nq, nkv, G,
+             max_blocks, causal, num_tiles, splits, 0, scale * LOG2E};
+  static const int env_dyn = [] { const char* e = getenv("DLLM_ATTN_WL_DYNAMIC"); return e ? atoi(e) : 0; }();
+  a.wl_dynamic = items != nullptr && env_dyn ? 1 : 0;
   // 8 waves per workgroup when the grid alone cannot fill the CUs with memory requests
   // (decode at moderate batch: tiles x kv-heads x splits workgroups are all resident at once).
   static const int env_w = [] { const char* e = getenv("DLLM_ATTN_WAVES"); return e ? atoi(e) : 0; }();
   const long wgs = (long)num_tiles * nkv * splits;
   // (dynamic splitting bounds every block's key range, where 8 waves measured best)
-  const int W = env_w == 4 || env_w == 8 ? env_w : ((split_len != nullptr || wgs <= 2048) ? 8 : 4);
-  dim3 grid(num_tiles, nkv, splits);
+  const int W = env_w == 4 || env_w == 8 ? env_w
+                : ((items != nullptr || split_len != nullptr || wgs <= 2048) ? 8 : 4);
+  const dim3 grid = items != nullptr ? dim3(grid_items, 1, 1) : dim3(num_tiles, nkv, splits);
 switch (d) {
     case 64: W == 8 ? launch_attn<64, 8>(grid, a, stream) : launch_attn<64, 4>(grid, a, stream); break;
     case 96: W == 8 ? launch_attn<96, 8>(grid, a, stream) : launch_attn<96, 4>(grid, a, stream); break;

@@ -93,6 +93,22 @@ class _Seq:
         return len(self.prompt) + len(self.out)
 
 
+def decode_buckets(R: int, mode: Optional[str] = None) -> List[int]:
+    """Batch sizes that get a captured decode graph (a step runs the smallest bucket >= its batch).
+
+    Powers of two up to 64, then every 32 rows to 256, then every 64 rows (``fine``, default).
+    A decode batch drains continuously as conversations finish, so with power-of-two buckets a
+    step at 300 rows ran the 512-row graph: the weight GEMMs above 128 rows scale with M and paid
+    for up to 40 % padding.  ``pow2`` (DLLM_BUCKETS=pow2) restores the coarse ladder.
+    """
+    mode = mode or os.environ.get("DLLM_BUCKETS", "fine")
+    if mode == "pow2":
+        ladder = [1 << i for i in range(0, 20)]
+    else:
+        ladder = [1, 2, 4, 8, 16, 32, 48, 64] + list(range(96, 257, 32)) + list(range(320, 1 << 16, 64))
+    return [b for b in ladder if b < R] + [R]
+
+
 class LLMEngine:
     def __init__(self, model: Union[str, ModelConfig], device: str = "cuda", par: ParallelContext = SINGLE,
                  kv_cache_gb: Optional[float] = None, max_num_seqs: int = 256, max_model_len: Optional[int] = None,
@@ -160,7 +176,7 @@ class LLMEngine:
         self.bt_dev = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, device=self.device)
         self._bt_dirty = True          # whole-table copy needed (admissions / releases)
         self._bt_upd: List[int] = []   # (flat index, block) pairs applied inside the decode graph
-        self.buckets = [b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512) if b < R] + [R]
+        self.buckets = decode_buckets(R)
         mb = self.buckets[-1]
         # packed decode buffer: ids | pos | slots | tile_seq  (mb each) | qstart | qlen | ctx (R+1 each)
         #                       | attention split length
@@ -199,7 +215,14 @@ class LLMEngine:
         ws = mb * nkv * self.max_splits * 16
         self.dec_ws = (torch.empty(ws * dh, dtype=torch.float32, device=self.device),
                        torch.empty(ws * 2, dtype=torch.float32, device=self.device),
-                       torch.zeros(mb * nkv, dtype=torch.int32, device=self.device))
+                       torch.zeros(mb * nkv + 2, dtype=torch.int32, device=self.device))
+        # persistent decode attention: host-built work list, copied with the step's metadata
+        self.attn_worklist = self.ATTN_WORKLIST and not self.ATTN_DYNAMIC
+        if self.attn_worklist:
+            cap = 1 + 2 * mb * nkv * self.max_splits
+            self.items_host_t = torch.zeros(cap, dtype=torch.int32, pin_memory=pin)
+            self.items_host = self.items_host_t.numpy()
+            self.items_dev = torch.zeros(cap, dtype=torch.int32, device=self.device)
 
     def _autotune(self) -> None:
         """Pick the fastest GEMM plan for every decode bucket and weight shape (before capture)."""
@@ -223,6 +246,19 @@ class LLMEngine:
     ATTN_DYNAMIC = os.environ.get("DLLM_ATTN_DYNAMIC") == "1"
     SORT_TILES = os.environ.get("DLLM_DECODE_SORT", "1") == "1"   # decode tiles longest context first
     ATTN_TARGET_WGS = int(os.environ.get("DLLM_ATTN_TARGET_WGS", "2048"))
+    # Default: persistent work-list attention (ops.decode_work_items): a fixed grid of at most
+    # ATTN_PGRID workgroups walks ~ATTN_ITEMS_PER_WG equal key ranges each, longest first.
+    ATTN_WORKLIST = os.environ.get("DLLM_ATTN_WORKLIST", "1") == "1"
+    ATTN_PGRID = int(os.environ.get("DLLM_ATTN_PGRID", "512"))
+    ATTN_ITEMS_PER_WG = int(os.environ.get("DLLM_ATTN_ITEMS_PER_WG", "1"))
+    # below this batch the static split-K grid measured faster (scripts/microbench.py attn_wl)
+    ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "128"))
+
+    def _use_worklist(self, bs: int) -> bool:
+        return self.attn_worklist and bs >= self.ATTN_WL_MIN_BS
+
+    def _attn_grid(self, bs: int) -> int:
+        return int(max(1, min(self.ATTN_PGRID, bs * self.model.nkv * self.max_splits)))
 
     def _decode_splits(self, bs: int) -> int:
         if self.ATTN_DYNAMIC:
@@ -635,7 +671,14 @@ class LLMEngine:
         h[o[2]:o[2] + bs] = -1
         h[o[2]:o[2] + B] = blocks * BS + pos % BS
         h[o[3]:o[3] + bs] = R            # padding tiles -> dummy row (qlen 0)
-        h[o[3]:o[3] + B] = rows[np.argsort(-lens, kind="stable")] if self.SORT_TILES else rows
+        order = np.argsort(-lens, kind="stable") if (self.SORT_TILES or self._use_worklist(bs)) else None
+        h[o[3]:o[3] + B] = rows[order] if order is not None else rows
+        n_items = 0
+        if self._use_worklist(bs):
+            grid = self._attn_grid(bs)
+            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, self.ATTN_ITEMS_PER_WG * grid,
+                                  out=self.items_host)
+            n_items = 1 + 2 * int(self.items_host[0])
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)
         h[o[5] + rows] = 1
@@ -650,6 +693,8 @@ class LLMEngine:
             h[o[8] + 1:o[8] + 1 + 2 * nu] = self._bt_upd
             self._bt_upd.clear()
         self.dec_dev[:o[8] + 1 + 2 * nu].copy_(self.dec_host_t[:o[8] + 1 + 2 * nu], non_blocking=True)
+        if n_items:
+            self.items_dev[:n_items].copy_(self.items_host_t[:n_items], non_blocking=True)
         _t1 = time.perf_counter()
         if self.use_graphs:
             g = self._graphs.get(bs)
@@ -692,6 +737,11 @@ class LLMEngine:
         self.timers["decode_host_post"] += time.perf_counter() - _t2
 
     def _decode_meta(self, bs: int) -> AttnMeta:
+        if self._use_worklist(bs):
+            return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart,
+                            qlen=self.d_qlen, ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
+                            last_idx=self.d_last[:bs], splits=self.max_splits, workspace=self.dec_ws,
+                            items=self.items_dev, grid_items=self._attn_grid(bs))
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
                         ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
                         last_idx=self.d_last[:bs], splits=self._decode_splits(bs), workspace=self.dec_ws,

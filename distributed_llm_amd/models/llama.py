@@ -42,6 +42,8 @@ class AttnMeta:
     workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
     split_len: Optional[torch.Tensor] = None  # int32 device scalar: dynamic split-K (opt-in)
     xcd_remap: bool = False                    # prefill: XCD-contiguous attention block order
+    items: Optional[torch.Tensor] = None       # decode: persistent attention work list (ops.decode_work_items)
+    grid_items: int = 0                        # workgroups walking ``items``
 
 
 class LlamaModel:
@@ -198,7 +200,7 @@ class LlamaModel:
             o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                     meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
                                     splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
-                                    xcd_remap=meta.xcd_remap)
+                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
             h = self.par.all_reduce(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
             h = self.par.all_reduce(self._mlp(L, x))

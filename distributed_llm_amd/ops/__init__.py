@@ -16,6 +16,7 @@ import os
 import struct
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import reference as ref
@@ -134,13 +135,16 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                     tile_seq: torch.Tensor, tile_tok0: torch.Tensor, scale: Optional[float] = None,
                     causal: bool = True, splits: int = 1, out: Optional[torch.Tensor] = None,
                     workspace: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                    split_len: Optional[torch.Tensor] = None, xcd_remap: bool = False) -> torch.Tensor:
+                    split_len: Optional[torch.Tensor] = None, xcd_remap: bool = False,
+                    items: Optional[torch.Tensor] = None, grid_items: int = 0) -> torch.Tensor:
     """Paged attention over new query tokens ``q [T, nq, d]`` (see csrc/kernels/attention.hip).
 
     ``splits`` is the split-K grid depth; with ``split_len`` (int32 device scalar, keys per split)
     each tile uses only ceil(its keys / split_len) of them (dynamic, balanced split-K).
     ``xcd_remap``: XCD-contiguous block order, for prefill (K/V re-read by a sequence's tiles hits
-    one XCD's L2)."""
+    one XCD's L2).
+    ``items`` (decode): a work list from :func:`decode_work_items`; a fixed grid of ``grid_items``
+    workgroups walks it (``splits`` is then the workspace split stride)."""
     d = q.shape[-1]
     scale = (1.0 / math.sqrt(d)) if scale is None else scale
     ext = _native(q)
@@ -157,8 +161,39 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         else:
             po, pml, cnt = workspace
     ext.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
-                        po, pml, cnt, splits, causal, scale, split_len if splits > 1 else None, xcd_remap)
+                        po, pml, cnt, splits, causal, scale, split_len if splits > 1 and items is None else None,
+                        xcd_remap, items, int(grid_items))
     return o
+
+
+def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,
+                      out: Optional[np.ndarray] = None) -> np.ndarray:
+    """Work list for persistent decode attention (one query token per tile, tiles in ``ctx`` order).
+
+    Every (tile, kv head) is cut into ``ceil(ctx / chunk)`` splits (at most ``max_splits``) with
+    ``chunk`` sized so the batch yields about ``target_items`` units; units are emitted tile by
+    tile, so with tiles sorted longest context first the list runs from the largest units to the
+    smallest (round-robin over the grid then approximates longest-processing-time scheduling).
+    Returns int32 ``[1 + 2n]``: ``n``, then ``(tile | kvh << 16, split | nsplit << 8)`` pairs.
+    """
+    ctx = np.asarray(ctx, dtype=np.int64)
+    B = ctx.shape[0]
+    total = int(ctx.sum())
+    chunk = max(min_chunk, -(-total * nkv // max(1, target_items)))
+    chunk = (chunk + 31) & ~31
+    ns = np.clip(-(-ctx // chunk), 1, max_splits)
+    rep = ns * nkv
+    n = int(rep.sum())
+    starts = np.cumsum(rep) - rep
+    j = np.arange(n, dtype=np.int64) - np.repeat(starts, rep)
+    ns_r = np.repeat(ns, rep)
+    tile = np.repeat(np.arange(B, dtype=np.int64), rep)
+    buf = out if out is not None else np.empty(1 + 2 * n, dtype=np.int32)
+    buf[0] = n
+    w = buf[1:1 + 2 * n].reshape(n, 2)
+    w[:, 0] = tile | ((j // ns_r) << 16)
+    w[:, 1] = (j % ns_r) | (ns_r << 8)
+    return buf
 
 
 # ----------------------------------------------------------------------------- activations

@@ -61,6 +61,39 @@ def bench_attn_dyn(B, C, nq, nkv, d, z, target, var=True):
             "GBps": round(kv_bytes / ms / 1e6, 1), "max_err_vs_1split": err}
 
 
+def bench_attn_wl(B, C, nq, nkv, d, grid, per_wg, var=True, min_chunk=256, waves="auto"):
+    """Persistent work-list decode attention (engine default): tiles longest context first."""
+    import numpy as np
+    g = torch.Generator().manual_seed(0)
+    ctxs = (torch.randint(C // 4, 7 * C // 4 + 1, (B,), generator=g).tolist() if var else [C] * B)
+    Cm = max(ctxs)
+    NB = B * ((Cm + 15) // 16) + 8
+    kc = torch.randn(NB, nkv, 16, d, device="cuda").to(torch.bfloat16)
+    vc = torch.randn(NB, nkv, d, 16, device="cuda").to(torch.bfloat16)
+    nb = (Cm + 15) // 16
+    bt = torch.randperm(NB - 8, device="cuda")[:B * nb].view(B, nb).to(torch.int32)
+    q = torch.randn(B, nq, d, device="cuda").to(torch.bfloat16)
+    I = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    qs, ql, cx = I(list(range(B))), I([1] * B), I(ctxs)
+    order = np.argsort(-np.array(ctxs), kind="stable")
+    ts, tt = I(order.astype(np.int32).tolist()), I([0] * B)
+    z = 16
+    ws = (torch.empty(B * nkv * z * 16 * d, device="cuda"), torch.empty(B * nkv * z * 16 * 2, device="cuda"),
+          torch.zeros(B * nkv + 2, dtype=torch.int32, device="cuda"))
+    items = ops.decode_work_items(np.array(ctxs)[order], nkv, z, per_wg * grid, min_chunk=min_chunk)
+    it = torch.tensor(items, device="cuda")
+    run = lambda: ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, workspace=ws, items=it,
+                                      grid_items=grid)
+    ms = timeit(run)
+    ref_o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=1)
+    err = (ref_o.float() - run().float()).abs().max().item()
+    kv_bytes = sum(ctxs) * nkv * d * 2 * 2
+    return {"bench": "attn_decode_worklist", "B": B, "C": sum(ctxs) // B, "var": var, "nq": nq, "nkv": nkv,
+            "d": d, "grid": grid, "per_wg": per_wg, "items": int(items[0]), "min_chunk": min_chunk,
+            "waves": os.environ.get("DLLM_ATTN_WAVES", "auto"), "us": round(ms * 1000, 1),
+            "GBps": round(kv_bytes / ms / 1e6, 1), "max_err_vs_1split": err}
+
+
 def bench_attn(B, C, nq, nkv, d, splits, var=False):
     """var=True: contexts uniform in [C/4, 7C/4] (mean C) like a serving batch, else all C."""
     g = torch.Generator().manual_seed(0)
@@ -184,6 +217,14 @@ if __name__ == "__main__":
                 for z in (4, 8):
                     for target in (1024, 2048, 4096):
                         print(json.dumps(bench_attn_dyn(B, C, nq, nkv, d, z, target, var)), flush=True)
+    if "attn_wl" in what:
+        for (B, C, var) in [(1, 2048, False), (16, 2048, False), (64, 2048, True), (128, 2021, True),
+                            (256, 1024, False), (256, 2034, True), (512, 2034, True), (512, 4000, True)]:
+            for (nq, nkv, d) in [(32, 4, 64), (32, 8, 128)]:
+                print(json.dumps(bench_attn(B, C, nq, nkv, d, 1, var)), flush=True)
+                for grid in (512, 1024):
+                    for per_wg in (1, 2, 4):
+                        print(json.dumps(bench_attn_wl(B, C, nq, nkv, d, grid, per_wg, var)), flush=True)
     if "decode" in what or "prefill" in what:
         eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
         if "decode" in what:
