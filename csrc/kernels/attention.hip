@@ -65,7 +65,7 @@ struct AttnSmem {
 
 // One work unit: (16-row tile, kv head, split `split` of `nsplit`).  Returns with the LDS free
 // for reuse only after a __syncthreads by the caller.
-template <int D, int W, int CH>
+template <int D, int W, int CH, bool PF>
 __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, const int tile, const int kvh,
                                           const int split, int nsplit) {
   constexpr int KSTEPS = D / 32;
@@ -127,14 +127,30 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   // CH 32-key chunks per wave trip: all CH chunks' K/V loads are issued before the first chunk's
   // MFMAs, so a wave keeps CH x 8 KB (d = 64) in flight (CH = 2 for decode: more bytes in flight
   // per CU at the cost of VGPRs).
+  // Block-table entries are prefetched one trip ahead (PF): the K/V addresses of a trip then do
+  // not wait on a dependent block-table load, so each trip has one memory latency, not two.
+  // (a macro, not a lambda: a by-reference lambda over these arrays put them in scratch)
+#define DLLM_BT_LOOKUP(KB, B0, B1)                                   \
+  _Pragma("unroll") for (int c = 0; c < CH; ++c) {                   \
+    const int kc_ = (KB) + 32 * c;                                   \
+    B0[c] = kc_ < k_end ? bt[kc_ >> 4] : bt[(KB) >> 4];              \
+    B1[c] = (kc_ + 16 < k_end) ? bt[(kc_ >> 4) + 1] : B0[c];         \
+  }
+  int nb0[CH], nb1[CH];
+  if (PF && k_begin + 32 * CH * wave < k_end) { DLLM_BT_LOOKUP(k_begin + 32 * CH * wave, nb0, nb1) }
   for (int kb = k_begin + 32 * CH * wave; kb < k_end; kb += 32 * CH * W) {
     uint4 kr[CH][2][KSTEPS];
     uint2 vr[CH][2][NT];
+    int cb0[CH], cb1[CH];
+    if (PF) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) { cb0[c] = nb0[c]; cb1[c] = nb1[c]; }
+    } else {
+      DLLM_BT_LOOKUP(kb, cb0, cb1)
+    }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int kc = kb + 32 * c;
-      const int b0 = kc < k_end ? bt[kc >> 4] : bt[kb >> 4];
-      const int b1 = (kc + 16 < k_end) ? bt[(kc >> 4) + 1] : b0;
+      const int b0 = cb0[c], b1 = cb1[c];
       const u16* k0 = a.kc + ((long)b0 * a.nkv + kvh) * head_stride + rl * D + 8 * g;
       const u16* k1 = a.kc + ((long)b1 * a.nkv + kvh) * head_stride + rl * D + 8 * g;
       const u16* v0 = a.vc + ((long)b0 * a.nkv + kvh) * head_stride + rl * BS + 4 * g;
@@ -150,6 +166,7 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
         vr[c][1][n] = *reinterpret_cast<const uint2*>(v1 + 16 * n * BS);
       }
     }
+    if (PF && kb + 32 * CH * W < k_end) { DLLM_BT_LOOKUP(kb + 32 * CH * W, nb0, nb1) }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int kc = kb + 32 * c;
@@ -192,6 +209,8 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
       }
     }
   }
+
+#undef DLLM_BT_LOOKUP
 
   // ---- combine the waves through LDS.  acc[n][r] = O^T[dim 16n + 4g + r][row rl]
   if constexpr (W == 8) {  // waves 4..7 fold into waves 0..3 first (keeps LDS at 4 slots)
@@ -322,7 +341,7 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   }
 }
 
-template <int D, int W, int CH>
+template <int D, int W, int CH, bool PF>
 __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   __shared__ AttnSmem<D> sm;
   if (a.items != nullptr) {
@@ -331,30 +350,35 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     // ~(total keys / grid) per workgroup instead of the longest sequence's keys (no surplus
     // early-exit blocks, no tail of one long chain).
     const int n = a.items[0];
-    auto run = [&](int it) {
+    // static: units blockIdx.x, + gridDim.x, ...; dynamic: workgroups take the next unit from an
+    // atomic cursor (greedy longest-first scheduling of unequal units) and the last workgroup to
+    // leave re-arms cursor and exit count.  (One attn_unit call site: a lambda wrapper here made
+    // hipcc spill 176 B/lane to scratch.)
+    int* cur = a.counters + (long)a.num_tiles * a.nkv;
+    int it = blockIdx.x;
+    if (a.wl_dynamic) {
+      if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      it = sm.last;
+      __syncthreads();
+    }
+    while (it < n) {
       const int w0 = a.items[1 + 2 * it], w1 = a.items[2 + 2 * it];
       const int tile = w0 & 0xffff, kvh = w0 >> 16, split = w1 & 0xff, nsplit = w1 >> 8;
       // a malformed unit is skipped rather than trusted (it would index past the workspaces)
       if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.split_stride && split < nsplit)
-        attn_unit<D, W, CH>(a, sm, tile, kvh, split, nsplit);
+        attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, nsplit);
       __syncthreads();
-    };
-    if (!a.wl_dynamic) {
-      for (int it = blockIdx.x; it < n; it += gridDim.x) run(it);
-      return;
+      if (a.wl_dynamic) {
+        if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        it = sm.last;
+        __syncthreads();
+      } else {
+        it += gridDim.x;
+      }
     }
-    // dynamic: workgroups take the next unit from an atomic cursor (greedy longest-first
-    // scheduling of unequal units); the last workgroup to leave re-arms cursor and exit count
-    int* cur = a.counters + (long)a.num_tiles * a.nkv;
-    for (;;) {
-      if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const int it = sm.last;
-      __syncthreads();
-      if (it >= n) break;
-      run(it);
-    }
-    if (threadIdx.x == 0) {
+    if (a.wl_dynamic && threadIdx.x == 0) {
       const int done = __hip_atomic_fetch_add(cur + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (done == (int)gridDim.x - 1) {
         __hip_atomic_store(cur, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -381,16 +405,21 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     kvh = (int)(rest % ny);
     split = (int)(rest / ny);
   }
-  attn_unit<D, W, CH>(a, sm, tile, kvh, split, splits);
+  attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, splits);
 }
 
 template <int D, int W>
 void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
   static const int ch = [] { const char* e = getenv("DLLM_ATTN_CH"); return e ? atoi(e) : 1; }();
-  if (ch == 2)
-    hipLaunchKernelGGL((paged_attn_kernel<D, W, 2>), grid, dim3(64 * W), 0, stream, a);
+  static const int pf = [] { const char* e = getenv("DLLM_ATTN_BT_PREFETCH"); return e ? atoi(e) : 0; }();
+  if (ch == 2 && pf)
+    hipLaunchKernelGGL((paged_attn_kernel<D, W, 2, true>), grid, dim3(64 * W), 0, stream, a);
+  else if (ch == 2)
+    hipLaunchKernelGGL((paged_attn_kernel<D, W, 2, false>), grid, dim3(64 * W), 0, stream, a);
+  else if (pf)
+    hipLaunchKernelGGL((paged_attn_kernel<D, W, 1, true>), grid, dim3(64 * W), 0, stream, a);
   else
-    hipLaunchKernelGGL((paged_attn_kernel<D, W, 1>), grid, dim3(64 * W), 0, stream, a);
+    hipLaunchKernelGGL((paged_attn_kernel<D, W, 1, false>), grid, dim3(64 * W), 0, stream, a);
 }
 }  // namespace
 

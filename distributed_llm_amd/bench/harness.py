@@ -95,7 +95,8 @@ def _done_keys(path: str) -> set:
     if not os.path.exists(path):
         return set()
     with open(path, newline="") as f:
-        return {(r["strategy"], r["cache_mode"], int(r["token_threshold"])) for r in csv.DictReader(f)}
+        return {(r["query_set"], r["strategy"], r["cache_mode"], int(r["token_threshold"]))
+                for r in csv.DictReader(f)}
 
 
 def summarize(rows: List[Dict[str, Any]], query_set: str, strategy: str, cache_mode: str, thr: int,
@@ -149,7 +150,7 @@ def run_experiment(items: List[QueryItem], cfg: RunConfig, pools, tier_gpus: Dic
             cache_on = cache_mode.lower() == "on"
             thrs = cfg.thresholds if strategy == "token" else [cfg.fixed_threshold_for_non_token]
             for thr in thrs:
-                if (strategy, cache_mode, int(thr)) in done:
+                if (cfg.query_set_name, strategy, cache_mode, int(thr)) in done:
                     log(f"[resume] skip {strategy}/{cache_mode}/{thr}")
                     continue
                 try:

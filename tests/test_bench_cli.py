@@ -1,0 +1,41 @@
+"""bench.py driver contract on CPU (gloo): one JSON line from rank 0 with the required keys, for
+the default replicated topology (dp) and the disjoint-pool topology (small replicas + large TP)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n,extra,par", [(1, [], "dp1"), (2, [], "dp2"), (4, ["--topology", "pools"], "pools:")])
+def test_bench_json_line(n, extra, par):
+    args = ["bench.py", "--cpu", "--gpus", str(n), "--steps", "1", "--warmup", "1", "--convs", "2",
+            "--small-new", "4", "--large-new", "6"] + extra
+    if n > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    env = dict(os.environ, DLLM_EMBEDDER="hash", OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert KEYS <= set(out)
+    assert out["n_gpus"] == n and out["steps"] == 1 and out["warmup"] == 1
+    assert out["value"] > 0 and out["higher_is_better"] is True and out["scaling"] == "weak"
+    assert out["config"]["parallelism"].startswith(par)
+    assert out["requests"] == 2 * n and out["p50_latency_ms"] > 0

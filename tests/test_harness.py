@@ -66,6 +66,13 @@ def test_harness_resume(tmp_path):
     with open(out) as f:
         rows = list(csv.reader(f))
     assert [r[1] for r in rows[1:]] == ["heuristic", "token"]
+    # a different query set with the same (strategy, cache, threshold) is NOT skipped on resume
+    args2 = [a if a != "technical_coding" else "personal_health" for a in args]
+    harness.main(args2 + ["--resume"])
+    with open(out) as f:
+        rows = list(csv.reader(f))
+    assert [(r[0], r[1]) for r in rows[1:]] == [("technical_coding", "heuristic"), ("technical_coding", "token"),
+                                                ("personal_health", "heuristic")]
 
 
 def test_legacy_final_results(tmp_path):
