@@ -138,7 +138,8 @@ class LLMEngine:
         self._memo_cap = 200_000
         self._memo_lock = threading.Lock()
         self.on_gpu = self.device.type == "cuda"
-        self.use_graphs = use_graphs and self.on_gpu
+        # expert-parallel MoE exchanges split sizes on the host (parallel.expert_parallel): eager
+        self.use_graphs = use_graphs and self.on_gpu and not getattr(self.model, "moe_ep", False)
         self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
         self._gen.manual_seed(seed + 1)
         self._seed_base = (seed * 0x9E3779B1 + 0x5851F42D) & 0x7FFFFFFF

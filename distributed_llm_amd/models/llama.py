@@ -61,6 +61,12 @@ class LlamaModel:
         self.d = cfg.head_dim
         self.I = cfg.intermediate // tp
         self.vocab_shard = shard_range(cfg.vocab, r, tp)
+        # MoE sharding: TP-within-expert (default; one all-reduce, graph-capturable) or expert
+        # parallel (E/tp whole experts per rank, all-to-all dispatch/combine: parallel.expert_parallel)
+        self.moe_ep = bool(cfg.is_moe and tp > 1 and (par.moe_ep or os.environ.get("DLLM_MOE_PARALLEL") == "ep"))
+        if self.moe_ep and cfg.n_experts % tp:
+            raise ValueError(f"{cfg.name}: n_experts {cfg.n_experts} must divide ep={tp}")
+        self.expert_shard = shard_range(cfg.n_experts, r, tp) if self.moe_ep else slice(0, cfg.n_experts)
         self.scale = 1.0 / math.sqrt(self.d)
         self.layers: List[Dict[str, torch.Tensor]] = []
         self._init_random(seed, init_std)
@@ -98,10 +104,13 @@ class LlamaModel:
                 L["wgate"] = rnd(E, H)
                 w13 = []
                 w2 = []
-                for _e in range(E):
+                esl = self.expert_shard
+                fsl = slice(0, cfg.intermediate) if self.moe_ep else isl
+                for e in range(E):  # every rank draws every expert (same stream), keeps its part
                     gate, up, down = rnd(cfg.intermediate, H), rnd(cfg.intermediate, H), rnd(H, cfg.intermediate)
-                    w13.append(torch.cat([gate[isl], up[isl]], 0))
-                    w2.append(down[:, isl])
+                    if esl.start <= e < esl.stop:
+                        w13.append(torch.cat([gate[fsl], up[fsl]], 0))
+                        w2.append(down[:, fsl])
                 L["w13"] = torch.stack(w13).contiguous()   # [E, 2I, H]
                 L["w2"] = torch.stack(w2).contiguous()     # [E, H, I]
             else:
@@ -143,11 +152,13 @@ class LlamaModel:
             if cfg.is_moe:
                 pm = p + "block_sparse_moe."
                 L["wgate"] = put(tensors[pm + "gate.weight"])
-                L["w13"] = put(torch.stack([torch.cat([tensors[pm + f"experts.{e}.w1.weight"][isl],
-                                                       tensors[pm + f"experts.{e}.w3.weight"][isl]], 0)
-                                            for e in range(cfg.n_experts)]))
-                L["w2"] = put(torch.stack([tensors[pm + f"experts.{e}.w2.weight"][:, isl]
-                                           for e in range(cfg.n_experts)]))
+                esl = self.expert_shard
+                fsl = slice(0, cfg.intermediate) if self.moe_ep else isl
+                L["w13"] = put(torch.stack([torch.cat([tensors[pm + f"experts.{e}.w1.weight"][fsl],
+                                                       tensors[pm + f"experts.{e}.w3.weight"][fsl]], 0)
+                                            for e in range(esl.start, esl.stop)]))
+                L["w2"] = put(torch.stack([tensors[pm + f"experts.{e}.w2.weight"][:, fsl]
+                                           for e in range(esl.start, esl.stop)]))
             elif p + "mlp.gate_up_proj.weight" in tensors:
                 w = tensors[p + "mlp.gate_up_proj.weight"]
                 I = cfg.intermediate
@@ -186,6 +197,19 @@ class LlamaModel:
         ids, w = ops.moe_gate(F.linear(x, L["wgate"]).float(), self.cfg.experts_per_token)
         return ops.moe_ffn(x, ids, w, L["w13"], L["w2"])
 
+    def _mlp_out(self, L, x: torch.Tensor) -> torch.Tensor:
+        """Complete (replicated) MLP output: TP partial sums all-reduced, or the expert-parallel
+        path (token slice per rank -> all-to-all dispatch/combine -> all-gather)."""
+        if not self.moe_ep:
+            return self.par.all_reduce(self._mlp(L, x))
+        from ..parallel.expert_parallel import all_gather_rows, ep_moe_ffn, token_slice
+        par, T = self.par, x.shape[0]
+        lo, hi = token_slice(T, par.tp_rank, par.tp_size)
+        xl = x[lo:hi]
+        ids, w = ops.moe_gate(F.linear(xl, L["wgate"]).float(), self.cfg.experts_per_token)
+        yl = ep_moe_ffn(xl, ids, w, L["w13"], L["w2"], self.cfg.n_experts, par.tp_group, par.tp_size)
+        return all_gather_rows(yl, T, par.tp_group, par.tp_size)
+
     def hidden_states(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Final-normed hidden states of each sequence's last new token: [S, H]."""
@@ -203,7 +227,7 @@ class LlamaModel:
                                     xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
             h = self.par.all_reduce(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
-            h = self.par.all_reduce(self._mlp(L, x))
+            h = self._mlp_out(L, x)
         last_h = h.index_select(0, meta.last_idx)
         last_r = residual.index_select(0, meta.last_idx)
         return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)

@@ -28,6 +28,7 @@ class ParallelContext:
     global_rank: int = 0
     world_size: int = 1
     custom_ar: Optional[object] = None  # parallel.custom_ar.CustomAllReduce (GPU TP groups)
+    moe_ep: bool = False                # MoE layers expert-parallel over the TP group (parallel.expert_parallel)
 
     @property
     def enabled(self) -> bool:
