@@ -16,6 +16,7 @@ int dllm_paged_attention(const void*, const void*, const void*, const int*, cons
                          const int*, const int*, void*, float*, float*, int*, const int*, const int*, int, int, int,
                          int, int, int, int, int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
+int dllm_embed(const int*, const void*, void*, long, int, long, long, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
 int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
@@ -200,6 +201,17 @@ void silu_mul(torch::Tensor gu, torch::Tensor out) {
   const int I = gu.size(1) / 2;
   TORCH_CHECK(out.size(0) == T && out.size(1) == I, "out shape");
   ok(dllm_silu_mul(gu.data_ptr(), out.data_ptr(), T, I, gu.stride(0), stream()), "silu_mul");
+}
+
+void embed(torch::Tensor ids, torch::Tensor table, torch::Tensor out, int64_t lo) {
+  TORCH_CHECK(ids.scalar_type() == torch::kInt && ids.is_contiguous() && ids.is_cuda(), "ids: contiguous int32");
+  check_bf16(table, "table");
+  check_bf16(out, "out");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && out.is_contiguous(), "table [rows, H] contiguous");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == ids.numel() && out.size(1) == table.size(1), "out [T, H]");
+  ok(dllm_embed(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), table.size(1), lo,
+                table.size(0), stream()),
+     "embed");
 }
 
 void gelu(torch::Tensor x, torch::Tensor y) {
@@ -457,6 +469,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("kv_write", &kv_write);
   m.def("paged_attention", &paged_attention);
   m.def("silu_mul", &silu_mul);
+  m.def("embed", &embed);
   m.def("gelu", &gelu);
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("moe_gate", &moe_gate);

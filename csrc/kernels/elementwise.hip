@@ -3,6 +3,8 @@
 //   gelu         : y = 0.5 x (1 + erf(x / sqrt 2))                    (MiniLM FFN)
 //   mean_pool_l2 : out[b] = normalize(sum_s mask[b,s] x[b,s,:] / sum_s mask[b,s])   (sentence embedding)
 //   moe_gate_topk: softmax over E experts, top-k, renormalised weights (Mixtral routing)
+//   embed        : out[t] = table[ids[t] - lo] if lo <= ids[t] < lo + rows else 0   (token embedding;
+//                  the masked form is the vocab-parallel shard of a TP rank, summed by the all-reduce)
 #include "common.h"
 
 namespace {
@@ -19,6 +21,20 @@ __global__ void silu_mul_kernel(const u16* __restrict__ gu, u16* __restrict__ ou
     for (int j = 0; j < 8; ++j) o[j] = gf[j] / (1.f + __expf(-gf[j])) * uf[j];
     st16(out + t * (long)I + c, pack8(o));
   }
+}
+
+// one wave per token row, 16-B vectors; rows of a 288 GB-resident table are gathered straight to
+// registers (a random-row gather reads at ~5.5 TB/s: MI355X_MICROARCH.md)
+__global__ void __launch_bounds__(256) embed_kernel(const int* __restrict__ ids, const u16* __restrict__ table,
+                                                    u16* __restrict__ out, long T, int H, long lo, long rows) {
+  const long t = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const long r = ids[t] - lo;
+  const bool ok = r >= 0 && r < rows;
+  const u16* src = table + (ok ? r : 0) * (long)H;
+  u16* dst = out + t * (long)H;
+  for (int c = (threadIdx.x & 63) * 8; c < H; c += 64 * 8)
+    st16(dst + c, ok ? ld16(src + c) : make_uint4(0, 0, 0, 0));
 }
 
 __global__ void gelu_kernel(const u16* __restrict__ x, u16* __restrict__ y, long n8) {
@@ -102,6 +118,15 @@ extern "C" int dllm_silu_mul(const void* gu, void* out, long T, int I, long in_s
   if (n == 0) return 0;
   hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u16*)gu, (u16*)out, T, I,
                      in_stride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_embed(const int* ids, const void* table, void* out, long T, int H, long lo, long rows,
+                          hipStream_t stream) {
+  if (H % 8 != 0) return -1;
+  if (T == 0) return 0;
+  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, stream, ids, (const u16*)table,
+                     (u16*)out, T, H, lo, rows);
   return (int)hipGetLastError();
 }
 

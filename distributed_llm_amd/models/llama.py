@@ -177,13 +177,10 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ forward
     def _embed(self, ids: torch.Tensor) -> torch.Tensor:
-        if self.par.tp_size == 1:
-            return F.embedding(ids, self.embed)
-        lo = self.vocab_shard.start
-        local = ids - lo
-        ok = (local >= 0) & (local < self.embed.shape[0])
-        h = F.embedding(local.clamp(0, self.embed.shape[0] - 1), self.embed) * ok.unsqueeze(-1).to(self.dtype)
-        return self.par.all_reduce(h)
+        # HIP row gather; under TP each rank gathers its vocab shard (zero rows elsewhere) and the
+        # all-reduce assembles the embeddings
+        h = ops.embedding(ids, self.embed, self.vocab_shard.start)
+        return self.par.all_reduce(h) if self.par.tp_size > 1 else h
 
     def _mlp(self, L, x: torch.Tensor) -> torch.Tensor:
         if not self.cfg.is_moe:

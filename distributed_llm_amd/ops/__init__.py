@@ -208,6 +208,18 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     return o
 
 
+def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0) -> torch.Tensor:
+    """Row gather ``table[ids - lo]`` -> [T, H]; ids outside ``[lo, lo + rows)`` give zero rows
+    (vocab-parallel shard of a TP rank: the all-reduce then sums the owners' rows)."""
+    ext = _native(table)
+    if ext is None:
+        return ref.embedding(ids, table, lo)
+    ids = ids.reshape(-1).to(torch.int32).contiguous()
+    out = torch.empty((ids.numel(), table.shape[1]), dtype=table.dtype, device=table.device)
+    ext.embed(ids, table, out, int(lo))
+    return out
+
+
 def gelu(x: torch.Tensor) -> torch.Tensor:
     ext = _native(x)
     if ext is None:

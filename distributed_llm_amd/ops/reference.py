@@ -239,3 +239,10 @@ def masked_cosine_argmax(q, table, norms, ctx, cid, thr) -> Tuple[int, float]:
     j = int(torch.argmax(sims))
     s = float(sims[j])
     return (j, s) if s >= thr else (-1, 0.0)
+
+
+def embedding(ids, table, lo=0):
+    """fp32-free reference of ops.embedding (exact row copies, zero rows outside the shard)."""
+    local = ids.reshape(-1).long() - lo
+    ok = (local >= 0) & (local < table.shape[0])
+    return table[local.clamp(0, table.shape[0] - 1)] * ok.unsqueeze(-1).to(table.dtype)

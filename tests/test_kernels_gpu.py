@@ -367,3 +367,14 @@ def test_mm_gemm(M, N, K, swiglu, nt, splits):
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
     y2 = gemm._run_plan(("mm", nt, splits), x, w, swiglu, None)   # counters re-armed
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("H,lo,rows", [(2048, 0, 1000), (4096, 500, 300), (384, 0, 77)])
+def test_embedding(H, lo, rows):
+    """HIP row gather vs torch indexing; ids outside the vocab shard [lo, lo + rows) give zero rows."""
+    torch.manual_seed(0)
+    table = bf(rows, H)
+    ids = torch.randint(0, lo + rows + 50, (257,), device=DEV, dtype=torch.int32)
+    got = ops.embedding(ids, table, lo)
+    want = ref.embedding(ids.cpu(), table.cpu(), lo).to(DEV)
+    assert torch.equal(got, want)
