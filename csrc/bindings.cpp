@@ -17,6 +17,7 @@ int dllm_paged_attention(const void*, const void*, const void*, const int*, cons
                          int, int, int, int, int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_embed(const int*, const void*, void*, long, int, long, long, hipStream_t);
+int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, int, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
 int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
@@ -359,6 +360,25 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
         part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
      "skinny_gemm");
 }
+// Small-batch GEMV (M in {1, 2, 4, 8}; csrc/kernels/gemv.hip): y = x . w^T (x = silu(g)*u if swiglu).
+void gemv(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t R, bool swiglu) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous() && y.dim() == 2 &&
+                  y.stride(1) == 1,
+              "2-D row-major operands");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M == 1 || M == 2 || M == 4 || M == 8, "gemv: M in {1, 2, 4, 8}");
+  TORCH_CHECK(x.size(1) == (swiglu ? 2 * K : K) && K % 8 == 0, "gemv: x inner dim, K % 8 == 0");
+  TORCH_CHECK((int64_t)M * K * 2 <= 64 * 1024, "gemv: M x K bf16 must fit the 64 KB LDS stage");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) >= N && y.size(0) == M && y.size(1) == N, "gemv: y shape / alignment");
+  TORCH_CHECK(R == 1 || R == 2 || R == 4, "gemv: R in {1, 2, 4}");
+  ok(dllm_gemv(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, (int)R, swiglu ? 1 : 0,
+               stream()),
+     "gemv");
+}
+
 // Mid-size decode GEMM (64 < M <= 256; csrc/kernels/mm_gemm.hip): y = x . w^T (x = silu(g)*u if swiglu).
 void mm_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t nt, int64_t splits, bool swiglu,
              torch::Tensor part, torch::Tensor counters) {
@@ -480,4 +500,5 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("cosine_scores", &cosine_scores);
   m.def("masked_cosine_argmax", &masked_cosine_argmax);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("gemv", &gemv);
 }

@@ -252,8 +252,10 @@ class LLMEngine:
     ATTN_WORKLIST = os.environ.get("DLLM_ATTN_WORKLIST", "1") == "1"
     ATTN_PGRID = int(os.environ.get("DLLM_ATTN_PGRID", "512"))
     ATTN_ITEMS_PER_WG = int(os.environ.get("DLLM_ATTN_ITEMS_PER_WG", "1"))
-    # below this batch the static split-K grid measured faster (scripts/microbench.py attn_wl)
-    ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "128"))
+    # Work list at every batch size: in a whole decode step (scripts/microbench.py decode, 1x
+    # MI355X, TinyLlama) it cut B=1 from 1.14 to 0.89 ms and B=16 from 1.51 to 1.29 ms vs the
+    # static split grid (a kernel-only sweep had B=16-64 about even)
+    ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "1"))
 
     def _use_worklist(self, bs: int) -> bool:
         return self.attn_worklist and bs >= self.ATTN_WL_MIN_BS

@@ -28,6 +28,8 @@ _SPLITS = (1, 2, 4, 8, 16)
 _NTWS = (1, 2, 4)
 _MM_NTS = (2, 4)
 _MM_SPLITS = (1, 2, 4, 8)
+_GEMV_MS = (1, 2, 4, 8)   # csrc/kernels/gemv.hip instantiations (decode buckets below 16)
+_GEMV_RS = (1, 2, 4)
 
 
 class _Planner:
@@ -90,8 +92,12 @@ def _run_plan(plan, x, w, swiglu, out):
         if swiglu:
             x = ref_silu_mul(x)
         return torch.matmul(x, w.t(), out=out) if out is not None else F.linear(x, w)
-    kind, ntw, splits = plan
     ext = _native(x)
+    if plan[0] == "gemv":
+        y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+        ext.gemv(x, w, y, plan[1], swiglu)
+        return y
+    kind, ntw, splits = plan
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
     if kind == "mm":
@@ -199,6 +205,8 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                         if floats * 4 > 256 << 20:
                             continue
                         cands.append(("mm", nt, s))
+            if M in _GEMV_MS and K % 8 == 0 and M * K * 2 <= 64 * 1024 and os.environ.get("DLLM_GEMM_NO_GEMV") != "1":
+                cands.extend(("gemv", r) for r in _GEMV_RS)
             for kind, ntws in ((("skinny", _NTWS), ("lds", (1, 2))) if M <= SKINNY_MAX_M else ()):
                 for ntw in ntws:
                     if M > 64 and (ntw == 4 or (kind == "lds" and ntw == 2)):
@@ -218,7 +226,7 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
             _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
-                      for k in ("skinny", "lds", "mm")}
+                      for k in ("gemv", "skinny", "lds", "mm")}
                 extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
                       f"({N * K * 2 / res[best] / 1e3:.0f} GB/s; blas {res[('blas',)]:.1f}us; {extra})", flush=True)

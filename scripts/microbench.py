@@ -228,8 +228,10 @@ if __name__ == "__main__":
     if "decode" in what or "prefill" in what:
         eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
         if "decode" in what:
-            for B in (1, 8, 32, 64, 128, 256):
-                for C in (512, 2048):
+            Bs = [int(x) for x in os.environ.get("MB_DECODE_B", "1,8,32,64,128,256").split(",")]
+            Cs = [int(x) for x in os.environ.get("MB_DECODE_C", "512,2048").split(",")]
+            for B in Bs:
+                for C in Cs:
                     print(json.dumps(bench_decode(eng, B, C)), flush=True)
         if "prefill" in what:
             for B, L in ((1, 512), (8, 1024), (32, 2048)):

@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-KERNELS = ["attention.hip", "skinny_gemm.hip", "skinny_lds.hip", "mm_gemm.hip", "sampling.hip", "moe.hip"]
+KERNELS = ["attention.hip", "gemv.hip", "skinny_gemm.hip", "skinny_lds.hip", "mm_gemm.hip", "sampling.hip", "moe.hip"]
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
