@@ -17,7 +17,8 @@ int dllm_paged_attention(const void*, const void*, const void*, const int*, cons
                          int, int, int, int, int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_embed(const int*, const void*, void*, long, int, long, long, hipStream_t);
-int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, int, hipStream_t);
+int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, int, const void*, void*, const void*,
+              float, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
 int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
@@ -375,8 +376,27 @@ void gemv(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t R, bool swi
   TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) >= N && y.size(0) == M && y.size(1) == N, "gemv: y shape / alignment");
   TORCH_CHECK(R == 1 || R == 2 || R == 4, "gemv: R in {1, 2, 4}");
   ok(dllm_gemv(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, (int)R, swiglu ? 1 : 0,
-               stream()),
+               nullptr, nullptr, nullptr, 0.f, stream()),
      "gemv");
+}
+
+// RMSNorm-fused GEMV: r = x + res_in -> res_out (bf16), y = rmsnorm(r) * norm_w . w^T
+void gemv_norm(torch::Tensor x, torch::Tensor res_in, torch::Tensor res_out, torch::Tensor norm_w, double eps,
+               torch::Tensor w, torch::Tensor y, int64_t R) {
+  for (auto* t : {&x, &res_in, &res_out, &norm_w, &w, &y}) check_bf16(*t, "gemv_norm operand");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M == 1 || M == 2 || M == 4 || M == 8, "gemv_norm: M in {1, 2, 4, 8}");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) == K && K % 8 == 0, "gemv_norm: x [M, K]");
+  TORCH_CHECK(res_in.is_contiguous() && res_out.is_contiguous() && res_in.sizes() == x.sizes() &&
+                  res_out.sizes() == x.sizes() && res_in.data_ptr() != res_out.data_ptr(),
+              "gemv_norm: res_in/res_out [M, K], distinct");
+  TORCH_CHECK(norm_w.numel() == K && w.is_contiguous() && y.dim() == 2 && y.size(0) == M && y.size(1) == N &&
+                  y.stride(1) == 1,
+              "gemv_norm: shapes");
+  TORCH_CHECK((int64_t)M * K * 2 <= 64 * 1024 && (R == 1 || R == 2 || R == 4), "gemv_norm: LDS stage / R");
+  ok(dllm_gemv(x.data_ptr(), K, w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, (int)R, 0, res_in.data_ptr(),
+               res_out.data_ptr(), norm_w.data_ptr(), (float)eps, stream()),
+     "gemv_norm");
 }
 
 // Mid-size decode GEMM (64 < M <= 256; csrc/kernels/mm_gemm.hip): y = x . w^T (x = silu(g)*u if swiglu).
@@ -501,4 +521,5 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("masked_cosine_argmax", &masked_cosine_argmax);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);
+  m.def("gemv_norm", &gemv_norm);
 }

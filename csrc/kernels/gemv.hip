@@ -13,6 +13,8 @@
 //     [M, 2K] and silu(gate) * up is formed in the staging pass (the down projection absorbs the
 //     activation kernel);
 //   * the next W trip is issued before the current one is consumed (register double buffer);
+//   * NORM: the pre-projection RMSNorm (+ residual add) runs in the staging pass, so a decode
+//     layer at batch <= 8 drops both norm launches (norm.hip) from its chain;
 //   * f32 FMA, one 64-lane butterfly reduction per (row, column) at the end; no split-K, no
 //     workspace, no inter-workgroup traffic: one launch per projection, graph-capturable.
 // Chosen per (M, N, K) by the host autotuner (ops.gemm) only where it beats the other plans.
@@ -20,9 +22,16 @@
 
 namespace {
 
-template <int M, int R, int UNR, bool SWIGLU>
+struct NormArgs {         // NORM: X is the sub-layer output h; the kernel forms r = h + res_in (bf16),
+  const u16* res_in;     // workgroup 0 stores r to res_out (a different buffer: every workgroup
+  u16* res_out;          // reads res_in), and the GEMV input is rmsnorm(r) * w  (norm.hip numerics)
+  const u16* w;
+  float eps;
+};
+
+template <int M, int R, int UNR, bool SWIGLU, bool NORM>
 __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, long ldx, const u16* __restrict__ W,
-                                                   u16* __restrict__ Y, long ldy, int N, int K) {
+                                                   u16* __restrict__ Y, long ldy, int N, int K, NormArgs na) {
   extern __shared__ uint4 xs_raw[];  // X (SwiGLU applied) staged once per workgroup: [M][K] bf16
   u16* xs = reinterpret_cast<u16*>(xs_raw);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -42,6 +51,45 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
         (active && k_ < K) ? __builtin_bit_cast(uint4, ldnt_bf16x8(wr[r] + k_)) : make_uint4(0, 0, 0, 0); \
   }
   DLLM_GEMV_LOAD(w, 0)  // the first trip of W is in flight while X is staged
+  if constexpr (NORM) {
+    float* red = reinterpret_cast<float*>(xs + (long)M * K);  // [4 waves][M]
+    float ss[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      ss[m] = 0.f;
+      for (int c8 = threadIdx.x; c8 < (K >> 3); c8 += 256) {
+        const int c = c8 << 3;
+        float a[8], b[8];
+        unpack8(ld16(X + (long)m * ldx + c), a);
+        unpack8(ld16(na.res_in + (long)m * K + c), b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        const uint4 pk = pack8(a);  // the residual stream stays bf16
+        if (blockIdx.x == 0) st16(na.res_out + (long)m * K + c, pk);
+        st16(xs + (long)m * K + c, pk);
+        unpack8(pk, a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss[m] += a[j] * a[j];
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) ss[m] += __shfl_xor(ss[m], o, 64);
+      if (lane == 0) red[wave * M + m] = ss[m];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float rstd = rsqrtf((red[m] + red[M + m] + red[2 * M + m] + red[3 * M + m]) / K + na.eps);
+      for (int c8 = threadIdx.x; c8 < (K >> 3); c8 += 256) {
+        const int c = c8 << 3;
+        float a[8], g[8];
+        unpack8(ld16(xs + (long)m * K + c), a);
+        unpack8(ld16(na.w + c), g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = a[j] * rstd * g[j];
+        st16(xs + (long)m * K + c, pack8(a));  // each thread rewrites only the vectors it wrote
+      }
+    }
+  } else {
   for (int v = threadIdx.x; v < M * (K >> 3); v += 256) {
     const int m = v / (K >> 3), c = (v - m * (K >> 3)) << 3;
     uint4 xv = ld16(X + (long)m * ldx + c);
@@ -54,6 +102,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
       xv = pack8(g);  // bf16, as the unfused silu_mul output the GEMM would read
     }
     st16(xs + (long)m * K + c, xv);
+  }
   }
   __syncthreads();
 
@@ -107,33 +156,36 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
   }
 }
 
-template <int M, int R, bool SW>
-void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, hipStream_t stream) {
+template <int M, int R, bool SW, bool NORM>
+void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
+                 hipStream_t stream) {
   constexpr int UNR = M <= 2 ? 4 : 2;
   const unsigned blocks = (unsigned)((N + 4 * R - 1) / (4 * R));
-  hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW>), dim3(blocks), dim3(256), (size_t)M * K * 2, stream, (const u16*)x, ldx,
-                     (const u16*)w, (u16*)y, ldy, N, K);
+  const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0);
+  hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM>), dim3(blocks), dim3(256), lds, stream, (const u16*)x, ldx,
+                     (const u16*)w, (u16*)y, ldy, N, K, na);
 }
 
-template <int M, bool SW>
-int dispatch_r(int R, const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, hipStream_t s) {
+template <int M, bool SW, bool NORM>
+int dispatch_r(int R, const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
+               hipStream_t s) {
   switch (R) {
-    case 1: launch_gemv<M, 1, SW>(x, ldx, w, y, ldy, N, K, s); break;
-    case 2: launch_gemv<M, 2, SW>(x, ldx, w, y, ldy, N, K, s); break;
-    case 4: launch_gemv<M, 4, SW>(x, ldx, w, y, ldy, N, K, s); break;
+    case 1: launch_gemv<M, 1, SW, NORM>(x, ldx, w, y, ldy, N, K, na, s); break;
+    case 2: launch_gemv<M, 2, SW, NORM>(x, ldx, w, y, ldy, N, K, na, s); break;
+    case 4: launch_gemv<M, 4, SW, NORM>(x, ldx, w, y, ldy, N, K, na, s); break;
     default: return -2;
   }
   return 0;
 }
 
-template <bool SW>
+template <bool SW, bool NORM>
 int dispatch_m(int Mp, int R, const void* x, long ldx, const void* w, void* y, long ldy, int N, int K,
-               hipStream_t s) {
+               const NormArgs& na, hipStream_t s) {
   switch (Mp) {
-    case 1: return dispatch_r<1, SW>(R, x, ldx, w, y, ldy, N, K, s);
-    case 2: return dispatch_r<2, SW>(R, x, ldx, w, y, ldy, N, K, s);
-    case 4: return dispatch_r<4, SW>(R, x, ldx, w, y, ldy, N, K, s);
-    case 8: return dispatch_r<8, SW>(R, x, ldx, w, y, ldy, N, K, s);
+    case 1: return dispatch_r<1, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
+    case 2: return dispatch_r<2, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
+    case 4: return dispatch_r<4, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
+    case 8: return dispatch_r<8, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
     default: return -1;
   }
 }
@@ -144,10 +196,19 @@ constexpr long GEMV_MAX_LDS = 64 * 1024;  // staged X bytes per workgroup (M x K
 // M must be 1, 2, 4 or 8 (the decode buckets below 16; the autotuner offers this kernel only
 // for them); K % 8 == 0; M x K x 2 B <= 64 KB; rows of X, W and Y 16-B aligned.
 extern "C" int dllm_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int M, int N, int K, int R,
-                         int swiglu, hipStream_t stream) {
+                         int swiglu, const void* res_in, void* res_out, const void* norm_w, float eps,
+                         hipStream_t stream) {
   if (K % 8 != 0 || N <= 0 || (long)M * K * 2 > GEMV_MAX_LDS) return -3;
-  const int rc = swiglu ? dispatch_m<true>(M, R, x, ldx, w, y, ldy, N, K, stream)
-                        : dispatch_m<false>(M, R, x, ldx, w, y, ldy, N, K, stream);
+  const bool norm = norm_w != nullptr;
+  if (norm && (swiglu || !res_in || !res_out || res_in == res_out || ldx % 8)) return -4;
+  const NormArgs na{(const u16*)res_in, (u16*)res_out, (const u16*)norm_w, eps};
+  int rc;
+  if (norm)
+    rc = dispatch_m<false, true>(M, R, x, ldx, w, y, ldy, N, K, na, stream);
+  else if (swiglu)
+    rc = dispatch_m<true, false>(M, R, x, ldx, w, y, ldy, N, K, na, stream);
+  else
+    rc = dispatch_m<false, false>(M, R, x, ldx, w, y, ldy, N, K, na, stream);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

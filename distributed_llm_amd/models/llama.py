@@ -6,6 +6,7 @@ tied embeddings and dense-vs-MoE MLP (models.configs).  MI355X-first layout deci
     (hipBLASLt via F.linear, K-contiguous "TN" operands);
   * RoPE + paged-KV write fused in one kernel reading the QKV GEMM output in place;
   * RMSNorm fused with the residual add (the residual stream is read/written once per norm);
+    ops.norm_linear can also fold it into a batch <= 8 GEMV (opt-in, measured slower);
   * the LM head runs only on the last position of each sequence;
   * tensor parallel (Megatron column/row split): QKV / gate|up column-parallel, o_proj /
     down_proj row-parallel + ONE all-reduce each, vocab-parallel embedding (masked lookup +
@@ -213,9 +214,10 @@ class LlamaModel:
         cfg = self.cfg
         h = self._embed(input_ids)
         residual = torch.zeros_like(h)
+        spare = torch.empty_like(h)   # ping-pong partner: a fused norm+GEMV writes the new residual here
         for li, L in enumerate(self.layers):
-            x = ops.rms_norm(h, L["ln1"], cfg.rms_eps, residual=residual)
-            qkv = ops.linear(x, L["wqkv"])
+            qkv, res = ops.norm_linear(h, residual, spare, L["ln1"], cfg.rms_eps, L["wqkv"])
+            residual, spare = res, (spare if res is residual else residual)
             kc, vc = kv_caches[li]
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
             o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
@@ -223,8 +225,13 @@ class LlamaModel:
                                     splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
                                     xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
             h = self.par.all_reduce(ops.linear(o.view(o.shape[0], -1), L["wo"]))
-            x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
-            h = self._mlp_out(L, x)
+            if not self.cfg.is_moe:
+                gu, res = ops.norm_linear(h, residual, spare, L["ln2"], cfg.rms_eps, L["wgu"])
+                residual, spare = res, (spare if res is residual else residual)
+                h = self.par.all_reduce(ops.linear_swiglu(gu, L["wd"]))
+            else:
+                x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
+                h = self._mlp_out(L, x)
         last_h = h.index_select(0, meta.last_idx)
         last_r = residual.index_select(0, meta.last_idx)
         return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)

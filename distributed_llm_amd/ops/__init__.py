@@ -335,7 +335,7 @@ def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tens
     return int(row), float(sim)
 
 
-from .gemm import autotune as gemm_autotune, linear, linear_swiglu  # noqa: E402
+from .gemm import autotune as gemm_autotune, linear, linear_swiglu, norm_linear  # noqa: E402
 
 
 def scatter_pairs(dst: torch.Tensor, buf: torch.Tensor) -> None:

@@ -128,6 +128,32 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     return _run_plan(plan, x, w, False, out)
 
 
+def norm_linear(h: torch.Tensor, residual: torch.Tensor, spare: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``linear(rmsnorm(h + residual) * norm_w, w)`` and the updated residual stream.
+
+    Where the tuned plan for this shape is the GEMV (batch <= 8), one launch does both
+    (csrc/kernels/gemv.hip NORM): the new residual goes to ``spare`` and is returned; otherwise
+    the norm kernel updates ``residual`` in place and it is returned.  Callers keep whichever
+    buffer comes back as the residual and the other one as the next spare.
+
+    Opt-in (DLLM_FUSED_NORM=1): measured SLOWER on MI355X at batch 1 (0.954 vs 0.889 ms per
+    TinyLlama decode step, profiles/r1_small_batch_decode.md) -- every GEMV workgroup redoes the
+    norm's reduction and two extra L2 round trips sit before its first FMA, which costs more
+    than the separate 4.5 us norm launch it removes."""
+    M, N, K = h.shape[0], w.shape[0], w.shape[1]
+    if h.is_cuda and M <= MAX_M and os.environ.get("DLLM_GEMM") != "blas" \
+            and os.environ.get("DLLM_FUSED_NORM", "0") == "1":
+        plan = _P.plans.get((M, N, K, False))
+        if plan is not None and plan[0] == "gemv" and h.is_contiguous() and M * K * 2 <= 64 * 1024:
+            y = torch.empty((M, N), dtype=h.dtype, device=h.device)
+            _native(h).gemv_norm(h, residual, spare, norm_w, float(eps), w, y, plan[1])
+            return y, spare
+    from . import rms_norm
+    x = rms_norm(h, norm_w, eps, residual=residual)
+    return linear(x, w), residual
+
+
 def linear_swiglu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``silu(gate) * up @ w.T`` with gu = [gate | up] of width 2K."""
     if not gu.is_cuda:

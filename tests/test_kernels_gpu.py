@@ -397,3 +397,22 @@ def test_gemv(M, N, K, swiglu, R):
     want = xe @ w.float().t()
     got = G._run_plan(("gemv", R), x, w, swiglu, None)
     torch.testing.assert_close(got.float(), want, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+@pytest.mark.parametrize("N,K", [(2560, 2048), (11264, 2048), (333, 1032)])
+def test_gemv_norm(M, N, K):
+    """RMSNorm-fused GEMV: y and the new residual match norm kernel semantics (bf16 residual)."""
+    if M * K * 2 > 64 * 1024:
+        pytest.skip("X stage exceeds the 64 KB LDS limit")
+    torch.manual_seed(M + N)
+    h, res, nw = bf(M, K), bf(M, K), bf(K)
+    w = bf(N, K, scale=0.05)
+    res_ref = res.clone()
+    xn = ref.rms_norm(h, nw, 1e-5, residual=res_ref)
+    want = xn.float() @ w.float().t()
+    spare = torch.full_like(res, 7.0)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops._load().gemv_norm(h, res, spare, nw, 1e-5, w, y, 2)
+    assert torch.equal(spare, res_ref)
+    torch.testing.assert_close(y.float(), want, atol=3e-2, rtol=2e-2)
