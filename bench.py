@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--kv-gb", type=float, default=64.0)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (tiny model)")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="G > 1: G independently pipelined groups of conversations, one thread each")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: turn pipelining (replicated topology): conversations advance independently")
     return ap.parse_args()
@@ -163,6 +165,67 @@ class PipelinedConversations(Conversations):
             t.join()
 
 
+class GroupedConversations(PipelinedConversations):
+    """Turn pipelining with few threads: G groups of conversations, each driven by ONE thread in
+    lock-step (route the group's turn as a batch -> serve -> next turn), groups independent.
+
+    A group still waits for its slowest answer, but while it routes and formats its next turn or
+    drains its long large-tier answers, the other groups' requests keep the engine's continuous
+    batch full; unlike one thread per conversation (``PipelinedConversations``) this adds only
+    G Python threads, so routing does not fight 512 threads for the GIL.  Same steady-state
+    window accounting as the parent (a step = ``n_convs`` completed turns)."""
+
+    def __init__(self, n: int, rank: int, groups: int):
+        super().__init__(n, rank)
+        self.groups = max(1, min(groups, n))
+
+    def start(self, router) -> None:
+        import threading
+        self._cv = threading.Condition()
+        self.completed = 0
+        self.records = None
+        self._stop = False
+        self.errors = []
+        idx = [list(range(g, len(self.convs), self.groups)) for g in range(self.groups)]
+
+        def worker(ids):
+            try:
+                while not self._stop:
+                    hs = []
+                    for i in ids:
+                        c = self.convs[i]
+                        q = c["set"][c["turn"]].text
+                        if c["turn"] == 0:
+                            q = c["tag"] + q
+                        c["hist"].append({"role": "user", "content": q})
+                        hs.append(c["hist"])
+                    res = router.route_batch(hs)
+                    recs = []
+                    for i, (payload, ntok, device) in zip(ids, res):
+                        c = self.convs[i]
+                        c["hist"].append({"role": "assistant", "content": payload["response"]})
+                        raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
+                        recs.append({"lat": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
+                                     "ovh": float(payload.get("routing_overhead_ms", 0.0)),
+                                     "ttft": float((raw.get("timing") or {}).get("ttft_ms", 0.0))})
+                        c["turn"] += 1
+                        if c["turn"] >= len(c["set"]):
+                            self.convs[i] = self._new(i)
+                    with self._cv:
+                        if self.records is not None:
+                            self.records.extend(recs)
+                        self.completed += len(recs)
+                        self._cv.notify_all()
+            except BaseException as e:  # surfaced by wait_turns
+                with self._cv:
+                    self.errors.append(e)
+                    self._cv.notify_all()
+
+        self._threads = [threading.Thread(target=worker, args=(ids,), daemon=True) for ids in idx]
+        for t in self._threads:
+            t.start()
+
+
 def main() -> int:
     a = parse()
     import torch
@@ -241,11 +304,12 @@ def main() -> int:
         pools_for_router = cluster.router_pools() if cluster is not None else pools
         router = Router(strategy=a.strategy, config=cfg, threshold_fallback=a.threshold, benchmark_mode=False,
                         pools=pools_for_router)
-        pipelined = bool(a.pipeline) and cluster is None
+        pipelined = (bool(a.pipeline) or a.groups > 1) and cluster is None
         if pipelined:
             for e in engines:
                 e.start()              # background step loop: callers only enqueue and wait
-            convs = PipelinedConversations(n_convs, rank)
+            convs = (GroupedConversations(n_convs, rank, a.groups) if a.groups > 1
+                     else PipelinedConversations(n_convs, rank))
             convs.start(router)
             convs.wait_turns(a.warmup * n_convs)
         else:
@@ -317,7 +381,8 @@ def main() -> int:
             "config": {"model": model_desc, "global_batch": a.convs * world,
                        "seq_len": "growing conversation (<=16384)", "parallelism": parallelism,
                        "strategy": a.strategy, "semantic_cache": True, "response_cache": False,
-                       "turn_pipelining": bool(a.pipeline) and topology == "replicated",
+                       "turn_pipelining": (bool(a.pipeline) or a.groups > 1) and topology == "replicated",
+                       "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
             "p50_latency_ms": round(statistics.median(lats), 1) if lats else None,
             "p90_latency_ms": round(pct(0.9), 1),
