@@ -59,6 +59,9 @@ def parse():
                     help="G > 1: G independently pipelined groups of conversations, one thread each")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: turn pipelining (replicated topology): conversations advance independently")
+    ap.add_argument("--trace", default=None,
+                    help="write a Chrome trace (router/pool/engine spans, GPU decode time) to this path; "
+                         "'{rank}' is replaced by the rank")
     return ap.parse_args()
 
 
@@ -235,6 +238,9 @@ def main() -> int:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if a.trace:
+        from distributed_llm_amd.utils.tracing import tracer
+        tracer.enable(a.trace.replace("{rank}", str(rank)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     on_gpu = torch.cuda.is_available() and not a.cpu
     if world > 1:
@@ -402,6 +408,9 @@ def main() -> int:
                                               "t_decode_host_post_s")},
         }
         print(json.dumps(out), flush=True)
+    if a.trace:
+        from distributed_llm_amd.utils.tracing import tracer
+        tracer.dump()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

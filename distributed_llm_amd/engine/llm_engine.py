@@ -33,6 +33,7 @@ from .. import ops
 from ..models.configs import ModelConfig, get_model_config
 from ..models.llama import AttnMeta, LlamaModel
 from ..parallel.comm import SINGLE, ParallelContext
+from ..utils.tracing import tracer
 from .sampling import SamplingParams
 from .tokenizer import get_tokenizer
 
@@ -476,7 +477,8 @@ class LLMEngine:
                 continue
             if prefilling:
                 _t = time.perf_counter()
-                done = self._prefill_step(prefilling)
+                with tracer.span("engine.prefill", "engine", seqs=len(prefilling)):
+                    done = self._prefill_step(prefilling)
                 self.timers["prefill"] += time.perf_counter() - _t
                 for s in done:
                     prefilling.remove(s)
@@ -485,7 +487,11 @@ class LLMEngine:
                     else:
                         running.append(s)
                 continue
-            self._decode_step(running)
+            with tracer.span("engine.decode", "engine", batch=len(running)):
+                self._decode_step(running)
+            if tracer.enabled:
+                tracer.counter("engine.batch", running=len(running), waiting=len(waiting),
+                               free_kv_blocks=self.bm.num_free_blocks())
             _t = time.perf_counter()
             for s in [s for s in running if self._finished(s)]:
                 running.remove(s)
@@ -699,13 +705,14 @@ class LLMEngine:
         if n_items:
             self.items_dev[:n_items].copy_(self.items_host_t[:n_items], non_blocking=True)
         _t1 = time.perf_counter()
-        if self.use_graphs:
-            g = self._graphs.get(bs)
-            if g is None:
-                g = self._capture(bs)
-            g.replay()
-        else:
-            self._decode_forward(bs)
+        with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=self.use_graphs):
+            if self.use_graphs:
+                g = self._graphs.get(bs)
+                if g is None:
+                    g = self._capture(bs)
+                g.replay()
+            else:
+                self._decode_forward(bs)
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
         if self.fused_sampler:

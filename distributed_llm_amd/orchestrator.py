@@ -29,6 +29,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 from .config import LARGE, PRODUCTION_CFG, BENCHMARK_CFG, SMALL, other_tier
 from .router.query_router import QueryRouter
 from .router.tokens import TokenCounter
+from .utils.tracing import tracer
 
 logger = logging.getLogger(__name__)
 
@@ -137,7 +138,9 @@ class Router:
     def _decide(self, query: str, context: Optional[str], ctx_hash: str, history) -> Dict[str, Any]:
         t0 = time.perf_counter()
         try:
-            d = self.query_router.route_query(query=query, context=context, context_key=ctx_hash)
+            with tracer.span("route.decide", "router") as targs:
+                d = self.query_router.route_query(query=query, context=context, context_key=ctx_hash)
+                targs.update(device=d.device, method=d.method, cache_hit=bool(d.cache_hit))
             out = {"device": d.device, "method": d.method, "confidence": float(d.confidence),
                    "reasoning": d.reasoning, "cache_hit": d.cache_hit}
         except Exception as exc:
@@ -195,7 +198,8 @@ class Router:
     def _run(self, device: str, history) -> Tuple[Any, str, float]:
         t0 = time.perf_counter()
         try:
-            raw = self.pools[device].process(history)
+            with tracer.span("pool.process", "pool", device=device):
+                raw = self.pools[device].process(history)
         except Exception as exc:  # a pool that raises is an error response, not a crash
             raw = {"error": f"pool {device} failed: {exc}"}
         return raw, device, (time.perf_counter() - t0) * 1000.0
@@ -317,7 +321,8 @@ class Router:
         hs = {dev: [histories[i] for i in idxs] for dev, idxs in groups.items() if idxs}
         t0 = time.perf_counter()
         try:
-            res = dispatch_groups(self.pools, hs)
+            with tracer.span("pool.dispatch_groups", "pool", **{dev: len(h) for dev, h in hs.items()}):
+                res = dispatch_groups(self.pools, hs)
         except Exception as exc:
             res = {dev: [{"error": f"pool {dev} failed: {exc}"}] * len(h) for dev, h in hs.items()}
         wall = (time.perf_counter() - t0) * 1000.0

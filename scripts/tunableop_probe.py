@@ -71,7 +71,7 @@ def main():
                      tune_s=round(tune_s, 2))
             print(json.dumps(r), flush=True)
             rows.append(r)
-    if mode == "tuned":
+    if mode == "tuned" and hasattr(tun, "write_file"):
         tun.write_file()
     if out:
         with open(out, "a") as f:
