@@ -3,6 +3,8 @@ engine / orchestrator spans of one routed request on CPU."""
 import json
 import threading
 
+import pytest
+
 from distributed_llm_amd.utils.tracing import Tracer, tracer
 
 
@@ -79,3 +81,20 @@ def test_routed_request_spans(tmp_path):
     doc = json.load(open(tracer.dump()))
     assert doc["traceEvents"]
     tracer.clear()
+
+
+@pytest.mark.gpu
+def test_gpu_span_times_device_work():
+    import torch
+    t = Tracer().enable()
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    with t.gpu_span("mm", n=4096):
+        for _ in range(8):
+            a = a @ a.t() * 1e-3
+    ev = [e for e in t.events() if e["name"] == "mm"]
+    gpu = [e for e in ev if str(e["tid"]).startswith("gpu:")]
+    host = [e for e in ev if not str(e["tid"]).startswith("gpu:")]
+    assert len(gpu) == 1 and len(host) == 1
+    # 8 x 137 GFLOP takes well over 100 us on the device even at peak
+    assert gpu[0]["dur"] > 100.0 and gpu[0]["args"] == {"n": 4096}
+    assert "mm[gpu]" in t.summary()
