@@ -1,259 +1,12 @@
-// Paged-KV block manager with hash-chained prefix caching (native serving runtime).
-//
-// The reference re-sends the WHOLE conversation every turn (src/router.py:161-167 ->
-// src/devices/nano_api.py:49-52) and Ollama re-prefills it.  Here every full 16-token KV block
-// is content-addressed by a hash chained over all tokens before it, so a new turn of the same
-// conversation re-uses the previous turn's blocks and only prefills the new suffix.
-//
-// Lifecycle of a block:  free -> owned (ref >= 1) -> [committed: hash registered] ->
-// ref drops to 0 -> evictable (LRU, still matchable) -> re-used by a later prompt, or
-// recycled for new data (oldest first).
-// Hashes are registered only by commit(), i.e. after the forward pass that wrote the block's
-// K/V, so a prompt can never match a block whose contents are not computed yet.
+// pybind11 module `_runtime`: Python binding of the native paged-KV block manager
+// (core in block_manager.h).
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <cstdint>
-#include <list>
-#include <stdexcept>
-#include <unordered_map>
-#include <vector>
+#include "block_manager.h"
 
 namespace py = pybind11;
-
-namespace {
-
-inline uint64_t mix(uint64_t h, int32_t tok) {
-  h ^= (uint64_t)(uint32_t)tok + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
-  h ^= h >> 31;
-  h *= 0xbf58476d1ce4e5b9ull;
-  h ^= h >> 29;
-  return h;
-}
-
-struct Block {
-  int ref = 0;
-  bool hashed = false;
-  uint64_t hash = 0;
-  std::list<int>::iterator lru_it;
-  bool in_lru = false;
-};
-
-struct Seq {
-  std::vector<int> blocks;
-  std::vector<int32_t> tokens;
-  std::vector<uint64_t> chain;  // chain hash per committed full block
-  int committed = 0;            // tokens whose K/V have been computed
-};
-
-class BlockManager {
- public:
-  BlockManager(int num_blocks, int block_size, bool prefix_cache)
-      : bs_(block_size), prefix_(prefix_cache), blocks_(num_blocks) {
-    if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad sizes");
-    free_.reserve(num_blocks);
-    for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
-  }
-
-  int block_size() const { return bs_; }
-  int num_blocks() const { return (int)blocks_.size(); }
-  int num_free_blocks() const { return (int)(free_.size() + lru_.size()); }
-  int num_cached_blocks() const { return (int)hash2block_.size(); }
-  bool has_seq(int64_t id) const { return seqs_.count(id) != 0; }
-
-  bool can_allocate(int num_tokens) const { return blocks_needed(num_tokens) <= num_free_blocks(); }
-
-  // Allocate blocks for a new sequence's prompt. Returns (block_table, cached_tokens); empty
-  // table when out of blocks (nothing is changed then).
-  std::pair<std::vector<int>, int> allocate(int64_t id, const std::vector<int32_t>& tokens) {
-    if (seqs_.count(id)) throw std::invalid_argument("sequence already allocated");
-    const int n = (int)tokens.size();
-    if (n <= 0) throw std::invalid_argument("empty prompt");
-    std::vector<int> matched;
-    std::vector<uint64_t> chain;
-    if (prefix_) {
-      const int max_full = (n - 1) / bs_;  // keep >= 1 token to compute logits from
-      uint64_t h = 0x51ed270b27ab3e5full;
-      for (int b = 0; b < max_full; ++b) {
-        for (int j = 0; j < bs_; ++j) h = mix(h, tokens[b * bs_ + j]);
-        auto it = hash2block_.find(h);
-        if (it == hash2block_.end()) break;
-        matched.push_back(it->second);
-        chain.push_back(h);
-      }
-    }
-    const int need = blocks_needed(n) - (int)matched.size();
-    int avail = (int)free_.size() + (int)lru_.size();
-    for (int b : matched)
-      if (blocks_[b].ref == 0) --avail;  // matched evictable blocks are taken out of the pool
-    if (need > avail) return {{}, 0};
-    Seq s;
-    for (int b : matched) take(b);
-    s.blocks = matched;
-    for (int i = 0; i < need; ++i) s.blocks.push_back(fresh());
-    s.tokens = tokens;
-    s.chain = chain;
-    s.committed = (int)matched.size() * bs_;
-    hit_tokens_ += s.committed;
-    query_tokens_ += n;
-    auto res = std::make_pair(s.blocks, s.committed);
-    seqs_.emplace(id, std::move(s));
-    return res;
-  }
-
-  // Append one generated token; returns its cache slot, or -1 when out of blocks.
-  int append_token(int64_t id, int32_t tok) {
-    Seq& s = get(id);
-    const int pos = (int)s.tokens.size();
-    if (pos >= (int)s.blocks.size() * bs_) {
-      if (num_free_blocks() == 0) return -1;
-      s.blocks.push_back(fresh());
-    }
-    s.tokens.push_back(tok);
-    return s.blocks[pos / bs_] * bs_ + pos % bs_;
-  }
-
-  // One decode step for a batch: commit the K/V of every sequence's current length, then append
-  // its new token.  Returns the new token's slot per sequence (-1: finished/skip or out of blocks).
-  std::vector<int> commit_append(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks,
-                                 const std::vector<uint8_t>& append) {
-    std::vector<int> out(ids.size(), -1);
-    for (size_t i = 0; i < ids.size(); ++i) {
-      Seq& s = get(ids[i]);
-      commit(ids[i], (int)s.tokens.size());
-      if (append[i]) out[i] = append_token(ids[i], toks[i]);
-    }
-    return out;
-  }
-
-  // Slots of token positions [start, end) of a sequence.
-  std::vector<int> slots(int64_t id, int start, int end) {
-    Seq& s = get(id);
-    if (end > (int)s.blocks.size() * bs_ || start < 0) throw std::out_of_range("slot range");
-    std::vector<int> out;
-    out.reserve(end - start);
-    for (int p = start; p < end; ++p) out.push_back(s.blocks[p / bs_] * bs_ + p % bs_);
-    return out;
-  }
-
-  // Mark K/V of positions [0, n) as computed; registers newly completed full blocks.
-  void commit(int64_t id, int n) {
-    Seq& s = get(id);
-    if (n > (int)s.tokens.size()) n = (int)s.tokens.size();
-    if (n <= s.committed) return;
-    s.committed = n;
-    if (!prefix_) return;
-    const int full = n / bs_;
-    uint64_t h = s.chain.empty() ? 0x51ed270b27ab3e5full : s.chain.back();
-    for (int b = (int)s.chain.size(); b < full; ++b) {
-      for (int j = 0; j < bs_; ++j) h = mix(h, s.tokens[b * bs_ + j]);
-      s.chain.push_back(h);
-      const int blk = s.blocks[b];
-      if (!blocks_[blk].hashed && !hash2block_.count(h)) {
-        blocks_[blk].hashed = true;
-        blocks_[blk].hash = h;
-        hash2block_[h] = blk;
-      }
-    }
-  }
-
-  std::vector<int> block_table(int64_t id) { return get(id).blocks; }
-  int seq_len(int64_t id) { return (int)get(id).tokens.size(); }
-  int committed(int64_t id) { return get(id).committed; }
-
-  void free(int64_t id) {
-    auto it = seqs_.find(id);
-    if (it == seqs_.end()) return;
-    // release newest first so older (prefix) blocks end up most-recently-used in the LRU
-    for (auto b = it->second.blocks.rbegin(); b != it->second.blocks.rend(); ++b) release(*b);
-    seqs_.erase(it);
-  }
-
-  void reset() {
-    seqs_.clear();
-    hash2block_.clear();
-    lru_.clear();
-    free_.clear();
-    for (int i = (int)blocks_.size() - 1; i >= 0; --i) {
-      blocks_[i] = Block();
-      free_.push_back(i);
-    }
-    hit_tokens_ = query_tokens_ = 0;
-  }
-
-  py::dict stats() const {
-    py::dict d;
-    d["num_blocks"] = (int)blocks_.size();
-    d["free_blocks"] = (int)free_.size();
-    d["evictable_blocks"] = (int)lru_.size();
-    d["cached_blocks"] = (int)hash2block_.size();
-    d["active_seqs"] = (int)seqs_.size();
-    d["prefix_hit_tokens"] = (long long)hit_tokens_;
-    d["prompt_tokens"] = (long long)query_tokens_;
-    return d;
-  }
-
- private:
-  int blocks_needed(int n) const { return (n + bs_ - 1) / bs_; }
-
-  Seq& get(int64_t id) {
-    auto it = seqs_.find(id);
-    if (it == seqs_.end()) throw std::out_of_range("unknown sequence");
-    return it->second;
-  }
-
-  void take(int b) {
-    Block& blk = blocks_[b];
-    if (blk.ref == 0 && blk.in_lru) {
-      lru_.erase(blk.lru_it);
-      blk.in_lru = false;
-    }
-    ++blk.ref;
-  }
-
-  int fresh() {
-    int b;
-    if (!free_.empty()) {
-      b = free_.back();
-      free_.pop_back();
-    } else {
-      if (lru_.empty()) throw std::runtime_error("out of KV blocks");
-      b = lru_.back();  // least recently used cached block
-      lru_.pop_back();
-      Block& old = blocks_[b];
-      old.in_lru = false;
-      if (old.hashed) {
-        hash2block_.erase(old.hash);
-        old.hashed = false;
-      }
-    }
-    blocks_[b].ref = 1;
-    return b;
-  }
-
-  void release(int b) {
-    Block& blk = blocks_[b];
-    if (--blk.ref > 0) return;
-    if (blk.hashed) {
-      lru_.push_front(b);
-      blk.lru_it = lru_.begin();
-      blk.in_lru = true;
-    } else {
-      free_.push_back(b);
-    }
-  }
-
-  int bs_;
-  bool prefix_;
-  std::vector<Block> blocks_;
-  std::vector<int> free_;
-  std::list<int> lru_;  // front = most recently released
-  std::unordered_map<uint64_t, int> hash2block_;
-  std::unordered_map<int64_t, Seq> seqs_;
-  long long hit_tokens_ = 0, query_tokens_ = 0;
-};
-
-}  // namespace
+using dllm::BlockManager;
 
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "distributed_llm_amd native serving runtime (paged-KV block manager)";
@@ -276,5 +29,10 @@ PYBIND11_MODULE(_runtime, m) {
       .def("committed", &BlockManager::committed)
       .def("free", &BlockManager::free)
       .def("reset", &BlockManager::reset)
-      .def("stats", &BlockManager::stats);
+      .def("stats", [](const BlockManager& b) {
+        py::dict d;
+        for (const auto& kv : b.stats()) d[kv.first.c_str()] = kv.second;
+        return d;
+      })
+      .def("check_invariants", &BlockManager::check_invariants);
 }

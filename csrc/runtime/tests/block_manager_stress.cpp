@@ -1,0 +1,139 @@
+// Randomised stress test of the paged-KV block manager (block_manager.h), built with
+// -fsanitize=address,undefined by tests/test_native_sanitizers.py (the reference has
+// no race/memory checking at all; our native runtime is checked on the host).
+//
+// Drives the same call pattern as the engine (allocate a prompt, commit prefill, decode steps via
+// commit_append, free; prompts that extend earlier conversations so prefix blocks are re-matched;
+// pool exhaustion so LRU eviction runs) and after every operation verifies:
+//   * check_invariants(): ref counts, free/LRU partition, hash table, no leaked blocks;
+//   * content: every block a sequence maps is "written" with that sequence's tokens (a shadow
+//     array per KV slot), so a prefix-cache hit can never hand out a block whose contents differ
+//     from the prompt's tokens, and an evicted block is never still matched.
+// Usage: block_manager_stress [iterations] [seed]
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <unordered_map>
+#include <vector>
+
+#include "../block_manager.h"
+
+using dllm::BlockManager;
+
+namespace {
+
+constexpr int kBS = 16;
+
+struct Model {
+  std::vector<int32_t> slot_tok;    // token id written at each KV slot (-1 = never written)
+  std::vector<int64_t> slot_owner;  // sequence that last wrote the slot
+};
+
+[[noreturn]] void die(const char* what, long it) {
+  std::fprintf(stderr, "FAIL at iteration %ld: %s\n", it, what);
+  std::exit(1);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const long iters = argc > 1 ? std::atol(argv[1]) : 20000;
+  const unsigned seed = argc > 2 ? (unsigned)std::atoi(argv[2]) : 1234u;
+  std::mt19937 rng(seed);
+  const int nblocks = 96;
+  BlockManager bm(nblocks, kBS, true);
+  Model m{std::vector<int32_t>(nblocks * kBS, -1), std::vector<int64_t>(nblocks * kBS, -1)};
+
+  std::unordered_map<int64_t, std::vector<int32_t>> live;   // id -> tokens
+  std::vector<std::vector<int32_t>> history;                // finished conversations (re-used as prefixes)
+  int64_t next_id = 1;
+  long hits = 0, evict_pressure = 0, preempt = 0;
+
+  auto write_range = [&](int64_t id, const std::vector<int32_t>& toks, int start, int end) {
+    auto sl = bm.slots(id, start, end);
+    for (int p = start; p < end; ++p) {
+      m.slot_tok[sl[p - start]] = toks[p];
+      m.slot_owner[sl[p - start]] = id;
+    }
+  };
+  auto verify_seq = [&](int64_t id, const std::vector<int32_t>& toks, long it) {
+    const int done = bm.committed(id);
+    auto sl = bm.slots(id, 0, done);
+    for (int p = 0; p < done; ++p)
+      if (m.slot_tok[sl[p]] != toks[p]) die("block content differs from sequence tokens", it);
+  };
+
+  for (long it = 0; it < iters; ++it) {
+    const int op = (int)(rng() % 10);
+    if (op < 3 || live.empty()) {
+      // new prompt: fresh, or an earlier conversation plus a new turn (prefix re-use)
+      std::vector<int32_t> toks;
+      if (!history.empty() && rng() % 2) {
+        toks = history[rng() % history.size()];
+        if (rng() % 3 == 0 && toks.size() > 20) toks.resize(toks.size() - rng() % 16);
+      }
+      const int extra = 1 + (int)(rng() % 40);
+      for (int i = 0; i < extra; ++i) toks.push_back((int32_t)(rng() % 50));
+      if (toks.size() > 600) toks.resize(1 + rng() % 64);
+      const int64_t id = next_id++;
+      auto res = bm.allocate(id, toks);
+      if (res.first.empty()) {
+        ++evict_pressure;
+        if (bm.has_seq(id)) die("failed allocate left a sequence behind", it);
+      } else {
+        const int cached = res.second;
+        if (cached % kBS || cached >= (int)toks.size()) die("bad cached token count", it);
+        hits += cached > 0;
+        verify_seq(id, toks, it);  // the matched prefix must hold exactly these tokens
+        write_range(id, toks, cached, (int)toks.size());  // "prefill" the suffix
+        bm.commit(id, (int)toks.size());
+        live[id] = toks;
+      }
+    } else if (op < 8) {
+      // decode step over a random subset of live sequences
+      std::vector<int64_t> ids;
+      std::vector<int32_t> nt;
+      std::vector<uint8_t> app;
+      for (auto& kv : live) {
+        if (rng() % 2) continue;
+        ids.push_back(kv.first);
+        nt.push_back((int32_t)(rng() % 50));
+        app.push_back((uint8_t)(rng() % 8 != 0));
+      }
+      auto slots = bm.commit_append(ids, nt, app);
+      for (size_t i = 0; i < ids.size(); ++i) {
+        auto& toks = live[ids[i]];
+        if (!app[i]) continue;
+        if (slots[i] < 0) {  // out of blocks: the engine preempts this sequence
+          ++preempt;
+          continue;
+        }
+        toks.push_back(nt[i]);
+        m.slot_tok[slots[i]] = nt[i];  // the next forward writes the new token's K/V here
+        m.slot_owner[slots[i]] = ids[i];
+        auto sl = bm.slots(ids[i], (int)toks.size() - 1, (int)toks.size());
+        if (sl[0] != slots[i]) die("append slot disagrees with slots()", it);
+      }
+    } else {
+      // finish a sequence (commit everything, remember it as a conversation prefix)
+      auto kv = live.begin();
+      std::advance(kv, rng() % live.size());
+      bm.commit(kv->first, (int)kv->second.size());
+      verify_seq(kv->first, kv->second, it);
+      if (bm.seq_len(kv->first) != (int)kv->second.size()) die("length mismatch", it);
+      history.push_back(kv->second);
+      if (history.size() > 64) history.erase(history.begin());
+      bm.free(kv->first);
+      live.erase(kv);
+    }
+    const std::string err = bm.check_invariants();
+    if (!err.empty()) die(err.c_str(), it);
+  }
+  for (auto& kv : live) bm.free(kv.first);
+  const std::string err = bm.check_invariants();
+  if (!err.empty()) die(err.c_str(), iters);
+  if (bm.num_free_blocks() != nblocks) die("blocks leaked after freeing everything", iters);
+  std::printf("ok iterations=%ld prefix_hits=%ld alloc_failures=%ld preempted=%ld\n", iters, hits,
+              evict_pressure, preempt);
+  return 0;
+}
