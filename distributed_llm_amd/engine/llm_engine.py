@@ -24,7 +24,7 @@ import threading
 import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Union
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -484,25 +484,32 @@ class LLMEngine:
                     prefilling.remove(s)
                     if self._finished(s):
                         self._release(s)
+                    elif s.error == "__preempt__":
+                        # no block for its first generated token: re-queue before it reaches a
+                        # decode step (its slot would otherwise point at an unowned block)
+                        self._release(s, keep=False)
+                        s.error = None
+                        waiting.insert(0, s)
                     else:
                         running.append(s)
                 continue
             with tracer.span("engine.decode", "engine", batch=len(running)):
-                self._decode_step(running)
+                finished, preempted = self._decode_step(running)
             if tracer.enabled:
                 tracer.counter("engine.batch", running=len(running), waiting=len(waiting),
                                free_kv_blocks=self.bm.num_free_blocks())
-            _t = time.perf_counter()
-            for s in [s for s in running if self._finished(s)]:
-                running.remove(s)
-                self._release(s)
-            # out of KV blocks for a running sequence: preempt the youngest and re-queue it
-            for s in [s for s in running if s.error == "__preempt__"]:
-                running.remove(s)
-                self._release(s, keep=False)
-                s.error = None
-                waiting.insert(0, s)  # re-admitted with fill = prompt + out (recompute)
-            self.timers["decode_host_post"] += time.perf_counter() - _t
+            if finished or preempted:
+                _t = time.perf_counter()
+                gone = set(map(id, finished)) | set(map(id, preempted))
+                running[:] = [s for s in running if id(s) not in gone]
+                for s in finished:
+                    self._release(s)
+                # out of KV blocks for a running sequence: preempt it and re-queue it
+                for s in preempted:
+                    self._release(s, keep=False)
+                    s.error = None
+                    waiting.insert(0, s)  # re-admitted with fill = prompt + out (recompute)
+                self.timers["decode_host_post"] += time.perf_counter() - _t
 
     def _finished(self, s: _Seq) -> bool:
         if s.error is not None and s.error != "__preempt__":
@@ -662,7 +669,7 @@ class LLMEngine:
                 return b
         raise ValueError(f"batch {n} exceeds max_num_seqs")
 
-    def _decode_step(self, running: List[_Seq]) -> None:
+    def _decode_step(self, running: List[_Seq]) -> Tuple[List[_Seq], List[_Seq]]:
         _t0 = time.perf_counter()
         B = len(running)
         bs = self._bucket(B)
@@ -726,18 +733,27 @@ class LLMEngine:
         # the new tokens of those that continue
         eos, mml = self.tok.eos_id, self.max_model_len
         cont = []
+        finished: List[_Seq] = []
         for s, t in zip(running, toks):
-            s.out.append(int(t))
+            t = int(t)
+            s.out.append(t)
             p = s.params
-            cont.append(not (len(s.out) >= p.max_new_tokens or (not p.ignore_eos and t == eos)
-                             or s.length >= mml))
-        slots = self.bm.commit_append([s.id for s in running], toks, cont)
-        mb_ = self.max_blocks
-        for s, c, slot in zip(running, cont, slots):
+            c = not (len(s.out) >= p.max_new_tokens or (not p.ignore_eos and t == eos)
+                     or len(s.prompt) + len(s.out) >= mml)
+            cont.append(c)
             if not c:
+                finished.append(s)
+        slots = self.bm.commit_append([s.id for s in running], [s.out[-1] for s in running], cont)
+        mb_ = self.max_blocks
+        preempted: List[_Seq] = []
+        for s, c, slot in zip(running, cont, slots):
+            # the appended token sits at position length-1; only a slot that opens a new block
+            # (position % BS == 0) can change the row's block table
+            if not c or (slot >= 0 and slot % BS != 0):
                 continue
             if slot < 0:
                 s.error = "__preempt__"
+                preempted.append(s)
                 continue
             nblk = (s.length + BS - 1) // BS
             blk = slot // BS
@@ -745,6 +761,7 @@ class LLMEngine:
                 self.bt_host[s.row, nblk - 1] = blk
                 self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
         self.timers["decode_host_post"] += time.perf_counter() - _t2
+        return finished, preempted
 
     def _decode_meta(self, bs: int) -> AttnMeta:
         if self._use_worklist(bs):

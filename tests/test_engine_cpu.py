@@ -144,3 +144,26 @@ def test_route_concurrent_matches_route_query():
         t.join(timeout=60)
     for (p1, t1, d1), (p2, t2, d2) in zip(ref, got):
         assert (p1["response"], t1, d1, p1["routing_method"]) == (p2["response"], t2, d2, p2["routing_method"])
+
+
+def test_preemption_under_kv_pressure_completes_every_request():
+    """16 KV blocks (256 tokens) for 6 requests needing ~6 blocks each: running sequences run out of
+    blocks, are preempted (recompute) and re-admitted; every request still finishes in full."""
+    eng = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.0, max_num_seqs=8, max_model_len=128, seed=0)
+    assert eng.num_blocks == 16
+    preempts = []
+    orig = eng._release
+
+    def counting_release(s, keep=True):
+        if not keep:
+            preempts.append(s.id)
+        return orig(s, keep)
+
+    eng._release = counting_release
+    sp = SamplingParams(max_new_tokens=60, temperature=0.0, ignore_eos=True)
+    prompts = [f"user: request {i} " + "tok " * (20 + 3 * i) for i in range(6)]
+    outs = eng.generate(prompts, sp)
+    assert all(o.error is None and o.num_generated == 60 for o in outs), [(o.error, o.num_generated) for o in outs]
+    assert preempts, "expected at least one preemption"
+    assert eng.bm.check_invariants() == ""
+    assert eng.bm.stats()["active_seqs"] == 0
