@@ -212,6 +212,8 @@ class LlamaModel:
                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Final-normed hidden states of each sequence's last new token: [S, H]."""
         cfg = self.cfg
+        if self.par.use_sp(input_ids.shape[0]) and not (input_ids.is_cuda and torch.cuda.is_current_stream_capturing()):
+            return self._hidden_states_sp(input_ids, positions, meta, kv_caches)
         h = self._embed(input_ids)
         residual = torch.zeros_like(h)
         spare = torch.empty_like(h)   # ping-pong partner: a fused norm+GEMV writes the new residual here
@@ -232,6 +234,43 @@ class LlamaModel:
             else:
                 x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
                 h = self._mlp_out(L, x)
+        last_h = h.index_select(0, meta.last_idx)
+        last_r = residual.index_select(0, meta.last_idx)
+        return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)
+
+    def _hidden_states_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
+                          kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """Sequence-parallel TP forward (Megatron-SP) for prefill-size batches.
+
+        The residual stream and both RMSNorms of every layer live on this rank's 1/tp token slice;
+        each row-parallel output (wo, down / MoE) is reduce-scattered to the slice instead of
+        all-reduced, and the normed slice is all-gathered before the column-parallel projection
+        (wqkv, gate|up). Same bytes on the wire as the all-reduces it replaces, but the norm work
+        and the [T, H] residual/activation buffers shrink by tp (long prompts: SURVEY §5.7)."""
+        cfg, par = self.cfg, self.par
+        T = input_ids.shape[0]
+        from ..parallel.expert_parallel import token_slice
+        lo, hi = token_slice(T, par.tp_rank, par.tp_size)
+        # embedding shards are vocab-parallel partial sums: reduce-scatter them straight to the slice
+        h = par.reduce_scatter_rows(ops.embedding(input_ids, self.embed, self.vocab_shard.start))
+        residual = torch.zeros_like(h)
+        for li, L in enumerate(self.layers):
+            x = par.all_gather_rows(ops.rms_norm(h, L["ln1"], cfg.rms_eps, residual=residual), T)
+            qkv = ops.linear(x, L["wqkv"])
+            kc, vc = kv_caches[li]
+            q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
+            o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
+                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
+                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
+                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+            h = par.reduce_scatter_rows(ops.linear(o.view(o.shape[0], -1), L["wo"]))
+            x = par.all_gather_rows(ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual), T)
+            if self.moe_ep:
+                h = self._mlp_out(L, x)[lo:hi]
+            else:
+                h = par.reduce_scatter_rows(self._mlp(L, x))
+        h = par.all_gather_rows(h, T)
+        residual = par.all_gather_rows(residual, T)
         last_h = h.index_select(0, meta.last_idx)
         last_r = residual.index_select(0, meta.last_idx)
         return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)

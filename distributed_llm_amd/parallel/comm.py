@@ -13,7 +13,7 @@ TP=4 group).  Collectives used on the serving path:
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import torch
@@ -29,6 +29,10 @@ class ParallelContext:
     world_size: int = 1
     custom_ar: Optional[object] = None  # parallel.custom_ar.CustomAllReduce (GPU TP groups)
     moe_ep: bool = False                # MoE layers expert-parallel over the TP group (parallel.expert_parallel)
+    # Megatron-style sequence parallelism for prefill-size batches under TP: the residual stream
+    # and the norms run on a 1/tp token shard (reduce-scatter + all-gather replace each all-reduce)
+    sequence_parallel: bool = field(default_factory=lambda: os.environ.get("DLLM_SEQ_PARALLEL", "0") == "1")
+    sp_min_tokens: int = field(default_factory=lambda: int(os.environ.get("DLLM_SP_MIN_TOKENS", "256")))
 
     @property
     def enabled(self) -> bool:
@@ -59,6 +63,32 @@ class ParallelContext:
             logging.getLogger(__name__).warning("custom all-reduce disabled: %s", e)
             return False
         return True
+
+    def use_sp(self, num_tokens: int) -> bool:
+        return self.sequence_parallel and self.tp_size > 1 and num_tokens >= max(self.sp_min_tokens, self.tp_size)
+
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum [T, H] partial activations over the TP group and keep this rank's token slice
+        (``expert_parallel.token_slice`` layout, uneven T allowed): half the bytes of an
+        all-reduce leave each rank, the other half return in the matching all-gather."""
+        from .expert_parallel import token_slice
+        T = t.shape[0]
+        lo, hi = token_slice(T, self.tp_rank, self.tp_size)
+        if not t.is_cuda:  # gloo has no reduce-scatter: all-reduce and slice (CPU tests)
+            dist.all_reduce(t, group=self.tp_group)
+            return t[lo:hi].contiguous()
+        mx = -(-T // self.tp_size)
+        buf = torch.zeros((self.tp_size, mx, *t.shape[1:]), dtype=t.dtype, device=t.device)
+        for r in range(self.tp_size):
+            a, b = token_slice(T, r, self.tp_size)
+            buf[r, :b - a] = t[a:b]
+        out = torch.empty((mx, *t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, buf.view(-1, *t.shape[1:]), group=self.tp_group)
+        return out[:hi - lo]
+
+    def all_gather_rows(self, t: torch.Tensor, T: int) -> torch.Tensor:
+        from .expert_parallel import all_gather_rows
+        return all_gather_rows(t.contiguous(), T, self.tp_group, self.tp_size)
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate ``t`` from every TP rank along a new leading dim -> [tp, *t.shape]."""

@@ -21,8 +21,9 @@ def _free_port() -> int:
 PROMPTS = ["user: hello there", "user: explain paged attention step by step", "x" * 70]
 
 
-def _worker(rank, world, port, model, q):
+def _worker(rank, world, port, model, q, env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    os.environ.update(env or {})
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -32,19 +33,21 @@ def _worker(rank, world, port, model, q):
         par = make_tp_groups(world)
         eng = LLMEngine(model, device="cpu", par=par, kv_cache_gb=0.05, max_num_seqs=4)
         outs = eng.generate(PROMPTS, SamplingParams(max_new_tokens=6))
-        q.put((rank, [o.token_ids for o in outs]))
+        q.put((rank, [o.token_ids for o in outs], eng.model.par.use_sp(64)))
     finally:
         dist.destroy_process_group()
 
 
-def _run_tp(model, world=2):
+def _run_tp(model, world=2, env=None, want_sp=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, env)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    got = [q.get(timeout=300) for _ in procs]
+    assert all(sp == want_sp for _, _, sp in got)
+    res = {r: toks for r, toks, _ in got}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -66,6 +69,19 @@ def test_tp2_matches_tp1(model):
         assert got[:3] == want[:3]
     same = sum(a == b for g, w in zip(res[0], ref) for a, b in zip(g, w))
     assert same >= 0.8 * sum(len(w) for w in ref)
+
+
+@pytest.mark.parametrize("model", ["tiny-llama-test", "tiny-moe-test"])
+def test_sequence_parallel_prefill_matches_plain_tp(model):
+    """Megatron-SP prefill (reduce-scatter / sharded norms / all-gather) must reproduce the plain
+    TP=2 engine: prefill batches here are >= 2 tokens, so every prefill step takes the SP path."""
+    plain = _run_tp(model)
+    sp = _run_tp(model, env={"DLLM_SEQ_PARALLEL": "1", "DLLM_SP_MIN_TOKENS": "2"}, want_sp=True)
+    assert sp[0] == sp[1]
+    for got, want in zip(sp[0], plain[0]):
+        assert got[:3] == want[:3]
+    same = sum(a == b for g, w in zip(sp[0], plain[0]) for a, b in zip(g, w))
+    assert same >= 0.8 * sum(len(w) for w in plain[0])
 
 
 def test_shard_range_validation():
