@@ -10,10 +10,13 @@
 namespace {
 
 __global__ void silu_mul_kernel(const u16* __restrict__ gu, u16* __restrict__ out, long T, int I, long in_stride) {
-  const long nvec = T * (I >> 3);
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
-    const long t = v / (I >> 3);
-    const int c = (int)(v % (I >> 3)) * 8;
+  // 32-bit index math (the launcher guarantees T * I / 8 < 2^30, so v + stride cannot overflow): a 64-bit divide is a long
+  // software sequence on CDNA, a 32-bit one a handful of VALU ops
+  const int nv = I >> 3;
+  const int nvec = (int)(T * nv);
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const int t = v / nv;
+    const int c = (v - t * nv) * 8;
     float gf[8], uf[8], o[8];
     unpack8(ld16(gu + t * in_stride + c), gf);
     unpack8(ld16(gu + t * in_stride + I + c), uf);
@@ -116,6 +119,7 @@ extern "C" int dllm_silu_mul(const void* gu, void* out, long T, int I, long in_s
   if (I % 8 != 0) return -1;
   const long n = T * (I / 8);
   if (n == 0) return 0;
+  if (n >= (1L << 30)) return -2;
   hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, (const u16*)gu, (u16*)out, T, I,
                      in_stride);
   return (int)hipGetLastError();

@@ -19,11 +19,16 @@ __global__ void __launch_bounds__(256) norm_kernel(const u16* __restrict__ x, co
   const int nvec = H >> 3;
   const u16* xr = x + row * x_stride;
   float v[MAXV][8];
+  // weight (and bias) vectors are issued together with the row loads, so the epilogue after the
+  // block reduction does not wait on a second dependent memory round trip
+  uint4 wv[MAXV], bv[MAXV];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nvec) {
+      wv[i] = ld16(w + c * 8);
+      if (LAYERNORM) bv[i] = ld16(b + c * 8);
       unpack8(ld16(xr + c * 8), v[i]);
       if (res_in) {
         float r[8];
@@ -60,10 +65,10 @@ __global__ void __launch_bounds__(256) norm_kernel(const u16* __restrict__ x, co
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nvec) {
       float wf[8], o[8];
-      unpack8(ld16(w + c * 8), wf);
+      unpack8(wv[i], wf);
       if (LAYERNORM) {
         float bf[8];
-        unpack8(ld16(b + c * 8), bf);
+        unpack8(bv[i], bf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * wf[j] + bf[j];
       } else {
