@@ -525,6 +525,8 @@ class LLMEngine:
     def _release(self, s: _Seq, keep: bool = True) -> None:
         if keep:
             s.finished = time.perf_counter()
+            if tracer.enabled:
+                self._trace_request(s)
         self.bm.free(s.id)
         if keep:
             s.done.set()
@@ -532,6 +534,15 @@ class LLMEngine:
             self.bt_host[s.row].fill(0)
             self._free_rows.append(s.row)
             s.row = -1
+
+    def _trace_request(self, s: _Seq) -> None:
+        lane = f"req {s.id % 64:02d}"   # 64 rotating lanes keep concurrent requests readable
+        args = dict(id=s.id, prompt=len(s.prompt), cached=s.num_cached, generated=len(s.out))
+        adm = s.admitted or s.finished
+        tracer.complete("request.queue", s.arrival, adm, lane=lane, **args)
+        if s.first_tok:
+            tracer.complete("request.prefill", adm, s.first_tok, lane=lane, **args)
+            tracer.complete("request.decode", s.first_tok, s.finished, lane=lane, **args)
 
     def _set_row_blocks(self, s: _Seq) -> None:
         t = self.bm.block_table(s.id)

@@ -9,7 +9,9 @@ for on top of the per-request queue / TTFT / decode split that `RequestOutput` a
 * optional GPU spans (`gpu_span()`): a pair of HIP events recorded on the current stream around
   the block; the elapsed GPU time is resolved lazily at `dump()` so recording never synchronises
   the device inside the decode loop;
-* counters (`counter()`), e.g. running batch size and free KV blocks per step.
+* counters (`counter()`), e.g. running batch size and free KV blocks per step;
+* per-request lifecycle spans (`complete()`): queue wait, prefill until the first token, decode,
+  on rotating `req NN` lanes, so each query's latency split is visible next to the engine steps.
 
 Tracing is off unless `DLLM_TRACE=<path>` is set or `enable()` is called; when off every call is
 a no-op costing one attribute check. Events go into a bounded deque (`DLLM_TRACE_MAX`, default
@@ -94,6 +96,19 @@ class Tracer:
             end.record()
             with self._lock:
                 self._gpu.append((name, cat, threading.get_ident(), ts, start, end, dict(args)))
+
+    def complete(self, name: str, t_start: float, t_end: float, cat: str = "request", lane: str = "requests",
+                 **args: Any) -> None:
+        """Span with explicit ``time.perf_counter()`` bounds on a named lane (per-request lifecycle
+        phases recorded after the fact: queue wait, prefill-to-first-token, decode)."""
+        if not self.enabled or t_end < t_start:
+            return
+        ev = {"name": name, "cat": cat, "ph": "X", "ts": (t_start - self._t0) * 1e6,
+              "dur": (t_end - t_start) * 1e6, "pid": self._pid, "tid": lane}
+        if args:
+            ev["args"] = args
+        with self._lock:
+            self._ev.append(ev)
 
     def instant(self, name: str, cat: str = "host", **args: Any) -> None:
         if not self.enabled:

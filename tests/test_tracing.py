@@ -75,7 +75,10 @@ def test_routed_request_spans(tmp_path):
         tracer.disable()
     assert payload["ok"]
     names = {e["name"] for e in tracer.events()}
-    assert {"route.decide", "pool.process", "engine.prefill"} <= names
+    assert {"route.decide", "pool.process", "engine.prefill", "request.queue", "request.prefill",
+            "request.decode"} <= names
+    req = [e for e in tracer.events() if e["name"] == "request.decode"][0]
+    assert req["args"]["generated"] == 4 and req["tid"].startswith("req ")
     dec = [e for e in tracer.events() if e["name"] == "route.decide"][0]
     assert dec["args"]["device"] == dev
     doc = json.load(open(tracer.dump()))
