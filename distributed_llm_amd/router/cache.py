@@ -402,12 +402,19 @@ class QueryCache:
             self.insert(q, ck, dev, q_emb=v)
 
     def save(self, path: str) -> None:
+        """Reference JSON format (`src/cache.py:426-432`); a ``.safetensors`` path writes the
+        binary snapshot instead (see :meth:`save_snapshot`)."""
+        if str(path).endswith(".safetensors"):
+            self.save_snapshot(path)
+            return
         self._evict_expired()
         with self._lock:
             data = [e.to_dict() for e in self._store.values()]
         Path(path).write_text(json.dumps(data, indent=2), encoding="utf-8")
 
     def load(self, path: str) -> int:
+        if str(path).endswith(".safetensors"):
+            return self.load_snapshot(path)
         p = Path(path)
         if not p.exists():
             return 0
@@ -416,9 +423,13 @@ class QueryCache:
         except json.JSONDecodeError as exc:
             logger.error("Cache load: JSON parse error: %s", exc)
             return 0
+        return self._ingest((d, None) for d in raw)
+
+    def _ingest(self, items) -> int:
+        """Insert (entry dict, optional embedding override) pairs; skips expired / malformed."""
         n = 0
         with self._lock:
-            for d in raw:
+            for d, emb_override in items:
                 try:
                     e = CacheEntry.from_dict(d)
                 except Exception as exc:
@@ -428,12 +439,56 @@ class QueryCache:
                     continue
                 if e.query_hash in self._store:
                     self._delete_entry(e.query_hash)
-                emb, e.embedding = e.embedding, None
+                emb, e.embedding = (emb_override if emb_override is not None else e.embedding), None
                 self._set_embedding(e, emb)
                 self._store[e.query_hash] = e
                 self._stamp(e, e.timestamp)
                 n += 1
         return n
+
+    def save_snapshot(self, path: str) -> None:
+        """Binary snapshot: the embedding table as one f32 [n, dim] safetensors
+        tensor plus the entries (without vectors) as JSON in the file's metadata. A million-entry
+        cache is ~1.5 GB of raw f32 instead of ~8 GB of JSON float text, and loads with one read."""
+        from safetensors.numpy import save_file
+        self._evict_expired()
+        with self._lock:
+            entries = list(self._store.values())
+            metas, rows = [], []
+            for e in entries:
+                d = e.to_dict()
+                d["embedding"] = None
+                d["emb_row"] = len(rows) if e.embedding is not None else -1
+                if e.embedding is not None:
+                    rows.append(np.asarray(e.embedding, dtype=np.float32).reshape(-1))
+                metas.append(d)
+        dim = rows[0].shape[0] if rows else self._index.dim
+        table = np.stack(rows) if rows else np.zeros((0, dim), dtype=np.float32)
+        save_file({"embeddings": np.ascontiguousarray(table)}, str(path),
+                  metadata={"format": "dllm-routing-cache-v1", "entries": json.dumps(metas)})
+
+    def load_snapshot(self, path: str) -> int:
+        from safetensors import safe_open
+        p = Path(path)
+        if not p.exists():
+            return 0
+        try:
+            with safe_open(str(p), framework="numpy") as f:
+                meta = f.metadata() or {}
+                table = f.get_tensor("embeddings")
+        except Exception as exc:
+            logger.error("Cache snapshot load failed: %s", exc)
+            return 0
+        if meta.get("format") != "dllm-routing-cache-v1":
+            logger.error("Cache snapshot load: unknown format %r", meta.get("format"))
+            return 0
+        metas = json.loads(meta.get("entries", "[]"))
+
+        def items():
+            for d in metas:
+                r = int(d.pop("emb_row", -1))
+                yield d, (table[r] if 0 <= r < table.shape[0] else None)
+        return self._ingest(items())
 
     def stats(self) -> Dict[str, Any]:
         with self._lock:

@@ -231,6 +231,38 @@ def test_cache_invalidate_warmup_persist(tmp_path):
     assert c2.stats()["size"] == 0
 
 
+def test_cache_binary_snapshot_roundtrip(tmp_path):
+    """Binary safetensors snapshot: same entries, routing history and vectors as the JSON format;
+    semantic lookups work after load; a corrupt file loads nothing instead of raising."""
+    rng = np.random.default_rng(3)
+    c = QueryCache(max_size=500, ttl_seconds=100, similarity_threshold=0.95, use_semantic=True, dim=32)
+    vecs = rng.standard_normal((300, 32)).astype(np.float32)
+    for i in range(300):
+        c.insert(f"q{i}", f"ctx{i % 3}", SMALL if i % 2 else LARGE, 0.7, "semantic",
+                 q_emb=vecs[i] if i % 5 else None)
+    c.insert("q7", "ctx1", LARGE, 0.9, "hybrid")          # second routing record
+    snap, js = tmp_path / "cache.safetensors", tmp_path / "cache.json"
+    c.save(str(snap))
+    c.save(str(js))
+    assert snap.stat().st_size < js.stat().st_size / 2   # dim 32 here; the gap grows with dim
+    a = QueryCache(max_size=500, ttl_seconds=100, similarity_threshold=0.95, use_semantic=True, dim=32)
+    b = QueryCache(max_size=500, ttl_seconds=100, similarity_threshold=0.95, use_semantic=True, dim=32)
+    assert a.load(str(snap)) == 300 and b.load(str(js)) == 300
+    ea, eb = a._store, b._store
+    assert list(ea) == list(eb)
+    for h in ea:
+        x, y = ea[h], eb[h]
+        assert x.to_dict() == y.to_dict()
+    # semantic hit on a perturbed vector of an entry with an embedding, within its context only
+    q = vecs[7] + 1e-3
+    r = a.lookup("different words", "ctx1", q_emb=q)
+    assert r is not None and r.entry.query == "q7"
+    assert a.lookup("different words", "ctx0", q_emb=q) is None
+    bad = tmp_path / "bad.safetensors"
+    bad.write_bytes(b"not a safetensors file")
+    assert QueryCache().load(str(bad)) == 0
+
+
 # ----------------------------------------------------------------------------- config
 
 def test_config_profiles_and_replace_semantics(monkeypatch):
