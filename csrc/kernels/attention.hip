@@ -201,6 +201,22 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
       l_run = l_run * alpha + lsum;
       m_run = m_new;
       const bf16x8 pf = __builtin_bit_cast(bf16x8, pack8(p));
+      // Keys past k_end sit in the tail of the last KV block: never written for this sequence
+      // (uninitialised or stale memory, possibly NaN/Inf bit patterns).  Their P is 0, but
+      // 0 * NaN = NaN inside the PV MFMA, so zero those V^T columns (wave-uniform tail test).
+      if (kc + 32 > k_end) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (kc + 16 * h + 4 * g + q >= k_end) {
+#pragma unroll
+              for (int n = 0; n < NT; ++n) {
+                uint32_t& w = (q < 2) ? vr[c][h][n].x : vr[c][h][n].y;
+                w &= (q & 1) ? 0x0000ffffu : 0xffff0000u;
+              }
+            }
+      }
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         acc[n] *= alpha;
