@@ -10,11 +10,15 @@
 // recycled for new data (oldest first).
 // Hashes are registered only by commit(), i.e. after the forward pass that wrote the block's
 // K/V, so a prompt can never match a block whose contents are not computed yet.
+// A match on the 64-bit chain hash alone is not trusted: every hashed block keeps the 16 tokens it
+// was computed from (and its parent block), and a match is taken only when both agree, so a hash
+// collision degrades to a cache miss instead of re-using another sequence's K/V.
 //
 // Header-only core (no Python): the pybind11 module in block_manager.cpp wraps it, and
 // csrc/runtime/tests/block_manager_stress.cpp drives it under ASan/UBSan.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <list>
 #include <map>
@@ -30,6 +34,9 @@ inline uint64_t mix(uint64_t h, int32_t tok) {
   h ^= h >> 31;
   h *= 0xbf58476d1ce4e5b9ull;
   h ^= h >> 29;
+#ifdef DLLM_BM_WEAK_HASH
+  h &= 0x7;  // test builds only: force frequent chain-hash collisions (token check must catch them)
+#endif
   return h;
 }
 
@@ -37,6 +44,7 @@ struct Block {
   int ref = 0;
   bool hashed = false;
   uint64_t hash = 0;
+  int parent = -1;  // block holding the previous 16 tokens of the chain (-1: first block)
   std::list<int>::iterator lru_it;
   bool in_lru = false;
 };
@@ -51,7 +59,8 @@ struct Seq {
 class BlockManager {
  public:
   BlockManager(int num_blocks, int block_size, bool prefix_cache)
-      : bs_(block_size), prefix_(prefix_cache), blocks_(num_blocks) {
+      : bs_(block_size), prefix_(prefix_cache), blocks_(num_blocks),
+        tok_store_(prefix_cache ? (size_t)num_blocks * block_size : 0) {
     if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad sizes");
     free_.reserve(num_blocks);
     for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
@@ -80,6 +89,10 @@ class BlockManager {
         for (int j = 0; j < bs_; ++j) h = mix(h, tokens[b * bs_ + j]);
         auto it = hash2block_.find(h);
         if (it == hash2block_.end()) break;
+        if (!same_block(it->second, matched.empty() ? -1 : matched.back(), &tokens[b * bs_])) {
+          ++collisions_;
+          break;
+        }
         matched.push_back(it->second);
         chain.push_back(h);
       }
@@ -154,6 +167,9 @@ class BlockManager {
       if (!blocks_[blk].hashed && !hash2block_.count(h)) {
         blocks_[blk].hashed = true;
         blocks_[blk].hash = h;
+        blocks_[blk].parent = b > 0 ? s.blocks[b - 1] : -1;
+        std::copy(s.tokens.begin() + (size_t)b * bs_, s.tokens.begin() + (size_t)(b + 1) * bs_,
+                  tok_store_.begin() + (size_t)blk * bs_);
         hash2block_[h] = blk;
       }
     }
@@ -180,7 +196,7 @@ class BlockManager {
       blocks_[i] = Block();
       free_.push_back(i);
     }
-    hit_tokens_ = query_tokens_ = 0;
+    hit_tokens_ = query_tokens_ = collisions_ = 0;
   }
 
   std::map<std::string, long long> stats() const {
@@ -190,6 +206,7 @@ class BlockManager {
             {"cached_blocks", (long long)hash2block_.size()},
             {"active_seqs", (long long)seqs_.size()},
             {"prefix_hit_tokens", hit_tokens_},
+            {"hash_collisions", collisions_},
             {"prompt_tokens", query_tokens_}};
   }
 
@@ -236,6 +253,13 @@ class BlockManager {
  private:
   int blocks_needed(int n) const { return (n + bs_ - 1) / bs_; }
 
+  // a hashed block matches a prompt block only if it follows the same parent block and holds the
+  // same tokens (the parent check makes the whole prefix, not just this block, equal by induction)
+  bool same_block(int blk, int parent, const int32_t* toks) const {
+    if (blocks_[blk].parent != parent) return false;
+    return std::equal(toks, toks + bs_, tok_store_.begin() + (size_t)blk * bs_);
+  }
+
   Seq& get(int64_t id) {
     auto it = seqs_.find(id);
     if (it == seqs_.end()) throw std::out_of_range("unknown sequence");
@@ -265,6 +289,7 @@ class BlockManager {
       if (old.hashed) {
         hash2block_.erase(old.hash);
         old.hashed = false;
+        old.parent = -1;
       }
     }
     blocks_[b].ref = 1;
@@ -290,7 +315,8 @@ class BlockManager {
   std::list<int> lru_;  // front = most recently released
   std::unordered_map<uint64_t, int> hash2block_;
   std::unordered_map<int64_t, Seq> seqs_;
-  long long hit_tokens_ = 0, query_tokens_ = 0;
+  std::vector<int32_t> tok_store_;  // tokens of every hashed block, bs_ per block
+  long long hit_tokens_ = 0, query_tokens_ = 0, collisions_ = 0;
 };
 
 }  // namespace dllm

@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
   const std::string err = bm.check_invariants();
   if (!err.empty()) die(err.c_str(), iters);
   if (bm.num_free_blocks() != nblocks) die("blocks leaked after freeing everything", iters);
-  std::printf("ok iterations=%ld prefix_hits=%ld alloc_failures=%ld preempted=%ld\n", iters, hits,
-              evict_pressure, preempt);
+  std::printf("ok iterations=%ld prefix_hits=%ld alloc_failures=%ld preempted=%ld collisions=%lld\n", iters, hits,
+              evict_pressure, preempt, bm.stats().at("hash_collisions"));
   return 0;
 }
