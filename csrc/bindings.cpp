@@ -6,6 +6,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include "kernels/tgemm_args.h"
+
 extern "C" {
 int dllm_norm(const void*, const void*, void*, const void*, const void*, void*, int, int, long, long, float, int,
               hipStream_t);
@@ -44,6 +46,8 @@ int dllm_car_open_handle(const char*, void**);
 int dllm_car_close_handle(void*);
 int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
+int dllm_tgemm(const void*, int, int, int, int, hipStream_t);
+int dllm_res_add_ssq(const void*, long, void*, long, float*, int, int, hipStream_t);
 int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
                               unsigned long long*, hipStream_t);
 }
@@ -492,10 +496,121 @@ void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
                         (unsigned*)counters.data_ptr<int>(), err.data_ptr<int>(), spin_limit, stream()),
      "car_allreduce");
 }
+
+// ---- fused-epilogue LDS-tiled GEMM (csrc/kernels/tgemm.hip).  epi: 0 plain y = x.w^T (optionally
+// row-scaled by rinv from ssq_in), 1 residual add (y = residual, in place; ssq_out partial row
+// sums), 2 QKV (RoPE + q_out + paged K/V writes), 3 SwiGLU (y = [M, N/2]).
+void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int64_t epi, int64_t bm, int64_t bn,
+           int64_t stages, int64_t splits, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> counters,
+           c10::optional<torch::Tensor> ssq_in, int64_t ssq_in_n, double norm_scale, double eps,
+           c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> pos,
+           c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
+           c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
+           int64_t nq, int64_t nkv, int64_t d) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && K % 64 == 0, "x [M, K], K % 64 == 0");
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && (stages == 2 || stages == 3), "tile");
+  TORCH_CHECK(splits >= 1 && splits <= 64, "splits");
+  int kchunk = (K + splits - 1) / splits;
+  kchunk = (kchunk + 63) / 64 * 64;
+  const int S = (K + kchunk - 1) / kchunk;
+  const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  dllm::GemmArgs a{};
+  a.A = (const uint16_t*)x.data_ptr();
+  a.lda = x.stride(0);
+  a.W = (const uint16_t*)w.data_ptr();
+  a.M = M; a.N = N; a.K = K; a.kchunk = kchunk; a.splits = S;
+  if (S > 1) {
+    TORCH_CHECK(part.has_value() && counters.has_value(), "split-K needs part/counters workspaces");
+    check_f32(*part, "part");
+    check_i32(*counters, "counters");
+    TORCH_CHECK(part->numel() >= (int64_t)S * tiles * bm * bn && counters->numel() >= tiles,
+                "split-K workspace too small");
+    a.part = part->data_ptr<float>();
+    a.counters = counters->data_ptr<int>();
+  }
+  if (ssq_in.has_value()) {
+    check_f32(*ssq_in, "ssq_in");
+    TORCH_CHECK(ssq_in->dim() == 2 && ssq_in->size(1) >= M && ssq_in_n >= 1 && ssq_in_n <= ssq_in->size(0),
+                "ssq_in [slots, >= M]");
+    TORCH_CHECK(epi != 1, "residual epilogue takes no row scale");
+    a.ssq_in = ssq_in->data_ptr<float>();
+    a.ssq_in_n = ssq_in_n;
+    a.ssq_in_ld = ssq_in->size(1);
+    a.norm_scale = (float)norm_scale;
+    a.eps = (float)eps;
+  }
+  if (epi == 0 || epi == 1 || epi == 3) {
+    TORCH_CHECK(y.has_value(), "y required");
+    check_bf16(*y, "y");
+    TORCH_CHECK(y->dim() == 2 && y->stride(1) == 1 && y->size(0) == M && y->size(1) == (epi == 3 ? N / 2 : N),
+                "y shape");
+    a.Y = (uint16_t*)y->data_ptr();
+    a.ldy = y->stride(0);
+  }
+  if (epi == 1 && ssq_out.has_value()) {
+    check_f32(*ssq_out, "ssq_out");
+    TORCH_CHECK(ssq_out->dim() == 2 && ssq_out->size(0) >= (N + bn - 1) / bn && ssq_out->size(1) >= M,
+                "ssq_out [>= n_tiles, >= M]");
+    a.ssq_out = ssq_out->data_ptr<float>();
+    a.ssq_out_ld = ssq_out->size(1);
+  }
+  if (epi == 3) TORCH_CHECK(N % 32 == 0, "swiglu: N % 32 == 0");
+  if (epi == 2) {
+    TORCH_CHECK(pos.has_value() && cos_sin.has_value() && slots.has_value() && q_out.has_value() && kc.has_value() &&
+                    vc.has_value(),
+                "qkv epilogue operands");
+    check_i32(*pos, "positions");
+    check_i32(*slots, "slots");
+    check_f32(*cos_sin, "cos_sin");
+    check_bf16(*q_out, "q_out");
+    check_bf16(*kc, "k_cache");
+    check_bf16(*vc, "v_cache");
+    TORCH_CHECK(d % 32 == 0 && N == (nq + 2 * nkv) * d, "qkv: N == (nq + 2 nkv) d, d % 32 == 0");
+    TORCH_CHECK(pos->numel() >= M && slots->numel() >= M, "positions/slots length");
+    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == d, "cos_sin [max_pos, d]");
+    TORCH_CHECK(q_out->is_contiguous() && q_out->numel() >= (int64_t)M * nq * d, "q_out [M, nq, d]");
+    TORCH_CHECK(kc->is_contiguous() && vc->is_contiguous() && kc->dim() == 4 && kc->size(1) == nkv &&
+                    kc->size(2) == 16 && kc->size(3) == d && vc->size(1) == nkv && vc->size(2) == d &&
+                    vc->size(3) == 16,
+                "cache layout: K [blocks, nkv, 16, d], V [blocks, nkv, d, 16]");
+    a.pos = pos->data_ptr<int>();
+    a.cos_sin = cos_sin->data_ptr<float>();
+    a.slots = slots->data_ptr<int>();
+    a.q_out = (uint16_t*)q_out->data_ptr();
+    a.kc = (uint16_t*)kc->data_ptr();
+    a.vc = (uint16_t*)vc->data_ptr();
+    a.nq = nq; a.nkv = nkv; a.d = d;
+  }
+  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)epi, stream()), "tgemm");
+}
+
+// r = h + r in place (h optional), ssq[m] = sum(r[m]^2)  (f32 [M])
+void res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tensor ssq) {
+  check_bf16(r, "r");
+  check_f32(ssq, "ssq");
+  TORCH_CHECK(r.dim() == 2 && r.stride(1) == 1 && ssq.numel() >= r.size(0), "r [M, H], ssq [>= M]");
+  const void* hp = nullptr;
+  long ldh = 0;
+  if (h.has_value()) {
+    check_bf16(*h, "h");
+    TORCH_CHECK(h->dim() == 2 && h->stride(1) == 1 && h->sizes() == r.sizes(), "h like r");
+    hp = h->data_ptr();
+    ldh = h->stride(0);
+  }
+  ok(dllm_res_add_ssq(hp, ldh, r.data_ptr(), r.stride(0), ssq.data_ptr<float>(), r.size(0), r.size(1), stream()),
+     "res_add_ssq");
+}
 }  // namespace
 
 PYBIND11_MODULE(_hip_kernels, m) {
   m.def("moe_ffn", &moe_ffn);
+  m.def("tgemm", &tgemm);
+  m.def("res_add_ssq", &res_add_ssq);
   m.def("mm_gemm", &mm_gemm);
   m.def("car_alloc", &car_alloc);
   m.def("car_handle", &car_handle);

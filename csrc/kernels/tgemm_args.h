@@ -1,0 +1,35 @@
+// Argument block of the fused-epilogue GEMM (csrc/kernels/tgemm.hip), shared with the host
+// bindings (csrc/bindings.cpp) so both sides agree on the layout.
+#pragma once
+#include <stdint.h>
+
+namespace dllm {
+struct GemmArgs {
+  const uint16_t* A;
+  long lda;
+  const uint16_t* W;  // [N, K] contiguous
+  uint16_t* Y;        // PLAIN [M, N]; RESADD residual [M, N] (in place); SWIGLU [M, N / 2]; QKV unused
+  long ldy;
+  int M, N, K;
+  int kchunk, splits;
+  float* part;    // split-K slabs
+  int* counters;  // split-K tickets, one per output tile (zeroed; re-armed by the last arriver)
+  // row scale rinv[m] = rsqrt(sum_s ssq_in[s * ssq_in_ld + m] * norm_scale + eps)  (null: none)
+  const float* ssq_in;
+  int ssq_in_n;
+  long ssq_in_ld;
+  float norm_scale, eps;
+  // RESADD: partial row sums of squares ssq_out[n_tile * ssq_out_ld + m]
+  float* ssq_out;
+  long ssq_out_ld;
+  // QKV
+  const int* pos;
+  const float* cos_sin;  // [max_pos, d]: cos in [:d/2], sin in [d/2:]
+  const int* slots;      // [M] cache slot (-1: skip the K/V write)
+  uint16_t* q_out;            // [M, nq, d]
+  uint16_t* kc;               // [blocks, nkv, 16, d]
+  uint16_t* vc;               // [blocks, nkv, d, 16]
+  int nq, nkv, d;
+};
+enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3 };
+}  // namespace dllm

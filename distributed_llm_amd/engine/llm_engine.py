@@ -139,6 +139,7 @@ class LLMEngine:
         self._memo_cap = 200_000
         self._memo_lock = threading.Lock()
         self.on_gpu = self.device.type == "cuda"
+        self._ws_owner = ("engine", id(self))   # split-K workspaces of this engine's kernels/graphs
         # expert-parallel MoE exchanges split sizes on the host (parallel.expert_parallel): eager
         self.use_graphs = use_graphs and self.on_gpu and not getattr(self.model, "moe_ep", False)
         self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
@@ -231,14 +232,17 @@ class LLMEngine:
         m = self.model
         shapes = set()
         L = m.layers[0]
-        for name in ("wqkv", "wo", "wgu"):
+        for name in ("wqkv", "wqkv_f", "wo", "wgu", "wgu_f"):
             if name in L:
                 shapes.add((L[name].shape[0], L[name].shape[1], False))
         if "wd" in L:
-            shapes.add((L["wd"].shape[0], L["wd"].shape[1], True))
+            # fused layers stream the SwiGLU activation as a plain operand (EPI_RESADD)
+            shapes.add((L["wd"].shape[0], L["wd"].shape[1], not m.fused))
         shapes.add((m.lm_head.shape[0], m.lm_head.shape[1], False))
-        ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= ops.gemm.MAX_M], self.device,
-                          verbose=os.environ.get("DLLM_VERBOSE") == "1")
+        with ops.gemm.workspace_owner(self._ws_owner):
+            ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= ops.gemm.MAX_M], self.device,
+                              verbose=os.environ.get("DLLM_VERBOSE") == "1")
+            ops.gemm.reserve(self.device)
 
     # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),
     # tiles ordered longest context first (the dispatcher then starts the longest chains first).
@@ -605,6 +609,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ prefill
     def _prefill_step(self, prefilling: List[_Seq]) -> List[_Seq]:
+        with ops.gemm.workspace_owner(self._ws_owner):
+            return self._prefill_step_inner(prefilling)
+
+    def _prefill_step_inner(self, prefilling: List[_Seq]) -> List[_Seq]:
         budget = self.max_prefill_tokens
         chunk: List[tuple] = []
         for s in prefilling:
@@ -786,6 +794,10 @@ class LLMEngine:
                         split_len=self.d_split if self.ATTN_DYNAMIC else None)
 
     def _decode_forward(self, bs: int) -> None:
+        with ops.gemm.workspace_owner(self._ws_owner):
+            self._decode_forward_inner(bs)
+
+    def _decode_forward_inner(self, bs: int) -> None:
         ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)
         hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches)
         if self.fused_sampler:

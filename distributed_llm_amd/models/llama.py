@@ -12,6 +12,13 @@ tied embeddings and dense-vs-MoE MLP (models.configs).  MI355X-first layout deci
     down_proj row-parallel + ONE all-reduce each, vocab-parallel embedding (masked lookup +
     all-reduce) and LM head (distributed arg-max / top-k; parallel.comm).
 Weights: random init with a fixed seed (no checkpoints in this environment) or HF safetensors.
+
+Fused decoder layer (GPU, tensor-parallel size 1; ``DLLM_FUSED=0`` disables): the residual stream
+``r`` is updated in place by GEMM epilogues (csrc/kernels/tgemm.hip) and every RMSNorm is folded
+into the GEMM that consumes it (gamma into the weight columns, rinv from the producer's partial
+row sums of squares), so a dense layer is five launches: QKV+RoPE+KV-write, attention,
+o_proj+residual, gate|up+SwiGLU, down+residual.  The fused weights are stored instead of the plain
+ones (same bytes); ``reference_layers()`` reconstructs the plain layout for reference checks.
 """
 from __future__ import annotations
 
@@ -47,6 +54,54 @@ class AttnMeta:
     grid_items: int = 0                        # workgroups walking ``items``
 
 
+def qk_dim_order(d: int) -> torch.Tensor:
+    """Row order of one q/k head in the fused QKV weight: 32-row groups holding dims
+    16g..16g+15 then d/2+16g..d/2+16g+15, so each RoPE pair (i, i + d/2) lands in two adjacent
+    16-column MFMA fragments of the same lane (tgemm EPI_QKV)."""
+    idx = []
+    for g in range(d // 32):
+        idx += list(range(16 * g, 16 * g + 16)) + list(range(d // 2 + 16 * g, d // 2 + 16 * g + 16))
+    return torch.tensor(idx, dtype=torch.long)
+
+
+def gate_up_order(I: int) -> torch.Tensor:
+    """Row order of the fused gate|up weight: 32-row groups of 16 gate rows then the 16 matching
+    up rows (tgemm EPI_SWIGLU pairs them in-register)."""
+    o = torch.arange(2 * I)
+    g, c = o // 32, o % 32
+    return torch.where(c < 16, 16 * g + c, I + 16 * g + (c - 16))
+
+
+def _qkv_rows(nq: int, nkv: int, d: int) -> torch.Tensor:
+    p = qk_dim_order(d)
+    rows = [h * d + p for h in range(nq + nkv)] + [torch.arange((nq + nkv) * d, (nq + 2 * nkv) * d)]
+    return torch.cat(rows)
+
+
+def fuse_qkv_weight(wqkv: torch.Tensor, ln: torch.Tensor, nq: int, nkv: int, d: int) -> torch.Tensor:
+    idx = _qkv_rows(nq, nkv, d).to(wqkv.device)
+    return (wqkv.index_select(0, idx).float() * ln.float()[None, :]).to(wqkv.dtype).contiguous()
+
+
+def unfuse_qkv_weight(wf: torch.Tensor, ln: torch.Tensor, nq: int, nkv: int, d: int) -> torch.Tensor:
+    idx = _qkv_rows(nq, nkv, d).to(wf.device)
+    out = torch.empty_like(wf, dtype=torch.float32)
+    out[idx] = wf.float() / ln.float()[None, :]
+    return out.to(wf.dtype)
+
+
+def fuse_gate_up_weight(wgu: torch.Tensor, ln: torch.Tensor) -> torch.Tensor:
+    idx = gate_up_order(wgu.shape[0] // 2).to(wgu.device)
+    return (wgu.index_select(0, idx).float() * ln.float()[None, :]).to(wgu.dtype).contiguous()
+
+
+def unfuse_gate_up_weight(wf: torch.Tensor, ln: torch.Tensor) -> torch.Tensor:
+    idx = gate_up_order(wf.shape[0] // 2).to(wf.device)
+    out = torch.empty_like(wf, dtype=torch.float32)
+    out[idx] = wf.float() / ln.float()[None, :]
+    return out.to(wf.dtype)
+
+
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, par: ParallelContext = SINGLE,
                  seed: int = 0, weights: Optional[str] = None, init_std: float = 0.02):
@@ -74,6 +129,38 @@ class LlamaModel:
         if weights:
             self.load_safetensors(weights)
         self.cos_sin = ops.rope_cos_sin(cfg.max_position, self.d, cfg.rope_theta, self.device, cfg.rope_scaling)
+        self.fused = self._fusable()
+        if self.fused:
+            self._fuse_weights()
+
+    # ------------------------------------------------------------------ fused layout
+    def _fusable(self) -> bool:
+        cfg = self.cfg
+        if self.device.type != "cuda" or self.par.tp_size != 1 or os.environ.get("DLLM_FUSED", "1") != "1":
+            return False
+        if not ops.native_available():
+            return False
+        return (self.d % 32 == 0 and cfg.hidden % 64 == 0 and (self.nq * self.d) % 64 == 0
+                and (cfg.is_moe or (self.I % 64 == 0)))
+
+    def _fuse_weights(self) -> None:
+        for L in self.layers:
+            L["wqkv_f"] = fuse_qkv_weight(L.pop("wqkv"), L["ln1"], self.nq, self.nkv, self.d)
+            if "wgu" in L:
+                L["wgu_f"] = fuse_gate_up_weight(L.pop("wgu"), L["ln2"])
+
+    def reference_layers(self) -> List[Dict[str, torch.Tensor]]:
+        """Layer weights in the plain (unfused) layout, e.g. for a CPU reference forward."""
+        if not self.fused:
+            return self.layers
+        out = []
+        for L in self.layers:
+            R = {k: v for k, v in L.items() if k not in ("wqkv_f", "wgu_f")}
+            R["wqkv"] = unfuse_qkv_weight(L["wqkv_f"], L["ln1"], self.nq, self.nkv, self.d)
+            if "wgu_f" in L:
+                R["wgu"] = unfuse_gate_up_weight(L["wgu_f"], L["ln2"])
+            out.append(R)
+        return out
 
     # ------------------------------------------------------------------ weights
     def _init_random(self, seed: int, std: float) -> None:
@@ -212,6 +299,8 @@ class LlamaModel:
                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Final-normed hidden states of each sequence's last new token: [S, H]."""
         cfg = self.cfg
+        if getattr(self, "fused", False):
+            return self._hidden_states_fused(input_ids, positions, meta, kv_caches)
         if self.par.use_sp(input_ids.shape[0]) and not (input_ids.is_cuda and torch.cuda.is_current_stream_capturing()):
             return self._hidden_states_sp(input_ids, positions, meta, kv_caches)
         h = self._embed(input_ids)
@@ -237,6 +326,36 @@ class LlamaModel:
         last_h = h.index_select(0, meta.last_idx)
         last_r = residual.index_select(0, meta.last_idx)
         return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)
+
+    def _hidden_states_fused(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
+                             kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """Fused layer path (module docstring): residual stream ``r`` updated in place by GEMM
+        epilogues; ``ssq``/``n`` = partial row sums of r^2 of the latest residual producer."""
+        cfg = self.cfg
+        T, H, eps = input_ids.shape[0], cfg.hidden, cfg.rms_eps
+        r = ops.embedding(input_ids, self.embed, self.vocab_shard.start)
+        slots_n = ops.gemm.max_slots(H)
+        ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
+        ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
+        ops.gemm.res_add_ssq(None, r, ssq_a[0])
+        n = 1
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,
+                                        self.nq, self.nkv, self.d)
+            o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
+                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
+                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
+                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+            nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b)
+            if not cfg.is_moe:
+                act = ops.gemm.swiglu_matmul(r, L["wgu_f"], ssq_b, nb, eps)
+                n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a)
+            else:
+                x = ops.rms_norm(r, L["ln2"], eps)
+                ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a[0])
+                n = 1
+        return ops.rms_norm(r.index_select(0, meta.last_idx), self.final_norm, eps)
 
     def _hidden_states_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
                           kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:

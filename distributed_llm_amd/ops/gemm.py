@@ -1,18 +1,32 @@
-"""Linear layers: decode-shaped GEMMs on the hand-written MFMA skinny kernel, autotuned.
+"""Linear layers on hand-written MFMA kernels, autotuned per decode bucket, with fused epilogues.
 
 ``linear(x, w)`` computes ``x @ w.T`` (w stored [N, K], K contiguous).
-``linear_swiglu(gu, w)`` computes ``silu(gu[:, :K]) * gu[:, K:] @ w.T`` — the SwiGLU activation is
-fused into the down projection's operand load, so decode runs no separate activation kernel.
+``linear_swiglu(gu, w)`` computes ``silu(gu[:, :K]) * gu[:, K:] @ w.T``.
 
-Dispatch (GPU): M <= 128 -> ``csrc/kernels/skinny_gemm.hip`` with the (ntw, split-K) plan that the
-autotuner measured fastest for this (M, N, K, swiglu) — including "blas" (hipBLASLt via
-``F.linear``) as a candidate, so the custom kernel is only used where it wins; M > 128 (prefill)
--> hipBLASLt.  Plans are tuned once per shape OUTSIDE graph capture (``autotune`` is called by the
-engine for every decode bucket before capturing); an unseen shape during capture falls back to
-a heuristic plan.  CPU tensors -> plain torch.
+Kernels (csrc/kernels):
+  * ``tgemm.hip``  — LDS-tiled MFMA GEMM (global_load_lds ring, XOR-swizzled LDS, XCD-aware
+    block order, optional in-launch split-K) with the transformer epilogues used by the fused
+    decoder layer (models/llama.py): QKV + RoPE + paged-KV write, residual add + row sums of
+    squares (RMSNorm folded into the next GEMM), SwiGLU.  Any M (decode buckets and prefill).
+  * ``gemv.hip`` (M <= 8), ``skinny_gemm.hip`` / ``skinny_lds.hip`` (M <= 128), ``mm_gemm.hip``
+    (M <= 256): register-streaming decode GEMMs without LDS tiling.
+  * hipBLASLt via ``F.linear`` stays a candidate, so a custom kernel is used only where it wins.
+
+Plans are measured once per (M, N, K) OUTSIDE graph capture (``autotune``, called by the engine
+for every decode bucket before capturing) as hipGraph replays over rotated weight copies (a
+decode step streams the whole model: weights come from HBM, not the Infinity Cache); an unseen
+shape (prefill) uses a heuristic plan.  CPU tensors -> plain torch.
+
+Split-K workspaces are FIXED-size per (device, owner) and never re-allocated: captured graphs
+keep raw pointers to them, so growing (freeing) a workspace after a capture would leave graph
+replays writing into freed memory.  Plans whose workspace need exceeds the fixed
+size are never chosen.  Engines capture under their own owner key (``workspace_owner``), so two
+engines replaying graphs concurrently on one device never share split-K tickets.
 """
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import math
 import os
 from typing import Dict, Iterable, Optional, Tuple
@@ -22,41 +36,67 @@ import torch.nn.functional as F
 
 from . import _native, reference as ref
 
-MAX_M = 256        # custom kernels cover decode buckets up to 256 rows
+MAX_M = 1024       # decode buckets up to this size are autotuned
 SKINNY_MAX_M = 128
+MM_MAX_M = 256
 _SPLITS = (1, 2, 4, 8, 16)
 _NTWS = (1, 2, 4)
 _MM_NTS = (2, 4)
 _MM_SPLITS = (1, 2, 4, 8)
 _GEMV_MS = (1, 2, 4, 8)   # csrc/kernels/gemv.hip instantiations (decode buckets below 16)
 _GEMV_RS = (1, 2, 4)
+_TG_TILES = ((64, 64), (64, 128), (128, 64), (128, 128))
+_TG_SPLITS = (1, 2, 3, 4, 6, 8)
+WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
+WS_COUNTERS = 1 << 16
+
+EPI_PLAIN, EPI_RESADD, EPI_QKV, EPI_SWIGLU = 0, 1, 2, 3
+
+_OWNER: contextvars.ContextVar = contextvars.ContextVar("dllm_gemm_ws_owner", default=None)
+
+
+@contextlib.contextmanager
+def workspace_owner(key):
+    """Route split-K workspace lookups of this thread/context to ``key``'s own buffers."""
+    tok = _OWNER.set(key)
+    try:
+        yield
+    finally:
+        _OWNER.reset(tok)
 
 
 class _Planner:
     def __init__(self):
-        self.plans: Dict[Tuple[int, int, int, bool], Tuple] = {}
-        self.part: Dict[torch.device, torch.Tensor] = {}
-        self.counters: Dict[torch.device, torch.Tensor] = {}
+        self.plans: Dict[Tuple[int, int, int, bool], Tuple] = {}     # best overall, for linear()
+        self.tg_plans: Dict[Tuple[int, int, int], Tuple] = {}        # best tgemm tile, for the fused ops
+        self.ws: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
         self.timings: Dict[Tuple[int, int, int, bool], Dict[str, float]] = {}
 
     def workspace(self, dev: torch.device, floats: int, tiles: int):
-        p = self.part.get(dev)
-        if p is None or p.numel() < floats:
+        """The fixed (part, counters) pair of the current owner on ``dev``; created once, outside
+        capture, never grown."""
+        if floats > WS_FLOATS or tiles > WS_COUNTERS:
+            raise RuntimeError(f"split-K plan needs {floats} floats / {tiles} tickets > fixed workspace")
+        key = (str(dev), _OWNER.get())
+        w = self.ws.get(key)
+        if w is None:
             if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("skinny_gemm workspace growth during graph capture")
-            p = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=dev)
-            self.part[dev] = p
-        c = self.counters.get(dev)
-        if c is None or c.numel() < tiles:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("skinny_gemm counter growth during graph capture")
-            c = torch.zeros(max(tiles, 4096), dtype=torch.int32, device=dev)
-            self.counters[dev] = c
-        return p, c
+                raise RuntimeError("split-K workspace first touched during graph capture (call reserve())")
+            w = (torch.empty(WS_FLOATS, dtype=torch.float32, device=dev),
+                 torch.zeros(WS_COUNTERS, dtype=torch.int32, device=dev))
+            self.ws[key] = w
+        return w
 
 
 _P = _Planner()
 
+
+def reserve(device) -> None:
+    """Create the current owner's workspace on ``device`` (call before capturing graphs)."""
+    _P.workspace(torch.device(device), 0, 0)
+
+
+# ----------------------------------------------------------------------------- workspace needs
 
 def _need_mm(M: int, N: int, K: int, nt: int, splits: int) -> Tuple[int, int]:
     bn = 16 * nt
@@ -72,11 +112,23 @@ def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tu
     tiles = (N + nc - 1) // nc
     kchunk = ((K + splits - 1) // splits + 31) // 32 * 32
     S = (K + kchunk - 1) // kchunk
-    # split-K slabs are laid out with the kernel's row-tile height (MT x 16 rows, MT in 1/2/4/8),
-    # not ceil(M/16) x 16: e.g. M = 100 runs the MT = 8 kernel and needs 128-row slabs
+    # split-K slabs are laid out with the kernel's row-tile height (MT x 16 rows, MT in 1/2/4/8)
     mp = 16 * (1 if M <= 16 else 2 if M <= 32 else 4 if M <= 64 else 8)
     return (S * tiles * nc * mp if S > 1 else 0), tiles
 
+
+def _tg_splits(K: int, splits: int) -> int:
+    kchunk = ((K + splits - 1) // splits + 63) // 64 * 64
+    return (K + kchunk - 1) // kchunk
+
+
+def _need_tg(M: int, N: int, K: int, bm: int, bn: int, splits: int) -> Tuple[int, int]:
+    tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
+    S = _tg_splits(K, splits)
+    return (S * tiles * bm * bn if S > 1 else 0), tiles
+
+
+# ----------------------------------------------------------------------------- plans
 
 def _heuristic(M: int, N: int, K: int) -> Tuple:
     if M > SKINNY_MAX_M:
@@ -87,12 +139,44 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
+def tg_plan(M: int, N: int, K: int) -> Tuple[int, int, int, int]:
+    """(bm, bn, stages, splits) of the fused GEMM for this shape: tuned, else a heuristic sized so
+    the grid covers the 256 CUs (bigger tiles first, split-K only for short grids)."""
+    p = _P.tg_plans.get((M, N, K))
+    if p is not None:
+        return p
+    mt128, nt128 = -(-M // 128), -(-N // 128)
+    if mt128 * nt128 >= 224:
+        return (128, 128, 3, 1)
+    mt64, nt64 = -(-M // 64), -(-N // 64)
+    if mt64 * nt128 >= 200:
+        return (64, 128, 3, 1)
+    tiles = mt64 * nt64
+    splits = 1
+    while tiles * splits * 2 <= 512 and K // (splits * 2) >= 256 and splits < 8:
+        splits *= 2
+    if _need_tg(M, N, K, 64, 64, splits)[0] > WS_FLOATS:
+        splits = 1
+    return (64, 64, 3, splits)
+
+
+def tg_slots(M: int, N: int, K: int) -> int:
+    """Row-sum-of-squares slots a RESADD GEMM of this shape writes (one per n-tile)."""
+    return -(-N // tg_plan(M, N, K)[1])
+
+
 def _run_plan(plan, x, w, swiglu, out):
     if plan[0] == "blas":
         if swiglu:
             x = ref_silu_mul(x)
         return torch.matmul(x, w.t(), out=out) if out is not None else F.linear(x, w)
     ext = _native(x)
+    if plan[0] == "tg":
+        if swiglu:
+            x = ref_silu_mul(x)
+        y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+        _tgemm(ext, x, w, EPI_PLAIN, plan[1:], y=y)
+        return y
     if plan[0] == "gemv":
         y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
         ext.gemv(x, w, y, plan[1], swiglu)
@@ -112,6 +196,18 @@ def _run_plan(plan, x, w, swiglu, out):
     return y
 
 
+def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
+           pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0):
+    bm, bn, st, sp = plan
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    part = cnt = None
+    if _tg_splits(K, sp) > 1:
+        floats, tiles = _need_tg(M, N, K, bm, bn, sp)
+        part, cnt = _P.workspace(x.device, floats, tiles)
+    ext.tgemm(x, w, y, epi, bm, bn, st, sp, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
+              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d))
+
+
 def ref_silu_mul(gu):
     from . import silu_mul
     return silu_mul(gu)
@@ -122,25 +218,28 @@ def _key(x, w, swiglu):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    if not x.is_cuda or x.shape[0] > MAX_M or os.environ.get("DLLM_GEMM") == "blas":
+    if not x.is_cuda or os.environ.get("DLLM_GEMM") == "blas":
         return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
-    plan = _P.plans.get(_key(x, w, False)) or _heuristic(x.shape[0], w.shape[0], w.shape[1])
+    plan = _P.plans.get(_key(x, w, False))
+    if plan is None:
+        if x.shape[0] > MAX_M and w.shape[1] % 64 == 0 and x.stride(0) % 8 == 0 and x.stride(1) == 1 \
+                and os.environ.get("DLLM_TG_PREFILL", "0") == "1":
+            plan = ("tg",) + tg_plan(x.shape[0], w.shape[0], w.shape[1])
+        elif x.shape[0] > MAX_M:
+            plan = ("blas",)
+        else:
+            plan = _heuristic(x.shape[0], w.shape[0], w.shape[1])
     return _run_plan(plan, x, w, False, out)
 
 
 def norm_linear(h: torch.Tensor, residual: torch.Tensor, spare: torch.Tensor, norm_w: torch.Tensor, eps: float,
                 w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """``linear(rmsnorm(h + residual) * norm_w, w)`` and the updated residual stream.
+    """``linear(rmsnorm(h + residual) * norm_w, w)`` and the updated residual stream (unfused
+    layer path: tensor parallel, CPU).
 
-    Where the tuned plan for this shape is the GEMV (batch <= 8), one launch does both
-    (csrc/kernels/gemv.hip NORM): the new residual goes to ``spare`` and is returned; otherwise
-    the norm kernel updates ``residual`` in place and it is returned.  Callers keep whichever
-    buffer comes back as the residual and the other one as the next spare.
-
-    Opt-in (DLLM_FUSED_NORM=1): measured SLOWER on MI355X at batch 1 (0.954 vs 0.889 ms per
-    TinyLlama decode step, profiles/r1_small_batch_decode.md) -- every GEMV workgroup redoes the
-    norm's reduction and two extra L2 round trips sit before its first FMA, which costs more
-    than the separate 4.5 us norm launch it removes."""
+    Where the tuned plan for this shape is the GEMV (batch <= 8), one launch can do both
+    (csrc/kernels/gemv.hip NORM, opt-in DLLM_FUSED_NORM=1: measured SLOWER at batch 1,
+    profiles/r1_small_batch_decode.md); the new residual then goes to ``spare`` and is returned."""
     M, N, K = h.shape[0], w.shape[0], w.shape[1]
     if h.is_cuda and M <= MAX_M and os.environ.get("DLLM_GEMM") != "blas" \
             and os.environ.get("DLLM_FUSED_NORM", "0") == "1":
@@ -160,17 +259,68 @@ def linear_swiglu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         return F.linear(ref.silu_mul(gu), w)
     if gu.shape[0] > MAX_M or os.environ.get("DLLM_GEMM") == "blas":
         from . import silu_mul
-        return F.linear(silu_mul(gu), w)
+        return linear(silu_mul(gu), w)
     plan = _P.plans.get(_key(gu, w, True)) or _heuristic(gu.shape[0], w.shape[0], w.shape[1])
     return _run_plan(plan, gu, w, True, None)
 
 
+# ----------------------------------------------------------------------------- fused decoder ops
+
+def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float,
+                   positions: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
+                   v_cache: torch.Tensor, nq: int, nkv: int, d: int) -> torch.Tensor:
+    """q [T, nq, d] of ``rope(rmsnorm(r) . Wqkv^T)``, K/V written to the paged caches, one launch.
+
+    ``w`` is the folded/permuted weight of models.llama.fuse_qkv_weight; ``ssq[:ssq_n]`` holds
+    the partial row sums of r^2 written by the producer of ``r``."""
+    T, H = r.shape
+    q = torch.empty((T, nq, d), dtype=r.dtype, device=r.device)
+    if T == 0:
+        return q
+    _tgemm(_native(r), r, w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
+           eps=eps, pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv,
+           d=d)
+    return q
+
+
+def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_out: torch.Tensor) -> int:
+    """``residual += x . w^T`` (bf16 rounding as ``rms_norm``'s residual add) and the partial row
+    sums of the new residual's squares into ``ssq_out[:slots]``; returns ``slots``."""
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    plan = tg_plan(M, N, K)
+    if M:
+        _tgemm(_native(x), x, w, EPI_RESADD, plan, y=residual, ssq_out=ssq_out)
+    return -(-N // plan[1])
+
+
+def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float) -> torch.Tensor:
+    """``silu(g) * u`` with ``[g | u] = rmsnorm(r) . Wgu^T`` (interleaved rows, models.llama
+    .fuse_gate_up_weight) -> [T, I]."""
+    T, H = r.shape
+    act = torch.empty((T, w.shape[0] // 2), dtype=r.dtype, device=r.device)
+    if T:
+        _tgemm(_native(r), r, w, EPI_SWIGLU, tg_plan(T, w.shape[0], H), y=act, ssq_in=ssq, ssq_n=ssq_n,
+               norm_scale=1.0 / H, eps=eps)
+    return act
+
+
+def res_add_ssq(h: Optional[torch.Tensor], r: torch.Tensor, ssq: torch.Tensor) -> None:
+    """``r += h`` in place (h may be None) and ``ssq[m] = sum(r[m]^2)`` (one slot)."""
+    if r.shape[0]:
+        _native(r).res_add_ssq(h, r, ssq)
+
+
+def max_slots(N: int) -> int:
+    return -(-N // 64)
+
+
+# ----------------------------------------------------------------------------- autotuning
+
 def _time(fn, iters=24) -> float:
     """GPU time per call of fn(i) in us, measured as a hipGraph replay of ``iters`` calls (the
     decode step is a graph replay too, so host launch cost is excluded exactly as in serving).
-    Callers rotate operands over i so weights come from HBM, not the 256 MiB Infinity Cache
-    (a decode step streams the whole model: its weights are cold)."""
-    fn(0)  # eager warm-up: allocates workspaces / initialises libraries outside capture
+    Callers rotate operands over i so weights come from HBM, not the 256 MiB Infinity Cache."""
+    fn(0)  # eager warm-up: initialises libraries outside capture
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     st = torch.cuda.Stream()
@@ -190,27 +340,60 @@ def _time(fn, iters=24) -> float:
     return s.elapsed_time(e) * 1000.0 / iters
 
 
+def _plan_key(k) -> str:
+    if len(k) == 3:
+        return "t,%d,%d,%d" % k
+    return "%d,%d,%d,%d" % (k[0], k[1], k[2], int(k[3]))
+
+
 def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False) -> None:
     """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest."""
     dev = torch.device(device)
     if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
         return
+    reserve(dev)
     cache = os.environ.get("DLLM_GEMM_PLANS")  # JSON plan cache: re-use a previous run's choices
     if cache and os.path.exists(cache):
         import json
         with open(cache) as f:
             for k, v in json.load(f).items():
-                M, N, K, sw = k.split(",")
-                _P.plans[(int(M), int(N), int(K), sw == "1")] = tuple(v)
+                parts = k.split(",")
+                if parts[0] == "t":
+                    _P.tg_plans[(int(parts[1]), int(parts[2]), int(parts[3]))] = tuple(v)
+                else:
+                    _P.plans[(int(parts[0]), int(parts[1]), int(parts[2]), parts[3] == "1")] = tuple(v)
     shapes = list(shapes)
     _autotune(shapes, list(ms), dev, verbose)
     if cache:
         import json
+        d = {_plan_key(k): list(v) for k, v in _P.plans.items()}
+        d.update({_plan_key(k): list(v) for k, v in _P.tg_plans.items()})
         with open(cache, "w") as f:
-            json.dump({f"{M},{N},{K},{int(sw)}": list(v) for (M, N, K, sw), v in _P.plans.items()}, f)
+            json.dump(d, f)
+
+
+def _tg_cands(M: int, N: int, K: int):
+    if K % 64:
+        return []
+    out = []
+    for bm, bn in _TG_TILES:
+        if bm == 128 and M <= 64:
+            continue
+        tiles = -(-M // bm) * -(-N // bn)
+        for sp in _TG_SPLITS:
+            if sp > 1 and (K // sp < 256 or tiles * sp > 2048):
+                continue
+            if _tg_splits(K, sp) != sp:
+                continue
+            if _need_tg(M, N, K, bm, bn, sp)[0] > WS_FLOATS:
+                continue
+            for st in (2, 3):
+                out.append((bm, bn, st, sp))
+    return out
 
 
 def _autotune(shapes, ms, dev, verbose: bool) -> None:
+    use_tg = os.environ.get("DLLM_GEMM_NO_TG") != "1"
     for (N, K, sw) in shapes:
         copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
         ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
@@ -218,17 +401,20 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
             if M > MAX_M:
                 continue
             key = (M, N, K, sw)
-            if key in _P.plans:
+            tkey = (M, N, K)
+            need_plain = key not in _P.plans
+            need_tg = use_tg and not sw and tkey not in _P.tg_plans and K % 64 == 0
+            if not (need_plain or need_tg):
                 continue
             x = torch.randn(M, 2 * K if sw else K, device=dev).to(torch.bfloat16)
             cands = [("blas",)]
-            if M > 16 and K % 64 == 0 and N % 8 == 0 and os.environ.get("DLLM_GEMM_NO_MM") != "1":
+            if M <= MM_MAX_M and M > 16 and K % 64 == 0 and N % 8 == 0 and os.environ.get("DLLM_GEMM_NO_MM") != "1":
                 for nt in _MM_NTS:
                     for s in _MM_SPLITS:
                         if s > 1 and K // s < 256:
                             continue
-                        floats, _ = _need_mm(M, N, K, nt, s)
-                        if floats * 4 > 256 << 20:
+                        floats, tiles = _need_mm(M, N, K, nt, s)
+                        if floats > WS_FLOATS or tiles > WS_COUNTERS:
                             continue
                         cands.append(("mm", nt, s))
             if M in _GEMV_MS and K % 8 == 0 and M * K * 2 <= 64 * 1024 and os.environ.get("DLLM_GEMM_NO_GEMV") != "1":
@@ -240,24 +426,33 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                     for s in _SPLITS:
                         if s > 1 and K // s < 128:
                             continue
-                        floats, _ = _need(M, N, K, ntw, s, 0 if kind == "skinny" else 1)
-                        if floats * 4 > 256 << 20:
+                        floats, tiles = _need(M, N, K, ntw, s, 0 if kind == "skinny" else 1)
+                        if floats > WS_FLOATS or tiles > WS_COUNTERS:
                             continue
                         cands.append((kind, ntw, s))
+            if use_tg and not sw:
+                cands.extend(("tg",) + c for c in _tg_cands(M, N, K))
             res = {}
             for c in cands:
                 res[c] = _time(lambda i: _run_plan(c, x, ws[i % copies], sw, None))
             best = min(res, key=res.get)
-            _P.plans[key] = best
-            _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
+            if need_plain:
+                _P.plans[key] = best
+                _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
+            tgc = [c for c in res if c[0] == "tg"]
+            if need_tg and tgc:
+                _P.tg_plans[tkey] = min(tgc, key=res.get)[1:]
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
-                      for k in ("gemv", "skinny", "lds", "mm")}
+                      for k in ("gemv", "skinny", "lds", "mm", "tg")}
                 extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
-                      f"({N * K * 2 / res[best] / 1e3:.0f} GB/s; blas {res[('blas',)]:.1f}us; {extra})", flush=True)
+                      f"({N * K * 2 / res[best] / 1e3:.0f} GB/s, {2 * M * N * K / res[best] / 1e6:.0f} TF/s; "
+                      f"blas {res[('blas',)]:.1f}us; {extra})", flush=True)
         del ws
 
 
 def plans() -> Dict:
-    return {str(k): v for k, v in _P.plans.items()}
+    d = {str(k): v for k, v in _P.plans.items()}
+    d.update({"tg" + str(k): v for k, v in _P.tg_plans.items()})
+    return d

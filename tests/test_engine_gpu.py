@@ -60,7 +60,8 @@ def test_hip_forward_matches_torch_reference():
     mc = copy.copy(m)
     mc.device = torch.device("cpu")
     mc.embed, mc.lm_head, mc.final_norm = m.embed.cpu(), m.lm_head.cpu(), m.final_norm.cpu()
-    mc.layers = [{k: v.cpu() for k, v in L.items()} for L in m.layers]
+    mc.layers = [{k: v.cpu() for k, v in L.items()} for L in m.reference_layers()]
+    mc.fused = False
     mc.cos_sin = m.cos_sin.cpu()
     kv = [(k.cpu().clone(), v.cpu().clone()) for k, v in eng.kv_caches]
     C = lambda t: t.cpu()

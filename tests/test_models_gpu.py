@@ -48,7 +48,8 @@ def _fp32_cpu_copy(m):
     mc.embed = f(m.embed)
     mc.lm_head = mc.embed if m.lm_head is m.embed else f(m.lm_head)
     mc.final_norm = f(m.final_norm)
-    mc.layers = [{k: f(v) for k, v in L.items()} for L in m.layers]
+    mc.layers = [{k: f(v) for k, v in L.items()} for L in m.reference_layers()]
+    mc.fused = False
     mc.cos_sin = m.cos_sin.cpu()
     return mc
 

@@ -1,0 +1,131 @@
+"""Numerics of the fused-epilogue MFMA GEMM (csrc/kernels/tgemm.hip) against plain-PyTorch fp32
+references, over every tile / pipeline depth / split-K plan and ragged M, N."""
+import math
+
+import pytest
+import torch
+
+from distributed_llm_amd import ops
+from distributed_llm_amd.ops import gemm as G
+from distributed_llm_amd.ops import reference as ref
+from distributed_llm_amd.models.llama import fuse_gate_up_weight, fuse_qkv_weight
+
+pytestmark = pytest.mark.gpu
+
+PLANS = [(bm, bn, st, sp) for bm, bn in G._TG_TILES for st in (2, 3) for sp in (1, 3)]
+
+
+def _rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
+
+
+def _ext():
+    return ops._native(torch.empty(1, device="cuda"))
+
+
+@pytest.mark.parametrize("plan", PLANS)
+@pytest.mark.parametrize("M,N,K", [(1, 64, 128), (37, 200, 192), (130, 320, 1024), (512, 2560, 2048)])
+def test_plain(plan, M, N, K):
+    torch.manual_seed(M + N + K)
+    G.reserve("cuda")
+    x, w = _rnd(M, K), _rnd(N, K, scale=0.05)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    G._tgemm(_ext(), x, w, G.EPI_PLAIN, plan, y=y)
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), want, atol=2e-2 * want.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("plan", PLANS)
+def test_plain_row_scale(plan):
+    torch.manual_seed(3)
+    M, N, K = 70, 128, 256
+    G.reserve("cuda")
+    x, w = _rnd(M, K), _rnd(N, K, scale=0.05)
+    ssq = torch.rand(5, 96, device="cuda") * 10
+    y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    G._tgemm(_ext(), x, w, G.EPI_PLAIN, plan, y=y, ssq_in=ssq, ssq_n=4, norm_scale=1.0 / K, eps=1e-5)
+    rinv = torch.rsqrt(ssq[:4, :M].sum(0) / K + 1e-5)
+    want = (x.float() @ w.float().t()) * rinv[:, None]
+    torch.testing.assert_close(y.float(), want, atol=2e-2 * want.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("plan", PLANS)
+@pytest.mark.parametrize("M", [5, 200])
+def test_residual_add_and_row_sums(plan, M):
+    torch.manual_seed(M)
+    N, K = 256, 512
+    G.reserve("cuda")
+    x, w = _rnd(M, K), _rnd(N, K, scale=0.05)
+    r = _rnd(M, N)
+    r0 = r.clone()
+    ssq = torch.full((G.max_slots(N), M), float("nan"), device="cuda")
+    G._tgemm(_ext(), x, w, G.EPI_RESADD, plan, y=r, ssq_out=ssq)
+    h = (x.float() @ w.float().t()).to(torch.bfloat16)
+    want = (h.float() + r0.float()).to(torch.bfloat16)
+    torch.testing.assert_close(r.float(), want.float(), atol=3e-2, rtol=2e-2)
+    slots = math.ceil(N / plan[1])
+    tot = ssq[:slots].sum(0)
+    torch.testing.assert_close(tot, (r.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("plan", PLANS)
+@pytest.mark.parametrize("d,nq,nkv", [(64, 8, 2), (128, 4, 4), (96, 3, 1)])
+def test_qkv_rope_cache(plan, d, nq, nkv):
+    torch.manual_seed(d)
+    M, H = 45, 256
+    G.reserve("cuda")
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wqkv = _rnd((nq + 2 * nkv) * d, H, scale=0.05)
+    wf = fuse_qkv_weight(wqkv, ln, nq, nkv, d)
+    ssq = torch.empty(1, M, device="cuda")
+    ops.gemm.res_add_ssq(None, r, ssq[0])
+    cos_sin = ops.rope_cos_sin(4096, d, 10000.0, "cuda")
+    pos = torch.randint(0, 4000, (M,), device="cuda", dtype=torch.int32)
+    nblk = 16
+    slots = torch.randperm(nblk * 16, device="cuda")[:M].to(torch.int32)
+    slots[3] = -1
+    kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
+    q = torch.empty(M, nq, d, dtype=torch.bfloat16, device="cuda")
+    G._tgemm(_ext(), r, wf, G.EPI_QKV, plan, ssq_in=ssq, ssq_n=1, norm_scale=1.0 / H, eps=1e-5, pos=pos,
+             cos_sin=cos_sin, slots=slots, q_out=q, kc=kc, vc=vc, nq=nq, nkv=nkv, d=d)
+    # reference: rmsnorm -> plain GEMM -> rope + cache write (ops.reference, f32 math)
+    x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
+    qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
+    kr = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16)
+    vr = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16)
+    qr = ref.rope_and_cache(qkv, pos.cpu(), cos_sin.cpu(), slots.cpu(), kr, vr, nq, nkv, d)
+    torch.testing.assert_close(q.cpu().float(), qr.float(), atol=4e-2, rtol=3e-2)
+    torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=4e-2, rtol=3e-2)
+    torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=4e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("plan", PLANS)
+def test_swiglu(plan):
+    torch.manual_seed(7)
+    M, H, I = 99, 256, 320
+    G.reserve("cuda")
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = _rnd(2 * I, H, scale=0.05)
+    wf = fuse_gate_up_weight(wgu, ln)
+    ssq = torch.empty(1, M, device="cuda")
+    ops.gemm.res_add_ssq(None, r, ssq[0])
+    act = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    G._tgemm(_ext(), r, wf, G.EPI_SWIGLU, plan, y=act, ssq_in=ssq, ssq_n=1, norm_scale=1.0 / H, eps=1e-5)
+    x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
+    gu = (x.float() @ wgu.cpu().float().t()).to(torch.bfloat16)
+    want = ref.silu_mul(gu)
+    torch.testing.assert_close(act.cpu().float(), want.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_res_add_ssq():
+    torch.manual_seed(1)
+    h, r = _rnd(33, 320), _rnd(33, 320)
+    r0 = r.clone()
+    ssq = torch.empty(33, device="cuda")
+    ops.gemm.res_add_ssq(h, r, ssq)
+    want = (h.float() + r0.float()).to(torch.bfloat16)
+    assert torch.equal(r, want)
+    torch.testing.assert_close(ssq, (want.float() ** 2).sum(1), rtol=1e-5, atol=1e-4)
