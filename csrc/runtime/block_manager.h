@@ -53,6 +53,8 @@ struct Seq {
   std::vector<int> blocks;
   std::vector<int32_t> tokens;
   std::vector<uint64_t> chain;  // chain hash per committed full block
+  std::vector<int> canon;       // canonical registered block holding each committed full block's
+                                // content (-2: none, e.g. a hash collision), the parent link of the next
   int committed = 0;            // tokens whose K/V have been computed
 };
 
@@ -108,6 +110,7 @@ class BlockManager {
     for (int i = 0; i < need; ++i) s.blocks.push_back(fresh());
     s.tokens = tokens;
     s.chain = chain;
+    s.canon = matched;
     s.committed = (int)matched.size() * bs_;
     hit_tokens_ += s.committed;
     query_tokens_ += n;
@@ -163,15 +166,26 @@ class BlockManager {
     for (int b = (int)s.chain.size(); b < full; ++b) {
       for (int j = 0; j < bs_; ++j) h = mix(h, s.tokens[b * bs_ + j]);
       s.chain.push_back(h);
-      const int blk = s.blocks[b];
-      if (!blocks_[blk].hashed && !hash2block_.count(h)) {
+      // Parent links always point at the CANONICAL registered block of the previous chunk (the one
+      // a later lookup will have matched), not necessarily this sequence's own copy: two sequences
+      // that prefilled the same prefix concurrently both keep matching each other's chains.
+      const int parent = b > 0 ? s.canon[b - 1] : -1;
+      const int32_t* toks = &s.tokens[(size_t)b * bs_];
+      int canon = -2;
+      auto it = hash2block_.find(h);
+      if (it != hash2block_.end()) {
+        if (parent != -2 && same_block(it->second, parent, toks)) canon = it->second;
+        else ++collisions_;
+      } else if (parent != -2 && !blocks_[s.blocks[b]].hashed) {
+        const int blk = s.blocks[b];
         blocks_[blk].hashed = true;
         blocks_[blk].hash = h;
-        blocks_[blk].parent = b > 0 ? s.blocks[b - 1] : -1;
-        std::copy(s.tokens.begin() + (size_t)b * bs_, s.tokens.begin() + (size_t)(b + 1) * bs_,
-                  tok_store_.begin() + (size_t)blk * bs_);
+        blocks_[blk].parent = parent;
+        std::copy(toks, toks + bs_, tok_store_.begin() + (size_t)blk * bs_);
         hash2block_[h] = blk;
+        canon = blk;
       }
+      s.canon.push_back(canon);
     }
   }
 
