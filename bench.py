@@ -252,7 +252,7 @@ def main() -> int:
     if not on_gpu:
         os.environ.setdefault("DLLM_EMBEDDER", "hash")
     topology = a.topology if world > 1 else "replicated"
-    cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False,
+    cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
 
     cluster = None

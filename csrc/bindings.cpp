@@ -46,7 +46,7 @@ int dllm_car_open_handle(const char*, void**);
 int dllm_car_close_handle(void*);
 int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
-int dllm_tgemm(const void*, int, int, int, int, hipStream_t);
+int dllm_tgemm(const void*, int, int, int, int, int, int, hipStream_t);
 int dllm_res_add_ssq(const void*, long, void*, long, float*, int, int, hipStream_t);
 int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
                               unsigned long long*, hipStream_t);
@@ -501,7 +501,7 @@ void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
 // row-scaled by rinv from ssq_in), 1 residual add (y = residual, in place; ssq_out partial row
 // sums), 2 QKV (RoPE + q_out + paged K/V writes), 3 SwiGLU (y = [M, N/2]).
 void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int64_t epi, int64_t bm, int64_t bn,
-           int64_t stages, int64_t splits, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> counters,
+           int64_t stages, int64_t splits, int64_t ks, int64_t nw, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> counters,
            c10::optional<torch::Tensor> ssq_in, int64_t ssq_in_n, double norm_scale, double eps,
            c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> pos,
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
@@ -512,11 +512,15 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
   const int M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(x.size(1) == K && K % 64 == 0, "x [M, K], K % 64 == 0");
-  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && (stages == 2 || stages == 3), "tile");
+  TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn == 128)), "ks in {1,2}; nw 4, or 8 with bn 128");
+  TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
+  TORCH_CHECK((bm == 64 || bm == 128 || (bm == 256 && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
+                  (stages == 2 || stages == 3) && (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024,
+              "tile / ring size");
   TORCH_CHECK(splits >= 1 && splits <= 64, "splits");
+  const int kq = 64 * (int)ks;
   int kchunk = (K + splits - 1) / splits;
-  kchunk = (kchunk + 63) / 64 * 64;
+  kchunk = (kchunk + kq - 1) / kq * kq;
   const int S = (K + kchunk - 1) / kchunk;
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   dllm::GemmArgs a{};
@@ -586,7 +590,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
     a.vc = (uint16_t*)vc->data_ptr();
     a.nq = nq; a.nkv = nkv; a.d = d;
   }
-  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)epi, stream()), "tgemm");
+  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)epi, stream()), "tgemm");
 }
 
 // r = h + r in place (h optional), ssq[m] = sum(r[m]^2)  (f32 [M])

@@ -59,14 +59,23 @@ __device__ __forceinline__ void block_sync_lds() {
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 __device__ __forceinline__ float bfr(float x) { return bf2f(f2bf(x)); }
 
-template <int BM, int BN, int EPI, int STAGES>
-__global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+// KS: 64-deep k sub-tiles per ring stage (one barrier per stage); NW: waves per workgroup, laid out
+// 2 (M) x NW/2 (N), each wave a (BM/2) x (BN/(NW/2)) tile.
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW>
+__global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
+  constexpr int NT = 64 * NW, NWN = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / NWN;
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int A_BYTES = BM * ROWB, STAGE_BYTES = (BM + BN) * ROWB;
-  constexpr int GA = BM / 32, GB = BN / 32, G = GA + GB;  // global_load_lds per wave per stage
-  constexpr int RING = STAGES * STAGE_BYTES;
-  constexpr int TPR = 256 / BM;  // threads per row in the rinv reduction (2 or 4)
+  static_assert(FN % 2 == 0 && FM >= 1, "wave tile: >= 16 rows, a multiple of 32 columns");
+  constexpr int A_BYTES = BM * ROWB, SUB_BYTES = (BM + BN) * ROWB, STAGE_BYTES = KS * SUB_BYTES;
+  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // global_load_lds per wave per sub-tile
+  constexpr int G = KS * (GA + GB);                      // ... per stage
+  static_assert(GA >= 1 && GB >= 1, "tile too small for the wave count");
+  constexpr int KSTEP = BK * KS;
+  constexpr int OW = (EPI == EPI_SWIGLU) ? BN / 2 : BN;  // staged output columns per row
+  constexpr int OLD = OW + 8;                             // staged row stride (bf16)
+  constexpr int RING = (STAGES * STAGE_BYTES > BM * OLD * 2) ? STAGES * STAGE_BYTES : BM * OLD * 2;
+  constexpr int TPR = NT >= BM ? NT / BM : 1;  // threads per row in the rinv reduction
   // one LDS array (a second __shared__ object can make hipcc drain the ring: §5 trap 4(a))
   //   [ring][rinv partials TPR x BM][row-sum partials 2 x BM][flag]
   __shared__ __attribute__((aligned(16))) unsigned char smem[RING + TPR * BM * 4 + 2 * BM * 4 + 16];
@@ -75,7 +84,7 @@ __global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
   int* s_last = reinterpret_cast<int*>(s_red + 2 * BM);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
   const int M = a.M, N = a.N, K = a.K, S = a.splits;
   const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
   const int nwg = mt * nt * S;
@@ -86,7 +95,7 @@ __global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
   const int m_tile = rest % mt, n_tile = rest / mt;
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int kbeg = split * a.kchunk;
-  const int nk = max(0, (min(K, kbeg + a.kchunk) - kbeg) / BK);
+  const int nk = max(0, (min(K, kbeg + a.kchunk) - kbeg) / KSTEP);
 
   // ---- row-scale prologue: the partial-sum loads are issued before the ring so they retire at
   // the ring's first wait; their sums go to LDS and are combined per row in the epilogue
@@ -119,16 +128,19 @@ __global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
     b_src[j] = a.W + (long)min(n0 + r, N - 1) * K + kbeg + 8 * (spos ^ ((r >> 1) & 7));
   }
   auto issue = [&](int t) {
-    unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
-    const int ko = t * BK;
 #pragma unroll
-    for (int j = 0; j < GA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + ko), (lds_void*)(base + (wave * GA + j) * 1024), 16,
-                                       0, 0);
+    for (int ks = 0; ks < KS; ++ks) {
+      unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + ks * SUB_BYTES;
+      const int ko = t * KSTEP + ks * BK;
 #pragma unroll
-    for (int j = 0; j < GB; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + ko),
-                                       (lds_void*)(base + A_BYTES + (wave * GB + j) * 1024), 16, 0, 0);
+      for (int j = 0; j < GA; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + ko), (lds_void*)(base + (wave * GA + j) * 1024),
+                                         16, 0, 0);
+#pragma unroll
+      for (int j = 0; j < GB; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + ko),
+                                         (lds_void*)(base + A_BYTES + (wave * GB + j) * 1024), 16, 0, 0);
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -164,11 +176,11 @@ __global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
     }
     block_sync_lds();
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
-    const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < 2 * KS; ++s) {
+      const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + (s >> 1) * SUB_BYTES;
       bf16x8 af[FM], bw[FN];
-      const int c = 4 * s + (lane >> 4);
+      const int c = 4 * (s & 1) + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * WM + 16 * i + (lane & 15);
@@ -238,106 +250,41 @@ __global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
       rinv[i][e] = r;
     }
 
-  if constexpr (EPI == EPI_PLAIN) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + rl0 + 16 * i + e;
-        if (m >= M) continue;
-        u16* yr = a.Y + (long)m * a.ldy;
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int n = n0 + wn * WN + 16 * j + cl;
-          if (n < N) yr[n] = f2bf(acc[i][j][e] * rinv[i][e]);
-        }
-      }
-  } else if constexpr (EPI == EPI_RESADD) {
-    float ss[FM][4];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        ss[i][e] = 0.f;
-        const int m = m0 + rl0 + 16 * i + e;
-        if (m >= M) continue;
-        u16* yr = a.Y + (long)m * a.ldy;
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int n = n0 + wn * WN + 16 * j + cl;
-          if (n < N) {
-            const float v = bfr(bfr(acc[i][j][e]) + bf2f(yr[n]));
-            yr[n] = f2bf(v);
-            ss[i][e] += v * v;
-          }
-        }
-      }
-    // row sums over the wave's 16 column lanes, then over the two column-waves through LDS
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = ss[i][e];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 8, 64);
-        if (cl == 0) s_red[wn * BM + rl0 + 16 * i + e] = v;
-      }
-    __syncthreads();
-    if (a.ssq_out != nullptr && threadIdx.x < BM && m0 + (int)threadIdx.x < M)
-      a.ssq_out[(long)n_tile * a.ssq_out_ld + m0 + threadIdx.x] = s_red[threadIdx.x] + s_red[BM + threadIdx.x];
-  } else if constexpr (EPI == EPI_SWIGLU) {
-    // fragment pairs (2jp, 2jp + 1) = (gate, up) of the same 16 intermediate columns
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + rl0 + 16 * i + e;
-        if (m >= M) continue;
-        u16* yr = a.Y + (long)m * a.ldy;
-#pragma unroll
-        for (int jp = 0; jp < FN / 2; ++jp) {
-          const int n = n0 + wn * WN + 32 * jp;  // 32-aligned group start
-          if (n >= N) continue;
-          const float g = bfr(acc[i][2 * jp][e] * rinv[i][e]), u = bfr(acc[i][2 * jp + 1][e] * rinv[i][e]);
-          yr[n / 2 + cl] = f2bf(silu(g) * u);
-        }
-      }
-  } else {  // EPI_QKV
+  // Output staging: every epilogue writes its bf16 results into an LDS image of the tile
+  // ([BM][OW + 8] bf16, row pad = one 16-B slot against bank conflicts; the ring is idle now)
+  // and the block then copies it out as 16-B row vectors, so global stores are full-width and
+  // coalesced instead of 2-B scattered lane stores (RESADD reads the residual the same way).
+  static_assert(BM * OLD * 2 <= RING, "output stage must fit the ring");
+  u16* so = reinterpret_cast<u16*>(smem);
+  const bool full_n = n0 + BN <= N;  // (N % 8 == 0 is required on the host side for vector stores)
+
+  if constexpr (EPI == EPI_QKV) {
+    // RoPE in registers (pairs in adjacent fragments of one lane), V written straight from the
+    // registers (transposed cache layout: no row vectors to form), q/k staged.
     const int d = a.d, hd = d / 2, nq = a.nq, nkv = a.nkv;
     const int qcols = nq * d, kcols = nkv * d;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = m0 + rl0 + 16 * i + e;
-        if (m >= M) continue;
-        const int slot = a.slots[m];
-        const float* cs = a.cos_sin + (long)a.pos[m] * d;
+        const int rl = rl0 + 16 * i + e, m = m0 + rl;
+        const int mm = min(m, M - 1);
+        const int slot = a.slots[mm];
+        const float* cs = a.cos_sin + (long)a.pos[mm] * d;
         const long blk = slot >> 4, off = slot & 15;
 #pragma unroll
         for (int jp = 0; jp < FN / 2; ++jp) {
-          const int nb = n0 + wn * WN + 32 * jp;  // 32-aligned group (never straddles a head)
+          const int cb = wn * WN + 32 * jp;  // tile column of this 32-aligned group
+          const int nb = n0 + cb;
           if (nb >= N) continue;
           const float x1 = bfr(acc[i][2 * jp][e] * rinv[i][e]), x2 = bfr(acc[i][2 * jp + 1][e] * rinv[i][e]);
           if (nb < qcols + kcols) {
-            const bool isq = nb < qcols;
-            const int cc = isq ? nb : nb - qcols;
-            const int head = cc / d, grp = (cc % d) >> 5;
-            const int d1 = 16 * grp + cl, d2 = hd + d1;
+            const int cc = nb < qcols ? nb : nb - qcols;
+            const int d1 = 16 * ((cc % d) >> 5) + cl;
             const float co = cs[d1], si = cs[hd + d1];
-            const u16 y1 = f2bf(x1 * co - x2 * si), y2 = f2bf(x2 * co + x1 * si);
-            if (isq) {
-              u16* qo = a.q_out + ((long)m * nq + head) * d;
-              qo[d1] = y1;
-              qo[d2] = y2;
-            } else if (slot >= 0) {
-              u16* ko = a.kc + ((blk * nkv + head) * 16 + off) * d;
-              ko[d1] = y1;
-              ko[d2] = y2;
-            }
-          } else if (slot >= 0) {  // V: natural dim order, transposed [d][16] per block
+            so[rl * OLD + cb + cl] = f2bf(x1 * co - x2 * si);
+            so[rl * OLD + cb + 16 + cl] = f2bf(x2 * co + x1 * si);
+          } else if (m < M && slot >= 0) {
             const int cc = nb - qcols - kcols;
             const int head = cc / d, dim = cc % d + cl;
             u16* vo = a.vc + ((blk * nkv + head) * d) * 16 + off;
@@ -346,27 +293,116 @@ __global__ void __launch_bounds__(256) tgemm_kernel(GemmArgs a) {
           }
         }
       }
+    __syncthreads();
+    // copy-out of q/k: an 8-column chunk of a 16-column half-group is 8 consecutive natural dims
+    for (int e = threadIdx.x; e < BM * (BN / 8); e += NT) {
+      const int rl = e / (BN / 8), c0 = (e % (BN / 8)) * 8;
+      const int m = m0 + rl, n = n0 + c0;
+      if (m >= M || n >= qcols + kcols || n >= N) continue;
+      const bool isq = n < qcols;
+      const int cc = isq ? n : n - qcols;
+      const int head = cc / d, o = cc % d;
+      const int dim = ((o & 31) >> 4) * hd + 16 * (o >> 5) + (o & 15);
+      const uint4 v = *reinterpret_cast<const uint4*>(so + rl * OLD + c0);
+      if (isq) {
+        st16(a.q_out + ((long)m * nq + head) * d + dim, v);
+      } else {
+        const int slot = a.slots[m];
+        if (slot >= 0) st16(a.kc + (((long)(slot >> 4) * nkv + head) * 16 + (slot & 15)) * d + dim, v);
+      }
+    }
+    return;
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rl = rl0 + 16 * i + e;
+        if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+          for (int jp = 0; jp < FN / 2; ++jp) {
+            const float g = bfr(acc[i][2 * jp][e] * rinv[i][e]), u = bfr(acc[i][2 * jp + 1][e] * rinv[i][e]);
+            so[rl * OLD + (wn * WN + 32 * jp) / 2 + cl] = f2bf(silu(g) * u);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) so[rl * OLD + wn * WN + 16 * j + cl] = f2bf(acc[i][j][e] * rinv[i][e]);
+        }
+      }
+    __syncthreads();
+  }
+
+  constexpr int CPR = OW / 8;  // 16-B chunks per staged row
+  const int ncol0 = (EPI == EPI_SWIGLU) ? n0 / 2 : n0;
+  const int nlim = (EPI == EPI_SWIGLU) ? N / 2 : N;
+  if constexpr (EPI == EPI_RESADD) {
+    // each thread owns chunks of one row per pass; CPR consecutive lanes share a row -> the row's
+    // sum of squares is reduced with shuffles and written once per (n-tile, row)
+    constexpr int RPP = NT / CPR;  // rows per pass
+    const int c0 = (threadIdx.x % CPR) * 8;
+    for (int r0 = 0; r0 < BM; r0 += RPP) {
+      const int rl = r0 + threadIdx.x / CPR, m = m0 + rl, n = ncol0 + c0;
+      float ss = 0.f;
+      if (m < M && (full_n || n < nlim)) {
+        u16* yp = a.Y + (long)m * a.ldy + n;
+        float h[8], r[8];
+        unpack8(*reinterpret_cast<const uint4*>(so + rl * OLD + c0), h);
+        unpack8(ld16(yp), r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          r[j] = bfr(h[j] + r[j]);
+          ss += r[j] * r[j];
+        }
+        st16(yp, pack8(r));
+      }
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) ss += __shfl_xor(ss, o, 64);
+      if (a.ssq_out != nullptr && threadIdx.x % CPR == 0 && m < M) a.ssq_out[(long)n_tile * a.ssq_out_ld + m] = ss;
+    }
+  } else {
+    for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+      const int rl = e / CPR, c0 = (e % CPR) * 8, m = m0 + rl, n = ncol0 + c0;
+      if (m < M && (full_n || n < nlim))
+        st16(a.Y + (long)m * a.ldy + n, *reinterpret_cast<const uint4*>(so + rl * OLD + c0));
+    }
   }
 }
 
-template <int BM, int BN, int EPI, int ST>
+template <int BM, int BN, int EPI, int ST, int KS, int NW>
 int launch_t(const GemmArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST>), dim3(mt * nt * a.splits), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW>), dim3(mt * nt * a.splits), dim3(64 * NW), 0, st, a);
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int EPI>
-int by_stages(int stages, const GemmArgs& a, hipStream_t st) {
-  return stages == 2 ? launch_t<BM, BN, EPI, 2>(a, st) : launch_t<BM, BN, EPI, 3>(a, st);
+template <int BM, int BN, int EPI, int ST, int KS, int NW>
+int launch_fit(const GemmArgs& a, hipStream_t st) {
+  if constexpr (ST * KS * (BM + BN) * ROWB > 150 * 1024) {
+    return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
+  } else {
+    return launch_t<BM, BN, EPI, ST, KS, NW>(a, st);
+  }
+}
+
+template <int BM, int BN, int EPI, int NW>
+int by_pipe(int stages, int ks, const GemmArgs& a, hipStream_t st) {
+  if (ks == 1) return stages == 2 ? launch_fit<BM, BN, EPI, 2, 1, NW>(a, st) : launch_fit<BM, BN, EPI, 3, 1, NW>(a, st);
+  return stages == 2 ? launch_fit<BM, BN, EPI, 2, 2, NW>(a, st) : launch_fit<BM, BN, EPI, 3, 2, NW>(a, st);
 }
 
 template <int EPI>
-int by_tile(int bm, int bn, int stages, const GemmArgs& a, hipStream_t st) {
-  if (bm == 64 && bn == 64) return by_stages<64, 64, EPI>(stages, a, st);
-  if (bm == 64 && bn == 128) return by_stages<64, 128, EPI>(stages, a, st);
-  if (bm == 128 && bn == 64) return by_stages<128, 64, EPI>(stages, a, st);
-  if (bm == 128 && bn == 128) return by_stages<128, 128, EPI>(stages, a, st);
+int by_tile(int bm, int bn, int stages, int ks, int nw, const GemmArgs& a, hipStream_t st) {
+  if (nw == 4) {
+    if (bm == 64 && bn == 64) return by_pipe<64, 64, EPI, 4>(stages, ks, a, st);
+    if (bm == 64 && bn == 128) return by_pipe<64, 128, EPI, 4>(stages, ks, a, st);
+    if (bm == 128 && bn == 64) return by_pipe<128, 64, EPI, 4>(stages, ks, a, st);
+    if (bm == 128 && bn == 128) return by_pipe<128, 128, EPI, 4>(stages, ks, a, st);
+  } else if (nw == 8) {
+    if (bm == 64 && bn == 128) return by_pipe<64, 128, EPI, 8>(stages, ks, a, st);
+    if (bm == 128 && bn == 128) return by_pipe<128, 128, EPI, 8>(stages, ks, a, st);
+    if (bm == 256 && bn == 128) return by_pipe<256, 128, EPI, 8>(stages, ks, a, st);
+    if (bm == 256 && bn == 256) return by_pipe<256, 256, EPI, 8>(stages, ks, a, st);
+  }
   return -20;
 }
 
@@ -412,19 +448,22 @@ extern "C" int dllm_tgemm_sizeof_args() { return (int)sizeof(GemmArgs); }
 // Host contract (checked again by csrc/bindings.cpp): K % 64 == 0, 16-B aligned rows (lda % 8),
 // splits >= 1 with kchunk % 64 == 0, part >= splits * tiles * bm * bn floats and counters >= tiles
 // (zeroed) when splits > 1; QKV/SWIGLU need N % 32 == 0 (and d % 32 == 0).
-extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int epi, hipStream_t stream) {
+extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, int nw, int epi,
+                          hipStream_t stream) {
   const GemmArgs& a = *reinterpret_cast<const GemmArgs*>(args);
   if (a.M <= 0 || a.N <= 0) return 0;
-  if (a.K % BK || a.kchunk % BK || a.kchunk <= 0 || a.splits < 1 || a.lda % 8) return -1;
+  if ((ks != 1 && ks != 2) || (nw != 4 && nw != 8)) return -8;
+  if (a.K % (BK * ks) || a.kchunk % (BK * ks) || a.kchunk <= 0 || a.splits < 1 || a.lda % 8) return -1;
   if (a.splits > 1 && (!a.part || !a.counters)) return -2;
   if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
+  if (a.N % 8 || (a.Y && a.ldy % 8)) return -7;  // 16-B output row vectors
   if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
   if (stages != 2 && stages != 3) return -5;
   switch (epi) {
-    case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, a, stream);
-    case EPI_RESADD: return by_tile<EPI_RESADD>(bm, bn, stages, a, stream);
-    case EPI_QKV: return by_tile<EPI_QKV>(bm, bn, stages, a, stream);
-    case EPI_SWIGLU: return by_tile<EPI_SWIGLU>(bm, bn, stages, a, stream);
+    case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, ks, nw, a, stream);
+    case EPI_RESADD: return by_tile<EPI_RESADD>(bm, bn, stages, ks, nw, a, stream);
+    case EPI_QKV: return by_tile<EPI_QKV>(bm, bn, stages, ks, nw, a, stream);
+    case EPI_SWIGLU: return by_tile<EPI_SWIGLU>(bm, bn, stages, ks, nw, a, stream);
     default: return -6;
   }
 }

@@ -135,6 +135,8 @@ class LLMEngine:
         self._bg: Optional[threading.Thread] = None   # background step-loop thread (start())
         self._bg_stop = False
         self._active: List[_Seq] = []
+        self._mirror = None                     # TP lockstep channel (enable_tp_mirror)
+        self._mirror_pending = None
         self._memo: "OrderedDict[str, List[int]]" = OrderedDict()
         self._memo_cap = 200_000
         self._memo_lock = threading.Lock()
@@ -340,9 +342,9 @@ class LLMEngine:
         (HTTP handlers, pool dispatchers) join ONE running batch.  The first caller to find the
         engine idle drives the step loop until every submitted sequence is done; later callers
         only enqueue and wait — their sequences are admitted at the driver's next step."""
-        if self.par.enabled:
-            # TP ranks must run IDENTICAL batches in lockstep: no cross-caller merging (the TP
-            # leader serialises requests and broadcasts each one to the members).
+        if self.par.enabled and self._mirror is None:
+            # TP ranks without a mirror channel: every rank calls generate() with the same
+            # requests in the same order (lockstep by construction, no cross-caller merging)
             with self._lock:
                 self._run(seqs)
             return
@@ -383,11 +385,73 @@ class LLMEngine:
         self._bt_dirty = True
 
     def _take_inbox(self, final: bool) -> List[_Seq]:
+        if self._mirror is not None and not self._mirror[2]:
+            return self._mirror_take()
         with self._inbox_lock:
             new, self._inbox = self._inbox, []
             if final and not new and self._bg is None:
                 self._driving = False   # atomically with the empty check: no submission is lost
+        if self._mirror is not None:    # TP leader: members replay exactly this admission
+            self._mirror_send({"seqs": [[s.id, s.prompt, s.params.to_dict()] for s in new]})
         return new
+
+    # ------------------------------------------------------------------ tensor-parallel lockstep
+    def enable_tp_mirror(self, group, leader: int) -> "LLMEngine":
+        """Continuous batching for a tensor-parallel pool.
+
+        Every TP rank must run identical scheduler decisions (same admissions, same batch, same
+        collectives).  The leader (the rank that receives requests) broadcasts, once per scheduler
+        iteration, the requests it takes from its inbox — sequence id, prompt token ids, sampling
+        parameters — over ``group`` (a CPU/gloo group of the TP ranks); members replay them in
+        ``follow()``.  Scheduling is deterministic given those inputs (block manager, stop rules,
+        seeded sampling), so the members' engines stay in step while concurrent callers keep
+        joining the leader's running batch (instead of one lockstep batch at a time)."""
+        import torch.distributed as dist
+        self._mirror = (group, leader, dist.get_rank() == leader)
+        return self
+
+    def _mirror_send(self, msg) -> None:
+        from ..parallel import p2p
+        p2p.bcast_obj(msg, self._mirror[1], self._mirror[0])
+
+    def _mirror_recv(self):
+        from ..parallel import p2p
+        return p2p.bcast_obj(None, self._mirror[1], self._mirror[0])
+
+    def _mirror_take(self) -> List[_Seq]:
+        msg, self._mirror_pending = self._mirror_pending, None
+        if msg is None:
+            msg = self._mirror_recv()
+        if "seqs" not in msg:
+            raise RuntimeError(f"TP mirror out of step: expected an admission, got {msg!r}")
+        now = time.perf_counter()
+        return [_Seq(int(i), list(p), SamplingParams.from_dict(sp), now) for i, p, sp in msg["seqs"]]
+
+    def mirror_control(self, msg) -> None:
+        """Leader: a control message (``{"sync": True}`` / ``{"stop": True}``) for the members,
+        sent between scheduler runs (holds the step lock)."""
+        if self._mirror is None or not self._mirror[2]:
+            return
+        with self._lock:
+            self._mirror_send(msg)
+
+    def follow(self, on_sync=None) -> None:
+        """Member: replay the leader's scheduler until it sends stop."""
+        if self._mirror is None or self._mirror[2]:
+            raise RuntimeError("follow() is for TP members with a mirror channel")
+        if self.on_gpu:
+            torch.cuda.set_device(self.device)
+        while True:
+            msg = self._mirror_recv()
+            if msg.get("stop"):
+                return
+            if msg.get("sync"):
+                if on_sync is not None:
+                    on_sync()
+                continue
+            self._mirror_pending = msg
+            with self._lock:
+                self._run([])
 
     # ------------------------------------------------------------------ background serving loop
     def start(self) -> "LLMEngine":
@@ -398,8 +462,8 @@ class LLMEngine:
         held back until every other caller is done.  With a background loop callers only enqueue
         and wait for THEIR sequences: a conversation can submit its next turn while the rest of
         the batch is still decoding (turn pipelining, bench.py --pipeline)."""
-        if self.par.enabled:
-            return self   # TP ranks run the leader's batches in lockstep (parallel.cluster)
+        if self.par.enabled and (self._mirror is None or not self._mirror[2]):
+            return self   # TP members follow the leader's scheduler (follow())
         with self._inbox_lock:
             if self._bg is not None:
                 return self
@@ -424,6 +488,8 @@ class LLMEngine:
         with self._inbox_lock:
             self._bg = None
             self._driving = False
+        if self._mirror is not None and self._mirror[2]:
+            self.mirror_control({"stop": True})
 
     def _bg_loop(self) -> None:
         if self.on_gpu:

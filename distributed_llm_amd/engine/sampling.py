@@ -6,7 +6,7 @@ i.e. until EOS; src/devices/nano_api.py:20-21); the large tier uses Ollama's def
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import asdict, dataclass
 
 
 @dataclass
@@ -27,6 +27,13 @@ class SamplingParams:
     @property
     def k(self) -> int:
         return self.top_k if self.top_k > 0 else self.CANDIDATES
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "SamplingParams":
+        return cls(**{k: v for k, v in d.items() if k in cls.__dataclass_fields__})
 
 
 OLLAMA_DEFAULTS = SamplingParams(max_new_tokens=256, temperature=0.8, top_k=40, top_p=0.9)

@@ -45,7 +45,8 @@ _MM_NTS = (2, 4)
 _MM_SPLITS = (1, 2, 4, 8)
 _GEMV_MS = (1, 2, 4, 8)   # csrc/kernels/gemv.hip instantiations (decode buckets below 16)
 _GEMV_RS = (1, 2, 4)
-_TG_TILES = ((64, 64), (64, 128), (128, 64), (128, 128))
+_TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8), (128, 128, 8), (256, 128, 8),
+             (256, 256, 8))
 _TG_SPLITS = (1, 2, 3, 4, 6, 8)
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
 WS_COUNTERS = 1 << 16
@@ -117,14 +118,15 @@ def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tu
     return (S * tiles * nc * mp if S > 1 else 0), tiles
 
 
-def _tg_splits(K: int, splits: int) -> int:
-    kchunk = ((K + splits - 1) // splits + 63) // 64 * 64
+def _tg_splits(K: int, splits: int, ks: int = 1) -> int:
+    q = 64 * ks
+    kchunk = ((K + splits - 1) // splits + q - 1) // q * q
     return (K + kchunk - 1) // kchunk
 
 
-def _need_tg(M: int, N: int, K: int, bm: int, bn: int, splits: int) -> Tuple[int, int]:
+def _need_tg(M: int, N: int, K: int, bm: int, bn: int, splits: int, ks: int = 1) -> Tuple[int, int]:
     tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
-    S = _tg_splits(K, splits)
+    S = _tg_splits(K, splits, ks)
     return (S * tiles * bm * bn if S > 1 else 0), tiles
 
 
@@ -139,25 +141,26 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
-def tg_plan(M: int, N: int, K: int) -> Tuple[int, int, int, int]:
-    """(bm, bn, stages, splits) of the fused GEMM for this shape: tuned, else a heuristic sized so
-    the grid covers the 256 CUs (bigger tiles first, split-K only for short grids)."""
+def tg_plan(M: int, N: int, K: int) -> Tuple[int, int, int, int, int, int]:
+    """(bm, bn, stages, splits, ks, waves) of the fused GEMM for this shape: tuned, else a
+    heuristic sized so the grid covers the 256 CUs (bigger tiles first, split-K only for short
+    grids)."""
     p = _P.tg_plans.get((M, N, K))
     if p is not None:
-        return p
+        return tuple(p) + (1, 4)[len(p) - 4:] if len(p) < 6 else tuple(p)
     mt128, nt128 = -(-M // 128), -(-N // 128)
     if mt128 * nt128 >= 224:
-        return (128, 128, 3, 1)
+        return (128, 128, 3, 1, 1, 4)
     mt64, nt64 = -(-M // 64), -(-N // 64)
     if mt64 * nt128 >= 200:
-        return (64, 128, 3, 1)
+        return (64, 128, 3, 1, 1, 4)
     tiles = mt64 * nt64
     splits = 1
     while tiles * splits * 2 <= 512 and K // (splits * 2) >= 256 and splits < 8:
         splits *= 2
     if _need_tg(M, N, K, 64, 64, splits)[0] > WS_FLOATS:
         splits = 1
-    return (64, 64, 3, splits)
+    return (64, 64, 3, splits, 1, 4)
 
 
 def tg_slots(M: int, N: int, K: int) -> int:
@@ -198,13 +201,16 @@ def _run_plan(plan, x, w, swiglu, out):
 
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
            pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0):
-    bm, bn, st, sp = plan
+    bm, bn, st, sp = plan[:4]
+    ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    if K % (64 * ks):
+        ks = 1
     part = cnt = None
-    if _tg_splits(K, sp) > 1:
-        floats, tiles = _need_tg(M, N, K, bm, bn, sp)
+    if _tg_splits(K, sp, ks) > 1:
+        floats, tiles = _need_tg(M, N, K, bm, bn, sp, ks)
         part, cnt = _P.workspace(x.device, floats, tiles)
-    ext.tgemm(x, w, y, epi, bm, bn, st, sp, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
+    ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
               pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d))
 
 
@@ -376,19 +382,24 @@ def _tg_cands(M: int, N: int, K: int):
     if K % 64:
         return []
     out = []
-    for bm, bn in _TG_TILES:
-        if bm == 128 and M <= 64:
+    for bm, bn, nw in _TG_TILES:
+        if (bm == 128 and M <= 64) or (bm == 256 and M <= 128):
             continue
         tiles = -(-M // bm) * -(-N // bn)
-        for sp in _TG_SPLITS:
-            if sp > 1 and (K // sp < 256 or tiles * sp > 2048):
+        for ks in (1, 2):
+            if K % (64 * ks):
                 continue
-            if _tg_splits(K, sp) != sp:
-                continue
-            if _need_tg(M, N, K, bm, bn, sp)[0] > WS_FLOATS:
-                continue
-            for st in (2, 3):
-                out.append((bm, bn, st, sp))
+            for sp in _TG_SPLITS:
+                if sp > 1 and (K // sp < 256 * ks or tiles * sp > 2048):
+                    continue
+                if _tg_splits(K, sp, ks) != sp:
+                    continue
+                if _need_tg(M, N, K, bm, bn, sp, ks)[0] > WS_FLOATS:
+                    continue
+                for st in (2, 3):
+                    if st * ks * (bm + bn) * 128 > 150 * 1024:
+                        continue   # the ring would not fit the LDS
+                    out.append((bm, bn, st, sp, ks, nw))
     return out
 
 
@@ -446,6 +457,8 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
                       for k in ("gemv", "skinny", "lds", "mm", "tg")}
                 extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
+                top = sorted(tgc, key=res.get)[:4]
+                extra += " | tg top: " + " ".join(f"{c[1:]}:{res[c]:.1f}" for c in top)
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
                       f"({N * K * 2 / res[best] / 1e3:.0f} GB/s, {2 * M * N * K / res[best] / 1e6:.0f} TF/s; "
                       f"blas {res[('blas',)]:.1f}us; {extra})", flush=True)

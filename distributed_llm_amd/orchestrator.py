@@ -107,6 +107,8 @@ class Router:
         self.cache_last_k = int(self.config.get("cache_last_k", 6))
         self.enable_failover = bool(self.config.get("enable_failover", True))
         self.penalise_failed_primary = bool(self.config.get("penalise_failed_primary", False))
+        self.tokens_from_engine = bool(self.config.get("tokens_from_engine", False))
+        self.pool_health: Dict[str, Dict[str, Any]] = {}
         self._responses: Dict[str, Dict[str, Any]] = {}
         self._lock = threading.RLock()
         if pools is None:
@@ -171,8 +173,11 @@ class Router:
                 primary_failed: Optional[str] = None):
         text = extract_text(raw) or "No response available"
         ntok = raw.get("num_tokens") if isinstance(raw, dict) else None
-        toks = int(ntok) if ntok is not None else self.token_counter.count_tokens(
-            {"role": "assistant", "content": text})
+        # reference: response tokens = TokenCounter over the returned text (src/router.py:286);
+        # ``tokens_from_engine`` reports the engine's generated-token count instead (bench.py:
+        # throughput in generated tokens), and the payload carries both
+        counted = self.token_counter.count_tokens({"role": "assistant", "content": text})
+        toks = int(ntok) if (ntok is not None and self.tokens_from_engine) else counted
         ok = not is_error(raw)
         try:
             self.query_router.update_perf(which, lat_ms, toks, ok=ok)
@@ -192,14 +197,36 @@ class Router:
                    "routing_confidence": round(dec["confidence"], 4),
                    "routing_reasoning": dec["reasoning"], "ok": ok}
         if isinstance(raw, dict) and "timing" in raw:
-            payload["timing"] = raw["timing"]
+            payload["timing"] = dict(raw["timing"], generated_tokens=ntok, counted_tokens=counted)
         return payload, toks, which
 
-    def _run(self, device: str, history) -> Tuple[Any, str, float]:
+    def on_pool_health(self, name: str, ok: bool, rtt_us: Optional[float]) -> None:
+        """Sink for periodic pool health probes (pools.remote.RemotePool.start_probes): the last
+        state per pool is kept for /metrics and a FAILED probe is fed to the perf router as a
+        failed request (its failure-rate penalty, query_router_engine.py:442-445), so a pool that
+        stops answering loses traffic before a user request has to time out on it."""
+        with self._lock:
+            st = self.pool_health.setdefault(name, {"ok": True, "probes": 0, "failures": 0, "rtt_us": None})
+            st["probes"] += 1
+            st["ok"] = bool(ok)
+            if ok:
+                st["rtt_us"] = rtt_us
+            else:
+                st["failures"] += 1
+        if not ok:
+            try:
+                self.query_router.update_perf(name, 5000.0, 0, ok=False)
+            except Exception:  # noqa: BLE001
+                pass
+
+    def _run(self, device: str, history, failover: bool = False) -> Tuple[Any, str, float]:
         t0 = time.perf_counter()
         try:
-            with tracer.span("pool.process", "pool", device=device):
-                raw = self.pools[device].process(history)
+            with tracer.span("pool.process", "pool", device=device, failover=failover):
+                pool = self.pools[device]
+                # a failover to a remote pool hands the prompt over as token ids (pools.remote)
+                fn = getattr(pool, "process_failover", None) if failover else None
+                raw = fn(history) if fn is not None else pool.process(history)
         except Exception as exc:  # a pool that raises is an error response, not a crash
             raw = {"error": f"pool {device} failed: {exc}"}
         return raw, device, (time.perf_counter() - t0) * 1000.0
@@ -214,7 +241,7 @@ class Router:
         raw, which, lat = self._run(dec["device"], conversation_history)
         failed = None
         if self.enable_failover and is_error(raw):
-            raw2, which2, lat2 = self._run(other_tier(which), conversation_history)
+            raw2, which2, lat2 = self._run(other_tier(which), conversation_history, failover=True)
             if not is_error(raw2):
                 failed = which
                 raw, which, lat = raw2, which2, lat2
@@ -294,7 +321,7 @@ class Router:
         raw, which, lat = self._run(dec["device"], conversation_history)
         failed = None
         if self.enable_failover and is_error(raw):
-            raw2, which2, lat2 = self._run(other_tier(which), conversation_history)
+            raw2, which2, lat2 = self._run(other_tier(which), conversation_history, failover=True)
             if not is_error(raw2):
                 failed = which
                 raw, which, lat = raw2, which2, lat2

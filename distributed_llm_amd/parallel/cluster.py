@@ -64,23 +64,33 @@ def default_topology(world: int, large_tp: Optional[int] = None) -> Topology:
 
 class Cluster:
     def __init__(self, topo: Topology, specs: Dict[str, TierSpec], device: Optional[str] = None,
-                 shared_single: bool = True):
+                 shared_single: bool = True, request_timeout_s: float = 180.0):
         self.topo = topo
         self.specs = specs
         self.rank = dist.get_rank() if dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.device = device or ("cuda" if torch.cuda.is_available() else "cpu")
+        self.request_timeout_s = request_timeout_s
         self.sync_times: List[float] = []
         # --- groups (collective: every rank creates every group in the same order)
+        #   tp_groups:     RCCL (default backend) per TP replica: model all-reduces
+        #   mirror_groups: gloo per TP replica: the leader's scheduler broadcast (engine mirror)
+        #   pair_groups:   router <-> remote leader, default backend: data plane (token ids, pings)
+        #   ctrl_groups:   router <-> remote leader, gloo: tagged control messages (pools.remote)
         self.tp_groups: Dict[tuple, Any] = {}
+        self.mirror_groups: Dict[tuple, Any] = {}
         self.pair_groups: Dict[int, Any] = {}
+        self.ctrl_groups: Dict[int, Any] = {}
+        init = dist.is_initialized()
         for tier, ranks in topo.all_groups():
             key = tuple(ranks)
-            if len(ranks) > 1 and key not in self.tp_groups and dist.is_initialized():
+            if len(ranks) > 1 and key not in self.tp_groups and init:
                 self.tp_groups[key] = dist.new_group(list(ranks))
+                self.mirror_groups[key] = dist.new_group(list(ranks), backend="gloo")
         leaders = sorted({ranks[0] for _, ranks in topo.all_groups() if ranks[0] != 0})
         for ld in leaders:
-            self.pair_groups[ld] = dist.new_group([0, ld]) if dist.is_initialized() else None
+            self.pair_groups[ld] = dist.new_group([0, ld]) if init else None
+            self.ctrl_groups[ld] = dist.new_group([0, ld], backend="gloo") if init else None
         # --- this rank's replica(s): a rank serves exactly one replica (both tiers only if shared)
         self.my: List[tuple] = [(tier, ranks) for tier, ranks in topo.all_groups() if self.rank in ranks]
         self.engines: Dict[tuple, Any] = {}
@@ -94,19 +104,27 @@ class Cluster:
                                   self.rank, self.world)
             if str(self.device).startswith("cuda"):
                 par.enable_custom_all_reduce(self.device)  # collective over this TP group
-            self.engines[key] = LLMEngine(spec.model, device=self.device, par=par, kv_cache_gb=spec.kv_cache_gb,
-                                          max_num_seqs=spec.max_num_seqs)
+            eng = LLMEngine(spec.model, device=self.device, par=par, kv_cache_gb=spec.kv_cache_gb,
+                            max_num_seqs=spec.max_num_seqs)
+            if len(ranks) > 1:
+                eng.enable_tp_mirror(self.mirror_groups[tuple(ranks)], ranks[0])
+            self.engines[key] = eng
 
     # ------------------------------------------------------------------ router side
     def _engine_for(self, tier: str, ranks: List[int]):
         return self.engines[(tuple(ranks), self.specs[tier].model)]
 
-    def router_pools(self):
+    def router_pools(self, on_health=None, probe_interval_s: Optional[float] = None):
+        """{tier: PoolClient} for the router on rank 0.  ``on_health(name, ok, rtt_us)`` receives
+        every remote health probe (``probe_interval_s``: start periodic probes)."""
+        from ..engine.tokenizer import get_tokenizer
+        from ..models.configs import get_model_config
         from ..pools.base import EnginePool
         from ..pools.remote import RemotePool, ReplicatedPool
         assert self.rank == 0, "router pools live on rank 0"
         out = {}
         self.remotes: List[RemotePool] = []
+        self.local_engines = []
         for tier in (SMALL, LARGE):
             spec = self.specs[tier]
             reps = []
@@ -114,13 +132,18 @@ class Cluster:
                 kw = dict(max_new_tokens=spec.max_new_tokens, temperature=spec.temperature, top_k=spec.top_k,
                           top_p=spec.top_p)
                 if 0 in ranks:
-                    if len(ranks) > 1:
-                        reps.append(_LeaderPool(tier, self._engine_for(tier, ranks), self.tp_groups[tuple(ranks)],
-                                                **kw))
-                    else:
-                        reps.append(EnginePool(tier, self._engine_for(tier, ranks), **kw))
+                    eng = self._engine_for(tier, ranks)
+                    if len(ranks) > 1:   # rank 0 leads a TP group: members follow its scheduler
+                        eng.start()
+                        self.local_engines.append(eng)
+                    reps.append(EnginePool(tier, eng, **kw))
                 else:
-                    rp = RemotePool(tier, ranks[0], self.pair_groups[ranks[0]], **kw)
+                    cfg = get_model_config(spec.model)
+                    rp = RemotePool(tier, ranks[0], self.ctrl_groups[ranks[0]], self.pair_groups[ranks[0]],
+                                    timeout_s=self.request_timeout_s, on_health=on_health,
+                                    tokenizer=get_tokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id), **kw)
+                    if probe_interval_s:
+                        rp.start_probes(probe_interval_s)
                     reps.append(rp)
                     self.remotes.append(rp)
             out[tier] = reps[0] if len(reps) == 1 else ReplicatedPool(tier, reps)
@@ -131,12 +154,10 @@ class Cluster:
         if self.world == 1:
             return
         for rp in getattr(self, "remotes", []):
-            rp.sync()
-        for tier, ranks in self.my:
-            if len(ranks) > 1 and ranks[0] == 0:
-                from . import p2p
-                p2p.bcast_obj({"op": "sync"}, 0, self.tp_groups[tuple(ranks)])
-                break
+            if rp.alive:
+                rp.sync()
+        for eng in getattr(self, "local_engines", []):
+            eng.mirror_control({"sync": True})
         self._barrier()
 
     def _barrier(self) -> None:
@@ -150,48 +171,19 @@ class Cluster:
             return
         for rp in getattr(self, "remotes", []):
             rp.stop()
-        for tier, ranks in self.my:
-            if len(ranks) > 1 and ranks[0] == 0:
-                from . import p2p
-                p2p.bcast_obj({"op": "stop"}, 0, self.tp_groups[tuple(ranks)])
-                break
+        for eng in getattr(self, "local_engines", []):
+            eng.stop()   # mirror leader: sends stop to its members
 
     # ------------------------------------------------------------------ pool side
     def serve(self) -> None:
-        from ..pools.remote import serve_pool
+        """Pool ranks: a remote leader serves the router's requests; TP members follow their
+        leader's scheduler.  Returns when the router stops the pool."""
+        from ..pools.remote import PoolLeader
         assert self.rank != 0
         tier, ranks = self.my[0]
         eng = self._engine_for(tier, ranks)
-        leader = ranks[0]
-        serve_pool(eng, 0, leader, self.pair_groups.get(leader), self.tp_groups.get(tuple(ranks)),
-                   on_sync=self._barrier)
-
-
-class _LeaderPool:
-    """Rank 0 leads a TP group: fan the request out to the members, then run it locally."""
-
-    def __new__(cls, tier, engine, tp_group, **kw):
-        from ..pools.base import Coalescer, EnginePool
-
-        class LeaderPool(EnginePool):
-            """Concurrent callers are coalesced into ONE broadcast + generate, so the members see
-            requests in exactly the leader's order and batch as the leader does."""
-
-            def __init__(self, *a, **k):
-                super().__init__(*a, **k)
-                self._coalesce = Coalescer(self._run_items)
-
-            def process_batch(self, histories, overrides=None):
-                params = self._params(overrides)
-                return self._coalesce.submit([(self.prompt_for(h), params) for h in histories])
-
-            def _run_items(self, items):
-                from . import p2p
-                prompts = [q for q, _ in items]
-                plist = [p for _, p in items]
-                p2p.bcast_obj({"op": "generate", "id": 0, "prompts": prompts,
-                               "params_list": [{"max_new_tokens": p.max_new_tokens, "temperature": p.temperature,
-                                                "top_k": p.top_k, "top_p": p.top_p} for p in plist]}, 0, tp_group)
-                return self.to_payloads(self.engine.generate(prompts, plist))
-
-        return LeaderPool(tier, engine, **kw)
+        if self.rank == ranks[0]:
+            PoolLeader(eng, self.ctrl_groups[self.rank], self.pair_groups[self.rank], 0,
+                       on_sync=self._barrier).serve()
+        else:
+            eng.follow(on_sync=self._barrier)

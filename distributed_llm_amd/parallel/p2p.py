@@ -1,5 +1,9 @@
 """Point-to-point messaging between pools (RCCL send/recv over xGMI on GPU ranks; gloo on CPU).
 
+Control messages between the router and a pool leader travel on a CPU (gloo) group with tags
+(pools.remote: request tag 1, reply tag 2; many requests in flight); the RCCL pair group is the
+data plane (token ids, pings).
+
 The reference moves every request as HTTP/JSON through an SSH tunnel to a remote board
 (src/models/nano.py:23-35) and re-sends the full history on failover (src/router.py:277-282).
 On one MI355X node, pools are process groups and the router talks to a pool leader directly:
@@ -27,33 +31,33 @@ def _dev(group) -> torch.device:
     return torch.device("cpu")
 
 
-def send_bytes(data: bytes, dst: int, group=None) -> None:
+def send_bytes(data: bytes, dst: int, group=None, tag: int = 0) -> None:
     dev = _dev(group)
     hdr = torch.tensor([len(data)], dtype=torch.int64, device=dev)
-    dist.send(hdr, dst, group=group)
+    dist.send(hdr, dst, group=group, tag=tag)
     if data:
         buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
-        dist.send(buf, dst, group=group)
+        dist.send(buf, dst, group=group, tag=tag)
 
 
-def recv_bytes(src: int, group=None) -> bytes:
+def recv_bytes(src: int, group=None, tag: int = 0) -> bytes:
     dev = _dev(group)
     hdr = torch.empty(1, dtype=torch.int64, device=dev)
-    dist.recv(hdr, src, group=group)
+    dist.recv(hdr, src, group=group, tag=tag)
     n = int(hdr.item())
     if n == 0:
         return b""
     buf = torch.empty(n, dtype=torch.uint8, device=dev)
-    dist.recv(buf, src, group=group)
+    dist.recv(buf, src, group=group, tag=tag)
     return bytes(buf.cpu().numpy().tobytes())
 
 
-def send_obj(obj: Any, dst: int, group=None) -> None:
-    send_bytes(json.dumps(obj).encode("utf-8"), dst, group)
+def send_obj(obj: Any, dst: int, group=None, tag: int = 0) -> None:
+    send_bytes(json.dumps(obj).encode("utf-8"), dst, group, tag)
 
 
-def recv_obj(src: int, group=None) -> Any:
-    return json.loads(recv_bytes(src, group).decode("utf-8"))
+def recv_obj(src: int, group=None, tag: int = 0) -> Any:
+    return json.loads(recv_bytes(src, group, tag).decode("utf-8"))
 
 
 def bcast_obj(obj: Any, src: int, group=None) -> Any:

@@ -1,13 +1,30 @@
 """Pools that live on other ranks of the node, and data-parallel replica sets.
 
-* ``RemotePool``  — the router-side client of a pool whose leader is another rank: request batches
-  and results travel as point-to-point messages (parallel.p2p: RCCL send/recv over xGMI on a side
-  HIP stream), replacing the reference's HTTP-over-SSH hop (src/models/nano.py:23-35).
-* ``serve_pool``  — the pool-side loop: the leader receives work from the router and fans it out
-  to its tensor-parallel group (every TP rank runs the same ``generate`` in lockstep; RCCL
-  all-reduces inside the model), then returns the results.
-* ``ReplicatedPool`` — several replicas of one tier (data parallel); a batch is split across
-  replicas by outstanding load (least-loaded dispatch), replicas run concurrently.
+The reference reaches a device with one blocking HTTP request per turn through an SSH tunnel,
+bounded by ``timeout=(5, 180)`` and failing over on any error (src/models/nano.py:23-38,
+src/router.py:277-282); liveness is a TCP connect and readiness a ``/health`` poll
+(src/models/server_manager.py:52-61,123-131).  Here a pool is a process group on this node:
+
+* **control plane** — JSON messages on a 2-rank CPU (gloo) group per remote pool leader.  Every
+  request carries an id; any number are in flight at once; replies come back out of order and a
+  receiver thread hands each to its waiting caller.  A caller waits at most ``timeout_s`` and
+  then gets an error payload (the orchestrator fails over); a pool process that dies closes its
+  sockets, which fails every in-flight request at once.  The router never blocks on a dead or
+  hung pool.
+* **data plane** — the router<->leader pair group (RCCL over xGMI on GPU ranks, gloo on CPU):
+  prompt token ids for a failover hand-off (``process_failover``: the router tokenises with the
+  target pool's tokenizer and ships int32 ids, so the surviving pool prefills ids directly) and
+  the periodic 4 KiB data-plane ping.
+* **health** — a probe thread pings every ``probe_interval_s`` on the control plane (answered by
+  the leader's receiver thread immediately, never queued behind generation) and every
+  ``data_probe_every``-th time on the data plane; two consecutive failures mark the pool dead;
+  every probe result is reported to ``on_health`` (the orchestrator feeds the perf router).
+* **pool side** (``PoolLeader``) — the receiver thread answers pings inline and hands each
+  generate request to a worker thread that calls ``engine.generate``; the engine runs its
+  background step loop, so concurrent requests from the router JOIN ONE continuous batch.
+  Tensor-parallel pools keep their members in lockstep with the engine's mirror channel
+  (``LLMEngine.enable_tp_mirror``), not per request.
+* ``ReplicatedPool`` — several replicas of one tier (data parallel), least-loaded dispatch.
 """
 from __future__ import annotations
 
@@ -15,10 +32,12 @@ import itertools
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 from ..parallel import p2p
-from .base import Coalescer, EnginePool, NullServerManager, PoolClient, format_prompt
+from .base import EnginePool, NullServerManager, PoolClient, format_prompt
+
+TAG_REQ, TAG_REP = 1, 2
 
 
 class RemoteServerManager(NullServerManager):
@@ -30,124 +49,296 @@ class RemoteServerManager(NullServerManager):
         return self.pool.alive
 
 
+class _Pending:
+    __slots__ = ("event", "reply")
+
+    def __init__(self):
+        self.event = threading.Event()
+        self.reply: Optional[Dict[str, Any]] = None
+
+
 class RemotePool(PoolClient):
-    def __init__(self, name: str, leader: int, group, max_new_tokens: int = 256, temperature: float = 0.0,
-                 top_k: int = 0, top_p: float = 1.0, generation_prompt: str = EnginePool.GENERATION_PROMPT):
+    def __init__(self, name: str, leader: int, ctrl_group, data_group=None, max_new_tokens: int = 256,
+                 temperature: float = 0.0, top_k: int = 0, top_p: float = 1.0,
+                 generation_prompt: str = EnginePool.GENERATION_PROMPT, timeout_s: float = 180.0,
+                 tokenizer=None, on_health: Optional[Callable[[str, bool, Optional[float]], None]] = None):
         super().__init__()
         self.name = name
         self.leader = leader
-        self.group = group
+        self.ctrl = ctrl_group
+        self.data = data_group
         self.params = {"max_new_tokens": max_new_tokens, "temperature": temperature, "top_k": top_k, "top_p": top_p}
         self.generation_prompt = generation_prompt
+        self.timeout_s = timeout_s
+        self.tokenizer = tokenizer          # the pool's tokenizer (token-id hand-off), optional
+        self.on_health = on_health
         self.alive = True
         self.server_manager = RemoteServerManager(self)
-        self._lock = threading.Lock()  # one outstanding exchange per pair group
-        self._ids = itertools.count()
+        self._send_lock = threading.Lock()
+        self._data_lock = threading.Lock()
+        self._pending: Dict[int, _Pending] = {}
+        self._plock = threading.Lock()
+        self._ids = itertools.count(1)
         self.last_rtt_us: Optional[float] = None
-        self._coalesce = Coalescer(self._generate_items)  # concurrent callers -> one exchange
+        self.last_data_rtt_us: Optional[float] = None
+        self.last_stats: Dict[str, Any] = {}
+        self.timeouts = 0
+        self.probe_failures = 0
+        self._probe_stop = threading.Event()
+        self._probe: Optional[threading.Thread] = None
+        self._rx = threading.Thread(target=self._rx_loop, name=f"dllm-rx-{name}", daemon=True)
+        self._rx.start()
 
+    # ------------------------------------------------------------------ transport
     def prompt_for(self, history: Any) -> str:
         return format_prompt(history) + self.generation_prompt
 
-    def _exchange(self, msg: Dict[str, Any]) -> Dict[str, Any]:
-        import torch
-        st = p2p.side_stream()
-        with self._lock:
-            if st is not None:
-                with torch.cuda.stream(st):
-                    p2p.send_obj(msg, self.leader, self.group)
-                    return p2p.recv_obj(self.leader, self.group)
-            p2p.send_obj(msg, self.leader, self.group)
-            return p2p.recv_obj(self.leader, self.group)
+    def _rx_loop(self) -> None:
+        while True:
+            try:
+                msg = p2p.recv_obj(self.leader, self.ctrl, tag=TAG_REP)
+            except Exception as e:  # peer died / transport closed: fail everything in flight
+                self._fail_all(f"pool {self.name} transport failed: {e}")
+                return
+            if msg.get("op") == "bye":
+                self._fail_all(f"pool {self.name} stopped")
+                return
+            with self._plock:
+                ent = self._pending.pop(msg.get("id"), None)
+            if ent is not None:
+                ent.reply = msg
+                ent.event.set()
 
+    def _fail_all(self, why: str) -> None:
+        self.alive = False
+        with self._plock:
+            pend, self._pending = self._pending, {}
+        for ent in pend.values():
+            ent.reply = {"error": why}
+            ent.event.set()
+
+    def _send(self, msg: Dict[str, Any]) -> None:
+        with self._send_lock:
+            p2p.send_obj(msg, self.leader, self.ctrl, tag=TAG_REQ)
+
+    def _call(self, msg: Dict[str, Any], timeout: Optional[float] = None, data_fn=None) -> Dict[str, Any]:
+        """Send one tagged request and wait for its reply at most ``timeout`` seconds."""
+        if not self.alive:
+            return {"error": f"pool {self.name} unavailable"}
+        rid = next(self._ids)
+        msg["id"] = rid
+        ent = _Pending()
+        with self._plock:
+            self._pending[rid] = ent
+        try:
+            if data_fn is None:
+                self._send(msg)
+            else:  # control message + its data-plane payload, in order w.r.t. other data ops
+                with self._data_lock:
+                    self._send(msg)
+                    data_fn()
+        except Exception as e:
+            with self._plock:
+                self._pending.pop(rid, None)
+            self._fail_all(f"pool {self.name} send failed: {e}")
+            return {"error": f"pool {self.name} send failed: {e}"}
+        if not ent.event.wait(self.timeout_s if timeout is None else timeout):
+            with self._plock:
+                self._pending.pop(rid, None)
+            self.timeouts += 1
+            return {"error": f"Request timed out on {self.name} after {timeout or self.timeout_s:.1f}s"}
+        return ent.reply or {"error": "empty reply"}
+
+    # ------------------------------------------------------------------ requests
     def process(self, history: Any) -> Dict[str, Any]:
         return self.process_batch([history])[0]
 
     def process_batch(self, histories: Sequence[Any], overrides: Optional[Dict[str, Any]] = None):
-        if not self.alive:
-            return [{"error": f"pool {self.name} unavailable"}] * len(histories)
         params = dict(self.params, **(overrides or {}))
-        return self._coalesce.submit([(self.prompt_for(h), params) for h in histories])
+        rep = self._call({"op": "generate", "prompts": [self.prompt_for(h) for h in histories], "params": params})
+        return self._results(rep, len(histories))
 
-    def _generate_items(self, items: List[tuple]) -> List[Dict[str, Any]]:
-        plist = [p for _, p in items]
-        msg = {"op": "generate", "id": next(self._ids), "prompts": [q for q, _ in items]}
-        if all(p == plist[0] for p in plist):
-            msg["params"] = plist[0]
-        else:
-            msg["params_list"] = plist
-        try:
-            rep = self._exchange(msg)
-        except Exception as e:  # transport failure -> error payloads (router fails over)
-            self.alive = False
-            return [{"error": f"pool {self.name} transport failed: {e}"}] * len(items)
+    def process_ids(self, prompt_ids: Sequence[Sequence[int]], overrides: Optional[Dict[str, Any]] = None):
+        """Generate from prompt token ids shipped over the data plane (int32 tensors)."""
+        params = dict(self.params, **(overrides or {}))
+        ids = [list(map(int, p)) for p in prompt_ids]
+
+        def ship():
+            for p in ids:
+                p2p.send_tokens(p, self.leader, self.data)
+        rep = self._call({"op": "generate_ids", "n": len(ids), "params": params}, data_fn=ship)
+        return self._results(rep, len(ids))
+
+    def process_failover(self, history: Any) -> Dict[str, Any]:
+        """Failover entry (orchestrator): hand the prompt over as token ids when this router has
+        the pool's tokenizer and a data plane, else as text."""
+        if self.tokenizer is not None and self.data is not None:
+            return self.process_ids([self.tokenizer.encode(self.prompt_for(history))])[0]
+        return self.process(history)
+
+    @staticmethod
+    def _results(rep: Dict[str, Any], n: int) -> List[Dict[str, Any]]:
         res = rep.get("results")
-        if not res or len(res) != len(items):
-            return [{"error": rep.get("error", "empty reply")}] * len(items)
+        if not res or len(res) != n:
+            return [{"error": rep.get("error", "empty reply")}] * n
         return res
 
-    def probe(self) -> Dict[str, Any]:
-        """Health probe: round trip + the pool's engine statistics."""
+    # ------------------------------------------------------------------ health
+    def probe(self, timeout: float = 5.0) -> Dict[str, Any]:
+        """Control-plane round trip + the pool's engine statistics (never queued behind work)."""
         t0 = time.perf_counter()
-        try:
-            rep = self._exchange({"op": "ping"})
-        except Exception as e:
-            self.alive = False
-            return {"ok": False, "error": str(e)}
+        rep = self._call({"op": "ping"}, timeout=timeout)
+        if "error" in rep:
+            return {"ok": False, "error": rep["error"]}
         self.last_rtt_us = (time.perf_counter() - t0) * 1e6
-        return {"ok": True, "rtt_us": self.last_rtt_us, **rep.get("stats", {})}
+        self.last_stats = rep.get("stats", {})
+        return {"ok": True, "rtt_us": self.last_rtt_us, **self.last_stats}
+
+    def probe_data(self, timeout: float = 5.0) -> Dict[str, Any]:
+        """4 KiB ping-pong on the data plane (RCCL over xGMI between GPU ranks).  Runs in a helper
+        thread so a peer that never answers cannot hang the caller past ``timeout``."""
+        if self.data is None or not self.alive:
+            return {"ok": False, "error": "no data plane"}
+        out: Dict[str, Any] = {}
+
+        def run():
+            try:
+                with self._data_lock:
+                    self._send({"op": "ping_data", "id": 0})
+                    out["rtt_us"] = p2p.ping(self.leader, self.data, initiator=True)
+            except Exception as e:  # noqa: BLE001
+                out["error"] = str(e)
+        t = threading.Thread(target=run, daemon=True)
+        t.start()
+        t.join(timeout)
+        if t.is_alive() or "error" in out:
+            return {"ok": False, "error": out.get("error", f"data-plane ping timed out after {timeout}s")}
+        self.last_data_rtt_us = out["rtt_us"]
+        return {"ok": True, "rtt_us": out["rtt_us"]}
+
+    def start_probes(self, interval_s: float = 2.0, timeout_s: float = 5.0, data_probe_every: int = 5) -> None:
+        """Periodic health probes on their own thread; two consecutive failures mark the pool dead."""
+        if self._probe is not None:
+            return
+
+        def loop():
+            k = 0
+            while not self._probe_stop.wait(interval_s):
+                if not self.alive:
+                    self._report(False, None)
+                    continue
+                k += 1
+                r = self.probe(timeout_s)
+                if r["ok"] and data_probe_every and k % data_probe_every == 0 and self.data is not None:
+                    d = self.probe_data(timeout_s)
+                    if not d["ok"]:
+                        r = d
+                if r["ok"]:
+                    self.probe_failures = 0
+                    self._report(True, r.get("rtt_us"))
+                else:
+                    self.probe_failures += 1
+                    if self.probe_failures >= 2:
+                        self._fail_all(f"pool {self.name} failed {self.probe_failures} health probes: {r['error']}")
+                    self._report(False, None)
+        self._probe = threading.Thread(target=loop, name=f"dllm-probe-{self.name}", daemon=True)
+        self._probe.start()
+
+    def _report(self, ok: bool, rtt_us: Optional[float]) -> None:
+        if self.on_health is not None:
+            try:
+                self.on_health(self.name, ok, rtt_us)
+            except Exception:  # noqa: BLE001 - a health sink must never kill the probe thread
+                pass
 
     def health(self) -> Dict[str, Any]:
         return self.probe()
 
-    def stop(self) -> None:
-        if self.alive:
-            with self._lock:
-                p2p.send_obj({"op": "stop"}, self.leader, self.group)
-            self.alive = False
-
+    # ------------------------------------------------------------------ lifecycle
     def sync(self) -> None:
-        with self._lock:
-            p2p.send_obj({"op": "sync"}, self.leader, self.group)
+        """Barrier hand-off (bench timing): the leader barriers with its members and the node."""
+        self._send({"op": "sync", "id": 0})
 
-
-def serve_pool(engine, router_rank: int, leader: int, pair_group, tp_group=None, on_sync=None) -> None:
-    """Pool-side loop (every rank of the pool calls it).  Returns on {"op": "stop"}."""
-    import torch.distributed as dist
-    from ..engine.sampling import SamplingParams
-    me = dist.get_rank()
-    while True:
-        if me == leader:
-            msg = p2p.recv_obj(router_rank, pair_group)
-            if tp_group is not None:
-                p2p.bcast_obj(msg, leader, tp_group)
-        else:
-            msg = p2p.bcast_obj(None, leader, tp_group)
-        op = msg.get("op")
-        if op == "stop":
-            return
-        if op == "sync":
-            if on_sync is not None:
-                on_sync()
-            continue
-        if op == "ping":
-            if me == leader:
-                p2p.send_obj({"op": "pong", "stats": {k: v for k, v in engine.stats().items()
-                                                      if isinstance(v, (int, float, str))}}, router_rank, pair_group)
-            continue
-        if op == "generate":
+    def stop(self) -> None:
+        self._probe_stop.set()
+        if self.alive:
             try:
-                if "params_list" in msg:
-                    sp = [SamplingParams(**p) for p in msg["params_list"]]
-                else:
-                    sp = SamplingParams(**msg["params"])
-                outs = engine.generate(msg["prompts"], sp)
-                res = EnginePool.to_payloads(outs)
-                rep = {"id": msg["id"], "results": res}
-            except Exception as e:  # report, never kill the pool loop
-                rep = {"id": msg["id"], "error": f"engine failed: {e}"}
-            if me == leader:
-                p2p.send_obj(rep, router_rank, pair_group)
+                self._send({"op": "stop", "id": 0})
+            except Exception:  # noqa: BLE001
+                pass
+            self._rx.join(timeout=30)
+        self.alive = False
+
+
+class PoolLeader:
+    """Pool-side server of one pool leader rank (see module docstring)."""
+
+    def __init__(self, engine, ctrl_group, data_group=None, router_rank: int = 0, on_sync=None,
+                 max_workers: int = 64):
+        self.engine = engine
+        self.ctrl = ctrl_group
+        self.data = data_group
+        self.router = router_rank
+        self.on_sync = on_sync
+        self._send_lock = threading.Lock()
+        self._ex = ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="dllm-pool")
+
+    def _reply(self, msg: Dict[str, Any]) -> None:
+        with self._send_lock:
+            p2p.send_obj(msg, self.router, self.ctrl, tag=TAG_REP)
+
+    def _generate(self, rid: int, prompts, params) -> None:
+        import os
+        from ..engine.sampling import SamplingParams
+        hang = os.environ.get("DLLM_FAULT_HANG_ON")
+        if hang and any(isinstance(p, str) and hang in p for p in prompts):
+            time.sleep(float(os.environ.get("DLLM_FAULT_HANG_S", "5")))   # fault injection (tests)
+        try:
+            sp = SamplingParams.from_dict(params or {})
+            outs = self.engine.generate(prompts, sp)
+            rep = {"id": rid, "results": EnginePool.to_payloads(outs)}
+        except Exception as e:  # report, never kill the pool loop
+            rep = {"id": rid, "error": f"engine failed: {e}"}
+        try:
+            self._reply(rep)
+        except Exception:  # noqa: BLE001 - router gone; nothing to report to
+            pass
+
+    def serve(self) -> None:
+        """Receive until the router sends stop (or disappears)."""
+        import os
+        self.engine.start()   # background step loop: concurrent requests join one batch
+        try:
+            while True:
+                try:
+                    msg = p2p.recv_obj(self.router, self.ctrl, tag=TAG_REQ)
+                except Exception:  # router died: stop serving
+                    return
+                op = msg.get("op")
+                if op == "stop":
+                    self._ex.shutdown(wait=True)
+                    self._reply({"op": "bye"})
+                    return
+                if op == "ping":
+                    self._reply({"id": msg["id"], "op": "pong",
+                                 "stats": {k: v for k, v in self.engine.stats().items()
+                                           if isinstance(v, (int, float, str))}})
+                elif op == "ping_data":
+                    p2p.ping(self.router, self.data, initiator=False)
+                elif op == "sync":
+                    self.engine.mirror_control({"sync": True})
+                    if self.on_sync is not None:
+                        self.on_sync()
+                elif op == "generate":
+                    if os.environ.get("DLLM_FAULT_DIE_ON") and any(
+                            os.environ["DLLM_FAULT_DIE_ON"] in p for p in msg.get("prompts", [])):
+                        os._exit(17)   # fault injection (tests): the pool process dies mid-request
+                    self._ex.submit(self._generate, msg["id"], msg["prompts"], msg.get("params"))
+                elif op == "generate_ids":
+                    prompts = [p2p.recv_tokens(self.router, self.data).tolist() for _ in range(int(msg["n"]))]
+                    self._ex.submit(self._generate, msg["id"], prompts, msg.get("params"))
+        finally:
+            self.engine.stop()
 
 
 class ReplicatedPool(PoolClient):
@@ -165,7 +356,8 @@ class ReplicatedPool(PoolClient):
 
     def _pick(self) -> int:
         with self._lock:
-            i = min(range(len(self.replicas)), key=lambda k: self.inflight[k])
+            live = [k for k in range(len(self.replicas)) if getattr(self.replicas[k], "alive", True)]
+            i = min(live or range(len(self.replicas)), key=lambda k: self.inflight[k])
             self.inflight[i] += 1
             return i
 
@@ -181,11 +373,12 @@ class ReplicatedPool(PoolClient):
         n = len(self.replicas)
         if n == 1 or len(histories) <= 1:
             return self.replicas[0].process_batch(histories) if n == 1 else [self.process(h) for h in histories]
-        with self._lock:  # assign round-robin starting from the least-loaded replica
-            order = sorted(range(n), key=lambda k: self.inflight[k])
-            shards: Dict[int, List[int]] = {k: [] for k in range(n)}
+        with self._lock:  # assign round-robin starting from the least-loaded live replica
+            live = [k for k in range(n) if getattr(self.replicas[k], "alive", True)] or list(range(n))
+            order = sorted(live, key=lambda k: self.inflight[k])
+            shards: Dict[int, List[int]] = {k: [] for k in order}
             for j in range(len(histories)):
-                shards[order[j % n]].append(j)
+                shards[order[j % len(order)]].append(j)
             for k, idx in shards.items():
                 self.inflight[k] += len(idx)
         futs = {k: self._ex.submit(self.replicas[k].process_batch, [histories[j] for j in idx])

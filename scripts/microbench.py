@@ -122,7 +122,9 @@ def bench_decode(eng, B, C):
     seqs = []
     for i in range(B):
         sid = 10_000_000 + i
-        bm.allocate(sid, [5] * C)
+        tbl, _ = bm.allocate(sid, [5 + (i % 1000)] + [5] * (C - 1))
+        if not tbl:
+            raise RuntimeError(f"KV cache too small for B={B} x C={C} (set MB_KV_GB)")
         row = eng._free_rows.pop()
         t = bm.block_table(sid)
         eng.bt_host[row, :len(t)] = t
@@ -198,7 +200,10 @@ if __name__ == "__main__":
         from distributed_llm_amd.ops import gemm as G
         shapes = [(2560, 2048, False), (2048, 2048, False), (11264, 2048, False), (2048, 5632, True),
                   (32000, 2048, False), (6144, 4096, False), (4096, 4096, False), (28672, 4096, False), (4096, 14336, True)]
-        G.autotune(shapes, [1, 8, 32, 64, 128, 256], "cuda", verbose=True)
+        ms = [int(x) for x in os.environ.get("MB_TUNE_M", "1,8,32,64,128,256,384,512").split(",")]
+        if os.environ.get("MB_TUNE_SHAPES"):
+            shapes = [tuple(int(v) for v in t.split("x")) + (False,) for t in os.environ["MB_TUNE_SHAPES"].split(",")]
+        G.autotune(shapes, ms, "cuda", verbose=True)
     if "gemm" in what:
         for M in (1, 16, 64, 128, 256):
             for (N, K) in [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632), (32000, 2048), (6144, 4096), (28672, 4096), (4096, 14336)]:
@@ -226,7 +231,8 @@ if __name__ == "__main__":
                     for per_wg in (1, 2, 4):
                         print(json.dumps(bench_attn_wl(B, C, nq, nkv, d, grid, per_wg, var)), flush=True)
     if "decode" in what or "prefill" in what:
-        eng = LLMEngine(a.model, device="cuda", kv_cache_gb=40, max_num_seqs=256)
+        eng = LLMEngine(a.model, device="cuda", kv_cache_gb=float(os.environ.get("MB_KV_GB", "40")),
+                        max_num_seqs=int(os.environ.get("MB_MAX_SEQS", "256")))
         if "decode" in what:
             Bs = [int(x) for x in os.environ.get("MB_DECODE_B", "1,8,32,64,128,256").split(",")]
             Cs = [int(x) for x in os.environ.get("MB_DECODE_C", "512,2048").split(",")]

@@ -1,0 +1,198 @@
+"""Cross-rank pool protocol (pools.remote) on CPU (gloo): tagged requests with many in flight,
+deadlines, dead-pool detection + failover, periodic health probes into the perf router, and the
+token-id failover hand-off over the data plane.
+
+Reference behaviour being matched: every device call is bounded (timeout=(5, 180)) and an error
+fails over to the other device (/root/reference/src/models/nano.py:26-38, src/router.py:277-282);
+liveness/readiness probing (src/models/server_manager.py:52-61,123-131)."""
+import os
+import socket
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.slow
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      DLLM_EMBEDDER="hash")
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _engine():
+    from distributed_llm_amd.engine.llm_engine import LLMEngine
+    return LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=16, seed=0)
+
+
+def _groups():
+    ctrl = dist.new_group([0, 1], backend="gloo")
+    data = dist.new_group([0, 1], backend="gloo")
+    return ctrl, data
+
+
+def _worker(rank, world, port, scenario, q, env):
+    os.environ.update(env)
+    _init(rank, world, port)
+    ctrl, data = _groups()
+    try:
+        if rank == 1:
+            from distributed_llm_amd.pools.remote import PoolLeader
+            PoolLeader(_engine(), ctrl, data, 0).serve()
+            q.put({"rank": 1, "ok": True})
+            return
+        q.put(_ROUTER[scenario](ctrl, data))
+    except Exception as e:  # noqa: BLE001 - surface in the parent
+        import traceback
+        q.put({"rank": rank, "error": f"{e!r}\n{traceback.format_exc()}"})
+    finally:
+        if scenario in ("concurrent", "handoff"):
+            dist.destroy_process_group()
+        else:
+            q.close()
+            q.join_thread()   # flush the result before skipping teardown
+            os._exit(0)       # the peer is dead: do not wait in gloo teardown
+
+
+def _router_concurrent(ctrl, data):
+    """Long and short requests in flight at once: replies come back in completion order."""
+    import threading
+    from distributed_llm_amd.pools.remote import RemotePool
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=4, timeout_s=120)
+    done = []
+    lock = threading.Lock()
+
+    def call(tag, n):
+        r = rp.process_batch([[{"role": "user", "content": f"request {tag}"}]], {"max_new_tokens": n})[0]
+        with lock:
+            done.append((tag, r))
+    long_t = threading.Thread(target=call, args=("long", 200))
+    long_t.start()
+    time.sleep(0.3)   # the long request is decoding when the short ones arrive
+    shorts = [threading.Thread(target=call, args=(f"s{i}", 3)) for i in range(3)]
+    for t in shorts:
+        t.start()
+    for t in shorts + [long_t]:
+        t.join(120)
+    probe = rp.probe()
+    rp.stop()
+    return {"order": [t for t, _ in done], "errors": [r.get("error") for _, r in done],
+            "tokens": {t: r.get("num_tokens") for t, r in done}, "probe": probe["ok"]}
+
+
+def _router_kill(ctrl, data):
+    """The pool process dies mid-request: the router fails over well inside the deadline, marks
+    the pool dead, and its probes report the failure to the perf router."""
+    from distributed_llm_amd.config import LARGE, SMALL
+    from distributed_llm_amd.orchestrator import Router
+    from distributed_llm_amd.pools.base import EnginePool
+    from distributed_llm_amd.pools.remote import RemotePool
+    health = []
+    rp = RemotePool(LARGE, 1, ctrl, data, max_new_tokens=6, timeout_s=60)
+    r = Router("heuristic", config={"cache_enabled": False}, pools={SMALL: EnginePool(SMALL, _engine(), 5),
+                                                                   LARGE: rp})
+    rp.on_health = lambda name, ok, rtt: (health.append(ok), r.on_pool_health(name, ok, rtt))
+    rp.start_probes(interval_s=0.2, timeout_s=1.0, data_probe_every=0)
+    time.sleep(0.6)
+    t0 = time.perf_counter()
+    payload, ntok, dev = r.route_query([{"role": "user", "content":
+                                         "Write a Python function with recursion __die__ and explain it"}])
+    dt = time.perf_counter() - t0
+    time.sleep(1.0)
+    return {"dev": dev, "ok": payload["ok"], "dt": dt, "alive": rp.alive, "health": health,
+            "pool_health": r.pool_health.get(LARGE)}
+
+
+def _router_hang(ctrl, data):
+    """A request that never finishes: the caller gets an error payload at its deadline (the
+    orchestrator then fails over), while health probes keep being answered."""
+    from distributed_llm_amd.pools.remote import RemotePool
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=4, timeout_s=2.0)
+    t0 = time.perf_counter()
+    rep = rp.process([{"role": "user", "content": "please __hang__ forever"}])
+    dt = time.perf_counter() - t0
+    probe = rp.probe(timeout=5.0)
+    ok_after = rp.process([{"role": "user", "content": "and now a normal request"}])
+    return {"err": rep.get("error", ""), "dt": dt, "probe": probe["ok"], "after": "response" in ok_after,
+            "timeouts": rp.timeouts}
+
+
+def _router_handoff(ctrl, data):
+    """Failover hand-off as token ids over the data plane gives the same answer as text."""
+    from distributed_llm_amd.engine.tokenizer import get_tokenizer
+    from distributed_llm_amd.models.configs import get_model_config
+    from distributed_llm_amd.pools.remote import RemotePool
+    cfg = get_model_config("tiny-llama-test")
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=7, timeout_s=60,
+                    tokenizer=get_tokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id))
+    h = [{"role": "user", "content": "hand this prompt over as token ids"}]
+    via_ids = rp.process_failover(h)
+    via_text = rp.process(h)
+    data_ping = rp.probe_data()
+    rp.stop()
+    return {"ids": via_ids.get("response"), "text": via_text.get("response"), "data_ping": data_ping["ok"]}
+
+
+_ROUTER = {"concurrent": _router_concurrent, "kill": _router_kill, "hang": _router_hang,
+           "handoff": _router_handoff}
+
+
+def _run(scenario, env=None, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, scenario, q, env or {})) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = []
+    try:
+        for _ in range(2 if scenario in ("concurrent", "handoff") else 1):
+            outs.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    for o in outs:
+        assert "error" not in o or o.get("rank") is None, o.get("error")
+    return [o for o in outs if o.get("rank") is None][0]
+
+
+def test_concurrent_requests_complete_out_of_order():
+    out = _run("concurrent")
+    assert out["errors"] == [None] * 4
+    assert out["order"][-1] == "long", out["order"]          # short requests overtook the long one
+    assert out["tokens"]["long"] > out["tokens"]["s0"]
+    assert out["probe"]
+
+
+def test_dead_pool_fails_over_within_deadline():
+    out = _run("kill", env={"DLLM_FAULT_DIE_ON": "__die__"})
+    assert out["ok"] and out["dev"] == "nano", out
+    assert out["dt"] < 30.0, out                              # transport error, not the 60 s deadline
+    assert out["alive"] is False
+    assert False in out["health"] and out["pool_health"]["failures"] >= 1
+
+
+def test_hung_request_times_out_and_pool_stays_usable():
+    out = _run("hang", env={"DLLM_FAULT_HANG_ON": "__hang__", "DLLM_FAULT_HANG_S": "4"})
+    assert "timed out" in out["err"] and 1.5 < out["dt"] < 10.0, out
+    assert out["probe"] and out["after"] and out["timeouts"] == 1
+
+
+def test_failover_token_id_handoff_matches_text():
+    out = _run("handoff")
+    assert out["ids"] and out["ids"] == out["text"]
+    assert out["data_ping"]
