@@ -512,7 +512,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
   const int M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn == 128)), "ks in {1,2}; nw 4, or 8 with bn 128");
+  TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)), "ks in {1,2}; nw 4, or 8 with bn >= 128");
   TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
   TORCH_CHECK((bm == 64 || bm == 128 || (bm == 256 && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
                   (stages == 2 || stages == 3) && (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024,

@@ -57,8 +57,9 @@ class Supervisor:
                 "--model", s.model, "--max-new-tokens", str(s.max_new_tokens), "--temperature", str(s.temperature),
                 *s.extra_args]
         if s.tp > 1:
+            # torchrun's -m runs the worker as a module in every rank (one rank per GPU of the pool)
             return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={s.tp}",
-                    "--master-addr", "127.0.0.1", "--master-port", str(29600 + s.port % 1000), *base[1:]]
+                    "--master-addr", "127.0.0.1", "--master-port", str(29600 + s.port % 1000), *base]
         return [sys.executable, *base]
 
     def healthy(self, name: str, timeout: float = 1.0) -> bool:
@@ -84,6 +85,8 @@ class Supervisor:
             if s.gpus:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, s.gpus))
             env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
             os.makedirs(self.log_dir, exist_ok=True)
             log = open(os.path.join(self.log_dir, f"{name}.log"), "ab")
             self.procs[name] = subprocess.Popen(self._cmd(s), env=env, stdout=log, stderr=subprocess.STDOUT,

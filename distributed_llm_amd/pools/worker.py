@@ -90,7 +90,29 @@ class _NoLock:
 _nolock = _NoLock()
 
 
+def _tp_setup(a):
+    """Under torchrun (WORLD_SIZE > 1): one process per GPU of the pool, bound to LOCAL_RANK; all
+    ranks form ONE tensor-parallel group (RCCL on GPU, gloo on CPU) plus a gloo group for the
+    scheduler mirror.  Returns (ParallelContext, mirror group, device)."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from ..parallel.comm import init_distributed, make_tp_groups
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    on_gpu = a.device == "cuda" and torch.cuda.is_available()
+    if on_gpu:
+        torch.cuda.set_device(local)
+    init_distributed("nccl" if on_gpu else "gloo")
+    par = make_tp_groups(dist.get_world_size())
+    mirror = dist.new_group(list(range(dist.get_world_size())), backend="gloo")
+    dev = f"cuda:{local}" if on_gpu else "cpu"
+    if on_gpu:
+        par.enable_custom_all_reduce(dev)
+    return par, mirror, dev
+
+
 def main(argv=None) -> None:
+    import os
     ap = argparse.ArgumentParser()
     ap.add_argument("--name", default="nano")
     ap.add_argument("--port", type=int, default=5001)
@@ -100,15 +122,36 @@ def main(argv=None) -> None:
     ap.add_argument("--max-new-tokens", type=int, default=256)
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--kv-gb", type=float, default=None)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     a = ap.parse_args(argv)
     if a.kind == "echo":
         pool: PoolClient = EchoPool(a.name, tokens_per_reply=min(a.max_new_tokens, 64))
-    else:
-        from ..engine.llm_engine import LLMEngine
-        eng = LLMEngine(a.model, device="cuda", kv_cache_gb=a.kv_gb)
+        create_worker_app(pool).run(host=a.host, port=a.port, threaded=True)
+        return
+    from ..engine.llm_engine import LLMEngine
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # tensor-parallel pool (supervisor launches torchrun, one rank per GPU): rank 0 serves HTTP
+        # and leads the scheduler; the other ranks replay it in lockstep (LLMEngine.follow)
+        import torch.distributed as dist
+        par, mirror, dev = _tp_setup(a)
+        eng = LLMEngine(a.model, device=dev, par=par, kv_cache_gb=a.kv_gb, max_num_seqs=a.max_num_seqs)
+        eng.enable_tp_mirror(mirror, 0)
+        if dist.get_rank() != 0:
+            eng.follow()
+            return
+        eng.start()
         pool = EnginePool(a.name, eng, max_new_tokens=a.max_new_tokens, temperature=a.temperature)
-    app = create_worker_app(pool)
-    app.run(host=a.host, port=a.port, threaded=True)
+        try:
+            create_worker_app(pool).run(host=a.host, port=a.port, threaded=True)
+        finally:
+            eng.stop()   # members leave follow()
+        return
+    dev = a.device
+    eng = LLMEngine(a.model, device=dev, kv_cache_gb=a.kv_gb, max_num_seqs=a.max_num_seqs)
+    eng.start()
+    pool = EnginePool(a.name, eng, max_new_tokens=a.max_new_tokens, temperature=a.temperature)
+    create_worker_app(pool).run(host=a.host, port=a.port, threaded=True)
 
 
 if __name__ == "__main__":

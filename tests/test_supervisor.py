@@ -78,3 +78,31 @@ def test_router_fails_over_when_pool_process_dies(sup):
     _crash(sup, SMALL)
     payload, tokens, dev = r.route_query(HIST)
     assert dev == LARGE and payload.get("ok") and tokens > 0   # failover served it
+
+
+def test_tensor_parallel_pool_worker_matches_tp1(tmp_path):
+    """A tp=2 pool: the supervisor launches torchrun (2 ranks, gloo on CPU); rank 0 serves HTTP and
+    leads the scheduler, rank 1 follows it in lockstep.  /query must give the same greedy tokens
+    as the in-process TP=1 engine (reference ServerManager.start_server brings up ONE working
+    server: /root/reference/src/models/server_manager.py:66-142)."""
+    from distributed_llm_amd.engine.llm_engine import LLMEngine
+    from distributed_llm_amd.pools.base import EnginePool
+    args = ["--device", "cpu", "--kv-gb", "0.05", "--max-num-seqs", "8"]
+    s = Supervisor([PoolSpec(LARGE, _port(), kind="engine", model="tiny-llama-test", max_new_tokens=9, tp=2,
+                             extra_args=args)], log_dir=str(tmp_path / "logs"), startup_timeout_s=240)
+    try:
+        assert s.start(LARGE), open(tmp_path / "logs" / f"{LARGE}.log").read()[-3000:]
+        pool = HTTPPool(LARGE, s.specs[LARGE].url, timeout_s=120)
+        hist = [{"role": "user", "content": "tensor parallel pools answer like one GPU"}]
+        got = pool.process(hist)
+        # concurrent requests join the TP pool's continuous batch (mirrored scheduler)
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(4) as ex:
+            many = list(ex.map(pool.process, [[{"role": "user", "content": f"question {i}"}] for i in range(4)]))
+    finally:
+        s.stop_all()
+    ref = EnginePool(LARGE, LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=8),
+                     max_new_tokens=9).process(hist)
+    assert "response" in got, got
+    assert got["response"] == ref["response"]
+    assert all("response" in m for m in many), many
