@@ -48,6 +48,11 @@ int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, hipStream_t);
 int dllm_res_add_ssq(const void*, long, void*, long, float*, int, int, hipStream_t);
+int dllm_qkv_post(const void*, long, const float*, int, long, float, float, const int*, const float*, const int*, void*,
+                  void*, void*, int, int, int, int, hipStream_t);
+int dllm_swiglu_post(const void*, long, const float*, int, long, float, float, void*, long, int, int, hipStream_t);
+int dllm_flash_prefill(const void*, const void*, const void*, const int*, const int*, const int*, const int*, const int*,
+                       const int*, void*, int, int, int, int, int, int, float, hipStream_t);
 int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
                               unsigned long long*, hipStream_t);
 }
@@ -197,6 +202,35 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
                           xcd_remap ? 1 : 0, num_tiles, nq, nkv, d, block_tables.size(1), splits, causal ? 1 : 0,
                           (float)scale, stream()),
      "paged_attention");
+}
+
+// Flash-style prefill attention (csrc/kernels/flash_prefill.hip): 128-row GQA tiles with K/V
+// staged once per workgroup in LDS.  tile_seq/tile_tok0 hold 128 / G tokens per tile.
+void flash_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
+                   torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
+                   torch::Tensor tile_tok0, torch::Tensor out, bool causal, double scale) {
+  check_bf16(q, "q");
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  check_bf16(out, "out");
+  for (auto* t : {&block_tables, &qstart, &qlen, &ctx, &tile_seq, &tile_tok0}) check_i32(*t, "attention metadata");
+  TORCH_CHECK(q.dim() == 3 && q.is_contiguous() && out.is_contiguous() && out.sizes() == q.sizes(), "q/out [T, nq, d]");
+  const int nq = q.size(1), d = q.size(2);
+  TORCH_CHECK(d == 64 || d == 128, "flash prefill: head_dim 64 or 128");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.size(2) == 16 && kc.size(3) == d &&
+                  vc.size(2) == d && vc.size(3) == 16,
+              "cache layout");
+  const int nkv = kc.size(1);
+  TORCH_CHECK(nq % nkv == 0 && 128 % (nq / nkv) == 0, "GQA group must divide 128");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(1) <= 1024, "block_tables [S, <= 1024] (16K context)");
+  const int S = block_tables.size(0);
+  TORCH_CHECK(qstart.numel() == S && qlen.numel() == S && ctx.numel() == S, "seq metadata len");
+  TORCH_CHECK(tile_tok0.numel() == tile_seq.numel(), "tile metadata len");
+  ok(dllm_flash_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(), qstart.data_ptr<int>(),
+                        qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(), tile_tok0.data_ptr<int>(),
+                        out.data_ptr(), tile_seq.numel(), nq, nkv, d, block_tables.size(1), causal ? 1 : 0,
+                        (float)scale, stream()),
+     "flash_prefill");
 }
 
 void silu_mul(torch::Tensor gu, torch::Tensor out) {
@@ -593,6 +627,43 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)epi, stream()), "tgemm");
 }
 
+// standalone EPI_QKV / EPI_SWIGLU for a vendor-GEMM output y (prefill)
+void qkv_post(torch::Tensor y, torch::Tensor ssq, int64_t ssq_n, double scale, double eps, torch::Tensor pos,
+              torch::Tensor cos_sin, torch::Tensor slots, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc,
+              int64_t nq, int64_t nkv, int64_t d) {
+  check_bf16(y, "y");
+  check_f32(ssq, "ssq");
+  check_i32(pos, "positions");
+  check_i32(slots, "slots");
+  check_f32(cos_sin, "cos_sin");
+  for (auto* t : {&q_out, &kc, &vc}) check_bf16(*t, "qkv outputs");
+  const int M = y.size(0);
+  TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && y.size(1) == (nq + 2 * nkv) * d && d % 32 == 0, "y [M, (nq+2nkv) d]");
+  TORCH_CHECK(ssq.dim() == 2 && ssq.size(1) >= M && ssq_n >= 1 && ssq_n <= ssq.size(0), "ssq [slots, >= M]");
+  TORCH_CHECK(pos.numel() >= M && slots.numel() >= M && cos_sin.size(1) == d, "positions/slots/cos_sin");
+  TORCH_CHECK(q_out.is_contiguous() && q_out.numel() >= (int64_t)M * nq * d, "q_out");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.size(1) == nkv && kc.size(2) == 16 && kc.size(3) == d &&
+                  vc.size(2) == d && vc.size(3) == 16,
+              "cache layout");
+  ok(dllm_qkv_post(y.data_ptr(), y.stride(0), ssq.data_ptr<float>(), ssq_n, ssq.size(1), (float)scale, (float)eps,
+                   pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(), kc.data_ptr(),
+                   vc.data_ptr(), M, nq, nkv, d, stream()),
+     "qkv_post");
+}
+
+void swiglu_post(torch::Tensor y, torch::Tensor ssq, int64_t ssq_n, double scale, double eps, torch::Tensor act) {
+  check_bf16(y, "y");
+  check_f32(ssq, "ssq");
+  check_bf16(act, "act");
+  const int M = y.size(0), N = y.size(1);
+  TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && N % 32 == 0, "y [M, 2I]");
+  TORCH_CHECK(act.dim() == 2 && act.stride(1) == 1 && act.size(0) == M && act.size(1) == N / 2, "act [M, I]");
+  TORCH_CHECK(ssq.dim() == 2 && ssq.size(1) >= M && ssq_n >= 1 && ssq_n <= ssq.size(0), "ssq [slots, >= M]");
+  ok(dllm_swiglu_post(y.data_ptr(), y.stride(0), ssq.data_ptr<float>(), ssq_n, ssq.size(1), (float)scale, (float)eps,
+                      act.data_ptr(), act.stride(0), M, N, stream()),
+     "swiglu_post");
+}
+
 // r = h + r in place (h optional), ssq[m] = sum(r[m]^2)  (f32 [M])
 void res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tensor ssq) {
   check_bf16(r, "r");
@@ -615,6 +686,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("moe_ffn", &moe_ffn);
   m.def("tgemm", &tgemm);
   m.def("res_add_ssq", &res_add_ssq);
+  m.def("qkv_post", &qkv_post);
+  m.def("swiglu_post", &swiglu_post);
   m.def("mm_gemm", &mm_gemm);
   m.def("car_alloc", &car_alloc);
   m.def("car_handle", &car_handle);
@@ -627,6 +700,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("rope_kv", &rope_kv);
   m.def("kv_write", &kv_write);
   m.def("paged_attention", &paged_attention);
+  m.def("flash_prefill", &flash_prefill);
   m.def("silu_mul", &silu_mul);
   m.def("embed", &embed);
   m.def("gelu", &gelu);

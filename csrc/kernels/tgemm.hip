@@ -432,7 +432,101 @@ __global__ void __launch_bounds__(256) res_add_ssq_kernel(const u16* __restrict_
   s = wave_sum(s);
   if (lane == 0) ssq[row] = s;
 }
+
+// ---- standalone epilogues for a vendor-GEMM output y (prefill-size M, where hipBLASLt's core is
+// faster than tgemm's): the same math as EPI_QKV / EPI_SWIGLU applied to y = r . W'^T.
+__device__ __forceinline__ float row_rinv(const float* ssq, int n, long ld, int m, float scale, float eps) {
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += ssq[(long)i * ld + m];
+  return rsqrtf(s * scale + eps);
+}
+
+// one block per row; a thread handles 8 RoPE pairs (q/k: 16-B loads of both halves of a 32-column
+// group) or 8 V columns
+__global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y, long ldy, const float* __restrict__ ssq,
+                                                       int ssq_n, long ssq_ld, float scale, float eps,
+                                                       const int* __restrict__ pos, const float* __restrict__ cos_sin,
+                                                       const int* __restrict__ slots, u16* __restrict__ q_out,
+                                                       u16* __restrict__ kc, u16* __restrict__ vc, int nq, int nkv, int d) {
+  const int m = blockIdx.x;
+  const float ri = ssq ? row_rinv(ssq, ssq_n, ssq_ld, m, scale, eps) : 1.f;
+  const int hd = d / 2, qcols = nq * d, kcols = nkv * d, N = qcols + kcols + nkv * d;
+  const int slot = slots[m];
+  const long blk = slot >> 4, off = slot & 15;
+  const float* cs = cos_sin + (long)pos[m] * d;
+  const u16* yr = y + (long)m * ldy;
+  for (int c = threadIdx.x * 8; c < N; c += blockDim.x * 8) {
+    if (c < qcols + kcols) {
+      if ((c & 31) >= 16) continue;  // the thread owning the group's first half rotates both halves
+      float x1[8], x2[8];
+      unpack8(ld16(yr + c), x1);
+      unpack8(ld16(yr + c + 16), x2);
+      const bool isq = c < qcols;
+      const int cc = isq ? c : c - qcols;
+      const int head = cc / d, o = cc % d;
+      const int d1 = 16 * (o >> 5) + (o & 15);
+      float r1[8], r2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a1 = bfr(x1[j] * ri), a2 = bfr(x2[j] * ri);
+        const float co = cs[d1 + j], si = cs[hd + d1 + j];
+        r1[j] = a1 * co - a2 * si;
+        r2[j] = a2 * co + a1 * si;
+      }
+      u16* dst = isq ? q_out + ((long)m * nq + head) * d
+                     : (slot >= 0 ? kc + ((blk * nkv + head) * 16 + off) * d : nullptr);
+      if (dst) {
+        st16(dst + d1, pack8(r1));
+        st16(dst + hd + d1, pack8(r2));
+      }
+    } else if (slot >= 0) {
+      float v[8];
+      unpack8(ld16(yr + c), v);
+      const int cc = c - qcols - kcols, head = cc / d, dim = cc % d;
+      u16* vo = vc + ((blk * nkv + head) * d) * 16 + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vo[(long)(dim + j) * 16] = f2bf(v[j] * ri);
+    }
+  }
+}
+
+// act[m, 16 G + c] = silu(g) * u for the interleaved [g16 | u16] groups of y; one block per row
+__global__ void __launch_bounds__(256) swiglu_post_kernel(const u16* __restrict__ y, long ldy, const float* __restrict__ ssq,
+                                                          int ssq_n, long ssq_ld, float scale, float eps, u16* __restrict__ act,
+                                                          long lda, int N) {
+  const int m = blockIdx.x;
+  const float ri = ssq ? row_rinv(ssq, ssq_n, ssq_ld, m, scale, eps) : 1.f;
+  const u16* yr = y + (long)m * ldy;
+  for (int o = threadIdx.x * 8; o < N / 2; o += blockDim.x * 8) {
+    const int g = o >> 4, c = o & 15;
+    float gv[8], uv[8];
+    unpack8(ld16(yr + 32 * g + c), gv);
+    unpack8(ld16(yr + 32 * g + 16 + c), uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gv[j] = silu(bfr(gv[j] * ri)) * bfr(uv[j] * ri);
+    st16(act + (long)m * lda + o, pack8(gv));
+  }
+}
 }  // namespace
+
+extern "C" int dllm_qkv_post(const void* y, long ldy, const float* ssq, int ssq_n, long ssq_ld, float scale, float eps,
+                             const int* pos, const float* cos_sin, const int* slots, void* q_out, void* kc, void* vc,
+                             int M, int nq, int nkv, int d, hipStream_t stream) {
+  if (d % 32 || ldy % 8) return -1;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(qkv_post_kernel, dim3(M), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale, eps,
+                     pos, cos_sin, slots, (u16*)q_out, (u16*)kc, (u16*)vc, nq, nkv, d);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_swiglu_post(const void* y, long ldy, const float* ssq, int ssq_n, long ssq_ld, float scale,
+                                float eps, void* act, long lda, int M, int N, hipStream_t stream) {
+  if (N % 32 || ldy % 8 || lda % 8) return -1;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(swiglu_post_kernel, dim3(M), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale,
+                     eps, (u16*)act, lda, N);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dllm_res_add_ssq(const void* h, long ldh, void* r, long ldr, float* ssq, int M, int H,
                                 hipStream_t stream) {

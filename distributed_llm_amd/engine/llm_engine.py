@@ -689,6 +689,8 @@ class LLMEngine:
             budget -= n
         ids, pos, slots, qstart, qlen, ctx, last = [], [], [], [], [], [], []
         G = self.model.nq // self.model.nkv
+        flash = self.on_gpu and ops.flash_supported(self.model.d, G, self.max_blocks)
+        tiler = ops.flash_tiles if flash else ops.build_tiles
         tseq, ttok = [], []
         t = 0
         for i, (s, a, b) in enumerate(chunk):
@@ -700,7 +702,7 @@ class LLMEngine:
             ctx.append(b)
             t += b - a
             last.append(t - 1)
-            ts, tt = ops.build_tiles([b - a], G)
+            ts, tt = tiler([b - a], G)
             tseq.extend([i] * len(ts))
             ttok.extend(tt)
         nb = max((ctx_i + BS - 1) // BS for ctx_i in ctx)
@@ -713,10 +715,11 @@ class LLMEngine:
         splits = self._splits_for(len(tseq))
         meta = AttnMeta(slots=T(slots), block_tables=torch.from_numpy(bt).to(dev), qstart=T(qstart), qlen=T(qlen),
                         ctx=T(ctx), tile_seq=T(tseq), tile_tok0=T(ttok), last_idx=T(last, torch.int64),
-                        splits=splits, xcd_remap=True)
+                        splits=splits, xcd_remap=True, flash=flash)
         hidden = self.model.hidden_states(T(ids), T(pos), meta, self.kv_caches)
         self.steps["prefill"] += 1
         self.steps["prefill_tokens"] += t
+        self._check_collectives()
         done_seqs = [s for (s, a, b) in chunk if b == len(s.fill)]
         for s, a, b in chunk:
             s.num_computed = b
@@ -807,6 +810,7 @@ class LLMEngine:
                 self._decode_forward(bs)
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
+        self._check_collectives()
         if self.fused_sampler:
             toks = self.d_out[:B].tolist()
         else:
@@ -847,6 +851,17 @@ class LLMEngine:
                 self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
         self.timers["decode_host_post"] += time.perf_counter() - _t2
         return finished, preempted
+
+    def _check_collectives(self) -> None:
+        """TP: a one-shot all-reduce that timed out on any rank fails this step (every rank the
+        same way) and switches the group to RCCL; captured graphs embed the old collective, so
+        they are dropped and re-captured on demand."""
+        if self.par.custom_ar is None:
+            return
+        if not self.par.check_collectives():
+            self._graphs.clear()
+            raise RuntimeError("tensor-parallel all-reduce timed out on a peer; step discarded, "
+                               "group switched to RCCL")
 
     def _decode_meta(self, bs: int) -> AttnMeta:
         if self._use_worklist(bs):

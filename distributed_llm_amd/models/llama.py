@@ -52,6 +52,7 @@ class AttnMeta:
     xcd_remap: bool = False                    # prefill: XCD-contiguous attention block order
     items: Optional[torch.Tensor] = None       # decode: persistent attention work list (ops.decode_work_items)
     grid_items: int = 0                        # workgroups walking ``items``
+    flash: bool = False                        # prefill: tile_seq/tile_tok0 are 128-row flash tiles
 
 
 def qk_dim_order(d: int) -> torch.Tensor:
@@ -295,6 +296,15 @@ class LlamaModel:
         yl = ep_moe_ffn(xl, ids, w, L["w13"], L["w2"], self.cfg.n_experts, par.tp_group, par.tp_size)
         return all_gather_rows(yl, T, par.tp_group, par.tp_size)
 
+    def _attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        if meta.flash:   # prefill: 128-row tiles, K/V staged once per workgroup (flash_prefill.hip)
+            return ops.flash_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
+                                       meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True)
+        return ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
+                                   meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
+                                   splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
+                                   xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+
     def hidden_states(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Final-normed hidden states of each sequence's last new token: [S, H]."""
@@ -311,10 +321,7 @@ class LlamaModel:
             residual, spare = res, (spare if res is residual else residual)
             kc, vc = kv_caches[li]
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
-            o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
-                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
-                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
-                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+            o = self._attention(q, kc, vc, meta)
             h = self.par.all_reduce(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             if not self.cfg.is_moe:
                 gu, res = ops.norm_linear(h, residual, spare, L["ln2"], cfg.rms_eps, L["wgu"])
@@ -343,10 +350,7 @@ class LlamaModel:
             kc, vc = kv_caches[li]
             q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,
                                         self.nq, self.nkv, self.d)
-            o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
-                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
-                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
-                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+            o = self._attention(q, kc, vc, meta)
             nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b)
             if not cfg.is_moe:
                 act = ops.gemm.swiglu_matmul(r, L["wgu_f"], ssq_b, nb, eps)
@@ -378,10 +382,7 @@ class LlamaModel:
             qkv = ops.linear(x, L["wqkv"])
             kc, vc = kv_caches[li]
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slots, kc, vc, self.nq, self.nkv, self.d)
-            o = ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
-                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
-                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
-                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+            o = self._attention(q, kc, vc, meta)
             h = par.reduce_scatter_rows(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             x = par.all_gather_rows(ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual), T)
             if self.moe_ep:

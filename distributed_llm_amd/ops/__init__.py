@@ -166,6 +166,42 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return o
 
 
+FLASH_ROWS = 128
+
+
+def flash_supported(d: int, group: int, max_blocks: int) -> bool:
+    return d in (64, 128) and FLASH_ROWS % group == 0 and max_blocks <= 1024 and \
+        os.environ.get("DLLM_FLASH_PREFILL", "1") == "1"
+
+
+def flash_tiles(q_lens, group: int) -> Tuple[list, list]:
+    """Host tile table of the flash prefill kernel: 128 / group query tokens per tile."""
+    tpt = FLASH_ROWS // group
+    ts, tt = [], []
+    for s, n in enumerate(q_lens):
+        for t0 in range(0, int(n), tpt):
+            ts.append(s)
+            tt.append(t0)
+    return ts, tt
+
+
+def flash_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                    seq_qstart: torch.Tensor, seq_qlen: torch.Tensor, seq_ctx: torch.Tensor, tile_seq: torch.Tensor,
+                    tile_tok0: torch.Tensor, scale: Optional[float] = None, causal: bool = True,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Flash-style prefill over the paged cache (csrc/kernels/flash_prefill.hip); tiles from
+    :func:`flash_tiles`.  Same contract as :func:`paged_attention` (CPU: the same reference)."""
+    d = q.shape[-1]
+    scale = (1.0 / math.sqrt(d)) if scale is None else scale
+    ext = _native(q)
+    if ext is None:
+        return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, scale, causal)
+    o = out if out is not None else torch.empty_like(q)
+    ext.flash_prefill(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
+                      causal, scale)
+    return o
+
+
 def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,
                       out: Optional[np.ndarray] = None) -> np.ndarray:
     """Work list for persistent decode attention (one query token per tile, tiles in ``ctx`` order).

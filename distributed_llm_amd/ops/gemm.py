@@ -70,6 +70,7 @@ class _Planner:
     def __init__(self):
         self.plans: Dict[Tuple[int, int, int, bool], Tuple] = {}     # best overall, for linear()
         self.tg_plans: Dict[Tuple[int, int, int], Tuple] = {}        # best tgemm tile, for the fused ops
+        self.fused_core: Dict[Tuple[int, int, int], str] = {}        # "tg" | "blas" per tuned shape
         self.ws: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
         self.timings: Dict[Tuple[int, int, int, bool], Dict[str, float]] = {}
 
@@ -271,6 +272,22 @@ def linear_swiglu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- fused decoder ops
+#
+# Two implementations of each fused op: the tgemm epilogue (one launch), or hipBLASLt's GEMM core
+# followed by the same epilogue as a standalone kernel (qkv_post / res_add_ssq / swiglu_post).
+# The autotuner records, per decode bucket and shape, which is faster (the standalone epilogue
+# is charged POST_US); shapes it never saw (prefill chunks above MAX_M) use the vendor core,
+# which wins at large M (profiles/r2_tgemm_tune.md).
+POST_US = 3.0
+
+
+def use_vendor_core(M: int, N: int, K: int) -> bool:
+    if os.environ.get("DLLM_FUSED_CORE") in ("tg", "blas"):
+        return os.environ["DLLM_FUSED_CORE"] == "blas"
+    c = _P.fused_core.get((M, N, K))
+    if c is not None:
+        return c == "blas"
+    return M > MAX_M
 
 def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float,
                    positions: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
@@ -283,6 +300,10 @@ def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: i
     q = torch.empty((T, nq, d), dtype=r.dtype, device=r.device)
     if T == 0:
         return q
+    if use_vendor_core(T, w.shape[0], H):
+        _native(r).qkv_post(F.linear(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
+                            k_cache, v_cache, nq, nkv, d)
+        return q
     _tgemm(_native(r), r, w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
            eps=eps, pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv,
            d=d)
@@ -293,6 +314,9 @@ def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_
     """``residual += x . w^T`` (bf16 rounding as ``rms_norm``'s residual add) and the partial row
     sums of the new residual's squares into ``ssq_out[:slots]``; returns ``slots``."""
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    if M and use_vendor_core(M, N, K):
+        _native(x).res_add_ssq(F.linear(x, w), residual, ssq_out[0])
+        return 1
     plan = tg_plan(M, N, K)
     if M:
         _tgemm(_native(x), x, w, EPI_RESADD, plan, y=residual, ssq_out=ssq_out)
@@ -304,6 +328,9 @@ def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: in
     .fuse_gate_up_weight) -> [T, I]."""
     T, H = r.shape
     act = torch.empty((T, w.shape[0] // 2), dtype=r.dtype, device=r.device)
+    if T and use_vendor_core(T, w.shape[0], H):
+        _native(r).swiglu_post(F.linear(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), act)
+        return act
     if T:
         _tgemm(_native(r), r, w, EPI_SWIGLU, tg_plan(T, w.shape[0], H), y=act, ssq_in=ssq, ssq_n=ssq_n,
                norm_scale=1.0 / H, eps=eps)
@@ -366,6 +393,8 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
                 parts = k.split(",")
                 if parts[0] == "t":
                     _P.tg_plans[(int(parts[1]), int(parts[2]), int(parts[3]))] = tuple(v)
+                elif parts[0] == "c":
+                    _P.fused_core[(int(parts[1]), int(parts[2]), int(parts[3]))] = v
                 else:
                     _P.plans[(int(parts[0]), int(parts[1]), int(parts[2]), parts[3] == "1")] = tuple(v)
     shapes = list(shapes)
@@ -374,6 +403,7 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
         import json
         d = {_plan_key(k): list(v) for k, v in _P.plans.items()}
         d.update({_plan_key(k): list(v) for k, v in _P.tg_plans.items()})
+        d.update({"c,%d,%d,%d" % k: v for k, v in _P.fused_core.items()})
         with open(cache, "w") as f:
             json.dump(d, f)
 
@@ -414,7 +444,7 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
             key = (M, N, K, sw)
             tkey = (M, N, K)
             need_plain = key not in _P.plans
-            need_tg = use_tg and not sw and tkey not in _P.tg_plans and K % 64 == 0
+            need_tg = use_tg and not sw and (tkey not in _P.tg_plans or tkey not in _P.fused_core) and K % 64 == 0
             if not (need_plain or need_tg):
                 continue
             x = torch.randn(M, 2 * K if sw else K, device=dev).to(torch.bfloat16)
@@ -452,7 +482,9 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
             tgc = [c for c in res if c[0] == "tg"]
             if need_tg and tgc:
-                _P.tg_plans[tkey] = min(tgc, key=res.get)[1:]
+                best_tg = min(tgc, key=res.get)
+                _P.tg_plans[tkey] = best_tg[1:]
+                _P.fused_core[tkey] = "tg" if res[best_tg] <= res[("blas",)] + POST_US else "blas"
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
                       for k in ("gemv", "skinny", "lds", "mm", "tg")}

@@ -64,6 +64,28 @@ class ParallelContext:
             return False
         return True
 
+    def check_collectives(self) -> bool:
+        """After a step: did any rank's one-shot all-reduce time out waiting for a peer (its error
+        flag, parallel.custom_ar)?  The flag is MAX-reduced over the TP group so every rank takes
+        the same decision; on a trip the custom all-reduce is dropped on ALL ranks (its epochs are
+        out of step from then on) and RCCL carries every later all-reduce.  Returns False on a
+        trip — the caller must discard the step (its sums may hold stale peer data)."""
+        car = self.custom_ar
+        if car is None:
+            return True
+        flag = car.err.detach().clone()
+        if self.tp_group is not None and dist.is_initialized():
+            if dist.get_backend(self.tp_group) != "nccl":
+                flag = flag.cpu()
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.tp_group)
+        if int(flag.reshape(-1)[0].item()) == 0:
+            return True
+        import logging
+        logging.getLogger(__name__).error("custom all-reduce timed out (peer mask %#x): falling back to RCCL",
+                                          int(flag.reshape(-1)[0].item()))
+        self.custom_ar = None
+        return False
+
     def use_sp(self, num_tokens: int) -> bool:
         return self.sequence_parallel and self.tp_size > 1 and num_tokens >= max(self.sp_min_tokens, self.tp_size)
 

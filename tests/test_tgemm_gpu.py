@@ -131,3 +131,47 @@ def test_res_add_ssq():
     want = (h.float() + r0.float()).to(torch.bfloat16)
     assert torch.equal(r, want)
     torch.testing.assert_close(ssq, (want.float() ** 2).sum(1), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("core", ["tg", "blas"])
+def test_fused_ops_both_cores(core, monkeypatch):
+    """The fused decoder ops give the same results through the tgemm epilogue and through the
+    vendor GEMM + standalone epilogue kernels (qkv_post / res_add_ssq / swiglu_post)."""
+    monkeypatch.setenv("DLLM_FUSED_CORE", core)
+    torch.manual_seed(11)
+    M, H, I, d, nq, nkv = 77, 256, 384, 64, 4, 2
+    G.reserve("cuda")
+    r = _rnd(M, H)
+    ln1 = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    ln2 = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wqkv, wo = _rnd((nq + 2 * nkv) * d, H, scale=0.05), _rnd(H, nq * d, scale=0.05)
+    wgu, wd = _rnd(2 * I, H, scale=0.05), _rnd(H, I, scale=0.05)
+    ssq = torch.empty(G.max_slots(H), M, device="cuda")
+    ops.gemm.res_add_ssq(None, r, ssq[0])
+    cos_sin = ops.rope_cos_sin(512, d, 10000.0, "cuda")
+    pos = torch.arange(M, device="cuda", dtype=torch.int32)
+    slots = torch.arange(M, device="cuda", dtype=torch.int32)
+    kc = torch.zeros(8, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(8, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
+    r_ref = r.cpu().clone()
+    q = G.qkv_rope_cache(r, fuse_qkv_weight(wqkv, ln1, nq, nkv, d), ssq, 1, 1e-5, pos, cos_sin, slots, kc, vc,
+                         nq, nkv, d)
+    o = _rnd(M, nq * d)
+    ssq2 = torch.empty(G.max_slots(H), M, device="cuda")
+    n2 = G.matmul_resadd(o, wo, r, ssq2)
+    act = G.swiglu_matmul(r, fuse_gate_up_weight(wgu, ln2), ssq2, n2, 1e-5)
+    # fp32 references
+    x = ref.rms_norm(r_ref, ln1.cpu(), 1e-5)
+    qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
+    kr = torch.zeros(8, nkv, 16, d, dtype=torch.bfloat16)
+    vr = torch.zeros(8, nkv, d, 16, dtype=torch.bfloat16)
+    qr = ref.rope_and_cache(qkv, pos.cpu(), cos_sin.cpu(), slots.cpu(), kr, vr, nq, nkv, d)
+    h = (o.cpu().float() @ wo.cpu().float().t()).to(torch.bfloat16)
+    r2 = (h.float() + r_ref.float()).to(torch.bfloat16)
+    x2 = ref.rms_norm(r2, ln2.cpu(), 1e-5)
+    ar = ref.silu_mul((x2.float() @ wgu.cpu().float().t()).to(torch.bfloat16))
+    torch.testing.assert_close(q.cpu().float(), qr.float(), atol=4e-2, rtol=3e-2)
+    torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=4e-2, rtol=3e-2)
+    torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=4e-2, rtol=3e-2)
+    torch.testing.assert_close(r.cpu().float(), r2.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(act.cpu().float(), ar.float(), atol=3e-2, rtol=3e-2)

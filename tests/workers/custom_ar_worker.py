@@ -56,6 +56,23 @@ def main():
         if not torch.equal(xs.cpu(), want):
             fails.append(f"graph replay {it}")
     car.check()
+    # a peer that never arrives: rank 1 skips one all-reduce while rank 0 spins out (bounded);
+    # the error flag trips on rank 0 only, and the consensus check drops the custom all-reduce on
+    # BOTH ranks (ParallelContext.check_collectives), so neither deadlocks nor diverges
+    from distributed_llm_amd.parallel.comm import ParallelContext
+    par = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, global_rank=rank,
+                          world_size=world, custom_ar=car)
+    assert par.check_collectives()
+    dist.barrier()
+    car.spin_limit = 20000
+    if rank == 0:
+        y = inputs(rank, 4096).cuda()
+        car.all_reduce(y)
+        torch.cuda.synchronize()
+    dist.barrier()
+    tripped = not par.check_collectives()
+    if not tripped or par.custom_ar is not None:
+        fails.append(f"rank {rank}: timeout not agreed (tripped={tripped})")
     dist.barrier()
     car.close()
     dist.destroy_process_group()
