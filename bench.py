@@ -59,6 +59,8 @@ def parse():
                     help="G > 1: G independently pipelined groups of conversations, one thread each")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1: turn pipelining (replicated topology): conversations advance independently")
+    ap.add_argument("--no-encoder-memo", action="store_true",
+                    help="encode every routed query with the GPU MiniLM encoder (no per-text memo)")
     ap.add_argument("--trace", default=None,
                     help="write a Chrome trace (router/pool/engine spans, GPU decode time) to this path; "
                          "'{rank}' is replaced by the rank")
@@ -251,6 +253,9 @@ def main() -> int:
     dev = f"cuda:{local}" if on_gpu else "cpu"
     if not on_gpu:
         os.environ.setdefault("DLLM_EMBEDDER", "hash")
+    if a.no_encoder_memo:
+        os.environ["DLLM_ENCODER_MEMO"] = "0"
+    from distributed_llm_amd.router.embedder import encoder_stats
     topology = a.topology if world > 1 else "replicated"
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
@@ -328,6 +333,7 @@ def main() -> int:
                 dist.barrier()         # replicas open their windows together
             with convs._cv:
                 st0 = [dict(e.stats()) for e in engines]
+                enc0 = encoder_stats()
                 if on_gpu:
                     torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -339,9 +345,11 @@ def main() -> int:
                     torch.cuda.synchronize()
                 elapsed = time.perf_counter() - t0
                 st1 = [dict(e.stats()) for e in engines]
+                enc1 = encoder_stats()
             convs.stop()
         else:
             st0 = [dict(e.stats()) for e in engines]
+            enc0 = encoder_stats()
             sync()
             t0 = time.perf_counter()
             for _ in range(a.steps):
@@ -349,6 +357,7 @@ def main() -> int:
             sync()
             elapsed = time.perf_counter() - t0
             st1 = [dict(e.stats()) for e in engines]
+            enc1 = encoder_stats()
         if cluster is not None:
             cluster.shutdown()
         for e in engines:
@@ -407,6 +416,10 @@ def main() -> int:
                                     for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
                                               "t_decode_host_post_s")},
         }
+        lk = enc1["lookups"] - enc0["lookups"]
+        out["router_encoder"] = {"kinds": enc1["kinds"], "memo": bool(enc1.get("memo_enabled", False)),
+                                 "lookups": lk, "memo_hit_rate": round((enc1["hits"] - enc0["hits"]) / lk, 3) if lk else None,
+                                 "texts_encoded_in_window": enc1["encoded_texts"] - enc0["encoded_texts"]}
         print(json.dumps(out), flush=True)
     if a.trace:
         from distributed_llm_amd.utils.tracing import tracer

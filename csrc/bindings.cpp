@@ -47,7 +47,10 @@ int dllm_car_close_handle(void*);
 int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, hipStream_t);
-int dllm_res_add_ssq(const void*, long, void*, long, float*, int, int, hipStream_t);
+int dllm_encoder_attention(const void*, const int*, void*, int, int, int, int, float, hipStream_t);
+int dllm_embed_ln(const int*, const void*, const void*, const void*, const void*, const void*, void*, int, int, int, int,
+                  float, hipStream_t);
+int dllm_res_add_ssq(const void*, long, void*, long, float*, long, int, int, int, hipStream_t);
 int dllm_qkv_post(const void*, long, const float*, int, long, float, float, const int*, const float*, const int*, void*,
                   void*, void*, int, int, int, int, hipStream_t);
 int dllm_swiglu_post(const void*, long, const float*, int, long, float, float, void*, long, int, int, hipStream_t);
@@ -533,17 +536,19 @@ void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
 
 // ---- fused-epilogue LDS-tiled GEMM (csrc/kernels/tgemm.hip).  epi: 0 plain y = x.w^T (optionally
 // row-scaled by rinv from ssq_in), 1 residual add (y = residual, in place; ssq_out partial row
-// sums), 2 QKV (RoPE + q_out + paged K/V writes), 3 SwiGLU (y = [M, N/2]).
+// sums), 2 QKV (RoPE + q_out + paged K/V writes), 3 SwiGLU (y = [M, N/2]), 4 GELU (y = gelu(x.w^T +
+// bias)).  bias [N] (epi 0, 1, 4) is added to the product before the epilogue op.
 void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int64_t epi, int64_t bm, int64_t bn,
            int64_t stages, int64_t splits, int64_t ks, int64_t nw, c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> counters,
            c10::optional<torch::Tensor> ssq_in, int64_t ssq_in_n, double norm_scale, double eps,
            c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> pos,
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
-           int64_t nq, int64_t nkv, int64_t d) {
+           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "epi");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
   const int M = x.size(0), N = w.size(0), K = w.size(1);
   TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)), "ks in {1,2}; nw 4, or 8 with bn >= 128");
@@ -582,7 +587,13 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
     a.norm_scale = (float)norm_scale;
     a.eps = (float)eps;
   }
-  if (epi == 0 || epi == 1 || epi == 3) {
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(epi == 0 || epi == 1 || epi == 4, "bias: plain, residual or gelu epilogue");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N, "bias [N]");
+    a.bias = (const uint16_t*)bias->data_ptr();
+  }
+  if (epi == 0 || epi == 1 || epi == 3 || epi == 4) {
     TORCH_CHECK(y.has_value(), "y required");
     check_bf16(*y, "y");
     TORCH_CHECK(y->dim() == 2 && y->stride(1) == 1 && y->size(0) == M && y->size(1) == (epi == 3 ? N / 2 : N),
@@ -664,11 +675,15 @@ void swiglu_post(torch::Tensor y, torch::Tensor ssq, int64_t ssq_n, double scale
      "swiglu_post");
 }
 
-// r = h + r in place (h optional), ssq[m] = sum(r[m]^2)  (f32 [M])
-void res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tensor ssq) {
+// r = h + r in place (h optional) and row sums of r^2: ssq f32 [M] (one slot) or [slots, >= M]
+// (partial sums over up to ``slots`` column slices); returns the number of slots written
+int64_t res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tensor ssq) {
   check_bf16(r, "r");
   check_f32(ssq, "ssq");
-  TORCH_CHECK(r.dim() == 2 && r.stride(1) == 1 && ssq.numel() >= r.size(0), "r [M, H], ssq [>= M]");
+  TORCH_CHECK(r.dim() == 2 && r.stride(1) == 1, "r [M, H]");
+  TORCH_CHECK((ssq.dim() == 1 && ssq.numel() >= r.size(0)) ||
+                  (ssq.dim() == 2 && ssq.size(1) >= r.size(0) && ssq.stride(1) == 1),
+              "ssq [>= M] or [slots, >= M]");
   const void* hp = nullptr;
   long ldh = 0;
   if (h.has_value()) {
@@ -677,12 +692,50 @@ void res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tensor 
     hp = h->data_ptr();
     ldh = h->stride(0);
   }
-  ok(dllm_res_add_ssq(hp, ldh, r.data_ptr(), r.stride(0), ssq.data_ptr<float>(), r.size(0), r.size(1), stream()),
-     "res_add_ssq");
+  const int slices = ssq.dim() == 2 ? (int)ssq.size(0) : 1;
+  const long ld = ssq.dim() == 2 ? ssq.stride(0) : 0;
+  const int n = dllm_res_add_ssq(hp, ldh, r.data_ptr(), r.stride(0), ssq.data_ptr<float>(), ld, slices, r.size(0),
+                                 r.size(1), stream());
+  TORCH_CHECK(n >= 1, "res_add_ssq failed (", n, ")");
+  return n;
+}
+
+// router encoder (csrc/kernels/encoder.hip): bidirectional attention over a padded batch
+void encoder_attention(torch::Tensor qkv, torch::Tensor lens, torch::Tensor out, int64_t B, int64_t S, int64_t nh,
+                       int64_t d, double scale) {
+  check_bf16(qkv, "qkv");
+  check_bf16(out, "out");
+  check_i32(lens, "lens");
+  TORCH_CHECK(d == 32 || d == 64, "encoder attention: head_dim 32 or 64");
+  TORCH_CHECK(S >= 1 && S <= 512, "encoder attention: 1 <= S <= 512");
+  TORCH_CHECK(qkv.is_contiguous() && qkv.dim() == 2 && qkv.size(0) == B * S && qkv.size(1) == 3 * nh * d,
+              "qkv [B*S, 3 nh d]");
+  TORCH_CHECK(out.is_contiguous() && out.dim() == 2 && out.size(0) == B * S && out.size(1) == nh * d, "out [B*S, nh d]");
+  TORCH_CHECK(lens.numel() >= B, "lens [B]");
+  ok(dllm_encoder_attention(qkv.data_ptr(), lens.data_ptr<int>(), out.data_ptr(), B, S, nh, d, (float)scale, stream()),
+     "encoder_attention");
+}
+
+void embed_ln(torch::Tensor ids, torch::Tensor word, torch::Tensor pos, torch::Tensor type0, torch::Tensor w,
+              torch::Tensor b, torch::Tensor out, int64_t S, double eps) {
+  check_i32(ids, "ids");
+  for (auto* t : {&word, &pos, &type0, &w, &b, &out}) check_bf16(*t, "embed_ln operand");
+  const int64_t T = ids.numel(), H = word.size(1);
+  TORCH_CHECK(ids.is_contiguous() && word.is_contiguous() && pos.is_contiguous() && type0.is_contiguous() &&
+                  w.is_contiguous() && b.is_contiguous() && out.is_contiguous(),
+              "contiguous operands");
+  TORCH_CHECK(S >= 1 && T % S == 0 && pos.size(0) >= S && pos.size(1) == H && type0.numel() == H && w.numel() == H &&
+                  b.numel() == H && out.numel() == T * H && H % 8 == 0 && H <= 2048,
+              "embed_ln shapes");
+  ok(dllm_embed_ln(ids.data_ptr<int>(), word.data_ptr(), pos.data_ptr(), type0.data_ptr(), w.data_ptr(), b.data_ptr(),
+                   out.data_ptr(), T, S, H, word.size(0), (float)eps, stream()),
+     "embed_ln");
 }
 }  // namespace
 
 PYBIND11_MODULE(_hip_kernels, m) {
+  m.def("encoder_attention", &encoder_attention);
+  m.def("embed_ln", &embed_ln);
   m.def("moe_ffn", &moe_ffn);
   m.def("tgemm", &tgemm);
   m.def("res_add_ssq", &res_add_ssq);

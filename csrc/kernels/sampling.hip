@@ -105,7 +105,7 @@ __global__ void sample_topp_kernel(const float* __restrict__ vals, const long* _
 //   4. wave 0: softmax weights at temperature t, inclusive prefix sums in rank order (wave scan),
 //      nucleus = shortest prefix with mass >= top_p, inverse-CDF pick with u = hash(seed, row).
 constexpr int SR_THREADS = 256;
-constexpr int SR_CAP = 1024;   // candidate list capacity (ties beyond it at the threshold are dropped)
+constexpr int SR_CAP = 1024;   // candidate list capacity (only ties AT the threshold key can be dropped)
 constexpr int SR_MAXN = 512;   // above this many candidates the exact-threshold pass runs
 constexpr int SR_KMAX = 256;
 
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
   __shared__ unsigned wsum[SR_THREADS / 64];
   __shared__ float sv[SR_THREADS / 64];
   __shared__ int si[SR_THREADS / 64];
-  __shared__ int s_bin, s_above, s_n, s_lo;
+  __shared__ int s_bin, s_above, s_n, s_nt, s_lo, s_amax;
   __shared__ float s_m;
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u16* l = logits + (long)row * stride;
@@ -234,44 +234,59 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
         acc += hist[b];
       }
       s_lo = lo;
+      s_amax = (int)acc;  // exactly the keys strictly above lo (< k)
     }
   } else if (tid == 0) {
     s_lo = bin << 4;
+    s_amax = s_above + (int)hist[bin];  // every candidate (<= SR_MAXN): none is ever dropped
   }
-  if (tid == 0) s_n = 0;
+  if (tid == 0) { s_n = 0; s_nt = 0; }
   __syncthreads();
 
-  // ---- 2. candidates: every logit at or above the threshold key
+  // ---- 2. candidates: every logit at or above the threshold key.  Keys strictly above it (at most
+  // s_amax: < k for a crowded bin, <= SR_MAXN otherwise) fill slots from the bottom; ties AT the
+  // threshold fill slots from the top, never below slot s_amax — so a crowded tie bin can only
+  // drop ties, never a strictly better logit, and the top-k stays exact.
   const unsigned lo = (unsigned)s_lo;
+  const int amax = min(s_amax, SR_CAP);
   for (int c = tid; c < nv; c += SR_THREADS) {
     const uint4 v = ld16(l + c * 8);
     const u16* e = reinterpret_cast<const u16*>(&v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const unsigned key = bf_key(e[j]);
-      if (key >= lo) {
+      if (key > lo) {
         const int p = atomicAdd(&s_n, 1);
-        if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+        if (p < amax) cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+      } else if (key == lo) {
+        const int p = atomicAdd(&s_nt, 1);
+        if (p < SR_CAP - amax) cand[SR_CAP - 1 - p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
       }
     }
   }
   for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
     const unsigned key = bf_key(l[i]);
-    if (key >= lo) {
+    if (key > lo) {
       const int p = atomicAdd(&s_n, 1);
-      if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(i));
+      if (p < amax) cand[p] = make_float2(key_f(key), __int_as_float(i));
+    } else if (key == lo) {
+      const int p = atomicAdd(&s_nt, 1);
+      if (p < SR_CAP - amax) cand[SR_CAP - 1 - p] = make_float2(key_f(key), __int_as_float(i));
     }
   }
   __syncthreads();
-  const int n = min(s_n, SR_CAP);
+  const int na = min(s_n, amax), nt = min(s_nt, SR_CAP - amax);
+  const int n = na + nt;
+  // candidate j of the union [0, na) u [SR_CAP - nt, SR_CAP)
+  auto cidx = [&](int j) { return j < na ? j : SR_CAP - nt + (j - na); };
 
   // ---- 3. rank = #strictly better candidates; ranks < k are the top-k
   for (int j = tid; j < n; j += SR_THREADS) {
-    const float2 cj = cand[j];
+    const float2 cj = cand[cidx(j)];
     const int ij = __float_as_int(cj.y);
     int r = 0;
     for (int i = 0; i < n; ++i) {
-      const float2 ci = cand[i];
+      const float2 ci = cand[cidx(i)];
       r += (ci.x > cj.x || (ci.x == cj.x && __float_as_int(ci.y) < ij)) ? 1 : 0;
     }
     if (r < k) { i_r[r] = ij; w_r[r] = cj.x; }

@@ -12,6 +12,7 @@
 //                per-(n-tile, row) partial sums of r^2 for the next RMSNorm
 //   EPI_SWIGLU : act = silu(g) * u with [g | u] = (r . Wgu'^T) * rinv[m]  (interleaved gate/up rows)
 //   EPI_RESADD : r += act . Wd^T  (+ partial sums of squares)
+//   EPI_GELU   : y = gelu(x . W^T + bias)  (encoder FFN; PLAIN and RESADD take the same bias)
 //
 // RMSNorm folding: rmsnorm(r) * gamma . W^T = rinv[m] * (r . (W * gamma)^T), gamma folded into the
 // weight columns once at load time; rinv[m] = rsqrt(sum(r^2) / K + eps) comes from the producer
@@ -42,6 +43,7 @@ using dllm::EPI_PLAIN;
 using dllm::EPI_RESADD;
 using dllm::EPI_QKV;
 using dllm::EPI_SWIGLU;
+using dllm::EPI_GELU;
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;  // 128 bytes per staged row
 
@@ -58,6 +60,7 @@ __device__ __forceinline__ void block_sync_lds() {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 __device__ __forceinline__ float bfr(float x) { return bf2f(f2bf(x)); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // KS: 64-deep k sub-tiles per ring stage (one barrier per stage); NW: waves per workgroup, laid out
 // 2 (M) x NW/2 (N), each wave a (BM/2) x (BN/(NW/2)) tile.
@@ -313,6 +316,13 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
     }
     return;
   } else {
+    // bias (encoder layers): one value per lane column, hoisted out of the row loop
+    float bcol[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WN + 16 * j + cl;
+      bcol[j] = (EPI != EPI_SWIGLU && a.bias != nullptr && n < N) ? bf2f(a.bias[n]) : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -326,7 +336,11 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
           }
         } else {
 #pragma unroll
-          for (int j = 0; j < FN; ++j) so[rl * OLD + wn * WN + 16 * j + cl] = f2bf(acc[i][j][e] * rinv[i][e]);
+          for (int j = 0; j < FN; ++j) {
+            float v = acc[i][j][e] * rinv[i][e] + bcol[j];
+            if constexpr (EPI == EPI_GELU) v = gelu_erf(bfr(v));  // GELU of the bf16 linear output
+            so[rl * OLD + wn * WN + 16 * j + cl] = f2bf(v);
+          }
         }
       }
     __syncthreads();
@@ -408,15 +422,19 @@ int by_tile(int bm, int bn, int stages, int ks, int nw, const GemmArgs& a, hipSt
 
 // Residual-stream helpers for the paths the GEMM epilogue cannot cover (first layer's embedding,
 // tensor-parallel all-reduced outputs, MoE outputs): one wave per row, 16-B vectors.
-//   res_add_ssq: r = bf16(h + r) in place (h may be null: r unchanged), ssq[m] = sum(r^2)
+//   res_add_ssq: r = bf16(h + r) in place (h may be null: r unchanged) and the row's partial sums
+//   of squares, one per column slice of ``cw`` columns: ssq[slice * ssq_ld + m] (grid.y = slices,
+//   so a decode-size M still spreads over many workgroups)
 __global__ void __launch_bounds__(256) res_add_ssq_kernel(const u16* __restrict__ h, long ldh, u16* __restrict__ r,
-                                                          long ldr, float* __restrict__ ssq, int M, int H) {
+                                                          long ldr, float* __restrict__ ssq, long ssq_ld, int M, int H,
+                                                          int cw) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   u16* rr = r + (long)row * ldr;
   const u16* hr = h ? h + (long)row * ldh : nullptr;
+  const int c1 = min(H, (int)(blockIdx.y + 1) * cw);
   float s = 0.f;
-  for (int c = lane * 8; c < H; c += 512) {
+  for (int c = blockIdx.y * cw + lane * 8; c < c1; c += 512) {
     float v[8];
     unpack8(ld16(rr + c), v);
     if (hr) {
@@ -430,7 +448,7 @@ __global__ void __launch_bounds__(256) res_add_ssq_kernel(const u16* __restrict_
     for (int j = 0; j < 8; ++j) s += v[j] * v[j];
   }
   s = wave_sum(s);
-  if (lane == 0) ssq[row] = s;
+  if (lane == 0) ssq[(long)blockIdx.y * ssq_ld + row] = s;
 }
 
 // ---- standalone epilogues for a vendor-GEMM output y (prefill-size M, where hipBLASLt's core is
@@ -441,7 +459,7 @@ __device__ __forceinline__ float row_rinv(const float* ssq, int n, long ld, int 
   return rsqrtf(s * scale + eps);
 }
 
-// one block per row; a thread handles 8 RoPE pairs (q/k: 16-B loads of both halves of a 32-column
+// one block per (row, 2048-column slice); a thread handles 8 RoPE pairs (q/k: 16-B loads of both halves of a 32-column
 // group) or 8 V columns
 __global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y, long ldy, const float* __restrict__ ssq,
                                                        int ssq_n, long ssq_ld, float scale, float eps,
@@ -455,7 +473,7 @@ __global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y
   const long blk = slot >> 4, off = slot & 15;
   const float* cs = cos_sin + (long)pos[m] * d;
   const u16* yr = y + (long)m * ldy;
-  for (int c = threadIdx.x * 8; c < N; c += blockDim.x * 8) {
+  for (int c = (blockIdx.y * blockDim.x + threadIdx.x) * 8; c < N; c += gridDim.y * blockDim.x * 8) {
     if (c < qcols + kcols) {
       if ((c & 31) >= 16) continue;  // the thread owning the group's first half rotates both halves
       float x1[8], x2[8];
@@ -490,14 +508,14 @@ __global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y
   }
 }
 
-// act[m, 16 G + c] = silu(g) * u for the interleaved [g16 | u16] groups of y; one block per row
+// act[m, 16 G + c] = silu(g) * u for the interleaved [g16 | u16] groups of y; one block per (row, 2048-output slice)
 __global__ void __launch_bounds__(256) swiglu_post_kernel(const u16* __restrict__ y, long ldy, const float* __restrict__ ssq,
                                                           int ssq_n, long ssq_ld, float scale, float eps, u16* __restrict__ act,
                                                           long lda, int N) {
   const int m = blockIdx.x;
   const float ri = ssq ? row_rinv(ssq, ssq_n, ssq_ld, m, scale, eps) : 1.f;
   const u16* yr = y + (long)m * ldy;
-  for (int o = threadIdx.x * 8; o < N / 2; o += blockDim.x * 8) {
+  for (int o = (blockIdx.y * blockDim.x + threadIdx.x) * 8; o < N / 2; o += gridDim.y * blockDim.x * 8) {
     const int g = o >> 4, c = o & 15;
     float gv[8], uv[8];
     unpack8(ld16(yr + 32 * g + c), gv);
@@ -514,7 +532,8 @@ extern "C" int dllm_qkv_post(const void* y, long ldy, const float* ssq, int ssq_
                              int M, int nq, int nkv, int d, hipStream_t stream) {
   if (d % 32 || ldy % 8) return -1;
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(qkv_post_kernel, dim3(M), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale, eps,
+  const int N = (nq + 2 * nkv) * d;
+  hipLaunchKernelGGL(qkv_post_kernel, dim3(M, (N + 2047) / 2048), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale, eps,
                      pos, cos_sin, slots, (u16*)q_out, (u16*)kc, (u16*)vc, nq, nkv, d);
   return (int)hipGetLastError();
 }
@@ -523,18 +542,22 @@ extern "C" int dllm_swiglu_post(const void* y, long ldy, const float* ssq, int s
                                 float eps, void* act, long lda, int M, int N, hipStream_t stream) {
   if (N % 32 || ldy % 8 || lda % 8) return -1;
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(swiglu_post_kernel, dim3(M), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale,
+  hipLaunchKernelGGL(swiglu_post_kernel, dim3(M, (N / 2 + 2047) / 2048), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale,
                      eps, (u16*)act, lda, N);
   return (int)hipGetLastError();
 }
 
-extern "C" int dllm_res_add_ssq(const void* h, long ldh, void* r, long ldr, float* ssq, int M, int H,
-                                hipStream_t stream) {
-  if (H % 8 || ldr % 8 || (h && ldh % 8)) return -1;
-  if (M <= 0) return 0;
-  hipLaunchKernelGGL(res_add_ssq_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, (const u16*)h, ldh, (u16*)r, ldr,
-                     ssq, M, H);
-  return (int)hipGetLastError();
+// slices: column slices (ssq rows) to split H into; returns the slice count used (< 0: error)
+extern "C" int dllm_res_add_ssq(const void* h, long ldh, void* r, long ldr, float* ssq, long ssq_ld, int slices, int M,
+                                int H, hipStream_t stream) {
+  if (H % 8 || ldr % 8 || (h && ldh % 8) || slices < 1) return -1;
+  const int cw = ((H + slices - 1) / slices + 511) / 512 * 512;  // whole 512-column wave passes
+  const int n = (H + cw - 1) / cw;
+  if (M <= 0) return n;
+  hipLaunchKernelGGL(res_add_ssq_kernel, dim3((M + 3) / 4, n), dim3(256), 0, stream, (const u16*)h, ldh, (u16*)r, ldr,
+                     ssq, ssq_ld, M, H, cw);
+  const int e = (int)hipGetLastError();
+  return e ? -100 - e : n;
 }
 
 extern "C" int dllm_tgemm_sizeof_args() { return (int)sizeof(GemmArgs); }
@@ -558,6 +581,7 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
     case EPI_RESADD: return by_tile<EPI_RESADD>(bm, bn, stages, ks, nw, a, stream);
     case EPI_QKV: return by_tile<EPI_QKV>(bm, bn, stages, ks, nw, a, stream);
     case EPI_SWIGLU: return by_tile<EPI_SWIGLU>(bm, bn, stages, ks, nw, a, stream);
+    case EPI_GELU: return by_tile<EPI_GELU>(bm, bn, stages, ks, nw, a, stream);
     default: return -6;
   }
 }

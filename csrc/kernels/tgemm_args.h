@@ -30,6 +30,8 @@ struct GemmArgs {
   uint16_t* kc;               // [blocks, nkv, 16, d]
   uint16_t* vc;               // [blocks, nkv, d, 16]
   int nq, nkv, d;
+  // PLAIN / RESADD / GELU: bias[n] added to the product before the epilogue op (null: none)
+  const uint16_t* bias;
 };
-enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3 };
+enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_GELU = 4 };
 }  // namespace dllm

@@ -344,8 +344,7 @@ class LlamaModel:
         slots_n = ops.gemm.max_slots(H)
         ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
         ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
-        ops.gemm.res_add_ssq(None, r, ssq_a[0])
-        n = 1
+        n = ops.gemm.res_add_ssq(None, r, ssq_a)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,
@@ -357,8 +356,7 @@ class LlamaModel:
                 n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a)
             else:
                 x = ops.rms_norm(r, L["ln2"], eps)
-                ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a[0])
-                n = 1
+                n = ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a)
         return ops.rms_norm(r.index_select(0, meta.last_idx), self.final_norm, eps)
 
     def _hidden_states_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,

@@ -2,9 +2,11 @@
 
 The reference embeds every query with sentence-transformers on the host CPU
 (src/query_router_engine.py:181 and :571 — twice per query when hybrid + cache are on).
-Here the encoder runs on the GPU in bf16: 6 BERT layers, H=384, 12 heads x 32, FFN 1536,
-post-LN residual blocks (HIP LayerNorm+residual kernel), GELU (HIP), bidirectional attention,
-masked mean-pool + L2 normalise (one HIP kernel).  Batched: one forward per batch of queries.
+Here the encoder runs on the GPU in bf16 on our own kernels: 6 BERT layers, H=384, 12 heads x
+32, FFN 1536, post-LN residual blocks.  Embedding sum + LayerNorm is one kernel; each projection
+is one tgemm launch with its bias (and GELU, or the residual add) in the epilogue; attention is
+the bidirectional MFMA kernel of csrc/kernels/encoder.hip; masked mean-pool + L2 normalise is one
+kernel.  Batched: one forward per batch of queries.
 Weights: HF ``model.safetensors`` of all-MiniLM-L6-v2 if provided, else random (seeded).
 Tokenizer: BERT WordPiece via ``tokenizers`` when a vocab file is given, else a deterministic
 hashing word tokenizer (vocab 30522).
@@ -88,7 +90,9 @@ class MiniLMEncoder:
         vocab_file = vocab_file or os.environ.get("DLLM_MINILM_VOCAB")
         self.tok = _WordPiece(vocab_file) if vocab_file and os.path.exists(vocab_file) else _HashWordTokenizer(cfg.vocab)
         self._memo: "OrderedDict[str, torch.Tensor]" = OrderedDict()
-        self._memo_size = memo_size
+        # per-text memo of embeddings (DLLM_ENCODER_MEMO=0 disables it: every query is encoded)
+        self._memo_size = memo_size if os.environ.get("DLLM_ENCODER_MEMO", "1") != "0" else 0
+        self.memo_hits = self.memo_misses = self.encoded_texts = 0
         self._lock = threading.Lock()
 
     def load_safetensors(self, path: str) -> None:
@@ -118,28 +122,57 @@ class MiniLMEncoder:
 
     @torch.no_grad()
     def _forward(self, texts: List[str], max_len: int) -> torch.Tensor:
+        """One padded batch through the HIP encoder: fused embedding+LN, per layer 4 tgemm launches
+        (QKV + bias, Wo + bias + residual, W1 + bias + GELU, W2 + bias + residual), the encoder
+        attention kernel and 2 LayerNorms; masked mean-pool + L2 (csrc/kernels/encoder.hip,
+        tgemm.hip, norm.hip, cosine.hip).  CPU tensors run the same graph on ops.reference."""
+        cfg = self.cfg
+        toks = [self.tok.encode(t, max_len) for t in texts]
+        B, S = len(toks), max(len(x) for x in toks)
+        ids = torch.zeros((B, S), dtype=torch.int32)
+        for i, x in enumerate(toks):
+            ids[i, :len(x)] = torch.tensor(x, dtype=torch.int32)
+        lens = torch.tensor([len(x) for x in toks], dtype=torch.int32)
+        ids, lens_d = ids.to(self.device), lens.to(self.device)
+        H, nh = cfg.hidden, cfg.heads
+        x = ops.embed_ln(ids, self.word, self.pos, self.type0, *self.emb_ln, S, cfg.eps)
+        for L in self.layers:
+            qkv = ops.gemm.linear_bias(x, L["wqkv"], L["bqkv"])
+            a = ops.encoder_attention(qkv, lens_d, B, S, nh, H // nh)
+            x = ops.layer_norm(ops.gemm.linear_bias_residual(a, L["wo"], L["bo"], x), *L["ln1"], cfg.eps)
+            f = ops.gemm.linear_bias(x, L["w1"], L["b1"], gelu=True)
+            x = ops.layer_norm(ops.gemm.linear_bias_residual(f, L["w2"], L["b2"], x), *L["ln2"], cfg.eps)
+        return ops.mean_pool_l2(x.view(B, S, H), lens_d)
+
+    @torch.no_grad()
+    def reference_forward(self, texts: List[str], max_len: int = 256) -> torch.Tensor:
+        """fp32 PyTorch forward of the same weights (numerics oracle for the HIP path)."""
         cfg = self.cfg
         toks = [self.tok.encode(t, max_len) for t in texts]
         B, S = len(toks), max(len(x) for x in toks)
         ids = torch.zeros((B, S), dtype=torch.int64)
         for i, x in enumerate(toks):
             ids[i, :len(x)] = torch.tensor(x)
-        lens = torch.tensor([len(x) for x in toks], dtype=torch.int32)
-        ids, lens_d = ids.to(self.device), lens.to(self.device)
+        lens = torch.tensor([len(x) for x in toks])
+        f = lambda t: t.detach().float().cpu()
         H, nh = cfg.hidden, cfg.heads
-        x = F.embedding(ids, self.word) + self.pos[:S].unsqueeze(0) + self.type0
-        x = ops.layer_norm(x.reshape(B * S, H).contiguous(), *self.emb_ln, cfg.eps)
-        keymask = (torch.arange(S, device=self.device)[None, :] < lens_d[:, None])  # [B, S]
-        attn_mask = keymask[:, None, None, :]
+        x = f(self.word)[ids] + f(self.pos)[:S][None] + f(self.type0)
+        x = F.layer_norm(x, (H,), f(self.emb_ln[0]), f(self.emb_ln[1]), cfg.eps)
+        keymask = (torch.arange(S)[None, :] < lens[:, None])[:, None, None, :]
         for L in self.layers:
-            qkv = F.linear(x, L["wqkv"], L["bqkv"]).view(B, S, 3, nh, H // nh).permute(2, 0, 3, 1, 4)
-            a = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=attn_mask)
-            a = a.permute(0, 2, 1, 3).reshape(B * S, H)
-            h = F.linear(a, L["wo"], L["bo"])
-            x = ops.layer_norm(h, *L["ln1"], cfg.eps, residual=x.clone())  # post-LN: LN(attn + x)
-            f = F.linear(ops.gelu(F.linear(x, L["w1"], L["b1"])), L["w2"], L["b2"])
-            x = ops.layer_norm(f, *L["ln2"], cfg.eps, residual=x.clone())
-        return ops.mean_pool_l2(x.view(B, S, H), lens_d)
+            qkv = F.linear(x, f(L["wqkv"]), f(L["bqkv"])).view(B, S, 3, nh, H // nh).permute(2, 0, 3, 1, 4)
+            a = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=keymask)
+            a = a.permute(0, 2, 1, 3).reshape(B, S, H)
+            x = F.layer_norm(x + F.linear(a, f(L["wo"]), f(L["bo"])), (H,), f(L["ln1"][0]), f(L["ln1"][1]), cfg.eps)
+            h = F.linear(F.gelu(F.linear(x, f(L["w1"]), f(L["b1"]))), f(L["w2"]), f(L["b2"]))
+            x = F.layer_norm(x + h, (H,), f(L["ln2"][0]), f(L["ln2"][1]), cfg.eps)
+        m = (torch.arange(S)[None, :] < lens[:, None]).float()[..., None]
+        return F.normalize((x * m).sum(1) / m.sum(1).clamp(min=1.0), dim=-1)
+
+    def memo_stats(self) -> Dict[str, float]:
+        n = self.memo_hits + self.memo_misses
+        return {"memo_enabled": bool(self._memo_size), "lookups": n, "hits": self.memo_hits,
+                "hit_rate": round(self.memo_hits / n, 4) if n else 0.0, "encoded_texts": self.encoded_texts}
 
     def encode(self, texts: List[str], max_len: int = 256) -> torch.Tensor:
         """[n, 384] f32 unit vectors on the device; memoised per text."""
@@ -147,12 +180,16 @@ class MiniLMEncoder:
         todo: Dict[str, List[int]] = {}
         with self._lock:
             for i, t in enumerate(texts):
-                v = self._memo.get(t)
+                v = self._memo.get(t) if self._memo_size else None
                 if v is None:
                     todo.setdefault(t, []).append(i)
                 else:
                     self._memo.move_to_end(t)
                     out[i] = v
+            missed = sum(len(v) for v in todo.values())
+            self.memo_hits += len(texts) - missed
+            self.memo_misses += missed
+            self.encoded_texts += len(todo)
         if todo:
             keys = list(todo)
             embs = self._forward(keys, max_len)
@@ -160,7 +197,8 @@ class MiniLMEncoder:
                 for k, e in zip(keys, embs):
                     for i in todo[k]:
                         out[i] = e
-                    self._memo[k] = e
+                    if self._memo_size:
+                        self._memo[k] = e
                 while len(self._memo) > self._memo_size:
                     self._memo.popitem(last=False)
         return torch.stack(out) if out else torch.zeros((0, self.cfg.hidden), device=self.device)

@@ -266,6 +266,31 @@ def gelu(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def encoder_attention(qkv: torch.Tensor, lens: torch.Tensor, B: int, S: int, nh: int, d: int,
+                      scale: Optional[float] = None) -> torch.Tensor:
+    """Bidirectional (encoder) attention over a padded batch, qkv [B*S, 3 nh d] -> [B*S, nh d];
+    keys at positions >= lens[b] are masked (csrc/kernels/encoder.hip)."""
+    scale = (1.0 / math.sqrt(d)) if scale is None else scale
+    ext = _native(qkv)
+    if ext is None:
+        return ref.encoder_attention(qkv, lens, B, S, nh, d, scale)
+    out = torch.empty((B * S, nh * d), dtype=qkv.dtype, device=qkv.device)
+    ext.encoder_attention(qkv.contiguous(), lens.to(torch.int32).contiguous(), out, B, S, nh, d, float(scale))
+    return out
+
+
+def embed_ln(ids: torch.Tensor, word: torch.Tensor, pos: torch.Tensor, type0: torch.Tensor, w: torch.Tensor,
+             b: torch.Tensor, S: int, eps: float) -> torch.Tensor:
+    """BERT embeddings: LayerNorm(word[ids] + pos[t % S] + type0) for ids [B, S] -> [B*S, H]."""
+    ext = _native(word)
+    if ext is None:
+        return ref.embed_ln(ids, word, pos, type0, w, b, S, eps)
+    ids = ids.reshape(-1).to(torch.int32).contiguous()
+    out = torch.empty((ids.numel(), word.shape[1]), dtype=word.dtype, device=word.device)
+    ext.embed_ln(ids, word, pos, type0, w, b, out, int(S), float(eps))
+    return out
+
+
 def mean_pool_l2(x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
     ext = _native(x)
     if ext is None:

@@ -51,7 +51,7 @@ _TG_SPLITS = (1, 2, 3, 4, 6, 8)
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
 WS_COUNTERS = 1 << 16
 
-EPI_PLAIN, EPI_RESADD, EPI_QKV, EPI_SWIGLU = 0, 1, 2, 3
+EPI_PLAIN, EPI_RESADD, EPI_QKV, EPI_SWIGLU, EPI_GELU = 0, 1, 2, 3, 4
 
 _OWNER: contextvars.ContextVar = contextvars.ContextVar("dllm_gemm_ws_owner", default=None)
 
@@ -201,7 +201,7 @@ def _run_plan(plan, x, w, swiglu, out):
 
 
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
-           pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0):
+           pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None):
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
@@ -212,7 +212,7 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
         floats, tiles = _need_tg(M, N, K, bm, bn, sp, ks)
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
-              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d))
+              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias)
 
 
 def ref_silu_mul(gu):
@@ -276,7 +276,7 @@ def linear_swiglu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # Two implementations of each fused op: the tgemm epilogue (one launch), or hipBLASLt's GEMM core
 # followed by the same epilogue as a standalone kernel (qkv_post / res_add_ssq / swiglu_post).
 # The autotuner records, per decode bucket and shape, which is faster (the standalone epilogue
-# is charged POST_US); shapes it never saw (prefill chunks above MAX_M) use the vendor core,
+# is charged its measured time, _post_us; POST_US only where it cannot be measured); shapes it never saw (prefill chunks above MAX_M) use the vendor core,
 # which wins at large M (profiles/r2_tgemm_tune.md).
 POST_US = 3.0
 
@@ -315,8 +315,7 @@ def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_
     sums of the new residual's squares into ``ssq_out[:slots]``; returns ``slots``."""
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if M and use_vendor_core(M, N, K):
-        _native(x).res_add_ssq(F.linear(x, w), residual, ssq_out[0])
-        return 1
+        return int(_native(x).res_add_ssq(F.linear(x, w), residual, ssq_out))
     plan = tg_plan(M, N, K)
     if M:
         _tgemm(_native(x), x, w, EPI_RESADD, plan, y=residual, ssq_out=ssq_out)
@@ -337,10 +336,41 @@ def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: in
     return act
 
 
-def res_add_ssq(h: Optional[torch.Tensor], r: torch.Tensor, ssq: torch.Tensor) -> None:
-    """``r += h`` in place (h may be None) and ``ssq[m] = sum(r[m]^2)`` (one slot)."""
-    if r.shape[0]:
-        _native(r).res_add_ssq(h, r, ssq)
+def res_add_ssq(h: Optional[torch.Tensor], r: torch.Tensor, ssq: torch.Tensor) -> int:
+    """``r += h`` in place (h may be None) and the row sums of ``r^2``: ``ssq`` [M] gets the full
+    sum, ``ssq`` [slots, >= M] partial sums over column slices.  Returns the slots written."""
+    return int(_native(r).res_add_ssq(h, r, ssq))
+
+
+# ----------------------------------------------------------------------------- encoder (bias) ops
+
+def _enc_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return x.is_cuda and w.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+
+
+def linear_bias(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, gelu: bool = False) -> torch.Tensor:
+    """``x . w^T + bias`` (optionally followed by erf-GELU) in one tgemm launch (bias / GELU
+    epilogue): the router encoder's QKV and FFN-up projections."""
+    if not _enc_ok(x, w):
+        y = F.linear(x, w, bias)
+        return ref.gelu(y) if gelu else y
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if M:
+        _tgemm(_native(x), x, w, EPI_GELU if gelu else EPI_PLAIN, tg_plan(M, N, K), y=y, bias=bias)
+    return y
+
+
+def linear_bias_residual(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+    """``residual += x . w^T + bias`` in place (tgemm residual epilogue with bias; bf16 rounding of
+    the projection before the add, as F.linear followed by an add); returns ``residual``."""
+    if not _enc_ok(x, w):
+        residual.copy_((F.linear(x, w, bias).float() + residual.float()).to(residual.dtype))
+        return residual
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    if M:
+        _tgemm(_native(x), x, w, EPI_RESADD, tg_plan(M, N, K), y=residual, bias=bias)
+    return residual
 
 
 def max_slots(N: int) -> int:
@@ -371,6 +401,19 @@ def _time(fn, iters=24) -> float:
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) * 1000.0 / iters
+
+
+def _post_us(M: int, N: int, dev) -> float:
+    """Measured cost of the standalone epilogue a vendor-core fused op adds: one pass reading two
+    [M, N] bf16 operands and writing one (res_add_ssq; qkv_post / swiglu_post move the same or
+    fewer bytes).  Charged to hipBLASLt when choosing the fused op's core."""
+    if N % 8:
+        return POST_US
+    y = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    r = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    ssq = torch.empty(max_slots(N), M, dtype=torch.float32, device=dev)
+    ext = _native(y)
+    return _time(lambda i: ext.res_add_ssq(y, r, ssq))
 
 
 def _plan_key(k) -> str:
@@ -481,16 +524,20 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 _P.plans[key] = best
                 _P.timings[key] = {str(c): round(t, 2) for c, t in res.items()}
             tgc = [c for c in res if c[0] == "tg"]
+            post = None
             if need_tg and tgc:
                 best_tg = min(tgc, key=res.get)
                 _P.tg_plans[tkey] = best_tg[1:]
-                _P.fused_core[tkey] = "tg" if res[best_tg] <= res[("blas",)] + POST_US else "blas"
+                post = _post_us(M, N, dev)
+                _P.fused_core[tkey] = "tg" if res[best_tg] <= res[("blas",)] + post else "blas"
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
                       for k in ("gemv", "skinny", "lds", "mm", "tg")}
                 extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
                 top = sorted(tgc, key=res.get)[:4]
                 extra += " | tg top: " + " ".join(f"{c[1:]}:{res[c]:.1f}" for c in top)
+                if post is not None:
+                    extra += f" | post {post:.1f}us -> core {_P.fused_core[tkey]}"
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
                       f"({N * K * 2 / res[best] / 1e3:.0f} GB/s, {2 * M * N * K / res[best] / 1e6:.0f} TF/s; "
                       f"blas {res[('blas',)]:.1f}us; {extra})", flush=True)

@@ -124,6 +124,28 @@ def gelu(x):
     return torch.nn.functional.gelu(x.float()).to(x.dtype)
 
 
+def encoder_attention(qkv, lens, B, S, nh, d, scale):
+    """Bidirectional attention of a padded batch: qkv [B*S, 3 nh d] -> [B*S, nh d]; keys >= lens[b]
+    masked (csrc/kernels/encoder.hip)."""
+    x = qkv.float().view(B, S, 3, nh, d).permute(2, 0, 3, 1, 4)   # [3, B, nh, S, d]
+    q, k, v = x[0], x[1], x[2]
+    s = (q @ k.transpose(-1, -2)) * scale
+    keymask = torch.arange(S, device=qkv.device)[None, :] < lens.to(qkv.device).long()[:, None]
+    s = s.masked_fill(~keymask[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, dim=-1).nan_to_num(0.0)
+    o = (p @ v).permute(0, 2, 1, 3).reshape(B * S, nh * d)
+    return o.to(qkv.dtype)
+
+
+def embed_ln(ids, word, pos, type0, w, b, S, eps):
+    """LayerNorm(word[ids] + pos[t % S] + type0) for flattened [B*S] ids (csrc/kernels/encoder.hip)."""
+    T = ids.numel()
+    p = pos[:S].float().repeat(T // S, 1)
+    x = word[ids.long().reshape(-1)].float() + p + type0.float()
+    y = torch.nn.functional.layer_norm(x, (x.shape[-1],), w.float(), b.float(), eps)
+    return y.to(word.dtype)
+
+
 def mean_pool_l2(x, lens):
     B, S, H = x.shape
     m = (torch.arange(S)[None, :].to(x.device) < lens.to(x.device)[:, None]).float()

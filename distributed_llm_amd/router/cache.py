@@ -147,7 +147,14 @@ class EmbeddingIndex:
         self.device = device
         self._free: List[int] = []
         self._next = 0
+        # context key -> small int id stored per slot; ids are reference-counted by the slots that
+        # hold them and recycled when the last slot goes (TTL / LRU eviction, replacement), so a
+        # long-running server does not keep one entry per routed turn forever
         self._ctx_ids: Dict[str, int] = {}
+        self._ctx_key: Dict[int, str] = {}
+        self._ctx_refs: Dict[int, int] = {}
+        self._free_cids: List[int] = []
+        self._slot_cid: Dict[int, int] = {}
         self._alloc(capacity)
 
     def _alloc(self, capacity: int) -> None:
@@ -172,8 +179,24 @@ class EmbeddingIndex:
     def ctx_id(self, key: str) -> int:
         i = self._ctx_ids.get(key)
         if i is None:
-            i = self._ctx_ids[key] = len(self._ctx_ids)
+            i = self._free_cids.pop() if self._free_cids else len(self._ctx_ids)
+            self._ctx_ids[key] = i
+            self._ctx_key[i] = key
+            self._ctx_refs[i] = 0
         return i
+
+    def _release(self, slot: int) -> None:
+        cid = self._slot_cid.pop(slot, None)
+        if cid is None:
+            return
+        self._ctx_refs[cid] -= 1
+        if self._ctx_refs[cid] == 0:
+            del self._ctx_refs[cid]
+            del self._ctx_ids[self._ctx_key.pop(cid)]
+            self._free_cids.append(cid)
+
+    def num_contexts(self) -> int:
+        return len(self._ctx_ids)
 
     def put(self, vec: np.ndarray, context_key: str, slot: int = -1) -> int:
         if slot < 0:
@@ -186,7 +209,10 @@ class EmbeddingIndex:
                 self._next += 1
         v = np.asarray(vec, dtype=np.float32).reshape(-1)
         n = float(np.linalg.norm(v))
+        self._release(slot)          # a replaced slot drops its old context reference
         cid = self.ctx_id(context_key)
+        self._ctx_refs[cid] += 1
+        self._slot_cid[slot] = cid
         if self.device is None:
             self.table[slot] = v
             self.norms[slot] = n
@@ -202,12 +228,17 @@ class EmbeddingIndex:
         if slot < 0:
             return
         self.ctx[slot] = -1
+        self._release(slot)
         self._free.append(slot)
 
     def clear(self) -> None:
         self._free.clear()
         self._next = 0
         self._ctx_ids.clear()
+        self._ctx_key.clear()
+        self._ctx_refs.clear()
+        self._free_cids.clear()
+        self._slot_cid.clear()
         self.ctx[:] = -1
 
     def best(self, q: Any, context_key: str, threshold: float) -> Tuple[int, float]:

@@ -10,8 +10,8 @@ Two implementations:
     character trigrams into 384 dims, L2-normalised.  No weights needed; lexical overlap
     gives meaningful cosine similarities, so it is the default for CPU runs and tests.
   * ``MiniLMEmbedder`` — the MiniLM-L6 encoder architecture (6 layers, H=384, 12 heads,
-    mean-pool + L2) executed on the GPU by ``models.minilm`` with the HIP LayerNorm / GELU /
-    mean-pool kernels.  Loads real weights from a safetensors file when
+    mean-pool + L2) executed on the GPU by ``models.minilm`` entirely on our HIP kernels
+    (embedding+LN, bias/GELU/residual GEMM epilogues, encoder attention, LayerNorm, pooling).  Loads real weights from a safetensors file when
     ``DLLM_MINILM_WEIGHTS`` points at one, else random-init with a fixed seed (timing-realistic,
     semantically meaningless — say so when quoting semantic accuracy).
 """
@@ -147,6 +147,24 @@ def get_embedder(model_name: str = "all-MiniLM-L6-v2", device: Optional[str] = N
             emb = MiniLMEmbedder(device=dev) if kind == "minilm" else HashEmbedder()
             _REGISTRY[key] = emb
     return emb
+
+
+def encoder_stats() -> Dict[str, float]:
+    """Summed per-text memo counters of the GPU encoders in the registry (hash embedders have no
+    kernels to report): lookups, hits, texts actually run through the encoder."""
+    tot = {"lookups": 0, "hits": 0, "encoded_texts": 0}
+    kinds = []
+    with _REG_LOCK:
+        embs = list(_REGISTRY.values())
+    for e in embs:
+        kinds.append(e.name)
+        if isinstance(e, MiniLMEmbedder):
+            st = e.model.memo_stats()
+            for k in tot:
+                tot[k] += st[k]
+            tot["memo_enabled"] = st["memo_enabled"]
+    tot["kinds"] = sorted(set(kinds))
+    return tot
 
 
 def clear_registry() -> None:

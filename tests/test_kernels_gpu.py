@@ -261,6 +261,21 @@ def test_sample_rows_crowded_ties_and_distribution():
     assert (freq - want).abs().max() < 0.02
 
 
+def test_sample_rows_tie_flood_keeps_strictly_better_candidates():
+    """more ties AT the top-k threshold than the candidate list holds must never push
+    out a strictly better logit.  10 clear winners sit at the END of the vocab (appended last by
+    the scan) behind 3000 exact ties; with top_p = 0.5 the nucleus lies inside the winners."""
+    B, V = 64, 32000
+    lg = torch.full((B, V), -4.0, device=DEV)
+    lg[:, 1000:4000] = 1.0
+    lg[:, V - 10:] = 5.0
+    lg = lg.to(torch.bfloat16)
+    p = lambda x: torch.full((B,), x, device=DEV)
+    a = ops.sample_rows(lg, p(1.0), p(0.5), torch.full((B,), 50, dtype=torch.int32, device=DEV),
+                        torch.tensor([17], dtype=torch.int32, device=DEV)).cpu()
+    assert bool((a >= V - 10).all()), a
+
+
 def test_cosine_kernels():
     torch.manual_seed(9)
     q, c = torch.randn(5, 384, device=DEV), torch.randn(7, 384, device=DEV)

@@ -288,3 +288,21 @@ def test_hash_embedder_deterministic_unit_norm():
     b = HashEmbedder().encode(["hello world", "what is 2+2"])
     assert a.shape == (2, 384) and np.allclose(a, b)
     assert np.allclose(np.linalg.norm(a, axis=1), 1.0, atol=1e-5)
+
+
+def test_cache_context_ids_are_reclaimed_on_eviction():
+    """context ids must not accumulate one per routed turn — LRU eviction of the last
+    entry of a context drops its id, and ids are recycled."""
+    from distributed_llm_amd.router.cache import QueryCache
+    c = QueryCache(max_size=8, ttl_seconds=300, similarity_threshold=0.85, use_semantic=True)
+    rng = np.random.default_rng(0)
+    for i in range(500):   # every turn has its own context key (per-turn prefix hash)
+        c.insert(f"query {i}", f"ctx-{i}", "nano", q_emb=rng.standard_normal(384).astype(np.float32))
+    idx = c._index
+    assert 1 <= idx.num_contexts() <= 8
+    assert max(idx._ctx_ids.values()) < 16
+    # the live entries still match within their own context
+    q = rng.standard_normal(384).astype(np.float32)
+    c.insert("query x", "ctx-live", "orin", q_emb=q)
+    assert c.lookup("query x?", "ctx-live", q_emb=q) is not None
+    assert c.lookup("query x?", "ctx-0", q_emb=q) is None

@@ -133,6 +133,21 @@ def test_res_add_ssq():
     torch.testing.assert_close(ssq, (want.float() ** 2).sum(1), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("H,slots", [(2048, 8), (2048, 3), (320, 5), (4096, 64)])
+def test_res_add_ssq_sliced(H, slots):
+    """Partial sums over column slices ([slots, M] form): the slices cover H exactly once."""
+    torch.manual_seed(H + slots)
+    h, r = _rnd(37, H), _rnd(37, H)
+    r0 = r.clone()
+    ssq = torch.full((slots, 40), float("nan"), device="cuda")
+    n = ops.gemm.res_add_ssq(h, r, ssq)
+    cw = math.ceil(math.ceil(H / slots) / 512) * 512   # whole 512-column wave passes per slice
+    assert n == math.ceil(H / cw) and 1 <= n <= slots
+    want = (h.float() + r0.float()).to(torch.bfloat16)
+    assert torch.equal(r, want)
+    torch.testing.assert_close(ssq[:n, :37].sum(0), (want.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("core", ["tg", "blas"])
 def test_fused_ops_both_cores(core, monkeypatch):
     """The fused decoder ops give the same results through the tgemm epilogue and through the
