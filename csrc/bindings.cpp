@@ -47,6 +47,12 @@ int dllm_car_close_handle(void*);
 int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, hipStream_t);
+int dllm_decode_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*, void*,
+                          float*, float*, int*, const int*, const int*, int, int, int, int, int, int, int, float,
+                          hipStream_t);
+int dllm_moe_max_tiles_bm(int, int, int);
+int dllm_moe_ffn_tg(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int,
+                    int*, int*, int*, void*, void*, void*, const int*, hipStream_t);
 int dllm_encoder_attention(const void*, const int*, void*, int, int, int, int, float, hipStream_t);
 int dllm_embed_ln(const int*, const void*, const void*, const void*, const void*, const void*, void*, int, int, int, int,
                   float, hipStream_t);
@@ -469,6 +475,49 @@ void mm_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t nt, int6
 // Mixtral-style MoE FFN: x [T, H] bf16, ids [T, k] int32, wts [T, k] f32, w13 [E, 2I, H], w2 [E, H, I]
 // -> out [T, H] bf16 (partial sum over this rank's I shard under TP).  Workspace from torch's
 // caching allocator, so the call is graph-capturable.
+// grouped-tgemm MoE (csrc/kernels/moe.hip dllm_moe_ffn_tg): w13 interleaved per 16-row group
+void moe_ffn_tg(torch::Tensor x, torch::Tensor ids, torch::Tensor wts, torch::Tensor w13, torch::Tensor w2,
+                torch::Tensor out, std::vector<int64_t> plan) {
+  check_bf16(x, "x");
+  check_i32(ids, "ids");
+  check_f32(wts, "wts");
+  check_bf16(w13, "w13");
+  check_bf16(w2, "w2");
+  check_bf16(out, "out");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && out.is_contiguous(), "x rows 16-B aligned");
+  TORCH_CHECK(w13.dim() == 3 && w2.dim() == 3 && w13.is_contiguous() && w2.is_contiguous(), "w13/w2 [E, N, K]");
+  const int64_t T = x.size(0), H = x.size(1), E = w13.size(0), I = w13.size(1) / 2;
+  TORCH_CHECK(w13.size(2) == H && w2.size(0) == E && w2.size(1) == H && w2.size(2) == I, "expert weight shapes");
+  TORCH_CHECK(H % 64 == 0 && I % 64 == 0 && E <= 64, "H, I multiples of 64; E <= 64");
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) == T && wts.sizes() == ids.sizes() && ids.is_contiguous() &&
+                  wts.is_contiguous(), "ids/wts [T, k]");
+  TORCH_CHECK(out.size(0) == T && out.size(1) == H, "out shape");
+  TORCH_CHECK(plan.size() == 9, "plan: bm, bn13, stages13, ks13, nw13, bn2, stages2, ks2, nw2");
+  const int bm = (int)plan[0];
+  for (int g = 0; g < 2; ++g) {
+    const int bn = (int)plan[1 + 4 * g], st = (int)plan[2 + 4 * g], ks = (int)plan[3 + 4 * g], nw = (int)plan[4 + 4 * g];
+    TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)) && (st == 2 || st == 3) &&
+                    (bm == 64 || bm == 128 || (bm == 256 && nw == 8)) &&
+                    (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) && st * ks * (bm + bn) * 128 <= 150 * 1024,
+                "moe plan tile / ring size");
+    TORCH_CHECK((g == 0 ? H : I) % (64 * ks) == 0, "K % (64 ks)");
+  }
+  const int k = ids.size(1);
+  auto iopt = ids.options();
+  const int P = (int)(T * k), mt = dllm_moe_max_tiles_bm(P, (int)E, bm);
+  auto perm = torch::empty({std::max(P, 1)}, iopt);
+  auto inv = torch::empty({std::max(P, 1)}, iopt);
+  auto tiles = torch::empty({4 * mt + 1}, iopt);
+  auto act = torch::empty({std::max(P, 1), I}, x.options());
+  auto y = torch::empty({std::max(P, 1), H}, x.options());
+  int pl[9];
+  for (int i = 0; i < 9; ++i) pl[i] = (int)plan[i];
+  ok(dllm_moe_ffn_tg(x.data_ptr(), x.stride(0), T, (int)H, ids.data_ptr<int>(), wts.data_ptr<float>(), k, (int)E,
+                     w13.data_ptr(), w2.data_ptr(), (int)I, perm.data_ptr<int>(), inv.data_ptr<int>(),
+                     tiles.data_ptr<int>(), act.data_ptr(), y.data_ptr(), out.data_ptr(), pl, stream()),
+     "moe_ffn_tg");
+}
+
 void moe_ffn(torch::Tensor x, torch::Tensor ids, torch::Tensor wts, torch::Tensor w13, torch::Tensor w2,
              torch::Tensor out) {
   check_bf16(x, "x");
@@ -700,6 +749,64 @@ int64_t res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tens
   return n;
 }
 
+// decode attention, wave-per-unit (csrc/kernels/decode_attn.hip): one query token per sequence
+void decode_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
+                      torch::Tensor qstart, torch::Tensor ctx, torch::Tensor tile_seq, torch::Tensor out,
+                      c10::optional<torch::Tensor> part_o, c10::optional<torch::Tensor> part_ml,
+                      c10::optional<torch::Tensor> counters, int64_t splits, double scale,
+                      c10::optional<torch::Tensor> split_len, c10::optional<torch::Tensor> items, int64_t grid_wgs) {
+  check_bf16(q, "q");
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  check_bf16(out, "out");
+  for (auto* t : {&block_tables, &qstart, &ctx, &tile_seq}) check_i32(*t, "attention metadata");
+  TORCH_CHECK(q.dim() == 3 && q.is_contiguous() && out.is_contiguous() && out.sizes() == q.sizes(), "q/out [T, nq, d]");
+  const int nq = q.size(1), d = q.size(2);
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && kc.size(2) == 16 && kc.size(3) == d &&
+                  vc.size(1) == kc.size(1) && vc.size(2) == d && vc.size(3) == 16,
+              "cache layout: K [blocks, nkv, 16, d], V [blocks, nkv, d, 16]");
+  const int nkv = kc.size(1);
+  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group <= 16");
+  TORCH_CHECK(d == 64 || d == 96 || d == 128, "head_dim must be 64, 96 or 128");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.is_contiguous(), "block_tables [num_seqs, max_blocks]");
+  const int num_seqs = block_tables.size(0);
+  TORCH_CHECK(qstart.numel() == num_seqs && ctx.numel() == num_seqs, "seq metadata len");
+  const int num_tiles = tile_seq.numel();
+  TORCH_CHECK(splits >= 1 && splits <= 255, "splits");
+  float* po = nullptr;
+  float* pml = nullptr;
+  int* cnt = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(counters.has_value() && part_o.has_value() && part_ml.has_value(), "split-K needs workspaces");
+    check_i32(*counters, "counters");
+    check_f32(*part_o, "part_o");
+    check_f32(*part_ml, "part_ml");
+    TORCH_CHECK(counters->numel() >= (int64_t)num_tiles * nkv &&
+                    part_o->numel() >= (int64_t)num_tiles * nkv * splits * 16 * d &&
+                    part_ml->numel() >= (int64_t)num_tiles * nkv * splits * 16 * 2,
+                "workspace too small");
+    po = part_o->data_ptr<float>();
+    pml = part_ml->data_ptr<float>();
+    cnt = counters->data_ptr<int>();
+  }
+  const int* sl = nullptr;
+  if (split_len.has_value()) {
+    check_i32(*split_len, "split_len");
+    sl = split_len->data_ptr<int>();
+  }
+  const int* it = nullptr;
+  if (items.has_value()) {
+    check_i32(*items, "items");
+    TORCH_CHECK(items->numel() >= 1 && grid_wgs >= 1, "items: work list and a grid");
+    it = items->data_ptr<int>();
+  }
+  ok(dllm_decode_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
+                           qstart.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(), out.data_ptr(), po,
+                           pml, cnt, sl, it, (int)grid_wgs, num_tiles, nq, nkv, d, block_tables.size(1), (int)splits,
+                           (float)scale, stream()),
+     "decode_attention");
+}
+
 // router encoder (csrc/kernels/encoder.hip): bidirectional attention over a padded batch
 void encoder_attention(torch::Tensor qkv, torch::Tensor lens, torch::Tensor out, int64_t B, int64_t S, int64_t nh,
                        int64_t d, double scale) {
@@ -735,8 +842,10 @@ void embed_ln(torch::Tensor ids, torch::Tensor word, torch::Tensor pos, torch::T
 
 PYBIND11_MODULE(_hip_kernels, m) {
   m.def("encoder_attention", &encoder_attention);
+  m.def("decode_attention", &decode_attention);
   m.def("embed_ln", &embed_ln);
   m.def("moe_ffn", &moe_ffn);
+  m.def("moe_ffn_tg", &moe_ffn_tg);
   m.def("tgemm", &tgemm);
   m.def("res_add_ssq", &res_add_ssq);
   m.def("qkv_post", &qkv_post);

@@ -13,7 +13,17 @@
 // B = 32 k x 16 weight rows (same pattern on the [N, K] weight), C row (lane>>4)*4+r, col lane&15.
 // Tiles are MT = 32 rows (two MFMA row groups share every weight load); blocks past the device
 // tile count exit immediately.  Weights stream with 4 k-steps of loads in flight per wave.
+//
+// moe_ffn_tg (the default on GPU): the same routing with BM-row tiles, then BOTH expert GEMMs on
+// the LDS-tiled MFMA GEMM of tgemm.hip in grouped mode — global_load_lds ring, XOR-swizzled LDS,
+// rows of the first GEMM gathered through perm by the staging addresses, the expert's weight
+// slice picked per row tile, SwiGLU in the epilogue over gate/up rows interleaved in 16-row
+// groups (models.llama.interleave_w13) — and a combine that applies the gate weights while
+// summing each token's k expert rows (inverse permutation, fixed order, no atomics).
 #include "common.h"
+#include "tgemm_args.h"
+
+extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, int nw, int epi, hipStream_t stream);
 
 namespace {
 constexpr int MT = 32;
@@ -21,7 +31,8 @@ constexpr int MT = 32;
 __global__ void __launch_bounds__(1024) moe_route_kernel(const int* __restrict__ ids, int P, int E, int max_tiles,
                                                          int* __restrict__ perm, int* __restrict__ tile_e,
                                                          int* __restrict__ tile_r0, int* __restrict__ tile_n,
-                                                         int* __restrict__ n_tiles) {
+                                                         int* __restrict__ n_tiles, int mt = MT,
+                                                         int* __restrict__ inv = nullptr) {
   __shared__ int cnt[64], off[65], cur[64];
   const int tid = threadIdx.x;
   if (tid < 64) { cnt[tid] = 0; cur[tid] = 0; }
@@ -33,17 +44,39 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const int* __restrict__
     for (int e = 0; e < E; ++e) off[e + 1] = off[e] + cnt[e];
     int nt = 0;
     for (int e = 0; e < E; ++e)
-      for (int r = 0; r < cnt[e] && nt < max_tiles; r += MT, ++nt) {
+      for (int r = 0; r < cnt[e] && nt < max_tiles; r += mt, ++nt) {
         tile_e[nt] = e;
         tile_r0[nt] = off[e] + r;
-        tile_n[nt] = min(MT, cnt[e] - r);
+        tile_n[nt] = min(mt, cnt[e] - r);
       }
     *n_tiles = nt;
   }
   __syncthreads();
   for (int p = tid; p < P; p += blockDim.x) {
     const int e = min(max(ids[p], 0), E - 1);
-    perm[off[e] + atomicAdd(&cur[e], 1)] = p;
+    const int pos = off[e] + atomicAdd(&cur[e], 1);
+    perm[pos] = p;
+    if (inv != nullptr) inv[p] = pos;
+  }
+}
+
+// out[t] = sum_j wts[t k + j] * y[inv[t k + j]]  (y: expert outputs in expert-sorted row order)
+__global__ void moe_combine_perm_kernel(const u16* __restrict__ y, const int* __restrict__ inv,
+                                        const float* __restrict__ wts, int k, int H, long T, u16* __restrict__ out) {
+  const long n8 = T * (H / 8);
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
+    const long t = v / (H / 8);
+    const int h = (int)(v % (H / 8)) * 8;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const long p = t * k + j;
+      float f[8];
+      unpack8(ld16(y + (long)inv[p] * H + h), f);
+      const float w = wts[p];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += w * f[q];
+    }
+    st16(out + t * (long)H + h, pack8(s));
   }
 }
 
@@ -236,5 +269,42 @@ extern "C" int dllm_moe_ffn(const void* x, long x_stride, long T, int H, const i
   long g = (n4 + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(moe_combine_kernel, dim3((int)g), dim3(256), 0, stream, y, k, H, T, (u16*)out);
+  return (int)hipGetLastError();
+}
+
+// Tile-list size for BM-row tiles: every expert may leave one partial tile.
+extern "C" int dllm_moe_max_tiles_bm(int P, int E, int bm) { return (P + bm - 1) / bm + E; }
+
+// plans: {bm, bn13, stages13, ks13, nw13, bn2, stages2, ks2, nw2}; w13 interleaved [E, 2I, H]
+// (16 gate rows, 16 up rows, ...), w2 [E, H, I]; scratch: perm/inv [P], tiles [4 * max_tiles + 1],
+// act [P, I], y [P, H] (bf16).
+extern "C" int dllm_moe_ffn_tg(const void* x, long x_stride, long T, int H, const int* ids, const float* wts, int k,
+                               int E, const void* w13, const void* w2, int I, int* perm, int* inv, int* tiles,
+                               void* act, void* y, void* out, const int* plan, hipStream_t stream) {
+  if (E < 1 || E > 64 || k < 1 || H % 64 != 0 || I % 64 != 0 || x_stride % 8) return -1;
+  if (T == 0) return 0;
+  const int bm = plan[0];
+  const int P = (int)(T * k);
+  const int max_tiles = (P + bm - 1) / bm + E;
+  int *te = tiles, *tr = tiles + max_tiles, *tn = tiles + 2 * max_tiles, *nt = tiles + 3 * max_tiles;
+  hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(1024), 0, stream, ids, P, E, max_tiles, perm, te, tr, tn, nt, bm,
+                     inv);
+  dllm::GemmArgs g{};
+  g.A = (const uint16_t*)x; g.lda = x_stride; g.W = (const uint16_t*)w13; g.Y = (uint16_t*)act; g.ldy = I;
+  g.M = max_tiles * bm; g.N = 2 * I; g.K = H; g.kchunk = H; g.splits = 1;
+  g.g_tiles = tiles; g.g_max = max_tiles; g.g_perm = perm; g.g_k = k; g.g_wstride = 2L * I * H;
+  int rc = dllm_tgemm(&g, bm, plan[1], plan[2], plan[3], plan[4], dllm::EPI_SWIGLU, stream);
+  if (rc) return 1000 + rc;
+  dllm::GemmArgs d{};
+  d.A = (const uint16_t*)act; d.lda = I; d.W = (const uint16_t*)w2; d.Y = (uint16_t*)y; d.ldy = H;
+  d.M = max_tiles * bm; d.N = H; d.K = I; d.kchunk = I; d.splits = 1;
+  d.g_tiles = tiles; d.g_max = max_tiles; d.g_perm = nullptr; d.g_k = 1; d.g_wstride = (long)H * I;
+  rc = dllm_tgemm(&d, bm, plan[5], plan[6], plan[7], plan[8], dllm::EPI_PLAIN, stream);
+  if (rc) return 2000 + rc;
+  long n8 = T * (H / 8);
+  long gr = (n8 + 255) / 256;
+  if (gr > 4096) gr = 4096;
+  hipLaunchKernelGGL(moe_combine_perm_kernel, dim3((int)gr), dim3(256), 0, stream, (const u16*)y, inv, wts, k, H, T,
+                     (u16*)out);
   return (int)hipGetLastError();
 }

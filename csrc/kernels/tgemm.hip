@@ -88,7 +88,8 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / NWN, wn = wave % NWN;
-  const int M = a.M, N = a.N, K = a.K, S = a.splits;
+  const int N = a.N, K = a.K, S = a.splits;
+  int M = a.M;
   const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
   const int nwg = mt * nt * S;
   // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD -> contiguous logical ids)
@@ -96,7 +97,15 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int split = wgid % S, rest = wgid / S;
   const int m_tile = rest % mt, n_tile = rest / mt;
-  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  int m0 = m_tile * BM;
+  const int n0 = n_tile * BN;
+  const u16* Wb = a.W;
+  if (a.g_tiles != nullptr) {  // grouped (MoE): row tile from the device list (block-uniform exit)
+    if (m_tile >= a.g_tiles[3 * a.g_max]) return;
+    m0 = a.g_tiles[a.g_max + m_tile];
+    M = m0 + a.g_tiles[2 * a.g_max + m_tile];
+    Wb = a.W + (long)a.g_tiles[m_tile] * a.g_wstride;
+  }
   const int kbeg = split * a.kchunk;
   const int nk = max(0, (min(K, kbeg + a.kchunk) - kbeg) / KSTEP);
 
@@ -123,12 +132,14 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
     const int r = 8 * (wave * GA + j) + srow;
-    a_src[j] = a.A + (long)min(m0 + r, M - 1) * a.lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+    const int row = min(m0 + r, M - 1);
+    const long arow = a.g_perm != nullptr ? (long)(a.g_perm[row] / a.g_k) : (long)row;  // MoE: gathered rows
+    a_src[j] = a.A + arow * a.lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
   }
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int r = 8 * (wave * GB + j) + srow;
-    b_src[j] = a.W + (long)min(n0 + r, N - 1) * K + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+    b_src[j] = Wb + (long)min(n0 + r, N - 1) * K + kbeg + 8 * (spos ^ ((r >> 1) & 7));
   }
   auto issue = [&](int t) {
 #pragma unroll
@@ -575,6 +586,7 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
   if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
   if (a.N % 8 || (a.Y && a.ldy % 8)) return -7;  // 16-B output row vectors
   if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
+  if (a.g_tiles != nullptr && (a.splits != 1 || a.M != a.g_max * bm || epi == EPI_QKV || a.ssq_in)) return -10;
   if (stages != 2 && stages != 3) return -5;
   switch (epi) {
     case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, ks, nw, a, stream);

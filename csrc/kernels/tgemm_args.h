@@ -32,6 +32,15 @@ struct GemmArgs {
   int nq, nkv, d;
   // PLAIN / RESADD / GELU: bias[n] added to the product before the epilogue op (null: none)
   const uint16_t* bias;
+  // Grouped mode (MoE experts, csrc/kernels/moe.hip): a device tile list g_tiles
+  // [expert | first row | rows] x g_max, then the live tile count at g_tiles[3 * g_max].  Row tile
+  // i covers rows [first, first + rows) of Y (and of A, or A rows g_perm[r] / g_k: a gather), and
+  // multiplies by W + expert * g_wstride.  M must be g_max * BM; splits 1.
+  const int* g_tiles;
+  int g_max;
+  const int* g_perm;
+  int g_k;
+  long g_wstride;
 };
 enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_GELU = 4 };
 }  // namespace dllm

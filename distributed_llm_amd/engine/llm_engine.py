@@ -263,6 +263,10 @@ class LLMEngine:
     # MI355X, TinyLlama) it cut B=1 from 1.14 to 0.89 ms and B=16 from 1.51 to 1.29 ms vs the
     # static split grid (a kernel-only sweep had B=16-64 about even)
     ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "1"))
+    # Alternative decode kernel (csrc/kernels/decode_attn.hip, one wave per unit, 1024 workgroups,
+    # 4096-unit list): measured equal at best, slower at small batch (profiles/r2_decode_attention_
+    # microbench.md), so opt-in only
+    DECODE_WAVE = os.environ.get("DLLM_DECODE_ATTN", "paged") == "wave"
 
     def _use_worklist(self, bs: int) -> bool:
         return self.attn_worklist and bs >= self.ATTN_WL_MIN_BS
@@ -780,8 +784,8 @@ class LLMEngine:
         n_items = 0
         if self._use_worklist(bs):
             grid = self._attn_grid(bs)
-            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, self.ATTN_ITEMS_PER_WG * grid,
-                                  out=self.items_host)
+            target = 4096 if self.DECODE_WAVE else self.ATTN_ITEMS_PER_WG * grid
+            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target, out=self.items_host)
             n_items = 1 + 2 * int(self.items_host[0])
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)
@@ -868,7 +872,8 @@ class LLMEngine:
             return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart,
                             qlen=self.d_qlen, ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
                             last_idx=self.d_last[:bs], splits=self.max_splits, workspace=self.dec_ws,
-                            items=self.items_dev, grid_items=self._attn_grid(bs))
+                            items=self.items_dev, grid_items=1024 if self.DECODE_WAVE else self._attn_grid(bs),
+                            wave=self.DECODE_WAVE)
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
                         ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
                         last_idx=self.d_last[:bs], splits=self._decode_splits(bs), workspace=self.dec_ws,

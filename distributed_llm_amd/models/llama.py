@@ -53,6 +53,7 @@ class AttnMeta:
     items: Optional[torch.Tensor] = None       # decode: persistent attention work list (ops.decode_work_items)
     grid_items: int = 0                        # workgroups walking ``items``
     flash: bool = False                        # prefill: tile_seq/tile_tok0 are 128-row flash tiles
+    wave: bool = False                         # decode: wave-per-unit kernel (decode_attn.hip) over ``items``
 
 
 def qk_dim_order(d: int) -> torch.Tensor:
@@ -133,6 +134,14 @@ class LlamaModel:
         self.fused = self._fusable()
         if self.fused:
             self._fuse_weights()
+        # MoE experts on the grouped LDS-tiled GEMM (csrc/kernels/moe.hip moe_ffn_tg): gate/up rows
+        # of every expert interleaved in place for the SwiGLU epilogue
+        self.moe_tg = bool(cfg.is_moe and not self.moe_ep and self.device.type == "cuda" and ops.native_available()
+                           and cfg.hidden % 64 == 0 and self.I % 64 == 0 and os.environ.get("DLLM_MOE_TG", "1") == "1")
+        if self.moe_tg:
+            idx = gate_up_order(self.I).to(self.device)
+            for L in self.layers:
+                L["w13"] = L["w13"].index_select(1, idx).contiguous()
 
     # ------------------------------------------------------------------ fused layout
     def _fusable(self) -> bool:
@@ -152,15 +161,22 @@ class LlamaModel:
 
     def reference_layers(self) -> List[Dict[str, torch.Tensor]]:
         """Layer weights in the plain (unfused) layout, e.g. for a CPU reference forward."""
-        if not self.fused:
+        if not self.fused and not getattr(self, "moe_tg", False):
             return self.layers
         out = []
         for L in self.layers:
             R = {k: v for k, v in L.items() if k not in ("wqkv_f", "wgu_f")}
-            R["wqkv"] = unfuse_qkv_weight(L["wqkv_f"], L["ln1"], self.nq, self.nkv, self.d)
+            if "wqkv_f" in L:
+                R["wqkv"] = unfuse_qkv_weight(L["wqkv_f"], L["ln1"], self.nq, self.nkv, self.d)
             if "wgu_f" in L:
                 R["wgu"] = unfuse_gate_up_weight(L["wgu_f"], L["ln2"])
             out.append(R)
+        if self.moe_tg:
+            idx = gate_up_order(self.I).to(self.device)
+            for R, L in zip(out, self.layers):
+                w = torch.empty_like(L["w13"])
+                w[:, idx] = L["w13"]
+                R["w13"] = w
         return out
 
     # ------------------------------------------------------------------ weights
@@ -281,6 +297,8 @@ class LlamaModel:
         permutation + grouped expert GEMMs, no host sync, so decode steps stay graph-captured).
         Experts are TP-sharded along I; the caller all-reduces the partial sums."""
         ids, w = ops.moe_gate(F.linear(x, L["wgate"]).float(), self.cfg.experts_per_token)
+        if self.moe_tg:
+            return ops.moe_ffn_tg(x, ids, w, L["w13"], L["w2"])
         return ops.moe_ffn(x, ids, w, L["w13"], L["w2"])
 
     def _mlp_out(self, L, x: torch.Tensor) -> torch.Tensor:
@@ -300,6 +318,10 @@ class LlamaModel:
         if meta.flash:   # prefill: 128-row tiles, K/V staged once per workgroup (flash_prefill.hip)
             return ops.flash_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                        meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True)
+        if meta.wave:    # decode alternative: one wave per (sequence, kv head, split) unit
+            return ops.decode_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.ctx, meta.tile_seq,
+                                        scale=self.scale, splits=meta.splits, workspace=meta.workspace,
+                                        items=meta.items, grid_wgs=meta.grid_items)
         return ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,

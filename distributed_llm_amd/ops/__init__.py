@@ -202,6 +202,37 @@ def flash_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return o
 
 
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                     seq_qstart: torch.Tensor, seq_ctx: torch.Tensor, tile_seq: torch.Tensor,
+                     scale: Optional[float] = None, splits: int = 1,
+                     workspace: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
+                     items: Optional[torch.Tensor] = None, grid_wgs: int = 0,
+                     split_len: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode attention, one query token per sequence (csrc/kernels/decode_attn.hip): every wave
+    owns a (tile, kv head, key split) unit — a static grid of ``tiles x nkv x splits`` units, or
+    with ``items`` (:func:`decode_work_items`) a fixed grid of ``grid_wgs`` 4-wave workgroups
+    striding over the list.  Splits merge in-launch (last wave per (tile, kv head))."""
+    d = q.shape[-1]
+    scale = (1.0 / math.sqrt(d)) if scale is None else scale
+    ext = _native(q)
+    if ext is None:   # sequences named by a tile carry one query token, the others none
+        ql = torch.zeros_like(seq_ctx)
+        ts = tile_seq[tile_seq >= 0].long()
+        ql[ts] = 1
+        o = ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, ql, seq_ctx, scale, True)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    o = out if out is not None else torch.empty_like(q)
+    po = pml = cnt = None
+    if splits > 1:
+        po, pml, cnt = workspace
+    ext.decode_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_ctx, tile_seq, o, po, pml, cnt,
+                         int(splits), float(scale), split_len, items, int(grid_wgs))
+    return o
+
+
 def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,
                       out: Optional[np.ndarray] = None) -> np.ndarray:
     """Work list for persistent decode attention (one query token per tile, tiles in ``ctx`` order).
@@ -321,6 +352,30 @@ def moe_ffn(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13: torch.Te
         return ref.moe_ffn(x, ids, wts, w13, w2)
     out = torch.empty((x.shape[0], x.shape[1]), dtype=x.dtype, device=x.device)
     ext.moe_ffn(x, ids.to(torch.int32).contiguous(), wts.float().contiguous(), w13, w2, out)
+    return out
+
+
+MOE_PLANS = {  # (bm, bn13, stages13, ks13, nw13, bn2, stages2, ks2, nw2) by routed-pair count
+    "decode": (64, 128, 3, 1, 4, 64, 3, 1, 4),
+    "prefill": (128, 128, 3, 1, 8, 128, 3, 1, 8),
+}
+
+
+def moe_ffn_tg(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13i: torch.Tensor, w2: torch.Tensor,
+               plan: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
+    """Top-k expert FFN on the grouped LDS-tiled MFMA GEMM (csrc/kernels/moe.hip moe_ffn_tg):
+    ``w13i`` [E, 2I, H] with gate/up rows interleaved in 16-row groups (models.llama.gate_up_order),
+    w2 [E, H, I].  Routing, both GEMMs and the weighted combine stay on the device."""
+    ext = _native(x)
+    if ext is None:
+        from ..models.llama import gate_up_order
+        w13 = torch.empty_like(w13i)
+        w13[:, gate_up_order(w13i.shape[1] // 2)] = w13i
+        return ref.moe_ffn(x, ids, wts, w13, w2)
+    out = torch.empty((x.shape[0], x.shape[1]), dtype=x.dtype, device=x.device)
+    if plan is None:
+        plan = MOE_PLANS["decode" if x.shape[0] * ids.shape[1] <= 1024 else "prefill"]
+    ext.moe_ffn_tg(x, ids.to(torch.int32).contiguous(), wts.float().contiguous(), w13i, w2, out, list(plan))
     return out
 
 

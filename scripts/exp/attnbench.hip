@@ -138,7 +138,7 @@ int main(int argc, char** argv) {
   // persistent work-list mode (engine path): units of ~equal key counts, longest first
   int* ditems;
   CHECK(hipMalloc(&ditems, (1 + 2L * B * nkv * NSMAX) * 4));
-  const int cfgs[][2] = {{2048, 256}, {4096, 256}, {8192, 256}, {4096, 128}, {8192, 64}};
+  const int cfgs[][2] = {{512, 256}, {2048, 256}, {4096, 256}, {4096, 128}};
   for (auto& cf : cfgs) {
     const int target = cf[0], min_chunk = cf[1];
     long chunk = std::max<long>(min_chunk, (long)((tot * nkv + target - 1) / target));
@@ -152,6 +152,16 @@ int main(int argc, char** argv) {
     }
     it[0] = (int)((it.size() - 1) / 2);
     CHECK(hipMemcpy(ditems, it.data(), it.size() * 4, hipMemcpyHostToDevice));
+    {  // the engine's current path: attention.hip walking the same list with 512 workgroups
+      float ms = timeit([&] {
+        int r = dllm_paged_attention(q, kc, vc, bt, dqs, dql, dcx, dts, dtt, o1, po, pml, cnt, nullptr, ditems, 512, 0,
+                                     B, nq, nkv, d, maxb, NSMAX, 1, scale, 0);
+        if (r) { printf("paged wl rc %d\n", r); exit(1); }
+      });
+      printf("{\"exp\": \"attnbench\", \"kernel\": \"paged_wl\", \"B\": %d, \"C\": %d, \"var\": %d, \"d\": %d, "
+             "\"target\": %d, \"min_chunk\": %d, \"items\": %d, \"grid_wgs\": 512, \"us\": %.1f, \"TBps\": %.3f}\n",
+             B, (int)(tot / B), var, d, target, min_chunk, it[0], ms * 1000, bytes / (ms * 1e-3) / 1e12);
+    }
     for (int grid : {512, 1024}) {
       float ms = timeit([&] {
         int r = dllm_decode_attention(q, kc, vc, bt, dqs, dcx, dts, o2, po, pml, cnt, nullptr, ditems, grid, B, nq, nkv,
