@@ -356,9 +356,15 @@ def moe_ffn(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13: torch.Te
 
 
 MOE_PLANS = {  # (bm, bn13, stages13, ks13, nw13, bn2, stages2, ks2, nw2) by routed-pair count
-    "decode": (64, 128, 3, 1, 4, 64, 3, 1, 4),
-    "prefill": (128, 128, 3, 1, 8, 128, 3, 1, 8),
+    # measured at Mixtral shapes (profiles/r2_moe_microbench.md)
+    "decode": (64, 128, 3, 1, 4, 64, 3, 1, 4),        # P <= 128: weight streaming, 64-row tiles
+    "mid": (128, 128, 3, 1, 8, 128, 3, 1, 8),         # P <= 1024
+    "prefill": (256, 256, 2, 1, 8, 128, 3, 1, 8),     # large P: 256x256 tiles (weight reuse)
 }
+
+
+def moe_plan(pairs: int) -> Tuple[int, ...]:
+    return MOE_PLANS["decode" if pairs <= 128 else "mid" if pairs <= 1024 else "prefill"]
 
 
 def moe_ffn_tg(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13i: torch.Tensor, w2: torch.Tensor,
@@ -374,7 +380,7 @@ def moe_ffn_tg(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13i: torc
         return ref.moe_ffn(x, ids, wts, w13, w2)
     out = torch.empty((x.shape[0], x.shape[1]), dtype=x.dtype, device=x.device)
     if plan is None:
-        plan = MOE_PLANS["decode" if x.shape[0] * ids.shape[1] <= 1024 else "prefill"]
+        plan = moe_plan(x.shape[0] * ids.shape[1])
     ext.moe_ffn_tg(x, ids.to(torch.int32).contiguous(), wts.float().contiguous(), w13i, w2, out, list(plan))
     return out
 

@@ -1,5 +1,5 @@
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_decode_attn_gpu.py tests/test_tgemm_gpu.py -x -q -k "moe or engine_wave or fused_ops or res_add or qkv_rope" --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-rc=$?; tail -5 gpurun_out/gpu_tests.log; exit $rc
+timeout -k 10 600 python -u scripts/microbench.py --what moe > gpurun_out/moe_bench.jsonl 2>&1
+rc=$?; cat gpurun_out/moe_bench.jsonl | tail -14; exit $rc

@@ -182,6 +182,35 @@ def bench_prefill(eng, B, L):
     return {"bench": "prefill", "B": B, "L": L, "s": round(dt, 4), "tok_s": round(B * L / dt, 1)}
 
 
+def bench_moe(T, H=4096, I=14336, E=8, k=2, plan=None):
+    """Mixtral expert FFN: the old per-wave kernel (moe_ffn) vs the grouped tgemm (moe_ffn_tg).
+    Bytes = the weights of the experts the batch touches (+ activations); FLOPs = 6 T k H I."""
+    from distributed_llm_amd.models.llama import gate_up_order
+    g = torch.Generator(device="cuda").manual_seed(T)
+    w13 = (torch.randn(E, 2 * I, H, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    w2 = (torch.randn(E, H, I, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    w13i = w13.index_select(1, gate_up_order(I).cuda()).contiguous()
+    x = (torch.randn(T, H, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    ids, w = ops.moe_gate(torch.randn(T, E, device="cuda", generator=g), k)
+    touched = len(set(ids.flatten().tolist()))
+    wbytes = touched * 3 * H * I * 2
+    flops = 6.0 * T * k * H * I
+    res = {"bench": "moe_ffn", "T": T, "H": H, "I": I, "E": E, "k": k, "experts_touched": touched}
+    iters = 10 if T <= 512 else 3
+    ms_old = timeit(lambda: ops.moe_ffn(x, ids, w, w13, w2), iters=iters, warm=2)
+    ms_new = timeit(lambda: ops.moe_ffn_tg(x, ids, w, w13i, w2, plan), iters=iters, warm=2)
+    for name, ms in (("old", ms_old), ("tg", ms_new)):
+        res[f"{name}_us"] = round(ms * 1000, 1)
+        res[f"{name}_weight_TBps"] = round(wbytes / ms / 1e9, 2)
+        res[f"{name}_TFLOPs"] = round(flops / ms / 1e9, 1)
+    err = (ops.moe_ffn_tg(x, ids, w, w13i, w2, plan).float() - ops.moe_ffn(x, ids, w, w13, w2).float()).abs().max()
+    res["max_abs_diff_tg_vs_old"] = round(float(err), 5)
+    res["plan"] = list(plan) if plan else "auto"
+    del w13, w2, w13i
+    torch.cuda.empty_cache()
+    return res
+
+
 def bench_gemm(M, N, K):
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
@@ -204,6 +233,14 @@ if __name__ == "__main__":
         if os.environ.get("MB_TUNE_SHAPES"):
             shapes = [tuple(int(v) for v in t.split("x")) + (False,) for t in os.environ["MB_TUNE_SHAPES"].split(",")]
         G.autotune(shapes, ms, "cuda", verbose=True)
+    if "moe" in what:
+        Ts = [int(x) for x in os.environ.get("MB_MOE_T", "1,16,64,256,1024,4096").split(",")]
+        for T in Ts:
+            print(json.dumps(bench_moe(T)), flush=True)
+        for T in (256, 4096):
+            for plan in ((64, 128, 3, 1, 4, 64, 3, 1, 4), (128, 128, 3, 1, 8, 128, 3, 1, 8),
+                         (128, 128, 2, 2, 8, 128, 2, 2, 8), (256, 256, 2, 1, 8, 128, 3, 1, 8)):
+                print(json.dumps(bench_moe(T, plan=plan)), flush=True)
     if "gemm" in what:
         for M in (1, 16, 64, 128, 256):
             for (N, K) in [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632), (32000, 2048), (6144, 4096), (28672, 4096), (4096, 14336)]:
