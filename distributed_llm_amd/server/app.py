@@ -77,12 +77,18 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
             snapshot = list(hist)
         try:
             payload, tokens, device = r.route_query(snapshot)
+            timing: Dict[str, Any] = {}
             if isinstance(payload, dict):
                 reply = payload.get("response", "")
                 reasoning = payload.get("routing_reasoning", f"Method: {strategy}")
                 method = payload.get("routing_method", strategy)
                 confidence = payload.get("routing_confidence", 0.0)
                 cache_hit = payload.get("cache_hit", False)
+                raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
+                # extra keys for the metadata panel (reference clients ignore unknown keys)
+                timing = {"latency_ms": raw.get("latency_ms"), "routing_ms": payload.get("routing_overhead_ms"),
+                          "ttft_ms": (payload.get("timing") or {}).get("ttft_ms"),
+                          "failover": bool(payload.get("failover") or raw.get("failover"))}
             else:
                 reply, reasoning, method, confidence, cache_hit = str(payload), "Direct response", strategy, 0.0, False
             with lock:
@@ -90,7 +96,7 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
                 hist.append({"role": "assistant", "content": reply})
                 state["histories"][session] = hist[-HISTORY_LIMIT:]
             return jsonify({"reply": reply, "device": device, "reasoning": reasoning, "method": method,
-                            "confidence": confidence, "cache_hit": cache_hit, "tokens": tokens})
+                            "confidence": confidence, "cache_hit": cache_hit, "tokens": tokens, "timing": timing})
         except Exception as e:
             with lock:
                 hist = state["histories"].get(session, [])
@@ -98,7 +104,7 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
                     hist.pop()
             return jsonify({"reply": "System Error: The router encountered an issue.", "device": "error",
                             "reasoning": str(e), "method": strategy, "confidence": 0.0, "cache_hit": False,
-                            "tokens": 0}), 500
+                            "tokens": 0, "timing": {}}), 500
 
     @app.route("/", methods=["GET"])
     def ui():

@@ -8,7 +8,9 @@ from distributed_llm_amd.pools.base import EchoPool, FaultInjectingPool
 from distributed_llm_amd.pools.worker import create_worker_app
 from distributed_llm_amd.server.app import BASE_CONFIG, HISTORY_LIMIT, create_app
 
-CHAT_KEYS = {"reply", "device", "reasoning", "method", "confidence", "cache_hit", "tokens"}
+# the reference client's keys (fyp-chat-frontend/src/App.tsx:115-123) plus our additive `timing`
+REF_KEYS = {"reply", "device", "reasoning", "method", "confidence", "cache_hit", "tokens"}
+CHAT_KEYS = REF_KEYS | {"timing"}
 
 
 @pytest.fixture()
@@ -25,6 +27,7 @@ def test_chat_contract(client):
     from distributed_llm_amd.router.tokens import TokenCounter
     want = TokenCounter().count_tokens({"role": "assistant", "content": d["reply"]})
     assert set(d) == CHAT_KEYS and d["device"] == SMALL and d["tokens"] == want
+    assert set(d["timing"]) == {"latency_ms", "routing_ms", "ttft_ms", "failover"} and d["timing"]["failover"] is False
     assert r.headers["Access-Control-Allow-Origin"] == "*"
     h = client.get("/history?session_id=s1").get_json()
     assert [m["role"] for m in h] == ["user", "assistant"] and h[1]["content"] == d["reply"]
@@ -65,7 +68,7 @@ def test_error_rolls_back_history():
     r = c.post("/chat", json={"message": "hi", "strategy": "token", "session_id": "e"})
     assert r.status_code == 500
     d = r.get_json()
-    assert set(d) == CHAT_KEYS and d["device"] == "error" and d["reasoning"] == "kaboom"
+    assert set(d) == CHAT_KEYS and d["device"] == "error" and d["reasoning"] == "kaboom" and d["timing"] == {}
     assert c.get("/history?session_id=e").get_json() == []
 
 
@@ -96,3 +99,8 @@ def test_browser_client_served(client):
     body = r.get_data(as_text=True)
     # same request contract as the reference React client (App.tsx:101-109)
     assert "/chat" in body and "session_id" in body and "token-counting" in body
+    # routing-metadata panel of ChatMessage.tsx:56-92: device badge, cache badge, method, confidence,
+    # tokens, reasoning (+ timing line and dark mode)
+    for needle in ("cache_hit", "r.method", "r.confidence", "r.tokens", "r.reasoning", "latency_ms", "ttft_ms",
+                   "dllm_dark"):
+        assert needle in body, needle
