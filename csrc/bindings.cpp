@@ -603,7 +603,8 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)), "ks in {1,2}; nw 4, or 8 with bn >= 128");
   TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
   TORCH_CHECK((bm == 64 || bm == 128 || (bm == 256 && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
-                  (stages == 2 || stages == 3) && (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024,
+                  (stages == 2 || stages == 3 || ((stages == 4 || stages == 6) && ks == 1 && bm <= 128)) &&
+                  (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024,
               "tile / ring size");
   TORCH_CHECK(splits >= 1 && splits <= 64, "splits");
   const int kq = 64 * (int)ks;

@@ -51,6 +51,15 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// wait until at most r stages of ring loads (G per stage per wave) are still in flight, r <= MAXR
+template <int G, int MAXR>
+__device__ __forceinline__ void wait_stages(int r) {
+  if constexpr (MAXR >= 4) { if (r >= 4) { wait_vm<4 * G>(); return; } }
+  if constexpr (MAXR >= 3) { if (r == 3) { wait_vm<3 * G>(); return; } }
+  if constexpr (MAXR >= 2) { if (r == 2) { wait_vm<2 * G>(); return; } }
+  if constexpr (MAXR >= 1) { if (r == 1) { wait_vm<G>(); return; } }
+  wait_vm<0>();
+}
 __device__ __forceinline__ void block_sync_lds() {
   // raw barrier: LDS accesses retired, VMEM (the in-flight global_load_lds ring) left alone
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -183,11 +192,8 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
 
   // ---- main loop: wait for tile t, barrier, refill the slot read at t-1, compute tile t
   for (int t = 0; t < nk; ++t) {
-    if constexpr (STAGES == 3) {
-      if (t + 1 < nk) wait_vm<G>(); else wait_vm<0>();
-    } else {
-      wait_vm<0>();
-    }
+    // tile t landed once at most min(STAGES - 2, nk - 1 - t) later stages are still in flight
+    wait_stages<G, (STAGES - 2 < 4 ? STAGES - 2 : 4)>(min(STAGES - 2, nk - 1 - t));
     block_sync_lds();
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
 #pragma unroll
@@ -415,16 +421,26 @@ int by_pipe(int stages, int ks, const GemmArgs& a, hipStream_t st) {
   return stages == 2 ? launch_fit<BM, BN, EPI, 2, 2, NW>(a, st) : launch_fit<BM, BN, EPI, 3, 2, NW>(a, st);
 }
 
+// deep rings (4 / 6 stages, k-step 64) for the 64- and 128-row tiles: at decode-size M a workgroup's
+// k-loop is a chain of load latencies, so more stages = more bytes in flight per CU and a shorter
+// chain (LDS holds up to 6 x 24 KB for 64 x 128; launch_fit rejects rings over 150 KB)
+template <int BM, int BN, int EPI, int NW>
+int by_pipe_deep(int stages, int ks, const GemmArgs& a, hipStream_t st) {
+  if (ks == 1 && stages == 4) return launch_fit<BM, BN, EPI, 4, 1, NW>(a, st);
+  if (ks == 1 && stages == 6) return launch_fit<BM, BN, EPI, 6, 1, NW>(a, st);
+  return by_pipe<BM, BN, EPI, NW>(stages, ks, a, st);
+}
+
 template <int EPI>
 int by_tile(int bm, int bn, int stages, int ks, int nw, const GemmArgs& a, hipStream_t st) {
   if (nw == 4) {
-    if (bm == 64 && bn == 64) return by_pipe<64, 64, EPI, 4>(stages, ks, a, st);
-    if (bm == 64 && bn == 128) return by_pipe<64, 128, EPI, 4>(stages, ks, a, st);
-    if (bm == 128 && bn == 64) return by_pipe<128, 64, EPI, 4>(stages, ks, a, st);
-    if (bm == 128 && bn == 128) return by_pipe<128, 128, EPI, 4>(stages, ks, a, st);
+    if (bm == 64 && bn == 64) return by_pipe_deep<64, 64, EPI, 4>(stages, ks, a, st);
+    if (bm == 64 && bn == 128) return by_pipe_deep<64, 128, EPI, 4>(stages, ks, a, st);
+    if (bm == 128 && bn == 64) return by_pipe_deep<128, 64, EPI, 4>(stages, ks, a, st);
+    if (bm == 128 && bn == 128) return by_pipe_deep<128, 128, EPI, 4>(stages, ks, a, st);
   } else if (nw == 8) {
-    if (bm == 64 && bn == 128) return by_pipe<64, 128, EPI, 8>(stages, ks, a, st);
-    if (bm == 128 && bn == 128) return by_pipe<128, 128, EPI, 8>(stages, ks, a, st);
+    if (bm == 64 && bn == 128) return by_pipe_deep<64, 128, EPI, 8>(stages, ks, a, st);
+    if (bm == 128 && bn == 128) return by_pipe_deep<128, 128, EPI, 8>(stages, ks, a, st);
     if (bm == 256 && bn == 128) return by_pipe<256, 128, EPI, 8>(stages, ks, a, st);
     if (bm == 256 && bn == 256) return by_pipe<256, 256, EPI, 8>(stages, ks, a, st);
   }
@@ -587,7 +603,7 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
   if (a.N % 8 || (a.Y && a.ldy % 8)) return -7;  // 16-B output row vectors
   if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
   if (a.g_tiles != nullptr && (a.splits != 1 || a.M != a.g_max * bm || epi == EPI_QKV || a.ssq_in)) return -10;
-  if (stages != 2 && stages != 3) return -5;
+  if (stages < 2 || stages > 6 || stages == 5 || (stages > 3 && (ks != 1 || bm > 128))) return -5;
   switch (epi) {
     case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, ks, nw, a, stream);
     case EPI_RESADD: return by_tile<EPI_RESADD>(bm, bn, stages, ks, nw, a, stream);

@@ -199,7 +199,8 @@ class LLMEngine:
         self._so = s0
         # the whole sampler runs inside the decode graph (ops.sample_rows) unless the vocab is
         # tensor-parallel (then the distributed arg-max / top-k of LlamaModel is used)
-        self.fused_sampler = self.par.tp_size == 1 and os.environ.get("DLLM_FUSED_SAMPLER", "1") == "1"
+        # one-launch sampler inside the decode graph (TP: merged per-shard top-256 candidates, LlamaModel.sample)
+        self.fused_sampler = os.environ.get("DLLM_FUSED_SAMPLER", "1") == "1"
         self._seed_ctr = 0
         dv = self.dec_dev
         self.d_temp = dv[s0:s0 + mb].view(torch.float32)
@@ -653,8 +654,9 @@ class LLMEngine:
             buf = np.zeros(3 * n + 1, dtype=np.int32)
             self._fill_sampler(buf, buf.view(np.float32), 0, n, seqs, n)
             t = torch.from_numpy(buf).to(dev, non_blocking=True)
-            return ops.sample_rows(self.model.logits(hidden[:n]), t[:n].view(torch.float32),
-                                   t[n:2 * n].view(torch.float32), t[2 * n:3 * n], t[3 * n:]).tolist()
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+            return self.model.sample(hidden[:n], t[:n].view(torch.float32), t[n:2 * n].view(torch.float32),
+                                     t[2 * n:3 * n], t[3 * n:], out).tolist()
         ids = greedy_ids[:n] if greedy_ids is not None else self.model.greedy(hidden[:n])
         sampled = [i for i, s in enumerate(seqs) if not s.params.greedy]
         if not sampled:
@@ -887,8 +889,8 @@ class LLMEngine:
         ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)
         hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches)
         if self.fused_sampler:
-            ops.sample_rows(self.model.logits(hid), self.d_temp[:bs], self.d_topp[:bs], self.d_topk[:bs],
-                            self.d_seed, out=self.d_out[:bs])
+            self.model.sample(hid, self.d_temp[:bs], self.d_topp[:bs], self.d_topk[:bs], self.d_seed,
+                              self.d_out[:bs])
             return
         self.d_hidden[:bs].copy_(hid)
         self.d_out[:bs].copy_(self.model.greedy(hid))

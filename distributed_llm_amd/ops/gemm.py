@@ -469,7 +469,7 @@ def _tg_cands(M: int, N: int, K: int):
                     continue
                 if _need_tg(M, N, K, bm, bn, sp, ks)[0] > WS_FLOATS:
                     continue
-                for st in ((2, 3, 4, 6) if bm == 64 and ks == 1 else (2, 3)):
+                for st in ((2, 3, 4, 6) if bm <= 128 and ks == 1 else (2, 3)):
                     if st * ks * (bm + bn) * 128 > 150 * 1024:
                         continue   # the ring would not fit the LDS
                     out.append((bm, bn, st, sp, ks, nw))

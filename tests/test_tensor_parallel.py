@@ -32,7 +32,9 @@ def _worker(rank, world, port, model, q, env=None):
         from distributed_llm_amd.parallel.comm import make_tp_groups
         par = make_tp_groups(world)
         eng = LLMEngine(model, device="cpu", par=par, kv_cache_gb=0.05, max_num_seqs=4)
-        outs = eng.generate(PROMPTS, SamplingParams(max_new_tokens=6))
+        sp = (SamplingParams(max_new_tokens=6, temperature=0.9, top_k=40, top_p=0.95)
+              if os.environ.get("TP_TEST_SAMPLED") == "1" else SamplingParams(max_new_tokens=6))
+        outs = eng.generate(PROMPTS, sp)
         q.put((rank, [o.token_ids for o in outs], eng.model.par.use_sp(64)))
     finally:
         dist.destroy_process_group()
@@ -69,6 +71,20 @@ def test_tp2_matches_tp1(model):
         assert got[:3] == want[:3]
     same = sum(a == b for g, w in zip(res[0], ref) for a, b in zip(g, w))
     assert same >= 0.8 * sum(len(w) for w in ref)
+
+
+def test_tp2_sampled_ranks_agree_and_follow_tp1():
+    """Sampling under TP (LlamaModel.sample: merged per-shard top-256 candidates + the fused
+    sampler with a shared seed): both ranks draw the same tokens, and the first draw matches TP=1
+    (same exact top-k set and the same counter-based uniform)."""
+    from distributed_llm_amd.engine.llm_engine import LLMEngine
+    from distributed_llm_amd.engine.sampling import SamplingParams
+    sp = SamplingParams(max_new_tokens=6, temperature=0.9, top_k=40, top_p=0.95)
+    ref = [o.token_ids for o in LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=4)
+           .generate(PROMPTS, sp)]
+    res = _run_tp("tiny-llama-test", env={"TP_TEST_SAMPLED": "1"})
+    assert res[0] == res[1]
+    assert [g[0] for g in res[0]] == [w[0] for w in ref]
 
 
 @pytest.mark.parametrize("model", ["tiny-llama-test", "tiny-moe-test"])
