@@ -496,7 +496,8 @@ void moe_ffn_tg(torch::Tensor x, torch::Tensor ids, torch::Tensor wts, torch::Te
   const int bm = (int)plan[0];
   for (int g = 0; g < 2; ++g) {
     const int bn = (int)plan[1 + 4 * g], st = (int)plan[2 + 4 * g], ks = (int)plan[3 + 4 * g], nw = (int)plan[4 + 4 * g];
-    TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)) && (st == 2 || st == 3) &&
+    TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)) &&
+                    (st == 2 || st == 3 || ((st == 4 || st == 6) && ks == 1 && bm <= 128)) &&
                     (bm == 64 || bm == 128 || (bm == 256 && nw == 8)) &&
                     (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) && st * ks * (bm + bn) * 128 <= 150 * 1024,
                 "moe plan tile / ring size");

@@ -237,9 +237,13 @@ if __name__ == "__main__":
         Ts = [int(x) for x in os.environ.get("MB_MOE_T", "1,16,64,256,1024,4096").split(",")]
         for T in Ts:
             print(json.dumps(bench_moe(T)), flush=True)
-        for T in (256, 4096):
-            for plan in ((64, 128, 3, 1, 4, 64, 3, 1, 4), (128, 128, 3, 1, 8, 128, 3, 1, 8),
-                         (128, 128, 2, 2, 8, 128, 2, 2, 8), (256, 256, 2, 1, 8, 128, 3, 1, 8)):
+        plans = {16: ((64, 128, 3, 1, 4, 64, 6, 1, 4), (64, 128, 6, 1, 4, 64, 6, 1, 4), (64, 128, 4, 1, 4, 128, 4, 1, 4),
+                      (64, 64, 6, 1, 4, 64, 6, 1, 4)),
+                 64: ((64, 128, 3, 1, 4, 64, 6, 1, 4), (64, 128, 6, 1, 4, 64, 6, 1, 4), (64, 128, 4, 1, 4, 128, 4, 1, 4)),
+                 256: ((128, 128, 3, 1, 8, 128, 3, 1, 8), (128, 128, 4, 1, 8, 128, 4, 1, 8)),
+                 4096: ((256, 256, 2, 1, 8, 128, 3, 1, 8), (128, 128, 4, 1, 8, 128, 4, 1, 8))}
+        for T in [int(x) for x in os.environ.get("MB_MOE_PLAN_T", "16,64,256,4096").split(",")]:
+            for plan in plans[T]:
                 print(json.dumps(bench_moe(T, plan=plan)), flush=True)
     if "gemm" in what:
         for M in (1, 16, 64, 128, 256):
