@@ -357,8 +357,9 @@ def moe_ffn(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13: torch.Te
 
 MOE_PLANS = {  # (bm, bn13, stages13, ks13, nw13, bn2, stages2, ks2, nw2) by routed-pair count
     # measured at Mixtral shapes (profiles/r2_moe_microbench.md)
-    "decode": (64, 128, 3, 1, 4, 64, 3, 1, 4),        # P <= 128: weight streaming, 64-row tiles
-    "mid": (128, 128, 3, 1, 8, 128, 3, 1, 8),         # P <= 1024
+    "decode": (64, 128, 3, 1, 4, 64, 6, 1, 4),        # P <= 128: weight streaming, 64-row tiles, 6-deep ring for
+                                                      # the long-K down projection
+    "mid": (128, 128, 4, 1, 8, 128, 4, 1, 8),         # P <= 1024
     "prefill": (256, 256, 2, 1, 8, 128, 3, 1, 8),     # large P: 256x256 tiles (weight reuse)
 }
 
