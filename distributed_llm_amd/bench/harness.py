@@ -39,7 +39,10 @@ SUMMARY_HEADERS = [
     "overall_total_latency_ms", "overall_total_energy_mJ", "overall_total_tokens",
     "overall_latency_per_token_ms", "overall_energy_per_token_mJ",
 ]
-SUMMARY_EXTRA = ["gpus", "p50_latency_ms", "p90_latency_ms", "tokens_per_sec", "mean_ttft_ms"]
+# extra columns appended after the reference's; tokens_per_sec counts like the reference (TokenCounter on
+# the returned text), generated_tokens_per_sec counts the tokens the engine actually decoded
+SUMMARY_EXTRA = ["gpus", "p50_latency_ms", "p90_latency_ms", "tokens_per_sec", "mean_ttft_ms",
+                 "generated_tokens", "generated_tokens_per_sec"]
 
 PER_QUERY_HEADERS = [
     "query_set", "strategy", "cache_mode", "token_threshold",
@@ -49,7 +52,8 @@ PER_QUERY_HEADERS = [
     "start_time", "end_time", "latency_ms", "response_tokens",
     "energy_mJ", "latency_per_token_ms", "energy_per_token_mJ",
 ]
-PER_QUERY_EXTRA = ["gpus", "small_pool", "large_pool", "ttft_ms", "prefill_tokens", "cached_tokens"]
+PER_QUERY_EXTRA = ["gpus", "small_pool", "large_pool", "ttft_ms", "prefill_tokens", "cached_tokens",
+                   "generated_tokens"]
 
 
 @dataclass
@@ -131,6 +135,9 @@ def summarize(rows: List[Dict[str, Any]], query_set: str, strategy: str, cache_m
                 "p90_latency_ms": lats[min(len(lats) - 1, int(0.9 * len(lats)))] if lats else "",
                 "tokens_per_sec": round(tot_t / (tot_l / 1000.0), 3) if tot_l > 0 else "",
                 "mean_ttft_ms": round(statistics.mean(ttfts), 3) if ttfts else ""})
+    gen = [int(r["generated_tokens"]) for r in rows if r.get("generated_tokens") not in ("", None)]
+    out.update({"generated_tokens": sum(gen) if gen else "",
+                "generated_tokens_per_sec": round(sum(gen) / (tot_l / 1000.0), 3) if gen and tot_l > 0 else ""})
     return out
 
 
@@ -202,7 +209,9 @@ def run_experiment(items: List[QueryItem], cfg: RunConfig, pools, tier_gpus: Dic
                         "start_time": t0, "end_time": t1, "latency_ms": int((t1 - t0).total_seconds() * 1000),
                         "response_tokens": int(ntok or 0), "ttft_ms": timing.get("ttft_ms", ""),
                         "prefill_tokens": timing.get("prefill_tokens", ""),
-                        "cached_tokens": timing.get("cached_tokens", "")})
+                        "cached_tokens": timing.get("cached_tokens", ""),
+                        "generated_tokens": timing.get("generated_tokens", "")
+                        if timing.get("generated_tokens") is not None else ""})
                     rows.append(row)
                 for r in rows:
                     dev = r.get("device_used")

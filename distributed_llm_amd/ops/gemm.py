@@ -273,8 +273,9 @@ def linear_swiglu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 # ----------------------------------------------------------------------------- fused decoder ops
 #
-# Two implementations of each fused op: the tgemm epilogue (one launch), or hipBLASLt's GEMM core
-# followed by the same epilogue as a standalone kernel (qkv_post / res_add_ssq / swiglu_post).
+# Two implementations of each fused op: the tgemm epilogue (one launch), or the shape's best plain
+# GEMM (GEMV / skinny / hipBLASLt, whatever the autotuner picked for linear()) followed by the same
+# epilogue as a standalone kernel (qkv_post / res_add_ssq / swiglu_post).
 # The autotuner records, per decode bucket and shape, which is faster (the standalone epilogue
 # is charged its measured time, _post_us; POST_US only where it cannot be measured); shapes it never saw (prefill chunks above MAX_M) use the vendor core,
 # which wins at large M (profiles/r2_tgemm_tune.md).
@@ -282,12 +283,22 @@ POST_US = 3.0
 
 
 def use_vendor_core(M: int, N: int, K: int) -> bool:
-    if os.environ.get("DLLM_FUSED_CORE") in ("tg", "blas"):
-        return os.environ["DLLM_FUSED_CORE"] == "blas"
+    """True: run the fused op as ``linear()`` (the shape's best plain plan — GEMV / skinny / mm /
+    hipBLASLt / plain tgemm) followed by the standalone epilogue kernel; False: one tgemm launch
+    with the epilogue fused."""
+    env = os.environ.get("DLLM_FUSED_CORE")
+    if env in ("tg", "blas", "lin"):
+        return env != "tg"
     c = _P.fused_core.get((M, N, K))
     if c is not None:
-        return c == "blas"
+        return c != "tg"
     return M > MAX_M
+
+
+def _core(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Plain product for the split (core + epilogue) form of a fused op: the tuned plan of this
+    shape (M <= MAX_M), hipBLASLt above."""
+    return linear(x, w) if x.shape[0] <= MAX_M else F.linear(x, w)
 
 def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float,
                    positions: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
@@ -301,7 +312,7 @@ def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: i
     if T == 0:
         return q
     if use_vendor_core(T, w.shape[0], H):
-        _native(r).qkv_post(F.linear(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
+        _native(r).qkv_post(_core(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
                             k_cache, v_cache, nq, nkv, d)
         return q
     _tgemm(_native(r), r, w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
@@ -315,7 +326,7 @@ def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_
     sums of the new residual's squares into ``ssq_out[:slots]``; returns ``slots``."""
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if M and use_vendor_core(M, N, K):
-        return int(_native(x).res_add_ssq(F.linear(x, w), residual, ssq_out))
+        return int(_native(x).res_add_ssq(_core(x, w), residual, ssq_out))
     plan = tg_plan(M, N, K)
     if M:
         _tgemm(_native(x), x, w, EPI_RESADD, plan, y=residual, ssq_out=ssq_out)
@@ -328,7 +339,7 @@ def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: in
     T, H = r.shape
     act = torch.empty((T, w.shape[0] // 2), dtype=r.dtype, device=r.device)
     if T and use_vendor_core(T, w.shape[0], H):
-        _native(r).swiglu_post(F.linear(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), act)
+        _native(r).swiglu_post(_core(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), act)
         return act
     if T:
         _tgemm(_native(r), r, w, EPI_SWIGLU, tg_plan(T, w.shape[0], H), y=act, ssq_in=ssq, ssq_n=ssq_n,
@@ -529,7 +540,9 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 best_tg = min(tgc, key=res.get)
                 _P.tg_plans[tkey] = best_tg[1:]
                 post = _post_us(M, N, dev)
-                _P.fused_core[tkey] = "tg" if res[best_tg] <= res[("blas",)] + post else "blas"
+                # the split form runs the shape's best plain plan (GEMV at M <= 8, skinny, ...)
+                best_plain = min(res[c] for c in res if c[0] != "tg")
+                _P.fused_core[tkey] = "tg" if res[best_tg] <= best_plain + post else "lin"
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
                       for k in ("gemv", "skinny", "lds", "mm", "tg")}

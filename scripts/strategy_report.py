@@ -26,27 +26,33 @@ for s in ["token", "heuristic", "semantic", "perf", "hybrid"]:
     p(f"| {s} | {d['value']:,.0f} | x{d['vs_baseline']:,.0f} | {d['p50_latency_ms']} | {d['p90_latency_ms']} | "
       f"{d['small_tier_share']} | {d['routing_overhead_ms_mean']} |")
 p("\nThe published best mean routed latency is 39.6 s/query (general_knowledge @200, Jetson Nano+Orin).\n")
-p("## B. Reference-style harness (`scripts/harness_sweep.sh`, CSVs in `r1_harness_1gpu/`)\n")
+p("## B. Reference-style harness (`scripts/harness_sweep.sh`, CSVs in `r2_harness_1gpu/`)\n")
 p("This is the reference protocol (`routing_chatbot_tester.py`): each query set is ONE growing conversation per")
 p("(strategy, cache mode, threshold). Queries are sent one at a time. The token strategy sweeps thresholds; the")
 p("others run at 1000. Energy is amdsmi socket power integrated per query window.")
 p("s/query and tok/s are directly comparable to the BASELINE.md table (mean s/query, routed tok/s).\n")
-p("| query set | strategy | cache | threshold | routing accuracy | mean s/query | routed tok/s | p50 ms | energy/token (mJ) |")
-p("|---|---|---|---|---|---|---|---|---|")
+p("| query set | strategy | cache | threshold | routing accuracy | mean s/query | routed tok/s (reference counting) | generated tok/s | p50 ms | energy/token (mJ) |")
+p("|---|---|---|---|---|---|---|---|---|---|")
 for r in csv.DictReader(open(os.path.join(G, "harness", "benchmark_results.csv"))):
     lat = float(r["overall_total_latency_ms"]) / 1000
     tok = float(r["overall_total_tokens"])
     ept = r["overall_energy_per_token_mJ"]
     ept = f"{float(ept):.1f}" if ept not in ("", "None") else "-"
+    gen = r.get("generated_tokens_per_sec") or ""
+    gen = f"{float(gen):.0f}" if gen not in ("", "None") else "-"
     p(f"| {r['query_set']} | {r['strategy']} | {r['cache_mode']} | {r['token_threshold']} | {r['routing_accuracy']} | "
-      f"{lat / N[r['query_set']]:.3f} | {tok / lat:.0f} | {r['p50_latency_ms']} | {ept} |")
+      f"{lat / N[r['query_set']]:.3f} | {tok / lat:.0f} | {gen} | {r['p50_latency_ms']} | {ept} |")
 p("""
 Published reference rows for comparison (BASELINE.md): general_knowledge @200 runs 39.6 s/query at 10.57 tok/s.
 technical_coding @400 runs 75.5 s/query at 8.91 tok/s. personal_health @400 runs 72.9 s/query at 8.32 tok/s.
 Orin energy is 0.37-0.65 J/token.
 
-Single-stream decode of the 1.1B model takes 0.89 ms per token after the small-batch GEMV and the work-list
-attention at batch 1, down from 1.41 ms. That is the latency floor of this sequential protocol. Throughput
-comes from concurrency (table A).""")
-dst = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r1_strategy_results.md")
+Single-stream decode of the 1.1B model takes ~0.9 ms per token (scripts/microbench.py --what decode, B=1);
+that is the latency floor of this sequential protocol. Throughput comes from concurrency (bench.py).
+
+Token counting: "routed tok/s (reference counting)" divides TokenCounter counts of the returned text by the
+latency, exactly as the reference does (src/router.py:286, litellm token_counter; without litellm the
+counter falls back to len(text)//4, which undercounts the gibberish of random-init weights); "generated
+tok/s" counts the tokens the engine decoded.""")
+dst = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r2_strategy_results.md")
 open(dst, "w").write("\n".join(out) + "\n")
