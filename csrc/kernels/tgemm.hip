@@ -480,9 +480,12 @@ __global__ void __launch_bounds__(256) res_add_ssq_kernel(const u16* __restrict_
 
 // ---- standalone epilogues for a vendor-GEMM output y (prefill-size M, where hipBLASLt's core is
 // faster than tgemm's): the same math as EPI_QKV / EPI_SWIGLU applied to y = r . W'^T.
+// lane-parallel: lane l sums slots l, l + 64, ... and the wave reduces (one load latency instead of
+// a chain of n); every wave of the block computes it (no LDS, no barrier)
 __device__ __forceinline__ float row_rinv(const float* ssq, int n, long ld, int m, float scale, float eps) {
   float s = 0.f;
-  for (int i = 0; i < n; ++i) s += ssq[(long)i * ld + m];
+  for (int i = threadIdx.x & 63; i < n; i += 64) s += ssq[(long)i * ld + m];
+  s = wave_sum(s);
   return rsqrtf(s * scale + eps);
 }
 

@@ -211,6 +211,26 @@ def bench_moe(T, H=4096, I=14336, E=8, k=2, plan=None):
     return res
 
 
+def bench_post(M, N=11264, H=2048):
+    """Standalone fused-op epilogues on a GEMM output y [M, N] (vendor-core split form)."""
+    from distributed_llm_amd.ops import gemm as G
+    ext = ops._native(torch.empty(1, device="cuda"))
+    y = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    slots = G.max_slots(H)
+    ssq = torch.rand(slots, M, device="cuda") + 1.0
+    act = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+    h = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+    res = {"bench": "post", "M": M, "N": N, "H": H}
+    for n_slots in (1, 32):
+        us = G._time(lambda i: ext.swiglu_post(y, ssq, n_slots, 1.0 / H, 1e-5, act)) 
+        res[f"swiglu_post_slots{n_slots}_us"] = round(us, 2)
+    res["swiglu_post_GBps"] = round(M * N * 3 / res["swiglu_post_slots1_us"] / 1e3, 1)
+    us = G._time(lambda i: ext.res_add_ssq(h, r, ssq))
+    res["res_add_ssq_us"] = round(us, 2)
+    return res
+
+
 def bench_gemm(M, N, K):
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
@@ -233,6 +253,9 @@ if __name__ == "__main__":
         if os.environ.get("MB_TUNE_SHAPES"):
             shapes = [tuple(int(v) for v in t.split("x")) + (False,) for t in os.environ["MB_TUNE_SHAPES"].split(",")]
         G.autotune(shapes, ms, "cuda", verbose=True)
+    if "post" in what:
+        for M in (64, 128, 320, 512):
+            print(json.dumps(bench_post(M)), flush=True)
     if "moe" in what:
         Ts = [int(x) for x in os.environ.get("MB_MOE_T", "1,16,64,256,1024,4096").split(",")]
         for T in Ts:
