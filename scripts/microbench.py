@@ -231,6 +231,34 @@ def bench_post(M, N=11264, H=2048):
     return res
 
 
+def bench_flash(L, nq, nkv, d, B=1):
+    """Cold causal prefill of B prompts of L tokens: flash_prefill.hip vs the 16-row paged kernel.
+    FLOPs = 4 * nq * d * (causal pairs) per prompt (QK^T and PV)."""
+    import numpy as np
+    g = torch.Generator(device="cuda").manual_seed(L + d)
+    nb = (L + 15) // 16
+    kc = (torch.randn(B * nb + 4, nkv, 16, d, device="cuda", generator=g)).to(torch.bfloat16)
+    vc = (torch.randn(B * nb + 4, nkv, d, 16, device="cuda", generator=g)).to(torch.bfloat16)
+    bt = (torch.randperm(B * nb, device="cuda", generator=g) + 1).view(B, nb).to(torch.int32)
+    q = torch.randn(B * L, nq, d, device="cuda", generator=g).to(torch.bfloat16)
+    I = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    qs, ql, cx = I([i * L for i in range(B)]), I([L] * B), I([L] * B)
+    G = nq // nkv
+    fts, ftt = ops.flash_tiles([L] * B, G)
+    pts, ptt = ops.build_tiles([L] * B, G)
+    fts, ftt, pts, ptt = I(fts), I(ftt), I(pts), I(ptt)
+    it = 10 if L <= 4096 else 3
+    ms_f = timeit(lambda: ops.flash_attention(q, kc, vc, bt, qs, ql, cx, fts, ftt), iters=it, warm=2)
+    ms_p = timeit(lambda: ops.paged_attention(q, kc, vc, bt, qs, ql, cx, pts, ptt, xcd_remap=True), iters=it, warm=2)
+    a = ops.flash_attention(q, kc, vc, bt, qs, ql, cx, fts, ftt)
+    b = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, pts, ptt, xcd_remap=True)
+    flops = 4.0 * nq * d * (L * (L + 1) / 2) * B
+    return {"bench": "flash_prefill", "B": B, "L": L, "nq": nq, "nkv": nkv, "d": d,
+            "flash_us": round(ms_f * 1000, 1), "flash_TFLOPs": round(flops / ms_f / 1e9, 1),
+            "paged16_us": round(ms_p * 1000, 1), "paged16_TFLOPs": round(flops / ms_p / 1e9, 1),
+            "speedup": round(ms_p / ms_f, 2), "max_abs_diff": round(float((a.float() - b.float()).abs().max()), 4)}
+
+
 def bench_gemm(M, N, K):
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
@@ -253,6 +281,11 @@ if __name__ == "__main__":
         if os.environ.get("MB_TUNE_SHAPES"):
             shapes = [tuple(int(v) for v in t.split("x")) + (False,) for t in os.environ["MB_TUNE_SHAPES"].split(",")]
         G.autotune(shapes, ms, "cuda", verbose=True)
+    if "flash" in what:
+        for (nq, nkv, d) in ((32, 4, 64), (32, 8, 128)):
+            for L in (1024, 4096, 16384):
+                print(json.dumps(bench_flash(L, nq, nkv, d)), flush=True)
+            print(json.dumps(bench_flash(2048, nq, nkv, d, B=8)), flush=True)
     if "post" in what:
         for M in (64, 128, 320, 512):
             print(json.dumps(bench_post(M)), flush=True)
