@@ -46,7 +46,7 @@ int dllm_car_open_handle(const char*, void**);
 int dllm_car_close_handle(void*);
 int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
-int dllm_tgemm(const void*, int, int, int, int, int, int, hipStream_t);
+int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t);
 int dllm_decode_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*, void*,
                           float*, float*, int*, const int*, const int*, int, int, int, int, int, int, int, float,
                           hipStream_t);
@@ -594,7 +594,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
            c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> pos,
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
-           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias) {
+           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
@@ -602,6 +602,8 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
   const int M = x.size(0), N = w.size(0), K = w.size(1);
   TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)), "ks in {1,2}; nw 4, or 8 with bn >= 128");
+  TORCH_CHECK(wk == 1 || (wk == 2 && nw == 4 && ks == 2 && stages <= 3 && bm <= 128 && bn <= 128),
+              "wk 2: two k-groups of 4 waves, ks 2, 2-3 stages, tiles up to 128 x 128");
   TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
   TORCH_CHECK((bm == 64 || bm == 128 || (bm == 256 && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
                   (stages == 2 || stages == 3 || ((stages == 4 || stages == 6) && ks == 1 && bm <= 128)) &&
@@ -686,7 +688,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
     a.vc = (uint16_t*)vc->data_ptr();
     a.nq = nq; a.nkv = nkv; a.d = d;
   }
-  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)epi, stream()), "tgemm");
+  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)wk, (int)epi, stream()), "tgemm");
 }
 
 // standalone EPI_QKV / EPI_SWIGLU for a vendor-GEMM output y (prefill)

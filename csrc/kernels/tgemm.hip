@@ -71,17 +71,22 @@ __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); 
 __device__ __forceinline__ float bfr(float x) { return bf2f(f2bf(x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-// KS: 64-deep k sub-tiles per ring stage (one barrier per stage); NW: waves per workgroup, laid out
-// 2 (M) x NW/2 (N), each wave a (BM/2) x (BN/(NW/2)) tile.
-template <int BM, int BN, int EPI, int STAGES, int KS, int NW>
-__global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
-  constexpr int NT = 64 * NW, NWN = NW / 2;
+// KS: 64-deep k sub-tiles per ring stage (one barrier per stage); NW: waves per k-group, laid out
+// 2 (M) x NW/2 (N), each wave a (BM/2) x (BN/(NW/2)) tile; WK: k-groups (1, or 2 with KS = 2): group g
+// stages and multiplies sub-tile g of every stage, and group 1's accumulators are added into group
+// 0's through LDS after the loop.  WK = 2 doubles the waves of a small output tile (decode-size M
+// has few tiles: 1 wave per SIMD leaves every LDS-read -> MFMA chain exposed) and halves each
+// wave's serial k chain without a global split-K combine.
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1>
+__global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
+  static_assert(WK == 1 || (WK == 2 && KS == 2), "k-groups split the KS sub-tiles of a stage");
+  constexpr int NT = 64 * NW * WK, NWN = NW / 2;  // NT: threads of the block
   constexpr int WM = BM / 2, WN = BN / NWN;
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(FN % 2 == 0 && FM >= 1, "wave tile: >= 16 rows, a multiple of 32 columns");
   constexpr int A_BYTES = BM * ROWB, SUB_BYTES = (BM + BN) * ROWB, STAGE_BYTES = KS * SUB_BYTES;
   constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // global_load_lds per wave per sub-tile
-  constexpr int G = KS * (GA + GB);                      // ... per stage
+  constexpr int G = (KS / WK) * (GA + GB);               // ... per stage
   static_assert(GA >= 1 && GB >= 1, "tile too small for the wave count");
   constexpr int KSTEP = BK * KS;
   constexpr int OW = (EPI == EPI_SWIGLU) ? BN / 2 : BN;  // staged output columns per row
@@ -95,8 +100,9 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
   float* s_red = s_rsp + TPR * BM;
   int* s_last = reinterpret_cast<int*>(s_red + 2 * BM);
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, kg = (threadIdx.x >> 6) / NW, wave = (threadIdx.x >> 6) % NW;
   const int wm = wave / NWN, wn = wave % NWN;
+  const bool fw = (WK == 1) || kg == 0;  // this wave owns the final accumulators
   const int N = a.N, K = a.K, S = a.splits;
   int M = a.M;
   const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
@@ -153,6 +159,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
   auto issue = [&](int t) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      if (WK == 2 && ks != kg) continue;  // each k-group stages its own sub-tile
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + ks * SUB_BYTES;
       const int ko = t * KSTEP + ks * BK;
 #pragma unroll
@@ -198,6 +205,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
 #pragma unroll
     for (int s = 0; s < 2 * KS; ++s) {
+      if (WK == 2 && (s >> 1) != kg) continue;
       const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + (s >> 1) * SUB_BYTES;
       bf16x8 af[FM], bw[FN];
       const int c = 4 * (s & 1) + (lane >> 4);
@@ -219,6 +227,28 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
     }
   }
   __syncthreads();  // ring idle (every load waited), rinv partials visible
+  if constexpr (WK == 2) {  // k-group 1 hands its partial tile to group 0 through the idle ring
+    static_assert(NW * FM * FN * 64 * 16 <= RING, "k-group exchange must fit the ring");
+    float4* xch = reinterpret_cast<float4*>(smem);
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          xch[((wave * FM + i) * FN + j) * 64 + lane] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const float4 v = xch[((wave * FM + i) * FN + j) * 64 + lane];
+          acc[i][j][0] += v.x; acc[i][j][1] += v.y; acc[i][j][2] += v.z; acc[i][j][3] += v.w;
+        }
+    }
+    __syncthreads();  // the ring is reused by the epilogue staging
+  }
 
   // ---- split-K: write-through f32 slabs, ticket per output tile; the last arriver sums all
   // slabs in split order (deterministic) and runs the epilogue
@@ -232,6 +262,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
+        if (!fw) continue;
         const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
         st_wt16(pr, (unsigned)((my + (long)c * BM + r) * 4),
                 make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
@@ -241,6 +272,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
+        if (!fw) continue;
         const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         for (int sp = 0; sp < S; ++sp) {
@@ -283,6 +315,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
     // registers (transposed cache layout: no row vectors to form), q/k staged.
     const int d = a.d, hd = d / 2, nq = a.nq, nkv = a.nkv;
     const int qcols = nq * d, kcols = nkv * d;
+    if (fw) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -313,6 +346,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
           }
         }
       }
+    }
     __syncthreads();
     // copy-out of q/k: an 8-column chunk of a 16-column half-group is 8 consecutive natural dims
     for (int e = threadIdx.x; e < BM * (BN / 8); e += NT) {
@@ -340,6 +374,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
       const int n = n0 + wn * WN + 16 * j + cl;
       bcol[j] = (EPI != EPI_SWIGLU && a.bias != nullptr && n < N) ? bf2f(a.bias[n]) : 0.f;
     }
+    if (fw) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -360,6 +395,7 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
           }
         }
       }
+    }
     __syncthreads();
   }
 
@@ -399,19 +435,20 @@ __global__ void __launch_bounds__(64 * NW) tgemm_kernel(GemmArgs a) {
   }
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1>
 int launch_t(const GemmArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW>), dim3(mt * nt * a.splits), dim3(64 * NW), 0, st, a);
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK>), dim3(mt * nt * a.splits), dim3(64 * NW * WK), 0, st,
+                     a);
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1>
 int launch_fit(const GemmArgs& a, hipStream_t st) {
   if constexpr (ST * KS * (BM + BN) * ROWB > 150 * 1024) {
     return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
   } else {
-    return launch_t<BM, BN, EPI, ST, KS, NW>(a, st);
+    return launch_t<BM, BN, EPI, ST, KS, NW, WK>(a, st);
   }
 }
 
@@ -431,8 +468,22 @@ int by_pipe_deep(int stages, int ks, const GemmArgs& a, hipStream_t st) {
   return by_pipe<BM, BN, EPI, NW>(stages, ks, a, st);
 }
 
+// two k-groups of 4 waves (WK = 2, KS = 2; 2 or 3 stages) for the 4-wave tiles
+template <int BM, int BN, int EPI>
+int by_pipe_wk2(int stages, const GemmArgs& a, hipStream_t st) {
+  return stages == 2 ? launch_fit<BM, BN, EPI, 2, 2, 4, 2>(a, st) : launch_fit<BM, BN, EPI, 3, 2, 4, 2>(a, st);
+}
+
 template <int EPI>
-int by_tile(int bm, int bn, int stages, int ks, int nw, const GemmArgs& a, hipStream_t st) {
+int by_tile(int bm, int bn, int stages, int ks, int nw, int wk, const GemmArgs& a, hipStream_t st) {
+  if (wk == 2) {
+    if (nw != 4 || ks != 2 || stages > 3) return -21;
+    if (bm == 64 && bn == 64) return by_pipe_wk2<64, 64, EPI>(stages, a, st);
+    if (bm == 64 && bn == 128) return by_pipe_wk2<64, 128, EPI>(stages, a, st);
+    if (bm == 128 && bn == 64) return by_pipe_wk2<128, 64, EPI>(stages, a, st);
+    if (bm == 128 && bn == 128) return by_pipe_wk2<128, 128, EPI>(stages, a, st);
+    return -20;
+  }
   if (nw == 4) {
     if (bm == 64 && bn == 64) return by_pipe_deep<64, 64, EPI, 4>(stages, ks, a, st);
     if (bm == 64 && bn == 128) return by_pipe_deep<64, 128, EPI, 4>(stages, ks, a, st);
@@ -595,11 +646,11 @@ extern "C" int dllm_tgemm_sizeof_args() { return (int)sizeof(GemmArgs); }
 // Host contract (checked again by csrc/bindings.cpp): K % 64 == 0, 16-B aligned rows (lda % 8),
 // splits >= 1 with kchunk % 64 == 0, part >= splits * tiles * bm * bn floats and counters >= tiles
 // (zeroed) when splits > 1; QKV/SWIGLU need N % 32 == 0 (and d % 32 == 0).
-extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, int nw, int epi,
+extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, int nw, int wk, int epi,
                           hipStream_t stream) {
   const GemmArgs& a = *reinterpret_cast<const GemmArgs*>(args);
   if (a.M <= 0 || a.N <= 0) return 0;
-  if ((ks != 1 && ks != 2) || (nw != 4 && nw != 8)) return -8;
+  if ((ks != 1 && ks != 2) || (nw != 4 && nw != 8) || (wk != 1 && wk != 2)) return -8;
   if (a.K % (BK * ks) || a.kchunk % (BK * ks) || a.kchunk <= 0 || a.splits < 1 || a.lda % 8) return -1;
   if (a.splits > 1 && (!a.part || !a.counters)) return -2;
   if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
@@ -608,11 +659,11 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
   if (a.g_tiles != nullptr && (a.splits != 1 || a.M != a.g_max * bm || epi == EPI_QKV || a.ssq_in)) return -10;
   if (stages < 2 || stages > 6 || stages == 5 || (stages > 3 && (ks != 1 || bm > 128))) return -5;
   switch (epi) {
-    case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, ks, nw, a, stream);
-    case EPI_RESADD: return by_tile<EPI_RESADD>(bm, bn, stages, ks, nw, a, stream);
-    case EPI_QKV: return by_tile<EPI_QKV>(bm, bn, stages, ks, nw, a, stream);
-    case EPI_SWIGLU: return by_tile<EPI_SWIGLU>(bm, bn, stages, ks, nw, a, stream);
-    case EPI_GELU: return by_tile<EPI_GELU>(bm, bn, stages, ks, nw, a, stream);
+    case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, ks, nw, wk, a, stream);
+    case EPI_RESADD: return by_tile<EPI_RESADD>(bm, bn, stages, ks, nw, wk, a, stream);
+    case EPI_QKV: return by_tile<EPI_QKV>(bm, bn, stages, ks, nw, wk, a, stream);
+    case EPI_SWIGLU: return by_tile<EPI_SWIGLU>(bm, bn, stages, ks, nw, wk, a, stream);
+    case EPI_GELU: return by_tile<EPI_GELU>(bm, bn, stages, ks, nw, wk, a, stream);
     default: return -6;
   }
 }

@@ -142,8 +142,8 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
-def tg_plan(M: int, N: int, K: int) -> Tuple[int, int, int, int, int, int]:
-    """(bm, bn, stages, splits, ks, waves) of the fused GEMM for this shape: tuned, else a
+def tg_plan(M: int, N: int, K: int) -> Tuple[int, ...]:
+    """(bm, bn, stages, splits, ks, waves[, k-groups]) of the fused GEMM for this shape: tuned, else a
     heuristic sized so the grid covers the 256 CUs (bigger tiles first, split-K only for short
     grids)."""
     p = _P.tg_plans.get((M, N, K))
@@ -202,17 +202,19 @@ def _run_plan(plan, x, w, swiglu, out):
 
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
            pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None):
+    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups]])"""
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
+    wk = plan[6] if len(plan) >= 7 else 1
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if K % (64 * ks):
-        ks = 1
+        ks, wk = 1, 1
     part = cnt = None
     if _tg_splits(K, sp, ks) > 1:
         floats, tiles = _need_tg(M, N, K, bm, bn, sp, ks)
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
-              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias)
+              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk))
 
 
 def ref_silu_mul(gu):
@@ -484,6 +486,8 @@ def _tg_cands(M: int, N: int, K: int):
                     if st * ks * (bm + bn) * 128 > 150 * 1024:
                         continue   # the ring would not fit the LDS
                     out.append((bm, bn, st, sp, ks, nw))
+                    if ks == 2 and nw == 4 and st <= 3 and bm <= 128 and bn <= 128:
+                        out.append((bm, bn, st, sp, ks, nw, 2))   # two k-groups of 4 waves
     return out
 
 

@@ -17,7 +17,10 @@ PLANS = [p for p in ([(bm, bn, st, sp, 1, nw) for bm, bn, nw in G._TG_TILES for 
                       # deep rings of the 64-row tiles (4 / 6 stages, k-step 64)
                       + [(bm, bn, st, sp, 1, nw) for bm, bn, nw in ((64, 64, 4), (64, 128, 4), (64, 128, 8),
                                                                    (128, 64, 4), (128, 128, 4), (128, 128, 8))
-                         for st in (4, 6) for sp in (1, 3)])
+                         for st in (4, 6) for sp in (1, 3)]
+                      # two k-groups of 4 waves (KS = 2)
+                      + [(bm, bn, st, sp, 2, 4, 2) for bm, bn in ((64, 64), (64, 128), (128, 64), (128, 128))
+                         for st in (2, 3) for sp in (1, 2)])
          if p[2] * p[4] * (p[0] + p[1]) * 128 <= 150 * 1024]
 
 
