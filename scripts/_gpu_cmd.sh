@@ -1,4 +1,7 @@
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 500 python -u scripts/exp/two_stream.py > gpurun_out/two_stream.log 2>&1
-rc=$?; tail -6 gpurun_out/two_stream.log; exit $rc
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_all.log 2>&1
+rc=$?; tail -4 gpurun_out/gpu_all.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/smoke.log; exit $rc

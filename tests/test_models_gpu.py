@@ -50,6 +50,7 @@ def _fp32_cpu_copy(m):
     mc.final_norm = f(m.final_norm)
     mc.layers = [{k: f(v) for k, v in L.items()} for L in m.reference_layers()]
     mc.fused = False
+    mc.moe_tg = False          # reference_layers() already restored the plain w13 layout
     mc.cos_sin = m.cos_sin.cpu()
     return mc
 
@@ -94,8 +95,6 @@ def test_true_shape_forward_matches_fp32_reference(name):
                                                  mt.tile_seq, mt.tile_tok0, mt.last_idx)))
     rp = mc.hidden_states(ids_p.cpu(), pos_p.cpu(), C(meta_p), kv)
     rd = mc.hidden_states(ids_d.cpu(), pos_d.cpu(), C(meta_d), kv)
-    rl = mc.hidden_states  # keep flake quiet
-    del rl
     ref_logits = rd @ mc.lm_head.t()
     eng.bm.free(sid)
     for what, a, b in (("prefill", hp, rp), ("decode", hd, rd), ("logits", lg, ref_logits)):
