@@ -110,6 +110,10 @@ __global__ void __launch_bounds__(256) flash_prefill_kernel(FlashArgs a) {
     const int wlast = min(tok0 + (32 * wave + 31) / G, last_tok);
     wave_lim = (tok0 + (32 * wave) / G > last_tok) ? 0 : (a.causal ? ctx - qlen + wlast + 1 : ctx);
   }
+  // keys below every row's causal limit in this wave: chunks entirely under it skip the masks
+  int wave_lo = min(row_lim[0], row_lim[1]);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) wave_lo = min(wave_lo, __shfl_xor(wave_lo, o, 64));
   __syncthreads();  // s_bt ready (no glds in flight yet: a plain barrier is fine)
 
   // staging: piece p (1 KB) of a stage; K pieces first, then V^T pieces
@@ -174,14 +178,23 @@ __global__ void __launch_bounds__(256) flash_prefill_kernel(FlashArgs a) {
     // online softmax per row fragment -> P^T (B operand of the PV product) and the rescale
     bf16x8 pf[2];
     float alpha[2];
+    const bool unmasked = kb + CK <= wave_lo;  // wave-uniform: every key of the chunk is visible to every row
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       float p[8];
+      if (unmasked) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int key0 = kb + 4 * g + q, key1 = kb + 16 + 4 * g + q;
-        p[q] = (key0 < row_lim[f] && key0 < kmax) ? sc[f][0][q] * a.scale_log2 : -INFINITY;
-        p[4 + q] = (key1 < row_lim[f] && key1 < kmax) ? sc[f][1][q] * a.scale_log2 : -INFINITY;
+        for (int q = 0; q < 4; ++q) {
+          p[q] = sc[f][0][q] * a.scale_log2;
+          p[4 + q] = sc[f][1][q] * a.scale_log2;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int key0 = kb + 4 * g + q, key1 = kb + 16 + 4 * g + q;
+          p[q] = (key0 < row_lim[f] && key0 < kmax) ? sc[f][0][q] * a.scale_log2 : -INFINITY;
+          p[4 + q] = (key1 < row_lim[f] && key1 < kmax) ? sc[f][1][q] * a.scale_log2 : -INFINITY;
+        }
       }
       float mloc = -INFINITY;
 #pragma unroll
@@ -190,10 +203,10 @@ __global__ void __launch_bounds__(256) flash_prefill_kernel(FlashArgs a) {
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float m_new = fmaxf(m_run[f], mloc);
       const float m_safe = (m_new == -INFINITY) ? 0.f : m_new;
-      alpha[f] = exp2f(m_run[f] - m_safe);
+      alpha[f] = __builtin_amdgcn_exp2f(m_run[f] - m_safe);   // v_exp_f32 (exp2(-inf) = 0)
       float lsum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { p[j] = exp2f(p[j] - m_safe); lsum += p[j]; }
+      for (int j = 0; j < 8; ++j) { p[j] = __builtin_amdgcn_exp2f(p[j] - m_safe); lsum += p[j]; }
       lsum += __shfl_xor(lsum, 16, 64);
       lsum += __shfl_xor(lsum, 32, 64);
       l_run[f] = l_run[f] * alpha[f] + lsum;
