@@ -419,7 +419,8 @@ def main() -> int:
         lk = enc1["lookups"] - enc0["lookups"]
         out["router_encoder"] = {"kinds": enc1["kinds"], "memo": bool(enc1.get("memo_enabled", False)),
                                  "lookups": lk, "memo_hit_rate": round((enc1["hits"] - enc0["hits"]) / lk, 3) if lk else None,
-                                 "texts_encoded_in_window": enc1["encoded_texts"] - enc0["encoded_texts"]}
+                                 "texts_encoded_in_window": enc1["encoded_texts"] - enc0["encoded_texts"],
+                                 "batch_reuse_hits": enc1["batch_hits"] - enc0["batch_hits"]}
         print(json.dumps(out), flush=True)
     if a.trace:
         from distributed_llm_amd.utils.tracing import tracer

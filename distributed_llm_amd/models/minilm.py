@@ -92,7 +92,10 @@ class MiniLMEncoder:
         self._memo: "OrderedDict[str, torch.Tensor]" = OrderedDict()
         # per-text memo of embeddings (DLLM_ENCODER_MEMO=0 disables it: every query is encoded)
         self._memo_size = memo_size if os.environ.get("DLLM_ENCODER_MEMO", "1") != "0" else 0
-        self.memo_hits = self.memo_misses = self.encoded_texts = 0
+        self.memo_hits = self.memo_misses = self.encoded_texts = self.batch_hits = 0
+        # embeddings of the current routing batch (prefetch): reused by the batch's own lookups
+        # (semantic router + semantic cache) even with the memo off, replaced by the next batch
+        self._scope: Dict[str, torch.Tensor] = {}
         self._lock = threading.Lock()
 
     def load_safetensors(self, path: str) -> None:
@@ -169,25 +172,50 @@ class MiniLMEncoder:
         m = (torch.arange(S)[None, :] < lens[:, None]).float()[..., None]
         return F.normalize((x * m).sum(1) / m.sum(1).clamp(min=1.0), dim=-1)
 
+    def prefetch(self, texts: List[str], max_len: int = 256) -> None:
+        """One batched forward for a routing batch's unique texts (memo hits excluded); the
+        results serve this batch's per-query lookups."""
+        uniq = list(dict.fromkeys(texts))
+        with self._lock:
+            todo = [t for t in uniq if not (self._memo_size and t in self._memo)]
+        scope: Dict[str, torch.Tensor] = {}
+        if todo:
+            embs = self._forward(todo, max_len)
+            scope = dict(zip(todo, embs))
+        with self._lock:
+            self.encoded_texts += len(todo)
+            if self._memo_size:
+                for k, e in scope.items():
+                    self._memo[k] = e
+                while len(self._memo) > self._memo_size:
+                    self._memo.popitem(last=False)
+            self._scope = scope
+
     def memo_stats(self) -> Dict[str, float]:
-        n = self.memo_hits + self.memo_misses
+        n = self.memo_hits + self.memo_misses + self.batch_hits
         return {"memo_enabled": bool(self._memo_size), "lookups": n, "hits": self.memo_hits,
-                "hit_rate": round(self.memo_hits / n, 4) if n else 0.0, "encoded_texts": self.encoded_texts}
+                "hit_rate": round(self.memo_hits / n, 4) if n else 0.0, "encoded_texts": self.encoded_texts,
+                "batch_hits": self.batch_hits}
 
     def encode(self, texts: List[str], max_len: int = 256) -> torch.Tensor:
         """[n, 384] f32 unit vectors on the device; memoised per text."""
         out: List[Optional[torch.Tensor]] = [None] * len(texts)
         todo: Dict[str, List[int]] = {}
         with self._lock:
+            scoped = 0
             for i, t in enumerate(texts):
                 v = self._memo.get(t) if self._memo_size else None
-                if v is None:
-                    todo.setdefault(t, []).append(i)
-                else:
+                if v is not None:
                     self._memo.move_to_end(t)
                     out[i] = v
+                elif t in self._scope:
+                    out[i] = self._scope[t]
+                    scoped += 1
+                else:
+                    todo.setdefault(t, []).append(i)
             missed = sum(len(v) for v in todo.values())
-            self.memo_hits += len(texts) - missed
+            self.batch_hits += scoped
+            self.memo_hits += len(texts) - missed - scoped
             self.memo_misses += missed
             self.encoded_texts += len(todo)
         if todo:

@@ -330,13 +330,14 @@ class Router:
         return self._finish(query, dec, raw, which, lat, failed)
 
     def _prefetch_embeddings(self, queries: List[str]) -> None:
-        """One batched encoder forward for every query of a batch (fills the embedder's memo, so
-        the semantic router and the semantic cache do no per-query encoder launches)."""
+        """One batched encoder forward for every query of a batch (the GPU encoder keeps it for the
+        batch's own lookups even with its memo off), so the semantic router and the semantic cache
+        do no per-query encoder launches."""
         emb = self.query_router.cache_embedder
         needs = self.query_router.cache_enabled or self.query_router.strategy in ("semantic", "hybrid")
         if emb is None or not needs or not queries:
             return
-        enc = getattr(emb, "encode_tensor", None) or emb.encode
+        enc = getattr(emb, "prefetch", None) or getattr(emb, "encode_tensor", None) or emb.encode
         try:
             enc(list(dict.fromkeys(queries)))
         except Exception as exc:  # routing still works, just unbatched

@@ -103,6 +103,10 @@ class MiniLMEmbedder(Embedder):
         self.max_len = max_len
         self.dim = cfg.hidden
 
+    def prefetch(self, texts: Sequence[str]) -> None:
+        """Encode a routing batch in one forward; its lookups reuse the result (memo or not)."""
+        self.model.prefetch(list(texts), max_len=self.max_len)
+
     def encode_tensor(self, texts: Sequence[str]):
         """Return a [n, dim] float32 device tensor (stays in HBM for the GPU scorer)."""
         return self.model.encode(list(texts), max_len=self.max_len)
@@ -152,7 +156,7 @@ def get_embedder(model_name: str = "all-MiniLM-L6-v2", device: Optional[str] = N
 def encoder_stats() -> Dict[str, float]:
     """Summed per-text memo counters of the GPU encoders in the registry (hash embedders have no
     kernels to report): lookups, hits, texts actually run through the encoder."""
-    tot = {"lookups": 0, "hits": 0, "encoded_texts": 0}
+    tot = {"lookups": 0, "hits": 0, "encoded_texts": 0, "batch_hits": 0}
     kinds = []
     with _REG_LOCK:
         embs = list(_REGISTRY.values())
