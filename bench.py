@@ -42,7 +42,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--topology", default="replicated", choices=["replicated", "pools"])
+    ap.add_argument("--topology", default="replicated", choices=["replicated", "pools", "tiers"],
+                    help="replicated: both tiers on one engine per GPU (BASELINE config 2); pools: tiers on "
+                         "disjoint GPU subsets (configs 3-5, N>1); tiers: --small-model and --large-model "
+                         "co-located as two engines on every GPU")
     ap.add_argument("--model", default="tinyllama-1.1b")
     ap.add_argument("--small-model", default="llama-3.2-1b")
     ap.add_argument("--large-model", default="llama-3-8b")
@@ -256,12 +259,33 @@ def main() -> int:
     if a.no_encoder_memo:
         os.environ["DLLM_ENCODER_MEMO"] = "0"
     from distributed_llm_amd.router.embedder import encoder_stats
-    topology = a.topology if world > 1 else "replicated"
+    topology = a.topology if (world > 1 or a.topology == "tiers") else "replicated"
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
 
     cluster = None
-    if topology == "replicated":
+    if topology == "tiers":
+        # heterogeneous tiers co-located on each GPU: a small-model engine and a large-model engine
+        # (BASELINE config 3's model pair; the reference runs them on two boards)
+        from distributed_llm_amd.engine.llm_engine import LLMEngine
+        from distributed_llm_amd.pools.base import EnginePool
+        sm = a.small_model if on_gpu else "tiny-llama-test"
+        lg = a.large_model if on_gpu else "tiny-llama-test"
+        kv = (a.kv_gb / 2) if on_gpu else 0.1
+        e_small = LLMEngine(sm, device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
+                            use_graphs=not a.no_graphs, seed=0)
+        e_large = LLMEngine(lg, device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
+                            use_graphs=not a.no_graphs, seed=1)
+        pools = {SMALL: EnginePool(SMALL, e_small, max_new_tokens=a.small_new, temperature=0.0),
+                 LARGE: EnginePool(LARGE, e_large, max_new_tokens=a.large_new, temperature=0.8, top_k=40,
+                                   top_p=0.9)}
+        if on_gpu:
+            for e in (e_small, e_large):
+                e.capture_all(max_bs=e._bucket(max(16, a.convs)))
+        engines = [e_small, e_large]
+        model_desc = f"{sm} small + {lg} large (two engines co-located per GPU)"
+        n_convs, parallelism = a.convs, f"dp{world}-colocated-tiers"
+    elif topology == "replicated":
         from distributed_llm_amd.engine.llm_engine import LLMEngine
         from distributed_llm_amd.pools.base import EnginePool
         model = a.model if on_gpu else "tiny-llama-test"

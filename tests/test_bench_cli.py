@@ -19,7 +19,8 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n,extra,par", [(1, [], "dp1"), (2, [], "dp2"), (4, ["--topology", "pools"], "pools:")])
+@pytest.mark.parametrize("n,extra,par", [(1, [], "dp1"), (2, [], "dp2"), (4, ["--topology", "pools"], "pools:"),
+                                         (1, ["--topology", "tiers"], "dp1-colocated")])
 def test_bench_json_line(n, extra, par):
     args = ["bench.py", "--cpu", "--gpus", str(n), "--steps", "1", "--warmup", "1", "--convs", "2",
             "--small-new", "4", "--large-new", "6"] + extra
