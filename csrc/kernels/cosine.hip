@@ -76,7 +76,8 @@ extern "C" int dllm_cosine_scores(const float* q, const float* c, float* s, int 
 
 extern "C" int dllm_masked_cosine_argmax(const float* q, const float* table, const float* norms, const int* ctx, int N,
                                          int d, int cid, float thr, unsigned long long* best, hipStream_t stream) {
-  hipMemsetAsync(best, 0, sizeof(unsigned long long), stream);
+  const hipError_t e = hipMemsetAsync(best, 0, sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return (int)e;
   if (N <= 0) return 0;
   long blocks = ((long)N * 64 + 255) / 256;
   if (blocks > 2048) blocks = 2048;  // ~8 waves per CU; grid-stride over the rest

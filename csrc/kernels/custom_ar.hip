@@ -29,6 +29,7 @@ constexpr int MAX_RANKS = 8;
 constexpr int MAX_BLOCKS = 64;
 constexpr int THREADS = 512;
 constexpr long SIG_BYTES = 4096;  // MAX_BLOCKS x MAX_RANKS x u32, padded
+static_assert(MAX_BLOCKS * MAX_RANKS * 4 <= SIG_BYTES, "signal slots must fit the signal buffer");
 
 struct CarArgs {
   const uint4* in;
@@ -136,7 +137,8 @@ extern "C" int dllm_car_allreduce(const void* in, void* out, long n_bytes, void*
   a.world = world;
   a.spin_limit = spin_limit;
   long blocks = (a.n8 + 4L * THREADS - 1) / (4L * THREADS);  // >= 4 vectors per thread before adding blocks
-  if (blocks > 32) blocks = 32;
+  if (blocks > 32) blocks = 32;  // (<= MAX_BLOCKS signal slots)
+  static_assert(32 <= MAX_BLOCKS, "grid cap within the signal slots");
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(car_kernel, dim3((int)blocks), dim3(THREADS), 0, stream, a);
   return (int)hipGetLastError();

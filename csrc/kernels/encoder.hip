@@ -52,8 +52,9 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const u16* __restrict
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, rl = lane & 15;
-  const int q = blockIdx.x * 64 + wave * 16 + rl;  // this lane's query row
-  if (blockIdx.x * 64 + wave * 16 >= S) return;    // wave-uniform: no barrier follows
+  const int q0 = (int)blockIdx.x * 64 + wave * 16;  // this wave's first query row
+  const int q = q0 + rl;                             // this lane's query row
+  if (q0 >= S) return;                               // wave-uniform: no barrier follows
   bf16x8 qf[KSTEPS];
 #pragma unroll
   for (int s = 0; s < KSTEPS; ++s)
@@ -169,12 +170,14 @@ extern "C" int dllm_encoder_attention(const void* qkv, const int* lens, void* ou
   const int SP = (S + 31) / 32 * 32;
   const size_t lds = (size_t)SP * d * 2 + (size_t)d * (SP + 8) * 2;
   const dim3 grid((S + 63) / 64, nh, B);
-  static const bool attr = [] {  // allow > 64 KB of dynamic LDS (S up to 512)
-    hipFuncSetAttribute((const void*)encoder_attn_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)encoder_attn_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return true;
+  static const int attr_rc = [] {  // allow > 64 KB of dynamic LDS (S up to 512)
+    int rc = (int)hipFuncSetAttribute((const void*)encoder_attn_kernel<32>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    rc |= (int)hipFuncSetAttribute((const void*)encoder_attn_kernel<64>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return rc;
   }();
-  (void)attr;
+  if (attr_rc != 0 && lds > 64 * 1024) return -3;
   switch (d) {
     case 32:
       hipLaunchKernelGGL(encoder_attn_kernel<32>, grid, dim3(256), lds, stream, (const u16*)qkv, lens, (u16*)out, S, SP,
