@@ -213,8 +213,8 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
      "paged_attention");
 }
 
-// Flash-style prefill attention (csrc/kernels/flash_prefill.hip): 128-row GQA tiles with K/V
-// staged once per workgroup in LDS.  tile_seq/tile_tok0 hold 128 / G tokens per tile.
+// Flash-style prefill attention (csrc/kernels/flash_prefill.hip): 256-row GQA tiles with K/V
+// staged once per workgroup in LDS.  tile_seq/tile_tok0 hold 256 / G tokens per tile.
 void flash_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
                    torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
                    torch::Tensor tile_tok0, torch::Tensor out, bool causal, double scale) {

@@ -1,33 +1,42 @@
 // Flash-style prefill attention over the paged KV cache (causal or bidirectional), GQA-packed.
 //
-// Work unit: (128-row query tile, kv head).  Rows pack (token, head-in-GQA-group) exactly like the
+// Work unit: (256-row query tile, kv head).  Rows pack (token, head-in-GQA-group) exactly like the
 // decode kernel (attention.hip): row r -> token tok0 + r / G, query head kvh * G + r % G, so a
-// tile covers 128 / G tokens and every K/V byte it reads serves all G heads of the group.
-// Four waves own 32 rows each (two 16-row MFMA fragments).  Per 32-key chunk (two 16-token KV
-// blocks) the WORKGROUP stages K and V^T once into LDS and all four waves consume them — 8x less
-// K/V traffic per query row than the 16-row decode-style tiles the prefill used before
-// ("each 16-row tile streams the whole K/V prefix").
+// tile covers 256 / G tokens and every K/V byte it reads serves all G heads of the group.  Eight
+// waves (two per SIMD) own 32 rows each.  Per 64-key chunk (four 16-token KV blocks) the WORKGROUP
+// stages K and V^T once into LDS and all eight waves consume them.
 //
-// Math per wave and chunk (the decode kernel's operand choice, cdna_hip_programming.md §3):
-//   S^T[32 keys][16 rows] = K . Q^T        (A = K rows from LDS, B = Q^T fragments in registers)
-//   online softmax per row (lane-local state + 2 xor-shuffles)
-//   O^T[d][16 rows]      += V^T . P^T      (A = V^T from LDS, B = P^T straight from the S^T
-//                                           accumulators with the key permutation of attention.hip)
+// Math per wave and chunk, on the 32x32x16 bf16 MFMA (cdna_hip_programming.md §3 operand maps):
+//   S^T[32 keys][32 rows] = K . Q^T          two key blocks, D/16 k-steps each
+//                                             (A = K rows from LDS, B = Q^T fragments in registers)
+//   online softmax: a lane holds 16 keys of ONE query row (col = lane & 31), so the row max is an
+//   in-lane fmax chain plus one exchange with lane ^ 32; exp2 via v_exp_f32 with the softmax scale
+//   folded into one FMA; the O rescale is skipped when no row's max moved (exact, wave-uniform)
+//   O^T[D][32 rows]      += V^T . P^T         four 16-key k-steps x D/32 dim blocks
+//                                             (A = V^T rows from LDS, B = P^T straight from the
+//                                             S^T accumulators, no lane movement)
+// The accumulator-as-operand step needs the S^T registers 8s..8s+7 of lane half h to be 8
+// CONSECUTIVE keys: the K image stores key perm(rho) in LDS row rho (bits 2 and 3 of the in-chunk
+// key index swapped), which makes registers 8s+j of half h hold key 16s + 8h + j, so the V^T
+// operand is one 16-B row read per k-step.
 // Staging: global_load_lds_dwordx4 into a 3-deep ring (counted vmcnt across a raw barrier, as in
-// tgemm.hip); the K image is XOR-swizzled through the per-lane source address (rule 21) so the
-// 16-lane fragment reads are conflict-free; the chunk's block-table entries are read from an LDS
-// copy of the tile's block-table row (an ordinary global load there would make hipcc drain the
-// ring).  Keys past the context tail (never written) get P = 0 AND a zeroed V column (0 * NaN).
+// tgemm.hip).  Both LDS images are XOR-swizzled through the per-lane source address so the
+// 16-lane row reads are conflict-free.  The chunk's block-table entries come from an LDS copy of
+// the tile's block-table row (an ordinary global load there would make hipcc drain the ring).
+// Keys past the context tail (never written) get P = 0 AND a zeroed V element (0 * NaN).
+// Grid order: consecutive workgroups (dealt round-robin to the 8 XCDs) take consecutive kv heads,
+// so the tiles sharing a head's K/V meet in one XCD's L2; the last (heaviest causal) tiles go first.
 #include "common.h"
 
 typedef __attribute__((address_space(3))) void lds_void;
 
 namespace {
 constexpr float LOG2E_F = 1.4426950408889634f;
-constexpr int ROWS = 128;   // query rows per workgroup
-constexpr int CK = 32;      // keys per chunk
+constexpr int NWAVES = 8;
+constexpr int ROWS = 32 * NWAVES;  // query rows per workgroup
+constexpr int CK = 64;             // keys per chunk (four cache blocks)
 constexpr int STAGES = 3;
-constexpr int MAXBT = 1024; // block-table entries staged per tile (16K-token context)
+constexpr int MAXBT = 1024;        // block-table entries staged per tile (16K-token context)
 
 struct FlashArgs {
   const u16* q;  // [T, nq, D]
@@ -40,7 +49,7 @@ struct FlashArgs {
   const int* tile_seq;
   const int* tile_tok0;
   u16* out;
-  int nq, nkv, G, max_blocks, causal;
+  int nq, nkv, G, max_blocks, causal, num_tiles;
   float scale_log2;
 };
 
@@ -54,28 +63,34 @@ __device__ __forceinline__ void sync_lds() {
   asm volatile("" ::: "memory");
 }
 
-// 16-B chunk position of chunk c of K row r in the swizzled image (conflict-free fragment reads)
+// 16-B chunk position of chunk c of K row r in the swizzled image
 template <int D>
 __device__ __forceinline__ int kswz(int r, int c) {
   if constexpr (D == 128) return c ^ (r & 15);
   else return c ^ ((r >> 1) & 7);
 }
+// in-chunk key held by K image row rho: bits 2 and 3 swapped (an involution)
+__device__ __forceinline__ int kperm(int rho) { return (rho & ~12) | ((rho & 4) << 1) | ((rho & 8) >> 1); }
+// in-block key of S^T accumulator register i of lane half h (C row (i&3) + 8(i>>2) + 4h, permuted)
+__device__ __forceinline__ int keyoff(int i, int h) { return (i & 7) | (h << 3) | ((i & 8) << 1); }
 
 template <int D>
-__global__ void __launch_bounds__(256) flash_prefill_kernel(FlashArgs a) {
-  constexpr int KS = D / 32;           // d-steps of S^T
-  constexpr int NT = D / 16;           // dim fragments of O^T
-  constexpr int KBYTES = CK * D * 2;   // K chunk (32 rows x D)
-  constexpr int VBYTES = CK * D * 2;   // V^T chunk (2 blocks x D x 16)
+__global__ void __launch_bounds__(512) flash_prefill_kernel(FlashArgs a) {
+  constexpr int KD = D / 16;            // k-steps of S^T
+  constexpr int NB = D / 32;            // 32-dim blocks of O^T
+  constexpr int KBYTES = CK * D * 2;    // K chunk: 64 rows x D
+  constexpr int VBYTES = CK * D * 2;    // V^T chunk: 4 blocks x D x 16
   constexpr int STAGE = KBYTES + VBYTES;
-  constexpr int GI = STAGE / 1024 / 4; // global_load_lds per wave per chunk
-  static_assert(STAGE % 4096 == 0, "whole 1-KB pieces per wave");
+  constexpr int GI = STAGE / 1024 / NWAVES;  // 1-KB global_load_lds pieces per wave per chunk
+  static_assert(STAGE % (1024 * NWAVES) == 0, "whole 1-KB pieces per wave");
+  static_assert(KBYTES % 1024 == 0 && 1024 % (2 * D) == 0, "a K piece covers whole rows of one block");
   __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + MAXBT * 4];
   int* s_bt = reinterpret_cast<int*>(smem + STAGES * STAGE);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, rl = lane & 15;
-  const int tile = blockIdx.x, kvh = blockIdx.y;
+  const int h = lane >> 5, rl = lane & 31;
+  const int kvh = blockIdx.x % a.nkv;
+  const int tile = a.num_tiles - 1 - (int)(blockIdx.x / a.nkv);
   const int seq = a.tile_seq[tile];
   if (seq < 0) return;  // uniform
   const int G = a.G, tpt = ROWS / G;
@@ -87,66 +102,58 @@ __global__ void __launch_bounds__(256) flash_prefill_kernel(FlashArgs a) {
   const int nchunks = (kmax + CK - 1) / CK;
   const int* bt = a.block_tables + (long)seq * a.max_blocks;
   const int nbt = min((kmax + 15) / 16, MAXBT);
-  for (int i = threadIdx.x; i < nbt; i += 256) s_bt[i] = bt[i];
+  for (int i = threadIdx.x; i < nbt; i += 64 * NWAVES) s_bt[i] = bt[i];
 
-  // this lane's two rows (fragments f = 0, 1 of the wave's 32 rows)
-  int row_lim[2], my_tok[2], my_head[2];
-  bool row_ok[2];
-  bf16x8 qf[2][KS];
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int r = 32 * wave + 16 * f + rl;
-    my_tok[f] = tok0 + r / G;
-    my_head[f] = kvh * G + r % G;
-    row_ok[f] = my_tok[f] < qlen && my_tok[f] <= last_tok;
-    row_lim[f] = !row_ok[f] ? 0 : (a.causal ? ctx - qlen + my_tok[f] + 1 : ctx);
-    const u16* qp = a.q + ((long)(qstart + (row_ok[f] ? my_tok[f] : tok0)) * a.nq + my_head[f]) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[f][s] = __builtin_bit_cast(bf16x8, row_ok[f] ? ld16(qp + 32 * s) : make_uint4(0, 0, 0, 0));
-  }
-  // keys this wave needs (causal: its last row's limit); chunks past it skip the math
-  int wave_lim = 0;
+  // this lane's query row (both lane halves hold the same row, different keys)
+  const int r = 32 * wave + rl;
+  const int my_tok = tok0 + r / G, my_head = kvh * G + r % G;
+  const bool row_ok = my_tok <= last_tok;
+  const int row_lim = !row_ok ? 0 : (a.causal ? ctx - qlen + my_tok + 1 : ctx);
+  bf16x8 qf[KD];
   {
-    const int wlast = min(tok0 + (32 * wave + 31) / G, last_tok);
-    wave_lim = (tok0 + (32 * wave) / G > last_tok) ? 0 : (a.causal ? ctx - qlen + wlast + 1 : ctx);
-  }
-  // keys below every row's causal limit in this wave: chunks entirely under it skip the masks
-  int wave_lo = min(row_lim[0], row_lim[1]);
+    const u16* qp = a.q + ((long)(qstart + (row_ok ? my_tok : tok0)) * a.nq + my_head) * D + 8 * h;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) wave_lo = min(wave_lo, __shfl_xor(wave_lo, o, 64));
+    for (int s = 0; s < KD; ++s) qf[s] = __builtin_bit_cast(bf16x8, ld16(qp + 16 * s));
+  }
+  // keys this wave needs (causal: its last row's limit) and keys every valid row of it sees
+  const int w_first = tok0 + (32 * wave) / G;
+  const int w_last = min(tok0 + (32 * wave + 31) / G, last_tok);
+  const int wave_lim = (w_first > last_tok) ? 0 : (a.causal ? ctx - qlen + w_last + 1 : ctx);
+  const int wave_lo = a.causal ? ctx - qlen + w_first + 1 : ctx;
   __syncthreads();  // s_bt ready (no glds in flight yet: a plain barrier is fine)
 
   // staging: piece p (1 KB) of a stage; K pieces first, then V^T pieces
   const long hstride = (long)16 * D;  // elements per (block, head) in either cache
   auto issue = [&](int t) {
     unsigned char* base = smem + (t % STAGES) * STAGE;
-    const int kb = t * CK;
-    const int b0 = s_bt[min(kb >> 4, nbt - 1)];
-    const int b1 = s_bt[min((kb >> 4) + 1, nbt - 1)];
+    const int bi = (t * CK) >> 4;
 #pragma unroll
     for (int j = 0; j < GI; ++j) {
-      const int p = wave * GI + j;                    // piece index within the stage
-      const int byte = p * 1024 + lane * 16;          // this lane's LDS byte within the stage
+      const int p = wave * GI + j;               // piece index within the stage (wave-uniform)
+      const int byte = p * 1024 + lane * 16;     // this lane's LDS byte within the stage
       const u16* src;
-      if (byte < KBYTES) {
-        const int r = byte / (2 * D), pos = (byte % (2 * D)) / 16;
-        const int c = kswz<D>(r, pos);                // source chunk landing at position pos
-        const int blk = (r < 16) ? b0 : b1;
-        src = a.kc + ((long)blk * a.nkv + kvh) * hstride + (r & 15) * D + 8 * c;
+      if (p * 1024 < KBYTES) {
+        const int rho = byte / (2 * D), pos = (byte % (2 * D)) / 16;
+        const int key = kperm(rho);
+        const int blk = s_bt[min(bi + (key >> 4), nbt - 1)];
+        src = a.kc + ((long)blk * a.nkv + kvh) * hstride + (key & 15) * D + 8 * kswz<D>(rho, pos);
       } else {
-        const int vb = byte - KBYTES, blk = (vb < 32 * D) ? b0 : b1;
-        src = a.vc + ((long)blk * a.nkv + kvh) * hstride + (vb % (32 * D)) / 2;
+        const int vb = byte - KBYTES, b = vb / (32 * D), w = vb % (32 * D);
+        const int dim = w / 32, c = ((w % 32) / 16) ^ ((dim >> 3) & 1);
+        const int blk = s_bt[min(bi + b, nbt - 1)];
+        src = a.vc + ((long)blk * a.nkv + kvh) * hstride + dim * 16 + 8 * c;
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + p * 1024), 16, 0, 0);
     }
   };
 
-  f32x4 acc[2][NT];
+  f32x16 acc[NB];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+  for (int n = 0; n < NB; ++n)
 #pragma unroll
-    for (int n = 0; n < NT; ++n) acc[f][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+    for (int i = 0; i < 16; ++i) acc[n][i] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;  // m in raw score units (the scale is folded into exp2)
+  const float cs = a.scale_log2;
 
 #pragma unroll
   for (int t = 0; t < STAGES - 1; ++t)
@@ -160,114 +167,109 @@ __global__ void __launch_bounds__(256) flash_prefill_kernel(FlashArgs a) {
     if (kb >= wave_lim) continue;  // wave-uniform: every row of this wave is past its causal limit
     const unsigned char* kbase = smem + (t % STAGES) * STAGE;
     const unsigned char* vbase = kbase + KBYTES;
-    // S^T = K . Q^T for both row fragments; K fragments (A operand: key row 16 h + rl, dims
-    // 32 s + 8 g) are read once per d-step and used by both
-    f32x4 sc[2][2];
+
+    f32x16 sc[2];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) sc[f][0] = sc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < 2; ++b) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+      for (int i = 0; i < 16; ++i) sc[b][i] = 0.f;
+      const int rho = 32 * b + rl;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = 16 * h + rl, c = 4 * s + g;
-        const bf16x8 kfr = *reinterpret_cast<const bf16x8*>(kbase + r * (2 * D) + (kswz<D>(r, c) << 4));
-#pragma unroll
-        for (int f = 0; f < 2; ++f) sc[f][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kfr, qf[f][s], sc[f][h], 0, 0, 0);
+      for (int s = 0; s < KD; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase + rho * (2 * D) + (kswz<D>(rho, 2 * s + h) << 4));
+        sc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sc[b], 0, 0, 0);
       }
     }
-    // online softmax per row fragment -> P^T (B operand of the PV product) and the rescale
-    bf16x8 pf[2];
-    float alpha[2];
-    const bool unmasked = kb + CK <= wave_lo;  // wave-uniform: every key of the chunk is visible to every row
+    if (kb + CK > wave_lo) {  // wave-uniform: a diagonal or tail chunk -> per-key masks
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      float p[8];
-      if (unmasked) {
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          p[q] = sc[f][0][q] * a.scale_log2;
-          p[4 + q] = sc[f][1][q] * a.scale_log2;
-        }
-      } else {
+        for (int i = 0; i < 16; ++i)
+          if (kb + 32 * b + keyoff(i, h) >= row_lim) sc[b][i] = -INFINITY;
+    }
+    float mloc = sc[0][0];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int key0 = kb + 4 * g + q, key1 = kb + 16 + 4 * g + q;
-          p[q] = (key0 < row_lim[f] && key0 < kmax) ? sc[f][0][q] * a.scale_log2 : -INFINITY;
-          p[4 + q] = (key1 < row_lim[f] && key1 < kmax) ? sc[f][1][q] * a.scale_log2 : -INFINITY;
+    for (int i = 1; i < 16; ++i) mloc = fmaxf(mloc, sc[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sc[1][i]);
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc);
+    if (__ballot(m_new != m_run)) {  // wave-uniform: some row's running max moved -> rescale
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * cs);  // exp2(-inf) = 0
+      l_run *= alpha;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[n] *= alpha;
+      m_run = m_new;
+    }
+    const float ms = (m_run == -INFINITY) ? 0.f : m_run * cs;
+    bf16x8 pf[4];
+    float lsum = 0.f;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[b][8 * s2 + j], cs, -ms));
+          lsum += p;
+          pf[2 * b + s2][j] = (__bf16)p;
         }
       }
-      float mloc = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) mloc = fmaxf(mloc, p[j]);
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run[f], mloc);
-      const float m_safe = (m_new == -INFINITY) ? 0.f : m_new;
-      alpha[f] = __builtin_amdgcn_exp2f(m_run[f] - m_safe);   // v_exp_f32 (exp2(-inf) = 0)
-      float lsum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { p[j] = __builtin_amdgcn_exp2f(p[j] - m_safe); lsum += p[j]; }
-      lsum += __shfl_xor(lsum, 16, 64);
-      lsum += __shfl_xor(lsum, 32, 64);
-      l_run[f] = l_run[f] * alpha[f] + lsum;
-      m_run[f] = m_new;
-      pf[f] = __builtin_bit_cast(bf16x8, pack8(p));
-    }
-    // O^T += V^T . P^T; one V^T fragment (dim 16 n + rl, keys 4g..4g+3 of each block) at a time
+    l_run += lsum;
+
+    // O^T += V^T . P^T: k-step s = cache block s of the chunk; lane half h holds keys 16s + 8h + j
     const bool tail = kb + CK > kmax;
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const unsigned char* vp = vbase + ((16 * n + rl) * 16 + 4 * g) * 2;
-      uint2 v0 = *reinterpret_cast<const uint2*>(vp);
-      uint2 v1 = *reinterpret_cast<const uint2*>(vp + 32 * D);
-      if (tail) {  // zero the columns of keys past the context end (never-written cache bytes)
+    for (int s = 0; s < 4; ++s) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t keep = (q & 1) ? 0x0000ffffu : 0xffff0000u;
-          if (kb + 4 * g + q >= kmax) { if (q < 2) v0.x &= keep; else v0.y &= keep; }
-          if (kb + 16 + 4 * g + q >= kmax) { if (q < 2) v1.x &= keep; else v1.y &= keep; }
+      for (int n = 0; n < NB; ++n) {
+        const int dim = 32 * n + rl;
+        uint4 v = ld16(vbase + s * (32 * D) + dim * 32 + ((h ^ ((dim >> 3) & 1)) << 4));
+        if (tail) {  // zero the elements of keys past the context end (never-written cache bytes)
+          const int k0 = kb + 16 * s + 8 * h;
+          uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (k0 + e >= kmax) w[e >> 1] &= (e & 1) ? 0x0000ffffu : 0xffff0000u;
+          v = make_uint4(w[0], w[1], w[2], w[3]);
         }
-      }
-      const bf16x8 vf = __builtin_bit_cast(bf16x8, make_uint4(v0.x, v0.y, v1.x, v1.y));
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        acc[f][n] *= alpha[f];
-        acc[f][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[f], acc[f][n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v), pf[s], acc[n], 0, 0, 0);
       }
     }
   }
 
-  // acc[f][n][e] = O^T[dim 16 n + 4 g + e][row rl]: 4 consecutive dims of the lane's row
+  // acc[n][i] = O^T[dim 32 n + 8 (i >> 2) + 4 h + (i & 3)][row rl]
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (!row_ok) return;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  u16* o = a.out + ((long)(qstart + my_tok) * a.nq + my_head) * D + 4 * h;
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    if (!row_ok[f]) continue;
-    const float inv = l_run[f] > 0.f ? 1.f / l_run[f] : 0.f;
-    u16* o = a.out + ((long)(qstart + my_tok[f]) * a.nq + my_head[f]) * D + 4 * g;
+  for (int n = 0; n < NB; ++n)
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const uint32_t lo = (uint32_t)f2bf(acc[f][n][0] * inv) | ((uint32_t)f2bf(acc[f][n][1] * inv) << 16);
-      const uint32_t hi = (uint32_t)f2bf(acc[f][n][2] * inv) | ((uint32_t)f2bf(acc[f][n][3] * inv) << 16);
-      *reinterpret_cast<uint2*>(o + 16 * n) = make_uint2(lo, hi);
+    for (int g = 0; g < 4; ++g) {
+      const uint32_t lo = (uint32_t)f2bf(acc[n][4 * g] * inv) | ((uint32_t)f2bf(acc[n][4 * g + 1] * inv) << 16);
+      const uint32_t hi = (uint32_t)f2bf(acc[n][4 * g + 2] * inv) | ((uint32_t)f2bf(acc[n][4 * g + 3] * inv) << 16);
+      *reinterpret_cast<uint2*>(o + 32 * n + 8 * g) = make_uint2(lo, hi);
     }
-  }
 }
 }  // namespace
 
-// Tiles: 128 / G query tokens per tile (host-built, ops.flash_tiles); grid = (tiles, nkv).
+// Tiles: 256 / G query tokens per tile (host-built, ops.flash_tiles); 1-D grid of tiles x nkv.
 extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc, const int* block_tables,
                                   const int* seq_qstart, const int* seq_qlen, const int* seq_ctx, const int* tile_seq,
                                   const int* tile_tok0, void* out, int num_tiles, int nq, int nkv, int d,
                                   int max_blocks, int causal, float scale, hipStream_t stream) {
   if (nq % nkv) return -1;
   const int G = nq / nkv;
-  if (ROWS % G || G > 16) return -2;
+  if (ROWS % G || G > 32) return -2;
   if (num_tiles <= 0) return 0;
+  if (max_blocks > MAXBT) return -3;
   FlashArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
-              tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, scale * LOG2E_F};
-  const dim3 grid(num_tiles, nkv);
+              tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, num_tiles, scale * LOG2E_F};
+  const dim3 grid((unsigned)num_tiles * (unsigned)nkv);
   switch (d) {
-    case 64: hipLaunchKernelGGL(flash_prefill_kernel<64>, grid, dim3(256), 0, stream, a); break;
-    case 128: hipLaunchKernelGGL(flash_prefill_kernel<128>, grid, dim3(256), 0, stream, a); break;
+    case 64: hipLaunchKernelGGL(flash_prefill_kernel<64>, grid, dim3(64 * NWAVES), 0, stream, a); break;
+    case 128: hipLaunchKernelGGL(flash_prefill_kernel<128>, grid, dim3(64 * NWAVES), 0, stream, a); break;
     default: return -4;
   }
   return (int)hipGetLastError();

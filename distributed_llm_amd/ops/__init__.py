@@ -166,7 +166,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return o
 
 
-FLASH_ROWS = 128
+FLASH_ROWS = 256
 
 
 def flash_supported(d: int, group: int, max_blocks: int) -> bool:
@@ -175,7 +175,7 @@ def flash_supported(d: int, group: int, max_blocks: int) -> bool:
 
 
 def flash_tiles(q_lens, group: int) -> Tuple[list, list]:
-    """Host tile table of the flash prefill kernel: 128 / group query tokens per tile."""
+    """Host tile table of the flash prefill kernel: 256 / group query tokens per tile."""
     tpt = FLASH_ROWS // group
     ts, tt = [], []
     for s, n in enumerate(q_lens):

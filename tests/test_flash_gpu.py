@@ -1,7 +1,8 @@
 """Flash-style prefill attention (csrc/kernels/flash_prefill.hip) against the fp32 PyTorch
 reference (ops.reference.paged_attention): ragged batches, cached prefixes (chunked prefill),
-causal and bidirectional, GQA groups 1/4/8, head dims 64/128, and never-written cache tails
-poisoned with NaN (they must not leak into the output)."""
+causal and bidirectional, GQA groups 1/4/8/16/32, head dims 64/128, scores whose running max
+keeps rising (the online-softmax rescale path), and never-written cache tails poisoned with NaN
+(they must not leak into the output)."""
 import math
 
 import pytest
@@ -13,7 +14,7 @@ from distributed_llm_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
-def _case(d, nq, nkv, seqs, seed=0):
+def _case(d, nq, nkv, seqs, seed=0, rising=False):
     g = torch.Generator().manual_seed(seed)
     nblocks = sum((c + 15) // 16 for _, c in seqs) + 8
     kc = torch.full((nblocks, nkv, 16, d), float("nan"), dtype=torch.bfloat16)
@@ -28,7 +29,8 @@ def _case(d, nq, nkv, seqs, seed=0):
         k += nb
         for t in range(c):   # only the sequence's own tokens are written
             blk, off = int(bt[i, t // 16]), t % 16
-            kc[blk, :, off, :] = torch.randn(nkv, d, generator=g).to(torch.bfloat16)
+            amp = (1.0 + t / 64.0) if rising else 1.0   # rising: the running max moves in late chunks
+            kc[blk, :, off, :] = (amp * torch.randn(nkv, d, generator=g)).to(torch.bfloat16)
             vc[blk, :, :, off] = torch.randn(nkv, d, generator=g).to(torch.bfloat16)
     T = sum(q for q, _ in seqs)
     q = torch.randn(T, nq, d, generator=g).to(torch.bfloat16)
@@ -41,10 +43,11 @@ def _case(d, nq, nkv, seqs, seed=0):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("d,nq,nkv", [(64, 32, 4), (128, 32, 8), (128, 8, 8), (64, 8, 1)])
-def test_flash_prefill_matches_fp32_reference(d, nq, nkv, causal):
+@pytest.mark.parametrize("d,nq,nkv", [(64, 32, 4), (128, 32, 8), (128, 8, 8), (64, 8, 1), (128, 64, 4), (64, 64, 2)])
+@pytest.mark.parametrize("rising", [False, True])
+def test_flash_prefill_matches_fp32_reference(d, nq, nkv, causal, rising):
     seqs = [(300, 300), (37, 37), (200, 777), (129, 129), (1, 50), (16, 33)]
-    q, kc, vc, bt, qs, ql, cx = _case(d, nq, nkv, seqs, seed=d + nq)
+    q, kc, vc, bt, qs, ql, cx = _case(d, nq, nkv, seqs, seed=d + nq, rising=rising)
     ts, tt = ops.flash_tiles(ql.tolist(), nq // nkv)
     C = lambda t: t.cuda()
     got = ops.flash_attention(C(q), C(kc), C(vc), C(bt), C(qs), C(ql), C(cx), C(torch.tensor(ts, dtype=torch.int32)),
