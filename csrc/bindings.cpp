@@ -225,7 +225,7 @@ void flash_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::T
   for (auto* t : {&block_tables, &qstart, &qlen, &ctx, &tile_seq, &tile_tok0}) check_i32(*t, "attention metadata");
   TORCH_CHECK(q.dim() == 3 && q.is_contiguous() && out.is_contiguous() && out.sizes() == q.sizes(), "q/out [T, nq, d]");
   const int nq = q.size(1), d = q.size(2);
-  TORCH_CHECK(d == 64 || d == 128, "flash prefill: head_dim 64 or 128");
+  TORCH_CHECK(d == 64 || d == 96 || d == 128, "flash prefill: head_dim 64, 96 or 128");
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.dim() == 4 && kc.size(2) == 16 && kc.size(3) == d &&
                   vc.size(2) == d && vc.size(3) == 16,
               "cache layout");

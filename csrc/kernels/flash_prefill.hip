@@ -5,6 +5,7 @@
 // tile covers 256 / G tokens and every K/V byte it reads serves all G heads of the group.  Eight
 // waves (two per SIMD) own 32 rows each.  Per 64-key chunk (four 16-token KV blocks) the WORKGROUP
 // stages K and V^T once into LDS and all eight waves consume them.
+// Head dims 64, 96 (Phi-3) and 128.
 //
 // Math per wave and chunk, on the 32x32x16 bf16 MFMA (cdna_hip_programming.md §3 operand maps):
 //   S^T[32 keys][32 rows] = K . Q^T          two key blocks, D/16 k-steps each
@@ -63,10 +64,14 @@ __device__ __forceinline__ void sync_lds() {
   asm volatile("" ::: "memory");
 }
 
-// 16-B chunk position of chunk c of K row r in the swizzled image
+// 16-B chunk position of chunk c of K row r in the swizzled image: 16 consecutive rows reading
+// one chunk hit 16 distinct 16-B bank slots (256-B / 128-B rows: XOR over the 16 / 8 chunks;
+// 192-B rows (d=96, 12 chunks): the row start cycles through 4 slots, so XOR inside aligned
+// groups of 4 chunks with (r >> 2) & 3)
 template <int D>
 __device__ __forceinline__ int kswz(int r, int c) {
   if constexpr (D == 128) return c ^ (r & 15);
+  else if constexpr (D == 96) return c ^ ((r >> 2) & 3);
   else return c ^ ((r >> 1) & 7);
 }
 // in-chunk key held by K image row rho: bits 2 and 3 swapped (an involution)
@@ -74,8 +79,8 @@ __device__ __forceinline__ int kperm(int rho) { return (rho & ~12) | ((rho & 4) 
 // in-block key of S^T accumulator register i of lane half h (C row (i&3) + 8(i>>2) + 4h, permuted)
 __device__ __forceinline__ int keyoff(int i, int h) { return (i & 7) | (h << 3) | ((i & 8) << 1); }
 
-template <int D>
-__global__ void __launch_bounds__(512) flash_prefill_kernel(FlashArgs a) {
+template <int D, int MINW>
+__global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   constexpr int KD = D / 16;            // k-steps of S^T
   constexpr int NB = D / 32;            // 32-dim blocks of O^T
   constexpr int KBYTES = CK * D * 2;    // K chunk: 64 rows x D
@@ -83,7 +88,7 @@ __global__ void __launch_bounds__(512) flash_prefill_kernel(FlashArgs a) {
   constexpr int STAGE = KBYTES + VBYTES;
   constexpr int GI = STAGE / 1024 / NWAVES;  // 1-KB global_load_lds pieces per wave per chunk
   static_assert(STAGE % (1024 * NWAVES) == 0, "whole 1-KB pieces per wave");
-  static_assert(KBYTES % 1024 == 0 && 1024 % (2 * D) == 0, "a K piece covers whole rows of one block");
+  static_assert(KBYTES % 1024 == 0, "K and V^T pieces do not share a 1-KB piece");
   __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + MAXBT * 4];
   int* s_bt = reinterpret_cast<int*>(smem + STAGES * STAGE);
 
@@ -267,9 +272,12 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   FlashArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
               tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, num_tiles, scale * LOG2E_F};
   const dim3 grid((unsigned)num_tiles * (unsigned)nkv);
+  // d=64: 4 waves per SIMD (<= 128 VGPRs, 52 KB LDS) = two workgroups per CU; measured 1.14-1.17x
+  // over one at 2k-16k tokens (profiles/r2_flash_prefill_microbench.md)
   switch (d) {
-    case 64: hipLaunchKernelGGL(flash_prefill_kernel<64>, grid, dim3(64 * NWAVES), 0, stream, a); break;
-    case 128: hipLaunchKernelGGL(flash_prefill_kernel<128>, grid, dim3(64 * NWAVES), 0, stream, a); break;
+    case 64: hipLaunchKernelGGL((flash_prefill_kernel<64, 4>), grid, dim3(64 * NWAVES), 0, stream, a); break;
+    case 96: hipLaunchKernelGGL((flash_prefill_kernel<96, 2>), grid, dim3(64 * NWAVES), 0, stream, a); break;
+    case 128: hipLaunchKernelGGL((flash_prefill_kernel<128, 2>), grid, dim3(64 * NWAVES), 0, stream, a); break;
     default: return -4;
   }
   return (int)hipGetLastError();

@@ -282,7 +282,7 @@ if __name__ == "__main__":
             shapes = [tuple(int(v) for v in t.split("x")) + (False,) for t in os.environ["MB_TUNE_SHAPES"].split(",")]
         G.autotune(shapes, ms, "cuda", verbose=True)
     if "flash" in what:
-        for (nq, nkv, d) in ((32, 4, 64), (32, 8, 128)):
+        for (nq, nkv, d) in ((32, 4, 64), (32, 8, 128), (32, 32, 96)):
             for L in (1024, 4096, 16384):
                 print(json.dumps(bench_flash(L, nq, nkv, d)), flush=True)
             print(json.dumps(bench_flash(2048, nq, nkv, d, B=8)), flush=True)

@@ -1,6 +1,6 @@
 """Flash-style prefill attention (csrc/kernels/flash_prefill.hip) against the fp32 PyTorch
 reference (ops.reference.paged_attention): ragged batches, cached prefixes (chunked prefill),
-causal and bidirectional, GQA groups 1/4/8/16/32, head dims 64/128, scores whose running max
+causal and bidirectional, GQA groups 1/4/8/16/32, head dims 64/96/128, scores whose running max
 keeps rising (the online-softmax rescale path), and never-written cache tails poisoned with NaN
 (they must not leak into the output)."""
 import math
@@ -43,7 +43,7 @@ def _case(d, nq, nkv, seqs, seed=0, rising=False):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("d,nq,nkv", [(64, 32, 4), (128, 32, 8), (128, 8, 8), (64, 8, 1), (128, 64, 4), (64, 64, 2)])
+@pytest.mark.parametrize("d,nq,nkv", [(64, 32, 4), (128, 32, 8), (128, 8, 8), (64, 8, 1), (128, 64, 4), (64, 64, 2), (96, 32, 32)])
 @pytest.mark.parametrize("rising", [False, True])
 def test_flash_prefill_matches_fp32_reference(d, nq, nkv, causal, rising):
     seqs = [(300, 300), (37, 37), (200, 777), (129, 129), (1, 50), (16, 33)]
