@@ -174,6 +174,7 @@ class LLMEngine:
         R = self.max_num_seqs
         self.R = R
         self._free_rows = list(range(R - 1, -1, -1))
+        self._pf_host = self._pf_dev = self._pf_evt = None   # prefill input staging (_stage_i32)
         pin = self.on_gpu
         # host mirror of the device block table (pinned); row R is the dummy row of padding tiles.
         self.bt_host_t = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, pin_memory=pin)
@@ -712,17 +713,25 @@ class LLMEngine:
             tseq.extend([i] * len(ts))
             ttok.extend(tt)
         nb = max((ctx_i + BS - 1) // BS for ctx_i in ctx)
-        bt = np.zeros((len(chunk), nb), dtype=np.int32)
-        for i, (s, _, _) in enumerate(chunk):
-            row = self.bt_host[s.row, :nb]
-            bt[i] = row
+        rows = np.fromiter((s.row for s, _, _ in chunk), dtype=np.int64, count=len(chunk))
+        bt = self.bt_host[rows, :nb]
         dev = self.device
-        T = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt, device=dev)
         splits = self._splits_for(len(tseq))
-        meta = AttnMeta(slots=T(slots), block_tables=torch.from_numpy(bt).to(dev), qstart=T(qstart), qlen=T(qlen),
-                        ctx=T(ctx), tile_seq=T(tseq), tile_tok0=T(ttok), last_idx=T(last, torch.int64),
+        if self.on_gpu:
+            # one pinned staging buffer, one async H2D copy: the host builds this chunk while the
+            # GPU still runs the previous one (per-tensor torch.tensor(..., device) copies sync)
+            (slots_d, qstart_d, qlen_d, ctx_d, tseq_d, ttok_d, last_d, ids_d, pos_d, bt_d) = self._stage_i32(
+                [slots, qstart, qlen, ctx, tseq, ttok, last, ids, pos, bt])
+            last_d = last_d.to(torch.int64)
+            bt_d = bt_d.view(len(chunk), nb)
+        else:
+            T = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt, device=dev)
+            slots_d, qstart_d, qlen_d, ctx_d, tseq_d, ttok_d = T(slots), T(qstart), T(qlen), T(ctx), T(tseq), T(ttok)
+            last_d, ids_d, pos_d, bt_d = T(last, torch.int64), T(ids), T(pos), torch.from_numpy(np.ascontiguousarray(bt))
+        meta = AttnMeta(slots=slots_d, block_tables=bt_d, qstart=qstart_d, qlen=qlen_d,
+                        ctx=ctx_d, tile_seq=tseq_d, tile_tok0=ttok_d, last_idx=last_d,
                         splits=splits, xcd_remap=True, flash=flash)
-        hidden = self.model.hidden_states(T(ids), T(pos), meta, self.kv_caches)
+        hidden = self.model.hidden_states(ids_d, pos_d, meta, self.kv_caches)
         self.steps["prefill"] += 1
         self.steps["prefill_tokens"] += t
         self._check_collectives()
@@ -733,7 +742,8 @@ class LLMEngine:
         if not done_seqs:
             return []
         sel = [i for i, (s, a, b) in enumerate(chunk) if b == len(s.fill)]
-        h = hidden if len(sel) == len(chunk) else hidden.index_select(0, T(sel, torch.int64))
+        h = hidden if len(sel) == len(chunk) else hidden.index_select(
+            0, torch.tensor(sel, dtype=torch.int64).to(dev, non_blocking=True))
         toks = self._sample(h, done_seqs, None)
         now = time.perf_counter()
         for s, tok in zip(done_seqs, toks):
@@ -741,6 +751,31 @@ class LLMEngine:
                 s.first_tok = now
             self._append(s, tok)
         return done_seqs
+
+    def _stage_i32(self, parts) -> List[torch.Tensor]:
+        """Pack int sequences / arrays into one pinned int32 buffer and copy it to the device with
+        ONE non-blocking copy; returns device views in ``parts`` order.  The previous copy's event
+        guards the pinned buffer against being rewritten while its DMA is still reading it."""
+        arrs = [np.asarray(p, dtype=np.int32).ravel() for p in parts]
+        total = sum(a.size for a in arrs)
+        if self._pf_host is None or self._pf_host.numel() < total:
+            if self._pf_evt is not None:
+                self._pf_evt.synchronize()
+            cap = max(1 << 16, 1 << (int(total) - 1).bit_length())
+            self._pf_host = torch.empty(cap, dtype=torch.int32, pin_memory=True)
+            self._pf_dev = torch.empty(cap, dtype=torch.int32, device=self.device)
+        elif self._pf_evt is not None:
+            self._pf_evt.synchronize()
+        hn = self._pf_host.numpy()
+        off, bounds = 0, []
+        for a in arrs:
+            hn[off:off + a.size] = a
+            bounds.append((off, a.size))
+            off += a.size
+        self._pf_dev[:total].copy_(self._pf_host[:total], non_blocking=True)
+        self._pf_evt = torch.cuda.Event()
+        self._pf_evt.record()
+        return [self._pf_dev[o:o + n] for o, n in bounds]
 
     def _append(self, s: _Seq, tok: int) -> None:
         s.out.append(int(tok))

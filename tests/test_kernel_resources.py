@@ -14,7 +14,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-KERNELS = ["attention.hip", "gemv.hip", "skinny_gemm.hip", "skinny_lds.hip", "mm_gemm.hip", "sampling.hip", "moe.hip"]
+KERNELS = ["attention.hip", "gemv.hip", "skinny_gemm.hip", "skinny_lds.hip", "mm_gemm.hip", "sampling.hip", "moe.hip",
+           "flash_prefill.hip", "decode_attn.hip", "tgemm.hip", "encoder.hip"]
+# measured exceptions (bytes/lane allowed): the d=64 flash prefill at 4 waves per SIMD (128-VGPR cap,
+# two workgroups per CU) keeps ~5 values in scratch around the chunk loop and is still 1.14-1.17x
+# faster than the spill-free one-workgroup build (profiles/r2_flash_prefill_microbench.md)
+ALLOW = {r"flash_prefill_kernelILi64ELi4E": 32}
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
@@ -28,5 +33,6 @@ def test_no_scratch_spills(src, tmp_path):
     names = re.findall(r"Function Name: (\S+)", r.stderr)
     scratch = [int(x) for x in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", r.stderr)]
     assert names and len(names) == len(scratch)
-    spilled = [(n, s) for n, s in zip(names, scratch) if s > 0]
+    budget = lambda n: max([v for k, v in ALLOW.items() if re.search(k, n)] or [0])
+    spilled = [(n, s) for n, s in zip(names, scratch) if s > budget(n)]
     assert not spilled, f"scratch spills: {spilled}"
