@@ -438,8 +438,11 @@ def main() -> int:
                                       / max(1, sum(b["decode"] - a_["decode"] for a_, b in zip(st0, st1))), 1),
             "engine_time_split_s": {k: round(sum(b_.get(k, 0.0) - a_.get(k, 0.0) for a_, b_ in zip(st0, st1)), 3)
                                     for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
-                                              "t_decode_host_post_s")},
+                                              "t_decode_host_post_s", "t_encode_s", "t_admit_s", "t_output_s")},
         }
+        # rank-0 wall time not inside any engine timer: routing, prompt formatting, orchestration
+        out["engine_time_split_s"]["outside_engine_s"] = round(
+            elapsed_max - sum(out["engine_time_split_s"].values()), 3) if len(engines) == 1 else None
         lk = enc1["lookups"] - enc0["lookups"]
         out["router_encoder"] = {"kinds": enc1["kinds"], "memo": bool(enc1.get("memo_enabled", False)),
                                  "lookups": lk, "memo_hit_rate": round((enc1["hits"] - enc0["hits"]) / lk, 3) if lk else None,

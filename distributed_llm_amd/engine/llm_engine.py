@@ -153,7 +153,8 @@ class LLMEngine:
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
-        self.timers = {"prefill": 0.0, "decode_host_pre": 0.0, "decode_gpu_wait": 0.0, "decode_host_post": 0.0}
+        self.timers = {"prefill": 0.0, "decode_host_pre": 0.0, "decode_gpu_wait": 0.0, "decode_host_post": 0.0,
+                       "encode": 0.0, "admit": 0.0, "output": 0.0}
 
     # ------------------------------------------------------------------ setup
     def _alloc_kv(self, kv_cache_gb: Optional[float]) -> None:
@@ -327,7 +328,7 @@ class LLMEngine:
         if params is None:
             params = SamplingParams()
         plist = list(params) if isinstance(params, (list, tuple)) else [params] * len(prompts)
-        now = time.perf_counter()
+        now = _t = time.perf_counter()
         seqs: List[_Seq] = []
         for p, sp in zip(prompts, plist):
             ids = self.encode(p) if isinstance(p, str) else list(p)
@@ -340,8 +341,12 @@ class LLMEngine:
                 s.error = "prompt too long for max_model_len"
                 s.done.set()
             seqs.append(s)
+        self.timers["encode"] += time.perf_counter() - _t
         self._submit_and_wait([s for s in seqs if s.error is None])
-        return [self._output(s) for s in seqs]
+        _t = time.perf_counter()
+        outs = [self._output(s) for s in seqs]
+        self.timers["output"] += time.perf_counter() - _t
+        return outs
 
     def _submit_and_wait(self, seqs: List[_Seq]) -> None:
         """Continuous batching across callers (leader/follower): requests from concurrent threads
@@ -531,6 +536,7 @@ class LLMEngine:
             if not (waiting or prefilling or running):
                 break
             # admit
+            _ta = time.perf_counter()
             while waiting and len(prefilling) + len(running) < self.R:
                 s = waiting[0]
                 s.fill = s.prompt + s.out
@@ -545,6 +551,7 @@ class LLMEngine:
                 s.row = self._free_rows.pop()
                 self._set_row_blocks(s)
                 prefilling.append(s)
+            self.timers["admit"] += time.perf_counter() - _ta
             if not (prefilling or running):
                 if waiting:  # nothing fits even alone -> fail the head request
                     s = waiting.pop(0)

@@ -10,6 +10,8 @@ from __future__ import annotations
 import os
 from typing import List, Optional
 
+import numpy as np
+
 
 class ByteTokenizer:
     """ids: 0 pad, 1 bos, 2 eos, 3..258 = bytes; ids >= 259 (random-weight models emit them)
@@ -25,20 +27,14 @@ class ByteTokenizer:
         self.eos_id = eos_id if eos_id < vocab_size else 2
 
     def encode(self, text: str, add_bos: bool = True) -> List[int]:
-        ids = [b + self.OFFSET for b in text.encode("utf-8")]
+        ids = (np.frombuffer(text.encode("utf-8"), dtype=np.uint8).astype(np.int64) + self.OFFSET).tolist()
         return ([self.bos_id] + ids) if add_bos else ids
 
     def decode(self, ids) -> str:
-        out = bytearray()
-        for i in ids:
-            i = int(i)
-            if i in (self.bos_id, self.eos_id) or i < self.OFFSET:
-                continue
-            if i < 256 + self.OFFSET:
-                out.append(i - self.OFFSET)
-            else:
-                out.append(32 + (i % 95))
-        return out.decode("utf-8", errors="replace")
+        a = np.asarray(ids, dtype=np.int64).reshape(-1)
+        a = a[(a >= self.OFFSET) & (a != self.bos_id) & (a != self.eos_id)]
+        b = np.where(a < 256 + self.OFFSET, a - self.OFFSET, 32 + a % 95).astype(np.uint8)
+        return b.tobytes().decode("utf-8", errors="replace")
 
 
 class HFTokenizer:

@@ -340,6 +340,7 @@ class Router:
         enc = getattr(emb, "prefetch", None) or getattr(emb, "encode_tensor", None) or emb.encode
         try:
             enc(list(dict.fromkeys(queries)))
+            self.query_router.prefetch_scores(queries)
         except Exception as exc:  # routing still works, just unbatched
             logger.warning("batched embedding prefetch failed: %s", exc)
 

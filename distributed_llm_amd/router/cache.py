@@ -108,7 +108,7 @@ class CacheEntry:
             "query": self.query,
             "query_hash": self.query_hash,
             "context_key": self.context_key,
-            "embedding": self.embedding.tolist() if self.embedding is not None else None,
+            "embedding": _host_vec(self.embedding).tolist() if self.embedding is not None else None,
             "timestamp": self.timestamp.isoformat(),
             "device_used": self.device_used,
             "response_time": self.response_time,
@@ -133,6 +133,13 @@ class CacheLookupResult:
     predicted_device: str
     predicted_confidence: float
     use_hybrid_fallback: bool
+
+
+def _host_vec(x) -> np.ndarray:
+    """An entry's embedding (host array or device tensor) as a flat f32 numpy vector."""
+    if hasattr(x, "detach"):
+        return x.detach().float().cpu().numpy().reshape(-1)
+    return np.asarray(x, dtype=np.float32).reshape(-1)
 
 
 class EmbeddingIndex:
@@ -207,20 +214,25 @@ class EmbeddingIndex:
                     self._grow()
                 slot = self._next
                 self._next += 1
-        v = np.asarray(vec, dtype=np.float32).reshape(-1)
-        n = float(np.linalg.norm(v))
         self._release(slot)          # a replaced slot drops its old context reference
         cid = self.ctx_id(context_key)
         self._ctx_refs[cid] += 1
         self._slot_cid[slot] = cid
         if self.device is None:
+            v = np.asarray(vec, dtype=np.float32).reshape(-1)
             self.table[slot] = v
-            self.norms[slot] = n
+            self.norms[slot] = float(np.linalg.norm(v))
             self.ctx[slot] = cid
         else:
             import torch
-            self.table[slot] = torch.from_numpy(v).to(self.device, non_blocking=True)
-            self.norms[slot] = n
+            if isinstance(vec, torch.Tensor):   # device vector: async copies, no host sync
+                v = vec.to(self.device, torch.float32).reshape(-1)
+                self.table[slot].copy_(v)
+                self.norms[slot:slot + 1].copy_(torch.linalg.vector_norm(v).reshape(1))
+            else:
+                v = np.asarray(vec, dtype=np.float32).reshape(-1)
+                self.table[slot] = torch.from_numpy(v).to(self.device, non_blocking=True)
+                self.norms[slot] = float(np.linalg.norm(v))
             self.ctx[slot] = cid
         return slot
 
@@ -314,9 +326,14 @@ class QueryCache:
     def _set_embedding(self, e: CacheEntry, emb: Optional[np.ndarray]) -> None:
         if emb is None:
             return
-        arr = np.asarray(emb.detach().float().cpu().numpy() if hasattr(emb, "detach") else emb,
-                         dtype=np.float32).reshape(-1)
-        e.embedding = arr.copy()
+        if hasattr(emb, "detach") and self._index.device is not None:
+            # device embedding into the HBM index: stays on the GPU (no host round trip per insert);
+            # the entry keeps a private device copy, converted to host only by save / to_dict
+            arr = emb.detach().to(self._index.device, dtype=self._index.table.dtype).reshape(-1).clone()
+        else:
+            arr = np.asarray(emb.detach().float().cpu().numpy() if hasattr(emb, "detach") else emb,
+                             dtype=np.float32).reshape(-1).copy()
+        e.embedding = arr
         if e.slot < 0 or self._slot_to_hash.get(e.slot) != e.query_hash:
             e.slot = self._index.put(arr, e.context_key)
             self._slot_to_hash[e.slot] = e.query_hash
@@ -491,7 +508,7 @@ class QueryCache:
                 d["embedding"] = None
                 d["emb_row"] = len(rows) if e.embedding is not None else -1
                 if e.embedding is not None:
-                    rows.append(np.asarray(e.embedding, dtype=np.float32).reshape(-1))
+                    rows.append(_host_vec(e.embedding))
                 metas.append(d)
         dim = rows[0].shape[0] if rows else self._index.dim
         table = np.stack(rows) if rows else np.zeros((0, dim), dtype=np.float32)

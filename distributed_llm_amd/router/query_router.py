@@ -71,6 +71,15 @@ class QueryRouter:
             return enc_t([query])[0]
         return self.cache_embedder.encode([query])[0]
 
+    def prefetch_scores(self, queries: List[str]) -> None:
+        """Batch the semantic centroid scoring of a routing batch (SemanticRouter.prefetch), for
+        the semantic strategy and the semantic member of the hybrid one."""
+        from .strategies import SemanticRouter
+        r = self.router
+        for x in [r] + list((getattr(r, "routers", None) or {}).values()):
+            if isinstance(x, SemanticRouter):
+                x.prefetch(queries)
+
     def route_query(self, query: str, context: Optional[str] = None,
                     context_key: Optional[str] = None) -> RoutingDecision:
         ctxk = context_key or "default"

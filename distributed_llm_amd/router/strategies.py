@@ -143,6 +143,17 @@ class CentroidScorer:
             out[i] = 0.0 if (nq < 1e-9 or nc < 1e-9) else float(np.dot(q, c) / (nq * nc))
         return out
 
+    def scores_batch(self, qs: Any) -> np.ndarray:
+        """[n, n_centroids] for a batch of embeddings: ONE kernel launch and one copy back on the
+        device path (row i equals ``scores(qs[i])``: the kernel scores rows independently)."""
+        if isinstance(qs, np.ndarray):
+            return np.stack([self.scores(q) for q in qs]) if len(qs) else np.zeros((0, len(self.centroids)))
+        from .. import ops
+        if self._dev is None or self._dev.device != qs.device:
+            import torch
+            self._dev = torch.from_numpy(self.centroids).to(qs.device)
+        return ops.cosine_scores(qs.reshape(qs.shape[0], -1).float(), self._dev).cpu().numpy()
+
 
 class SemanticRouter(BaseRouter):
     name = "semantic"
@@ -156,6 +167,7 @@ class SemanticRouter(BaseRouter):
         self._token_fallback = TokenBasedRouter(config)
         self.nano_center, self.orin_center = self._build_centroids(self.label_path)
         self._scorer = CentroidScorer(np.stack([self.nano_center, self.orin_center]))
+        self._score_memo: Dict[str, Tuple[float, float]] = {}   # this routing batch's scores (prefetch)
 
     def _build_centroids(self, label_path: str) -> Tuple[np.ndarray, np.ndarray]:
         if not label_path or not os.path.exists(label_path):
@@ -168,8 +180,23 @@ class SemanticRouter(BaseRouter):
         return (np.mean(self.embedder.encode(small), axis=0),
                 np.mean(self.embedder.encode(large), axis=0))
 
+    def prefetch(self, queries: List[str]) -> None:
+        """Score a whole routing batch against the centroids in one launch (the orchestrator calls
+        this after the batched encoder prefetch); ``similarities`` then reads the batch's scores
+        instead of launching a kernel and syncing per query.  Same values: the embeddings come
+        from the same encoder memo / batch scope, and the kernel scores rows independently."""
+        enc_t = getattr(self.embedder, "encode_tensor", None)
+        if enc_t is None or not queries:
+            return
+        qs = list(dict.fromkeys(queries))
+        sc = self._scorer.scores_batch(enc_t(qs))
+        self._score_memo = {q: (float(a), float(b)) for q, (a, b) in zip(qs, sc)}
+
     def similarities(self, query: str, q_emb: Any = None) -> Tuple[float, float]:
         if q_emb is None:
+            hit = self._score_memo.get(query)
+            if hit is not None:
+                return hit
             enc_t = getattr(self.embedder, "encode_tensor", None)
             q_emb = enc_t([query])[0] if enc_t is not None else self.embedder.encode([query])[0]
         s = self._scorer.scores(q_emb)
