@@ -498,7 +498,7 @@ void moe_ffn_tg(torch::Tensor x, torch::Tensor ids, torch::Tensor wts, torch::Te
     const int bn = (int)plan[1 + 4 * g], st = (int)plan[2 + 4 * g], ks = (int)plan[3 + 4 * g], nw = (int)plan[4 + 4 * g];
     TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)) &&
                     (st == 2 || st == 3 || ((st == 4 || st == 6) && ks == 1 && bm <= 128)) &&
-                    (bm == 64 || bm == 128 || (bm == 256 && nw == 8)) &&
+                    (bm == 64 || bm == 128 || ((bm == 192 || bm == 256) && nw == 8)) &&
                     (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) && st * ks * (bm + bn) * 128 <= 150 * 1024,
                 "moe plan tile / ring size");
     TORCH_CHECK((g == 0 ? H : I) % (64 * ks) == 0, "K % (64 ks)");
@@ -605,7 +605,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK(wk == 1 || (wk == 2 && nw == 4 && ks == 2 && stages <= 3 && bm <= 128 && bn <= 128),
               "wk 2: two k-groups of 4 waves, ks 2, 2-3 stages, tiles up to 128 x 128");
   TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
-  TORCH_CHECK((bm == 64 || bm == 128 || (bm == 256 && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
+  TORCH_CHECK((bm == 64 || bm == 128 || ((bm == 192 || bm == 256) && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
                   (stages == 2 || stages == 3 || ((stages == 4 || stages == 6) && ks == 1 && bm <= 128)) &&
                   (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024,
               "tile / ring size");

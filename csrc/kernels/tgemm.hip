@@ -129,9 +129,10 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   constexpr bool ROWSCALE = (EPI == EPI_QKV || EPI == EPI_SWIGLU || EPI == EPI_PLAIN);
   const bool has_rs = ROWSCALE && a.ssq_in != nullptr;
   const int rs_row = threadIdx.x % BM, rs_part = threadIdx.x / BM;
+  const bool rs_on = rs_part < TPR;  // BM = 192 with 512 threads: the last 128 threads sit out
   const int rs_m = min(m0 + rs_row, M - 1);
   float ssv[8];
-  if (has_rs) {
+  if (has_rs && rs_on) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int s = rs_part + TPR * u;
@@ -183,7 +184,7 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   for (int t = 0; t < STAGES - 1; ++t)
     if (t < nk) issue(t);
 
-  if (has_rs) {
+  if (has_rs && rs_on) {
     float s = 0.f;
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += ssv[u];
@@ -492,6 +493,7 @@ int by_tile(int bm, int bn, int stages, int ks, int nw, int wk, const GemmArgs& 
   } else if (nw == 8) {
     if (bm == 64 && bn == 128) return by_pipe_deep<64, 128, EPI, 8>(stages, ks, a, st);
     if (bm == 128 && bn == 128) return by_pipe_deep<128, 128, EPI, 8>(stages, ks, a, st);
+    if (bm == 192 && bn == 128) return by_pipe<192, 128, EPI, 8>(stages, ks, a, st);
     if (bm == 256 && bn == 128) return by_pipe<256, 128, EPI, 8>(stages, ks, a, st);
     if (bm == 256 && bn == 256) return by_pipe<256, 256, EPI, 8>(stages, ks, a, st);
   }

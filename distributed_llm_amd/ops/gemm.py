@@ -45,7 +45,8 @@ _MM_NTS = (2, 4)
 _MM_SPLITS = (1, 2, 4, 8)
 _GEMV_MS = (1, 2, 4, 8)   # csrc/kernels/gemv.hip instantiations (decode buckets below 16)
 _GEMV_RS = (1, 2, 4)
-_TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8), (128, 128, 8), (256, 128, 8),
+_TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8), (128, 128, 8), (192, 128, 8),
+             (256, 128, 8),
              (256, 256, 8))
 _TG_SPLITS = (1, 2, 3, 4, 6, 8)
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
@@ -469,7 +470,7 @@ def _tg_cands(M: int, N: int, K: int):
         return []
     out = []
     for bm, bn, nw in _TG_TILES:
-        if (bm == 128 and M <= 64) or (bm == 256 and M <= 128):
+        if (bm == 128 and M <= 64) or (bm >= 192 and M <= 128):
             continue
         tiles = -(-M // bm) * -(-N // bn)
         for ks in (1, 2):
