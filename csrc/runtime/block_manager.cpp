@@ -23,6 +23,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def("append_token", &BlockManager::append_token)
       .def("slots", &BlockManager::slots)
       .def("commit_append", &BlockManager::commit_append)
+      .def("set_last_tokens", &BlockManager::set_last_tokens)
       .def("commit", &BlockManager::commit)
       .def("block_table", &BlockManager::block_table)
       .def("seq_len", &BlockManager::seq_len)

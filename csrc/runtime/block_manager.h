@@ -144,6 +144,19 @@ class BlockManager {
     return out;
   }
 
+  // Pipelined decode: commit_append ran with a placeholder for a token still being sampled on
+  // the GPU; write the real token before that position is committed (hashed into the prefix
+  // cache).  Only the LAST token of each sequence may be rewritten, and only if uncommitted.
+  void set_last_tokens(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks) {
+    if (ids.size() != toks.size()) throw std::invalid_argument("ids / toks size mismatch");
+    for (size_t i = 0; i < ids.size(); ++i) {
+      Seq& s = get(ids[i]);
+      if (s.tokens.empty() || s.committed >= (int)s.tokens.size())
+        throw std::logic_error("set_last_tokens: last token already committed");
+      s.tokens.back() = toks[i];
+    }
+  }
+
   // Slots of token positions [start, end) of a sequence.
   std::vector<int> slots(int64_t id, int start, int end) {
     Seq& s = get(id);

@@ -194,9 +194,13 @@ class LLMEngine:
              s0 + 3 * mb + 1]
         self._dec_n = o[8] + 1 + 2 * R
         self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
-        self.dec_host_t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
-        self.dec_host = self.dec_host_t.numpy()
-        self.dec_host_f = self.dec_host.view(np.float32)
+        # two pinned staging buffers: the pipelined decode (_decode_burst) fills one while the
+        # previous step's async copy may still be reading the other
+        self._dec_bufs = []
+        for _ in range(2):
+            t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
+            self._dec_bufs.append((t, t.numpy(), t.numpy().view(np.float32)))
+        self.dec_host_t, self.dec_host, self.dec_host_f = self._dec_bufs[0]
         self._off = o
         self._so = s0
         # the whole sampler runs inside the decode graph (ops.sample_rows) unless the vocab is
@@ -217,6 +221,10 @@ class LLMEngine:
         self.d_tok0 = torch.zeros(mb, dtype=torch.int32, device=self.device)
         self.d_last = torch.arange(mb, dtype=torch.int64, device=self.device)
         self.d_out = torch.zeros(mb, dtype=torch.int32, device=self.device)
+        self.d_src = torch.zeros(mb, dtype=torch.int64, device=self.device)   # pipelined: id gather rows
+        self._out_bufs = [torch.zeros(mb, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._src_bufs = [torch.zeros(mb, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
+        self._out_evts = [torch.cuda.Event() for _ in range(2)] if self.on_gpu else None
         self.d_hidden = torch.zeros((mb, self.cfg.hidden), dtype=self.model.dtype, device=self.device)
         nkv, dh = self.model.nkv, self.model.d
         self.max_splits = 16
@@ -228,8 +236,11 @@ class LLMEngine:
         self.attn_worklist = self.ATTN_WORKLIST and not self.ATTN_DYNAMIC
         if self.attn_worklist:
             cap = 1 + 2 * mb * nkv * self.max_splits
-            self.items_host_t = torch.zeros(cap, dtype=torch.int32, pin_memory=pin)
-            self.items_host = self.items_host_t.numpy()
+            self._items_bufs = []
+            for _ in range(2):
+                t = torch.zeros(cap, dtype=torch.int32, pin_memory=pin)
+                self._items_bufs.append((t, t.numpy()))
+            self.items_host_t, self.items_host = self._items_bufs[0]
             self.items_dev = torch.zeros(cap, dtype=torch.int32, device=self.device)
 
     def _autotune(self) -> None:
@@ -577,7 +588,10 @@ class LLMEngine:
                         running.append(s)
                 continue
             with tracer.span("engine.decode", "engine", batch=len(running)):
-                finished, preempted = self._decode_step(running)
+                if self._pipeline_ok():
+                    finished, preempted = self._decode_burst(running, waiting)
+                else:
+                    finished, preempted = self._decode_step(running)
             if tracer.enabled:
                 tracer.counter("engine.batch", running=len(running), waiting=len(waiting),
                                free_kv_blocks=self.bm.num_free_blocks())
@@ -805,19 +819,24 @@ class LLMEngine:
                 return b
         raise ValueError(f"batch {n} exceeds max_num_seqs")
 
-    def _decode_step(self, running: List[_Seq]) -> Tuple[List[_Seq], List[_Seq]]:
-        _t0 = time.perf_counter()
+    def _prep_decode(self, running: List[_Seq], lens: np.ndarray, last: Optional[np.ndarray], p: int) -> int:
+        """Stage one decode step's inputs in pinned buffer ``p`` and copy them to the device (async).
+
+        ``lens``: context length per row including the input token (position = lens - 1);
+        ``last``: the input token per row, or None when it is the previous step's sampled token
+        still on the device (pipelined decode: ``_decode_burst`` gathers it from ``d_out``).
+        Returns the step's bucket."""
         B = len(running)
         bs = self._bucket(B)
-        o, h = self._off, self.dec_host
+        o = self._off
+        _, h, hf = self._dec_bufs[p]
         R = self.R
         rows = np.fromiter((s.row for s in running), dtype=np.int64, count=B)
-        lens = np.fromiter((s.length for s in running), dtype=np.int64, count=B)
-        last = np.fromiter((s.out[-1] for s in running), dtype=np.int64, count=B)
         pos = lens - 1
         blocks = self.bt_host[rows, pos // BS].astype(np.int64)
         h[o[0]:o[0] + bs] = 0
-        h[o[0]:o[0] + B] = last
+        if last is not None:
+            h[o[0]:o[0] + B] = last
         h[o[1]:o[1] + bs] = 0
         h[o[1]:o[1] + B] = pos
         h[o[2]:o[2] + bs] = -1
@@ -829,8 +848,9 @@ class LLMEngine:
         if self._use_worklist(bs):
             grid = self._attn_grid(bs)
             target = 4096 if self.DECODE_WAVE else self.ATTN_ITEMS_PER_WG * grid
-            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target, out=self.items_host)
-            n_items = 1 + 2 * int(self.items_host[0])
+            items_t, items = self._items_bufs[p]
+            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target, out=items)
+            n_items = 1 + 2 * int(items[0])
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)
         h[o[5] + rows] = 1
@@ -838,15 +858,23 @@ class LLMEngine:
         self._sync_bt()
         h[o[7]] = self._split_len(int(lens.sum()))
         if self.fused_sampler:
-            self._fill_sampler(h, self.dec_host_f, self._so, self.buckets[-1], running, bs)
+            self._fill_sampler(h, hf, self._so, self.buckets[-1], running, bs)
         nu = len(self._bt_upd) // 2
         h[o[8]] = nu
         if nu:
             h[o[8] + 1:o[8] + 1 + 2 * nu] = self._bt_upd
             self._bt_upd.clear()
-        self.dec_dev[:o[8] + 1 + 2 * nu].copy_(self.dec_host_t[:o[8] + 1 + 2 * nu], non_blocking=True)
+        self.dec_dev[:o[8] + 1 + 2 * nu].copy_(self._dec_bufs[p][0][:o[8] + 1 + 2 * nu], non_blocking=True)
         if n_items:
-            self.items_dev[:n_items].copy_(self.items_host_t[:n_items], non_blocking=True)
+            self.items_dev[:n_items].copy_(self._items_bufs[p][0][:n_items], non_blocking=True)
+        return bs
+
+    def _decode_step(self, running: List[_Seq]) -> Tuple[List[_Seq], List[_Seq]]:
+        _t0 = time.perf_counter()
+        B = len(running)
+        lens = np.fromiter((s.length for s in running), dtype=np.int64, count=B)
+        last = np.fromiter((s.out[-1] for s in running), dtype=np.int64, count=B)
+        bs = self._prep_decode(running, lens, last, 0)
         _t1 = time.perf_counter()
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=self.use_graphs):
             if self.use_graphs:
@@ -899,6 +927,149 @@ class LLMEngine:
                 self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
         self.timers["decode_host_post"] += time.perf_counter() - _t2
         return finished, preempted
+
+    # Pipelined decode (default on the single-GPU graph path): while the GPU runs step k, the host
+    # already commits step k's input tokens, reserves the KV slots of the tokens step k is sampling,
+    # stages step k+1's inputs and launches it, taking step k's sampled tokens straight from the
+    # device (d_out -> d_ids gather); only then does it read step k's tokens back and run the stop
+    # checks.  The host work of a step hides under the GPU time of the previous one.  A sequence
+    # that stops on EOS at step k has already been launched in step k+1: that one row is computed
+    # and discarded (its KV slot belongs to the finished sequence).  Count limits (max_new_tokens,
+    # max_model_len) are known in advance and never cost a row.
+    PIPELINE = os.environ.get("DLLM_DECODE_PIPELINE", "1") == "1"
+
+    def _pipeline_ok(self) -> bool:
+        return (self.PIPELINE and self.on_gpu and self.use_graphs and self.fused_sampler and not self.par.enabled
+                and self._mirror is None)
+
+    def _replay(self, bs: int) -> None:
+        with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=True):
+            g = self._graphs.get(bs)
+            if g is None:
+                g = self._capture(bs)
+            g.replay()
+
+    def _read_out(self, B: int, p: int) -> "torch.cuda.Event":
+        self._out_bufs[p][:B].copy_(self.d_out[:B], non_blocking=True)
+        ev = self._out_evts[p]
+        ev.record()
+        return ev
+
+    def _decode_burst(self, running: List[_Seq], waiting: List[_Seq]) -> Tuple[List[_Seq], List[_Seq]]:
+        """Pipelined decode steps until the batch must change (a new request arrived, a waiting
+        request could take a freed row, or the batch is empty).  Same contract as ``_decode_step``:
+        returns (finished, preempted); the caller releases / re-queues them.  On return every
+        continuing sequence is in the non-pipelined state (its last token appended with a slot)."""
+        eos, mml, mb_ = self.tok.eos_id, self.max_model_len, self.max_blocks
+        finished: List[_Seq] = []
+        preempted: List[_Seq] = []
+        gone: set = set()           # id(s): finished / preempted inside this burst (rows still in flight are ignored)
+        _t0 = time.perf_counter()
+        cur = list(running)
+        lens = np.fromiter((s.length for s in cur), dtype=np.int64, count=len(cur))
+        last = np.fromiter((s.out[-1] for s in cur), dtype=np.int64, count=len(cur))
+        pc = 0
+        self._replay(self._prep_decode(cur, lens, last, pc))
+        ev = self._read_out(len(cur), pc)
+        self.steps["decode"] += 1
+        self.timers["decode_host_pre"] += time.perf_counter() - _t0
+        freed = False               # a row finished while requests wait for one: end the burst
+        while True:
+            _t0 = time.perf_counter()
+            alive = [s for s in cur if id(s) not in gone]
+            # the next step's rows: sequences that cannot reach a count limit with the token in flight
+            nxt = [s for s in alive if len(s.out) + 1 < s.params.max_new_tokens and s.length + 1 < mml]
+            stop = (not nxt or freed or bool(self._inbox) or (bool(waiting) and len(nxt) < len(alive)))
+            launched = None
+            pending_pre: set = set()
+            if not stop:
+                # commit the in-flight step's input tokens (all alive rows) and reserve the slot of
+                # the token each continuing row is sampling right now (placeholder, fixed in post)
+                nset = set(map(id, nxt))
+                app = [1 if id(s) in nset else 0 for s in alive]
+                slots = self.bm.commit_append([s.id for s in alive], [0] * len(alive), app)
+                run, src = [], []
+                idx = {id(s): i for i, s in enumerate(cur)}
+                for s, a, slot in zip(alive, app, slots):
+                    if not a:
+                        continue
+                    if slot < 0:            # out of KV blocks: preempt once its token is known
+                        pending_pre.add(id(s))
+                        continue
+                    if slot % BS == 0:      # the reserved position opens a new block
+                        nblk = (s.length + 1 + BS - 1) // BS
+                        blk = slot // BS
+                        if self.bt_host[s.row, nblk - 1] != blk:
+                            self.bt_host[s.row, nblk - 1] = blk
+                            self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
+                    run.append(s)
+                    src.append(idx[id(s)])
+                if run:
+                    pn = pc ^ 1
+                    B = len(run)
+                    lens = np.fromiter((s.length + 1 for s in run), dtype=np.int64, count=B)
+                    bs = self._prep_decode(run, lens, None, pn)
+                    # input ids = the in-flight step's sampled tokens, gathered on the device
+                    if src == list(range(B)):
+                        self.d_ids[:B].copy_(self.d_out[:B])
+                    else:
+                        sb = self._src_bufs[pn]
+                        sb[:B] = torch.as_tensor(src, dtype=torch.int64)
+                        self.d_src[:B].copy_(sb[:B], non_blocking=True)
+                        self.d_ids[:B] = self.d_out[self.d_src[:B]]
+                    self._replay(bs)
+                    launched = (run, pn, self._read_out(B, pn))
+                    self.steps["decode"] += 1
+            _t1 = time.perf_counter()
+            ev.synchronize()
+            toks = self._out_bufs[pc][:len(cur)].tolist()
+            _t2 = time.perf_counter()
+            fix_ids, fix_toks, done_now = [], [], []
+            for s, t in zip(cur, toks):
+                if id(s) in gone:
+                    continue                # a row computed after its sequence stopped
+                s.out.append(t)
+                self.steps["decode_tokens"] += 1
+                pp = s.params
+                if (len(s.out) >= pp.max_new_tokens or (not pp.ignore_eos and t == eos)
+                        or len(s.prompt) + len(s.out) >= mml):
+                    finished.append(s)
+                    gone.add(id(s))
+                    done_now.append(s)
+                elif id(s) in pending_pre:
+                    s.error = "__preempt__"
+                    preempted.append(s)
+                    gone.add(id(s))
+                elif launched is not None:
+                    fix_ids.append(s.id)
+                    fix_toks.append(t)
+            if fix_ids:
+                self.bm.set_last_tokens(fix_ids, fix_toks)
+            if launched is None:
+                # drain: the non-pipelined post for the last step (commit its inputs, append the
+                # real tokens of the rows that continue)
+                rows_ = [s for s in cur if id(s) not in gone or s in done_now]
+                cont = [id(s) not in gone for s in rows_]
+                slots = self.bm.commit_append([s.id for s in rows_], [s.out[-1] for s in rows_], cont)
+                for s, c, slot in zip(rows_, cont, slots):
+                    if not c or (slot >= 0 and slot % BS != 0):
+                        continue
+                    if slot < 0:
+                        s.error = "__preempt__"
+                        preempted.append(s)
+                        continue
+                    nblk = (s.length + BS - 1) // BS
+                    blk = slot // BS
+                    if self.bt_host[s.row, nblk - 1] != blk:
+                        self.bt_host[s.row, nblk - 1] = blk
+                        self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
+            self.timers["decode_host_pre"] += _t1 - _t0
+            self.timers["decode_gpu_wait"] += _t2 - _t1
+            self.timers["decode_host_post"] += time.perf_counter() - _t2
+            if launched is None:
+                return finished, preempted
+            freed = bool(waiting) and bool(done_now or preempted)
+            cur, pc, ev = launched
 
     def _check_collectives(self) -> None:
         """TP: a one-shot all-reduce that timed out on any rank fails this step (every rank the

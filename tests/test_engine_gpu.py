@@ -79,3 +79,70 @@ def test_tinyllama_generate_and_sampling():
     assert [o.num_generated for o in outs] == [16, 9, 16, 3]
     assert all(o.error is None for o in outs)
     assert all(0 <= t < 32000 for o in outs for t in o.token_ids)
+
+
+def _stepwise(monkeypatch):
+    monkeypatch.setattr(LLMEngine, "PIPELINE", False)
+
+
+PROMPTS12 = [f"user: question {i} " + "about things " * (i % 5) for i in range(12)]
+
+
+def test_pipelined_decode_matches_stepwise(monkeypatch):
+    """Pipelined decode (one step of host lookahead, tokens gathered on the device) gives the
+    same tokens as the step-by-step loop: mixed max_new_tokens (count limits are predicted),
+    more requests than rows (admissions between bursts), greedy and seeded sampling."""
+    sps = [SamplingParams(max_new_tokens=3 + 5 * (i % 4), ignore_eos=True, temperature=0.0 if i % 3 else 0.8,
+                          top_k=40, top_p=0.9) for i in range(12)]
+    a = [o.token_ids for o in _engine(max_num_seqs=4).generate(PROMPTS12, sps)]
+    _stepwise(monkeypatch)
+    b = [o.token_ids for o in _engine(max_num_seqs=4).generate(PROMPTS12, sps)]
+    assert a == b
+    assert [len(x) for x in a] == [sp.max_new_tokens for sp in sps]
+
+
+def test_pipelined_decode_preemption_matches_stepwise(monkeypatch):
+    """Out of KV blocks mid-decode: the pipelined loop preempts the same sequences (slot
+    reservation fails at the look-ahead commit) and the outputs match the step-by-step loop."""
+    sp = SamplingParams(max_new_tokens=40, ignore_eos=True)
+    prompts = ["user: " + "word " * 30 + str(i) for i in range(6)]
+
+    def run():   # kv_cache_gb=0 -> the minimum pool (max_model_len / 16 + 8 = 24 blocks)
+        e = _engine(kv_cache_gb=0.0, max_num_seqs=6, max_model_len=256)
+        return [o.token_ids for o in e.generate(prompts, sp)], e
+
+    a, ea = run()
+    _stepwise(monkeypatch)
+    b, _ = run()
+    assert a == b and all(len(x) == 40 for x in a)
+    assert ea.bm.check_invariants() == ""
+
+
+def test_pipelined_decode_eos_zombie_rows(monkeypatch):
+    """A sequence that samples EOS is already in the next launched step: that row is discarded.
+    Outputs equal the step-by-step loop up to the first EOS step of the batch, end at EOS, and the
+    engine's block accounting is clean afterwards."""
+    sp = SamplingParams(max_new_tokens=24, ignore_eos=True)
+    probe = [o.token_ids for o in _engine().generate(PROMPTS, sp)]
+    # an EOS id that some sequences emit early and others late or never
+    cand = {}
+    for ids in probe:
+        for j, t in enumerate(ids[2:12], start=2):
+            cand.setdefault(t, j)
+    eos = min(cand, key=lambda t: (abs(cand[t] - 5), t))
+    sp2 = SamplingParams(max_new_tokens=24)
+
+    def run():
+        e = _engine()
+        e.tok.eos_id = eos
+        return [o.token_ids for o in e.generate(PROMPTS, sp2)], e
+
+    a, ea = run()
+    _stepwise(monkeypatch)
+    b, _ = run()
+    first = min((x.index(eos) for x in b if eos in x), default=24)
+    for x, y in zip(a, b):
+        assert x[:first + 1] == y[:first + 1]
+        assert eos not in x[:-1] and len(x) <= 24
+    assert any(x and x[-1] == eos for x in a)
+    assert ea.bm.check_invariants() == "" and ea.bm.stats()["active_seqs"] == 0
