@@ -57,6 +57,10 @@ int dllm_encoder_attention(const void*, const int*, void*, int, int, int, int, f
 int dllm_embed_ln(const int*, const void*, const void*, const void*, const void*, const void*, void*, int, int, int, int,
                   float, hipStream_t);
 int dllm_res_add_ssq(const void*, long, void*, long, float*, long, int, int, int, hipStream_t);
+int dllm_gemv_slots(int, int);
+int dllm_gemv_epi(const void*, long, const void*, void*, long, int, int, int, int, int, void*, long, float*, long,
+                  const float*, int, long, float, float, const int*, const float*, const int*, void*, void*, void*, int,
+                  int, int, hipStream_t);
 int dllm_qkv_post(const void*, long, const float*, int, long, float, float, const int*, const float*, const int*, void*,
                   void*, void*, int, int, int, int, hipStream_t);
 int dllm_swiglu_post(const void*, long, const float*, int, long, float, float, void*, long, int, int, hipStream_t);
@@ -444,6 +448,83 @@ void gemv_norm(torch::Tensor x, torch::Tensor res_in, torch::Tensor res_out, tor
   ok(dllm_gemv(x.data_ptr(), K, w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, (int)R, 0, res_in.data_ptr(),
                res_out.data_ptr(), norm_w.data_ptr(), (float)eps, stream()),
      "gemv_norm");
+}
+
+// GEMV with a fused decoder-layer epilogue (csrc/kernels/gemv.hip EPI; batch <= 8):
+//   gemv_resadd: r += x . w^T in place, partial row sums of r^2 -> ssq_out [slots, >= M]; returns slots
+//   gemv_qkv   : q [M, nq, d] of rope(rinv * x . w^T), K / V^T into the paged caches
+//   gemv_swiglu: act [M, N/2] = silu(g) * u of rinv * x . w^T (interleaved gate/up rows)
+static void gemv_epi_checks(const torch::Tensor& x, const torch::Tensor& w, int64_t R, const char* what) {
+  check_bf16(x, what);
+  check_bf16(w, what);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous(), what, ": 2-D row-major operands");
+  const int64_t M = x.size(0), K = w.size(1);
+  TORCH_CHECK(M == 1 || M == 2 || M == 4 || M == 8, what, ": M in {1, 2, 4, 8}");
+  TORCH_CHECK(x.size(1) == K && K % 8 == 0 && x.stride(0) % 8 == 0, what, ": x [M, K], K % 8 == 0, aligned rows");
+  TORCH_CHECK(M * K * 2 <= 64 * 1024 && (R == 1 || R == 2 || R == 4), what, ": LDS stage / R");
+}
+
+static void check_ssq_in(const torch::Tensor& ssq, int64_t ssq_n, int64_t M) {
+  check_f32(ssq, "ssq");
+  TORCH_CHECK(ssq.dim() == 2 && ssq.stride(1) == 1 && ssq.size(1) >= M && ssq_n >= 1 && ssq_n <= ssq.size(0),
+              "ssq [slots, >= M]");
+}
+
+int64_t gemv_slots(int64_t N, int64_t R) { return dllm_gemv_slots((int)N, (int)R); }
+
+int64_t gemv_resadd(torch::Tensor x, torch::Tensor w, torch::Tensor r, torch::Tensor ssq_out, int64_t R) {
+  gemv_epi_checks(x, w, R, "gemv_resadd");
+  check_bf16(r, "r");
+  check_f32(ssq_out, "ssq_out");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  const int slots = dllm_gemv_slots(N, (int)R);
+  TORCH_CHECK(r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N && r.stride(0) % 8 == 0, "r [M, N]");
+  TORCH_CHECK(ssq_out.dim() == 2 && ssq_out.stride(1) == 1 && ssq_out.size(0) >= slots && ssq_out.size(1) >= M,
+              "ssq_out [>= slots, >= M]");
+  ok(dllm_gemv_epi(x.data_ptr(), x.stride(0), w.data_ptr(), nullptr, 0, M, N, K, (int)R, 1, r.data_ptr(), r.stride(0),
+                   ssq_out.data_ptr<float>(), ssq_out.stride(0), nullptr, 0, 0, 0.f, 0.f, nullptr, nullptr, nullptr,
+                   nullptr, nullptr, nullptr, 0, 0, 0, stream()),
+     "gemv_resadd");
+  return slots;
+}
+
+void gemv_qkv(torch::Tensor x, torch::Tensor w, torch::Tensor ssq, int64_t ssq_n, double scale, double eps,
+              torch::Tensor pos, torch::Tensor cos_sin, torch::Tensor slots, torch::Tensor q_out, torch::Tensor kc,
+              torch::Tensor vc, int64_t nq, int64_t nkv, int64_t d, int64_t R) {
+  gemv_epi_checks(x, w, R, "gemv_qkv");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  check_ssq_in(ssq, ssq_n, M);
+  check_i32(pos, "positions");
+  check_i32(slots, "slots");
+  check_f32(cos_sin, "cos_sin");
+  for (auto* t : {&q_out, &kc, &vc}) check_bf16(*t, "qkv outputs");
+  TORCH_CHECK(N == (nq + 2 * nkv) * d && d % 32 == 0, "gemv_qkv: w rows (nq + 2 nkv) d, d % 32 == 0");
+  TORCH_CHECK(pos.numel() >= M && slots.numel() >= M && cos_sin.dim() == 2 && cos_sin.size(1) == d &&
+                  cos_sin.is_contiguous(),
+              "positions/slots/cos_sin");
+  TORCH_CHECK(q_out.is_contiguous() && q_out.numel() >= (int64_t)M * nq * d, "q_out");
+  TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.size(1) == nkv && kc.size(2) == 16 && kc.size(3) == d &&
+                  vc.size(2) == d && vc.size(3) == 16,
+              "cache layout");
+  ok(dllm_gemv_epi(x.data_ptr(), x.stride(0), w.data_ptr(), nullptr, 0, M, N, K, (int)R, 2, nullptr, 0, nullptr, 0,
+                   ssq.data_ptr<float>(), (int)ssq_n, ssq.stride(0), (float)scale, (float)eps, pos.data_ptr<int>(),
+                   cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                   (int)nq, (int)nkv, (int)d, stream()),
+     "gemv_qkv");
+}
+
+void gemv_swiglu(torch::Tensor x, torch::Tensor w, torch::Tensor ssq, int64_t ssq_n, double scale, double eps,
+                 torch::Tensor act, int64_t R) {
+  gemv_epi_checks(x, w, R, "gemv_swiglu");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  check_ssq_in(ssq, ssq_n, M);
+  check_bf16(act, "act");
+  TORCH_CHECK(N % 32 == 0 && act.dim() == 2 && act.stride(1) == 1 && act.size(0) == M && act.size(1) == N / 2,
+              "gemv_swiglu: act [M, N/2], N % 32 == 0");
+  ok(dllm_gemv_epi(x.data_ptr(), x.stride(0), w.data_ptr(), act.data_ptr(), act.stride(0), M, N, K, (int)R, 3, nullptr,
+                   0, nullptr, 0, ssq.data_ptr<float>(), (int)ssq_n, ssq.stride(0), (float)scale, (float)eps, nullptr,
+                   nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, stream()),
+     "gemv_swiglu");
 }
 
 // Mid-size decode GEMM (64 < M <= 256; csrc/kernels/mm_gemm.hip): y = x . w^T (x = silu(g)*u if swiglu).
@@ -881,4 +962,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);
   m.def("gemv_norm", &gemv_norm);
+  m.def("gemv_slots", &gemv_slots);
+  m.def("gemv_resadd", &gemv_resadd);
+  m.def("gemv_qkv", &gemv_qkv);
+  m.def("gemv_swiglu", &gemv_swiglu);
 }

@@ -17,10 +17,43 @@
 //     layer at batch <= 8 drops both norm launches (norm.hip) from its chain;
 //   * f32 FMA, one 64-lane butterfly reduction per (row, column) at the end; no split-K, no
 //     workspace, no inter-workgroup traffic: one launch per projection, graph-capturable.
+//   * EPI (fused decoder-layer epilogues, the GEMV twin of tgemm.hip's): at batch <= 8 a
+//     standalone epilogue kernel (qkv_post / res_add_ssq / swiglu_post) costs as much as the GEMV
+//     itself (one ~4 us launch each, profiles/r2_decode_replay_b1.md), so the GEMV applies them:
+//       EPI_RESADD : r[m, n] = bf16(bf16(acc) + r[m, n]) in place, and the workgroup's partial
+//                    row sums of r^2 into ssq_out[blockIdx.x][m] (one slot per workgroup);
+//       EPI_QKV    : row scale rinv[m] from the producer's partial sums (folded RMSNorm), RoPE on
+//                    the (c, c + 16) pairs of the permuted q/k rows, q out, K and V^T written
+//                    straight into the paged caches;
+//       EPI_SWIGLU : act = silu(g * rinv) * (u * rinv) for the interleaved 16-gate/16-up rows.
+//     QKV / SWIGLU need both members of a (c, c + 16) pair in one workgroup, so those modes map
+//     columns "paired": waves 0-1 take first-half columns of a 32-column group, waves 2-3 the
+//     matching second-half ones; the accumulators meet in LDS for the epilogue.  rinv is summed
+//     from the partials while the first W trip is in flight (no extra latency on the chain).
 // Chosen per (M, N, K) by the host autotuner (ops.gemm) only where it beats the other plans.
 #include "common.h"
 
 namespace {
+
+enum { GV_PLAIN = 0, GV_RESADD = 1, GV_QKV = 2, GV_SWIGLU = 3 };
+
+struct EpiArgs {                 // fused output epilogues (EPI != GV_PLAIN)
+  u16* res;                      // RESADD: residual stream [M, ldr], updated in place
+  long ldr;
+  float* ssq_out;                // RESADD: partial row sums of r^2, [gridDim.x][ssq_out_ld]
+  long ssq_out_ld;
+  const float* ssq_in;           // QKV / SWIGLU: producer partial sums [ssq_n][ssq_in_ld]
+  int ssq_n;
+  long ssq_in_ld;
+  float scale, eps;              // rinv = rsqrt(sum * scale + eps)
+  const int* pos;                // QKV: positions, cos|sin table [*, d], cache slots (-1: no write)
+  const float* cos_sin;
+  const int* slots;
+  u16* q_out;                    // QKV: q [M, nq, d]; kc [blocks, nkv, 16, d]; vc [blocks, nkv, d, 16]
+  u16* kc;
+  u16* vc;
+  int nq, nkv, d;
+};
 
 struct NormArgs {         // NORM: X is the sub-layer output h; the kernel forms r = h + res_in (bf16),
   const u16* res_in;     // workgroup 0 stores r to res_out (a different buffer: every workgroup
@@ -29,13 +62,29 @@ struct NormArgs {         // NORM: X is the sub-layer output h; the kernel forms
   float eps;
 };
 
-template <int M, int R, int UNR, bool SWIGLU, bool NORM>
+template <int M, int R, int UNR, bool SWIGLU, bool NORM, int EPI>
 __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, long ldx, const u16* __restrict__ W,
-                                                   u16* __restrict__ Y, long ldy, int N, int K, NormArgs na) {
+                                                   u16* __restrict__ Y, long ldy, int N, int K, NormArgs na,
+                                                   EpiArgs ea) {
   extern __shared__ uint4 xs_raw[];  // X (SwiGLU applied) staged once per workgroup: [M][K] bf16
   u16* xs = reinterpret_cast<u16*>(xs_raw);
+  // epilogue scratch after X (and NORM's reduction slots): rinv [M], accumulators [4][R][M],
+  // per-wave row sums [4][M]
+  float* s_ri = reinterpret_cast<float*>(xs + (long)M * K) + (NORM ? 4 * M : 0);
+  float* s_ep = s_ri + M;
+  float* s_red = s_ep + 4 * R * M;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + wave) * R;
+  constexpr bool PAIRED = EPI == GV_QKV || EPI == GV_SWIGLU;
+  int n0;
+  if constexpr (PAIRED) {
+    // 8/R workgroups per 32-column group; each takes 2R first-half columns (waves 0, 1) and the
+    // 2R second-half columns 16 further on (waves 2, 3)
+    constexpr int PER = 8 / R;
+    const int g = blockIdx.x / PER, j0 = (blockIdx.x % PER) * 2 * R;
+    n0 = g * 32 + (wave >> 1) * 16 + j0 + (wave & 1) * R;
+  } else {
+    n0 = (blockIdx.x * 4 + wave) * R;
+  }
   const bool active = n0 < N;  // inactive waves still stage X and pass the barrier
   const u16* wr[R];
 #pragma unroll
@@ -51,6 +100,26 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
         (active && k_ < K) ? __builtin_bit_cast(uint4, ldnt_bf16x8(wr[r] + k_)) : make_uint4(0, 0, 0, 0); \
   }
   DLLM_GEMV_LOAD(w, 0)  // the first trip of W is in flight while X is staged
+  if constexpr (PAIRED) {
+    // folded RMSNorm row scale: lane-parallel sum of the producer's partial sums, wave w -> rows w, w + 4
+    // (a GEMV producer leaves one slot per workgroup, e.g. 512 at N = 2048: 8 independent loads
+    // per lane are issued before the first add, so the sum costs one L2 round trip, not eight)
+    for (int m = wave; m < M; m += 4) {
+      float sacc = 0.f;
+      for (int i0 = 0; i0 < ea.ssq_n; i0 += 512) {
+        float part[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u * 64 + lane;
+          part[u] = i < ea.ssq_n ? ea.ssq_in[(long)i * ea.ssq_in_ld + m] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sacc += part[u];
+      }
+      sacc = wave_sum(sacc);
+      if (lane == 0) s_ri[m] = rsqrtf(sacc * ea.scale + ea.eps);
+    }
+  }
   if constexpr (NORM) {
     float* red = reinterpret_cast<float*>(xs + (long)M * K);  // [4 waves][M]
     float ss[M];
@@ -146,46 +215,122 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
       for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
       acc[m][r] = v;
     }
-  if (active && lane == 0) {
+  if constexpr (EPI == GV_PLAIN) {
+    if (active && lane == 0) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (n0 + r >= N) break;
+      for (int r = 0; r < R; ++r) {
+        if (n0 + r >= N) break;
 #pragma unroll
-      for (int m = 0; m < M; ++m) Y[(long)m * ldy + n0 + r] = f2bf(acc[m][r]);
+        for (int m = 0; m < M; ++m) Y[(long)m * ldy + n0 + r] = f2bf(acc[m][r]);
+      }
+    }
+  } else if constexpr (EPI == GV_RESADD) {
+    // r = bf16(bf16(acc) + r) (res_add_ssq numerics), then this workgroup's partial row sums of r^2
+    float ss[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ss[m] = 0.f;
+    if (active && lane == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (n0 + r >= N) break;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          u16* p = ea.res + (long)m * ea.ldr + n0 + r;
+          const float v = bf2f(f2bf(bf2f(f2bf(acc[m][r])) + bf2f(*p)));
+          *p = f2bf(v);
+          ss[m] += v * v;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) s_red[wave * M + m] = ss[m];
+    } else if (lane == 0) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) s_red[wave * M + m] = 0.f;
+    }
+    __syncthreads();
+    if (threadIdx.x < M) {
+      const int m = threadIdx.x;
+      ea.ssq_out[(long)blockIdx.x * ea.ssq_out_ld + m] = s_red[m] + s_red[M + m] + s_red[2 * M + m] + s_red[3 * M + m];
+    }
+  } else {
+    // paired modes: accumulators meet in LDS, thread (p, m) owns pair p of row m
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int m = 0; m < M; ++m) s_ep[(wave * R + r) * M + m] = acc[m][r];
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * R * M) {
+      constexpr int PER = 8 / R;
+      const int m = threadIdx.x % M, p = threadIdx.x / M;
+      const int g = blockIdx.x / PER, j = (blockIdx.x % PER) * 2 * R + p;  // column offset in the group
+      const float x1 = s_ep[p * M + m], x2 = s_ep[(2 * R + p) * M + m];      // columns 32g + j, + 16
+      const float ri = s_ri[m];
+      if constexpr (EPI == GV_SWIGLU) {
+        const float gv = bf2f(f2bf(x1 * ri)), uv = bf2f(f2bf(x2 * ri));
+        Y[(long)m * ldy + 16 * g + j] = f2bf(gv / (1.f + __expf(-gv)) * uv);
+      } else {
+        const int d = ea.d, hd = d / 2, qcols = ea.nq * d, kcols = ea.nkv * d;
+        const int c = 32 * g + j, slot = ea.slots[m];
+        const long blk = slot >> 4, off = slot & 15;
+        if (c < qcols + kcols) {
+          const bool isq = c < qcols;
+          const int cc = isq ? c : c - qcols, head = cc / d, o = cc % d;
+          const int d1 = 16 * (o >> 5) + (o & 15);
+          const float* cs = ea.cos_sin + (long)ea.pos[m] * d;
+          const float a1 = bf2f(f2bf(x1 * ri)), a2 = bf2f(f2bf(x2 * ri));
+          const float co = cs[d1], si = cs[hd + d1];
+          u16* dst = isq ? ea.q_out + ((long)m * ea.nq + head) * d
+                         : (slot >= 0 ? ea.kc + ((blk * ea.nkv + head) * 16 + off) * d : nullptr);
+          if (dst) {
+            dst[d1] = f2bf(a1 * co - a2 * si);
+            dst[hd + d1] = f2bf(a2 * co + a1 * si);
+          }
+        } else if (slot >= 0) {
+          const int cc = c - qcols - kcols, head = cc / d, dim = cc % d;  // V columns: unpermuted
+          u16* vo = ea.vc + ((blk * ea.nkv + head) * d) * 16 + off;
+          vo[(long)dim * 16] = f2bf(x1 * ri);
+          vo[(long)(dim + 16) * 16] = f2bf(x2 * ri);
+        }
+      }
     }
   }
 }
 
-template <int M, int R, bool SW, bool NORM>
+template <int R>
+constexpr unsigned gemv_blocks(int N) { return (unsigned)((N + 4 * R - 1) / (4 * R)); }
+
+template <int M, int R, bool SW, bool NORM, int EPI>
 void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
-                 hipStream_t stream) {
+                 const EpiArgs& ea, hipStream_t stream) {
   constexpr int UNR = M <= 2 ? 4 : 2;
-  const unsigned blocks = (unsigned)((N + 4 * R - 1) / (4 * R));
-  const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0);
-  hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM>), dim3(blocks), dim3(256), lds, stream, (const u16*)x, ldx,
-                     (const u16*)w, (u16*)y, ldy, N, K, na);
+  const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0) +
+                     (EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0);
+  hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
+                     (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
 }
 
-template <int M, bool SW, bool NORM>
+template <int M, bool SW, bool NORM, int EPI>
 int dispatch_r(int R, const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
-               hipStream_t s) {
+               const EpiArgs& ea, hipStream_t s) {
   switch (R) {
-    case 1: launch_gemv<M, 1, SW, NORM>(x, ldx, w, y, ldy, N, K, na, s); break;
-    case 2: launch_gemv<M, 2, SW, NORM>(x, ldx, w, y, ldy, N, K, na, s); break;
-    case 4: launch_gemv<M, 4, SW, NORM>(x, ldx, w, y, ldy, N, K, na, s); break;
+    case 1: launch_gemv<M, 1, SW, NORM, EPI>(x, ldx, w, y, ldy, N, K, na, ea, s); break;
+    case 2: launch_gemv<M, 2, SW, NORM, EPI>(x, ldx, w, y, ldy, N, K, na, ea, s); break;
+    case 4: launch_gemv<M, 4, SW, NORM, EPI>(x, ldx, w, y, ldy, N, K, na, ea, s); break;
     default: return -2;
   }
   return 0;
 }
 
-template <bool SW, bool NORM>
+template <bool SW, bool NORM, int EPI>
 int dispatch_m(int Mp, int R, const void* x, long ldx, const void* w, void* y, long ldy, int N, int K,
-               const NormArgs& na, hipStream_t s) {
+               const NormArgs& na, const EpiArgs& ea, hipStream_t s) {
   switch (Mp) {
-    case 1: return dispatch_r<1, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
-    case 2: return dispatch_r<2, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
-    case 4: return dispatch_r<4, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
-    case 8: return dispatch_r<8, SW, NORM>(R, x, ldx, w, y, ldy, N, K, na, s);
+    case 1: return dispatch_r<1, SW, NORM, EPI>(R, x, ldx, w, y, ldy, N, K, na, ea, s);
+    case 2: return dispatch_r<2, SW, NORM, EPI>(R, x, ldx, w, y, ldy, N, K, na, ea, s);
+    case 4: return dispatch_r<4, SW, NORM, EPI>(R, x, ldx, w, y, ldy, N, K, na, ea, s);
+    case 8: return dispatch_r<8, SW, NORM, EPI>(R, x, ldx, w, y, ldy, N, K, na, ea, s);
     default: return -1;
   }
 }
@@ -202,13 +347,50 @@ extern "C" int dllm_gemv(const void* x, long ldx, const void* w, void* y, long l
   const bool norm = norm_w != nullptr;
   if (norm && (swiglu || !res_in || !res_out || res_in == res_out || ldx % 8)) return -4;
   const NormArgs na{(const u16*)res_in, (u16*)res_out, (const u16*)norm_w, eps};
+  const EpiArgs ea{};
   int rc;
   if (norm)
-    rc = dispatch_m<false, true>(M, R, x, ldx, w, y, ldy, N, K, na, stream);
+    rc = dispatch_m<false, true, GV_PLAIN>(M, R, x, ldx, w, y, ldy, N, K, na, ea, stream);
   else if (swiglu)
-    rc = dispatch_m<true, false>(M, R, x, ldx, w, y, ldy, N, K, na, stream);
+    rc = dispatch_m<true, false, GV_PLAIN>(M, R, x, ldx, w, y, ldy, N, K, na, ea, stream);
   else
-    rc = dispatch_m<false, false>(M, R, x, ldx, w, y, ldy, N, K, na, stream);
+    rc = dispatch_m<false, false, GV_PLAIN>(M, R, x, ldx, w, y, ldy, N, K, na, ea, stream);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// Number of partial row-sum slots a GV_RESADD launch of N columns writes (one per workgroup).
+extern "C" int dllm_gemv_slots(int N, int R) {
+  return R == 1 ? (int)gemv_blocks<1>(N) : R == 2 ? (int)gemv_blocks<2>(N) : R == 4 ? (int)gemv_blocks<4>(N) : -1;
+}
+
+// GEMV with a fused decoder epilogue (epi: 1 RESADD, 2 QKV, 3 SWIGLU; see the header).
+//   RESADD: res[M, N] += x . w^T (y unused), partial row sums of res^2 -> ssq_out[slot][m]
+//   QKV   : w = the permuted/folded QKV weight, N = (nq + 2 nkv) d; q_out / kc / vc as qkv_post
+//   SWIGLU: w = interleaved gate|up rows (N = 2I), y = act [M, I]
+// Host contract (csrc/bindings.cpp checks it): M in {1, 2, 4, 8}, R in {1, 2, 4}, K % 8 == 0,
+// M x K x 2 B <= 64 KB, N % 32 == 0 for QKV / SWIGLU (and d % 32 == 0 for QKV), ssq_out rows >=
+// dllm_gemv_slots(N, R) for RESADD.
+extern "C" int dllm_gemv_epi(const void* x, long ldx, const void* w, void* y, long ldy, int M, int N, int K, int R,
+                             int epi, void* res, long ldr, float* ssq_out, long ssq_out_ld, const float* ssq_in,
+                             int ssq_n, long ssq_in_ld, float scale, float eps, const int* pos, const float* cos_sin,
+                             const int* slots, void* q_out, void* kc, void* vc, int nq, int nkv, int d,
+                             hipStream_t stream) {
+  if (K % 8 != 0 || N <= 0 || (long)M * K * 2 > GEMV_MAX_LDS) return -3;
+  if ((epi == GV_QKV || epi == GV_SWIGLU) && (N % 32 || !ssq_in || ssq_n < 1)) return -4;
+  if (epi == GV_QKV && (d % 32 || N != (nq + 2 * nkv) * d || !q_out || !kc || !vc || !pos || !cos_sin || !slots))
+    return -5;
+  if (epi == GV_RESADD && (!res || !ssq_out || ldr % 8)) return -6;
+  const NormArgs na{};
+  const EpiArgs ea{(u16*)res, ldr, ssq_out, ssq_out_ld, ssq_in, ssq_n, ssq_in_ld, scale, eps, pos, cos_sin, slots,
+                   (u16*)q_out, (u16*)kc, (u16*)vc, nq, nkv, d};
+  int rc;
+  switch (epi) {
+    case GV_RESADD: rc = dispatch_m<false, false, GV_RESADD>(M, R, x, ldx, w, y, ldy, N, K, na, ea, stream); break;
+    case GV_QKV: rc = dispatch_m<false, false, GV_QKV>(M, R, x, ldx, w, y, ldy, N, K, na, ea, stream); break;
+    case GV_SWIGLU: rc = dispatch_m<false, false, GV_SWIGLU>(M, R, x, ldx, w, y, ldy, N, K, na, ea, stream); break;
+    default: return -7;
+  }
   if (rc) return rc;
   return (int)hipGetLastError();
 }

@@ -363,7 +363,7 @@ class LlamaModel:
         cfg = self.cfg
         T, H, eps = input_ids.shape[0], cfg.hidden, cfg.rms_eps
         r = ops.embedding(input_ids, self.embed, self.vocab_shard.start)
-        slots_n = ops.gemm.max_slots(H)
+        slots_n = ops.gemm.max_slots(H, T)
         ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
         ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
         n = ops.gemm.res_add_ssq(None, r, ssq_a)

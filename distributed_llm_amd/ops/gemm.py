@@ -288,7 +288,7 @@ POST_US = 3.0
 def use_vendor_core(M: int, N: int, K: int) -> bool:
     """True: run the fused op as ``linear()`` (the shape's best plain plan — GEMV / skinny / mm /
     hipBLASLt / plain tgemm) followed by the standalone epilogue kernel; False: one tgemm launch
-    with the epilogue fused."""
+    with the epilogue fused.  (A ``gemvR`` choice is taken before this by ``fused_gemv_r``.)"""
     env = os.environ.get("DLLM_FUSED_CORE")
     if env in ("tg", "blas", "lin"):
         return env != "tg"
@@ -296,6 +296,21 @@ def use_vendor_core(M: int, N: int, K: int) -> bool:
     if c is not None:
         return c != "tg"
     return M > MAX_M
+
+
+def fused_gemv_r(x: torch.Tensor, N: int) -> int:
+    """R (output rows per wave) of the fused-epilogue GEMV (csrc/kernels/gemv.hip EPI) if the
+    autotuner picked it for this fused op's shape (``fused_core`` = ``gemvR``; forced by
+    ``DLLM_FUSED_CORE=gemvR``), else 0.  Batch <= 8 only: it replaces GEMV/skinny + a standalone
+    epilogue launch (qkv_post / res_add_ssq / swiglu_post) with one launch."""
+    M, K = x.shape[0], x.shape[1]
+    if M not in _GEMV_MS or K % 8 or M * K * 2 > 64 * 1024 or x.stride(1) != 1 or x.stride(0) % 8 or N % 32:
+        return 0
+    env = os.environ.get("DLLM_FUSED_CORE")
+    c = env if env else _P.fused_core.get((M, N, K))
+    if isinstance(c, str) and c.startswith("gemv") and c[4:] in ("1", "2", "4"):
+        return int(c[4:])
+    return 0
 
 
 def _core(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -314,6 +329,11 @@ def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: i
     q = torch.empty((T, nq, d), dtype=r.dtype, device=r.device)
     if T == 0:
         return q
+    R = fused_gemv_r(r, w.shape[0])
+    if R:
+        _native(r).gemv_qkv(r, w, ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q, k_cache,
+                            v_cache, nq, nkv, d, R)
+        return q
     if use_vendor_core(T, w.shape[0], H):
         _native(r).qkv_post(_core(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
                             k_cache, v_cache, nq, nkv, d)
@@ -328,6 +348,9 @@ def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_
     """``residual += x . w^T`` (bf16 rounding as ``rms_norm``'s residual add) and the partial row
     sums of the new residual's squares into ``ssq_out[:slots]``; returns ``slots``."""
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    R = fused_gemv_r(x, N) if M else 0
+    if R:
+        return int(_native(x).gemv_resadd(x, w, residual, ssq_out, R))
     if M and use_vendor_core(M, N, K):
         return int(_native(x).res_add_ssq(_core(x, w), residual, ssq_out))
     plan = tg_plan(M, N, K)
@@ -341,6 +364,10 @@ def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: in
     .fuse_gate_up_weight) -> [T, I]."""
     T, H = r.shape
     act = torch.empty((T, w.shape[0] // 2), dtype=r.dtype, device=r.device)
+    R = fused_gemv_r(r, w.shape[0]) if T else 0
+    if R:
+        _native(r).gemv_swiglu(r, w, ssq, int(ssq_n), 1.0 / H, float(eps), act, R)
+        return act
     if T and use_vendor_core(T, w.shape[0], H):
         _native(r).swiglu_post(_core(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), act)
         return act
@@ -387,8 +414,10 @@ def linear_bias_residual(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, r
     return residual
 
 
-def max_slots(N: int) -> int:
-    return -(-N // 64)
+def max_slots(N: int, M: int = 0) -> int:
+    """Rows a partial-row-sum buffer needs for a residual producer of N columns: one per 64-column
+    tgemm tile, or at batch <= 8 one per fused-GEMV workgroup (N / 4 at R = 1)."""
+    return -(-N // 4) if 0 < M <= max(_GEMV_MS) else -(-N // 64)
 
 
 # ----------------------------------------------------------------------------- autotuning
@@ -547,7 +576,17 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 post = _post_us(M, N, dev)
                 # the split form runs the shape's best plain plan (GEMV at M <= 8, skinny, ...)
                 best_plain = min(res[c] for c in res if c[0] != "tg")
-                _P.fused_core[tkey] = "tg" if res[best_tg] <= best_plain + post else "lin"
+                opts = {"tg": res[best_tg], "lin": best_plain + post}
+                # fused-epilogue GEMV (one launch): timed in its RESADD form (the paired QKV /
+                # SwiGLU forms stream the same rows with the same per-wave loads)
+                gv = [c for c in res if c[0] == "gemv"]
+                if gv and N % 32 == 0 and os.environ.get("DLLM_GEMV_EPI", "1") == "1":
+                    ext = _native(x)
+                    rr = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+                    sq = torch.empty(max_slots(N, M), M, dtype=torch.float32, device=dev)
+                    for c in gv:
+                        opts["gemv%d" % c[1]] = _time(lambda i: ext.gemv_resadd(x, ws[i % copies], rr, sq, c[1]))
+                _P.fused_core[tkey] = min(opts, key=opts.get)
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
                       for k in ("gemv", "skinny", "lds", "mm", "tg")}

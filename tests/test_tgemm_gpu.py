@@ -155,20 +155,23 @@ def test_res_add_ssq_sliced(H, slots):
     torch.testing.assert_close(ssq[:n, :37].sum(0), (want.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("core", ["tg", "blas"])
-def test_fused_ops_both_cores(core, monkeypatch):
-    """The fused decoder ops give the same results through the tgemm epilogue and through the
-    vendor GEMM + standalone epilogue kernels (qkv_post / res_add_ssq / swiglu_post)."""
+@pytest.mark.parametrize("core,M", [("tg", 77), ("blas", 77), ("gemv1", 1), ("gemv2", 8), ("gemv4", 4), ("gemv1", 2)])
+def test_fused_ops_both_cores(core, M, monkeypatch):
+    """The fused decoder ops give the same results through the tgemm epilogue, through the
+    vendor GEMM + standalone epilogue kernels (qkv_post / res_add_ssq / swiglu_post) and, at
+    batch <= 8, through the fused-epilogue GEMV (gemv.hip EPI)."""
     monkeypatch.setenv("DLLM_FUSED_CORE", core)
     torch.manual_seed(11)
-    M, H, I, d, nq, nkv = 77, 256, 384, 64, 4, 2
+    H, I, d, nq, nkv = 256, 384, 64, 4, 2
     G.reserve("cuda")
     r = _rnd(M, H)
+    if core.startswith("gemv"):
+        assert G.fused_gemv_r(r, (nq + 2 * nkv) * d) == int(core[4:])   # the GEMV path really runs
     ln1 = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
     ln2 = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
     wqkv, wo = _rnd((nq + 2 * nkv) * d, H, scale=0.05), _rnd(H, nq * d, scale=0.05)
     wgu, wd = _rnd(2 * I, H, scale=0.05), _rnd(H, I, scale=0.05)
-    ssq = torch.empty(G.max_slots(H), M, device="cuda")
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
     ops.gemm.res_add_ssq(None, r, ssq[0])
     cos_sin = ops.rope_cos_sin(512, d, 10000.0, "cuda")
     pos = torch.arange(M, device="cuda", dtype=torch.int32)
@@ -179,9 +182,12 @@ def test_fused_ops_both_cores(core, monkeypatch):
     q = G.qkv_rope_cache(r, fuse_qkv_weight(wqkv, ln1, nq, nkv, d), ssq, 1, 1e-5, pos, cos_sin, slots, kc, vc,
                          nq, nkv, d)
     o = _rnd(M, nq * d)
-    ssq2 = torch.empty(G.max_slots(H), M, device="cuda")
+    ssq2 = torch.empty(G.max_slots(H, M), M, device="cuda")
     n2 = G.matmul_resadd(o, wo, r, ssq2)
     act = G.swiglu_matmul(r, fuse_gate_up_weight(wgu, ln2), ssq2, n2, 1e-5)
+    r_after_wo = r.cpu().clone()
+    ssq3 = torch.full((G.max_slots(H, M), M), float("nan"), device="cuda")
+    n3 = G.matmul_resadd(act, wd, r, ssq3)
     # fp32 references
     x = ref.rms_norm(r_ref, ln1.cpu(), 1e-5)
     qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
@@ -195,5 +201,85 @@ def test_fused_ops_both_cores(core, monkeypatch):
     torch.testing.assert_close(q.cpu().float(), qr.float(), atol=4e-2, rtol=3e-2)
     torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=4e-2, rtol=3e-2)
     torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=4e-2, rtol=3e-2)
-    torch.testing.assert_close(r.cpu().float(), r2.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(r_after_wo.float(), r2.float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(act.cpu().float(), ar.float(), atol=3e-2, rtol=3e-2)
+    # down projection: residual add and the row sums of squares its slots hold
+    r3 = ((act.cpu().float() @ wd.cpu().float().t()).to(torch.bfloat16).float() + r_after_wo.float()).to(torch.bfloat16)
+    torch.testing.assert_close(r.cpu().float(), r3.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(ssq3[:n3].sum(0).cpu(), (r.cpu().float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+@pytest.mark.parametrize("R", [1, 2, 4])
+@pytest.mark.parametrize("N,K", [(256, 512), (2048, 2048), (4096, 5632)])
+def test_gemv_resadd(M, R, N, K):
+    """Fused-epilogue GEMV, residual form: r += bf16(x . w^T), one partial row sum per workgroup."""
+    if M * K * 2 > 64 * 1024:
+        pytest.skip("X does not fit the GEMV's 64 KB LDS stage")
+    torch.manual_seed(M * 7 + R + N)
+    x, w, r = _rnd(M, K), _rnd(N, K, scale=0.05), _rnd(M, N)
+    r0 = r.clone()
+    ssq = torch.full((G.max_slots(N, M), M), float("nan"), device="cuda")
+    n = _ext().gemv_resadd(x, w, r, ssq, R)
+    assert n == math.ceil(N / (4 * R)) == _ext().gemv_slots(N, R)
+    want = ((x.float() @ w.float().t()).to(torch.bfloat16).float() + r0.float()).to(torch.bfloat16)
+    torch.testing.assert_close(r.float(), want.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(ssq[:n].sum(0), (r.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+@pytest.mark.parametrize("R", [1, 2, 4])
+@pytest.mark.parametrize("d,nq,nkv,H", [(64, 8, 2, 256), (128, 32, 8, 4096), (96, 3, 1, 512), (64, 32, 4, 2048)])
+def test_gemv_qkv(M, R, d, nq, nkv, H):
+    """Fused-epilogue GEMV, QKV form (paired columns): folded RMSNorm row scale from partial sums,
+    RoPE, q out, K and V^T into the paged caches; vs rmsnorm -> fp32 GEMM -> rope + cache write."""
+    if M * H * 2 > 64 * 1024:
+        pytest.skip("X does not fit the GEMV's 64 KB LDS stage")
+    torch.manual_seed(M + R + d)
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wqkv = _rnd((nq + 2 * nkv) * d, H, scale=0.05)
+    wf = fuse_qkv_weight(wqkv, ln, nq, nkv, d)
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
+    n = ops.gemm.res_add_ssq(None, r, ssq)
+    cos_sin = ops.rope_cos_sin(4096, d, 10000.0, "cuda")
+    pos = torch.randint(0, 4000, (M,), device="cuda", dtype=torch.int32)
+    nblk = 4
+    slots = torch.randperm(nblk * 16, device="cuda")[:M].to(torch.int32)
+    if M > 2:
+        slots[1] = -1
+    kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
+    q = torch.empty(M, nq, d, dtype=torch.bfloat16, device="cuda")
+    _ext().gemv_qkv(r, wf, ssq, n, 1.0 / H, 1e-5, pos, cos_sin, slots, q, kc, vc, nq, nkv, d, R)
+    x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
+    qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
+    kr = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16)
+    vr = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16)
+    qr = ref.rope_and_cache(qkv, pos.cpu(), cos_sin.cpu(), slots.cpu(), kr, vr, nq, nkv, d)
+    # gamma folded into bf16 weights + the row scale applied after the K-sum: rounding differs from
+    # the normalise-then-multiply reference by up to ~1 bf16 ulp of the largest outputs
+    tol = max(4e-2, 8e-3 * qr.float().abs().max().item())
+    torch.testing.assert_close(q.cpu().float(), qr.float(), atol=tol, rtol=3e-2)
+    torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=tol, rtol=3e-2)
+    torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=tol, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+@pytest.mark.parametrize("R", [1, 2, 4])
+@pytest.mark.parametrize("H,I", [(256, 320), (2048, 5632)])
+def test_gemv_swiglu(M, R, H, I):
+    """Fused-epilogue GEMV, SwiGLU form: act = silu(g) * u of the folded-norm gate|up product."""
+    torch.manual_seed(M + R + I)
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = _rnd(2 * I, H, scale=0.05)
+    wf = fuse_gate_up_weight(wgu, ln)
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
+    n = ops.gemm.res_add_ssq(None, r, ssq)
+    act = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    _ext().gemv_swiglu(r, wf, ssq, n, 1.0 / H, 1e-5, act, R)
+    x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
+    want = ref.silu_mul((x.float() @ wgu.cpu().float().t()).to(torch.bfloat16))
+    tol = max(3e-2, 8e-3 * want.abs().max().item())   # about 1 bf16 ulp of the largest output (test_gemv_qkv)
+    torch.testing.assert_close(act.cpu().float(), want.float(), atol=tol, rtol=3e-2)
