@@ -225,28 +225,29 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
       }
     }
   } else if constexpr (EPI == GV_RESADD) {
-    // r = bf16(bf16(acc) + r) (res_add_ssq numerics), then this workgroup's partial row sums of r^2
-    float ss[M];
+    // r = bf16(bf16(acc) + r) (res_add_ssq numerics), then this workgroup's partial row sums of
+    // r^2.  Lane (m, r) = (lane / R, lane % R) owns one output, so a wave's residual
+    // read-modify-writes go out together (one round trip, not M x R dependent ones from lane 0);
+    // after the butterfly every lane holds every acc[m][r].
+    float v2 = 0.f;
+    if (active && lane < M * R) {
+      const int lm = lane / R, lr = lane % R;
+      float a = 0.f;
 #pragma unroll
-    for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    if (active && lane == 0) {
+      for (int m = 0; m < M; ++m)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (n0 + r >= N) break;
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-          u16* p = ea.res + (long)m * ea.ldr + n0 + r;
-          const float v = bf2f(f2bf(bf2f(f2bf(acc[m][r])) + bf2f(*p)));
-          *p = f2bf(v);
-          ss[m] += v * v;
-        }
+        for (int r = 0; r < R; ++r)
+          if (m == lm && r == lr) a = acc[m][r];
+      if (n0 + lr < N) {
+        u16* p = ea.res + (long)lm * ea.ldr + n0 + lr;
+        const float v = bf2f(f2bf(bf2f(f2bf(a)) + bf2f(*p)));
+        *p = f2bf(v);
+        v2 = v * v;
       }
-#pragma unroll
-      for (int m = 0; m < M; ++m) s_red[wave * M + m] = ss[m];
-    } else if (lane == 0) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) s_red[wave * M + m] = 0.f;
     }
+#pragma unroll
+    for (int o = 1; o < R; o <<= 1) v2 += __shfl_xor(v2, o, 64);  // the R lanes of a row (aligned groups)
+    if (lane < M * R && lane % R == 0) s_red[wave * M + lane / R] = v2;  // inactive waves store zeros
     __syncthreads();
     if (threadIdx.x < M) {
       const int m = threadIdx.x;
@@ -304,7 +305,7 @@ constexpr unsigned gemv_blocks(int N) { return (unsigned)((N + 4 * R - 1) / (4 *
 template <int M, int R, bool SW, bool NORM, int EPI>
 void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
                  const EpiArgs& ea, hipStream_t stream) {
-  constexpr int UNR = M <= 2 ? 4 : 2;
+  constexpr int UNR = M <= 4 ? 4 : 2;
   const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0) +
                      (EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0);
   hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,

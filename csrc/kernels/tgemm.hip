@@ -537,7 +537,18 @@ __global__ void __launch_bounds__(256) res_add_ssq_kernel(const u16* __restrict_
 // a chain of n); every wave of the block computes it (no LDS, no barrier)
 __device__ __forceinline__ float row_rinv(const float* ssq, int n, long ld, int m, float scale, float eps) {
   float s = 0.f;
-  for (int i = threadIdx.x & 63; i < n; i += 64) s += ssq[(long)i * ld + m];
+  // 8 independent loads per lane per pass: a GEMV producer leaves hundreds of slots, which must
+  // cost one round trip, not one per 64 slots
+  for (int i0 = 0; i0 < n; i0 += 512) {
+    float part[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + (threadIdx.x & 63);
+      part[u] = i < n ? ssq[(long)i * ld + m] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += part[u];
+  }
   s = wave_sum(s);
   return rsqrtf(s * scale + eps);
 }

@@ -255,9 +255,10 @@ class LLMEngine:
             # fused layers stream the SwiGLU activation as a plain operand (EPI_RESADD)
             shapes.add((L["wd"].shape[0], L["wd"].shape[1], not m.fused))
         shapes.add((m.lm_head.shape[0], m.lm_head.shape[1], False))
+        fused = [tuple(L[n].shape) for n in ("wqkv_f", "wo", "wgu_f", "wd") if m.fused and n in L]
         with ops.gemm.workspace_owner(self._ws_owner):
             ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= ops.gemm.MAX_M], self.device,
-                              verbose=os.environ.get("DLLM_VERBOSE") == "1")
+                              verbose=os.environ.get("DLLM_VERBOSE") == "1", fused=fused)
             ops.gemm.reserve(self.device)
 
     # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),
@@ -277,6 +278,10 @@ class LLMEngine:
     # MI355X, TinyLlama) it cut B=1 from 1.14 to 0.89 ms and B=16 from 1.51 to 1.29 ms vs the
     # static split grid (a kernel-only sweep had B=16-64 about even)
     ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "1"))
+    # shortest key range of one work-list unit (split-K granularity)
+    # (512: scripts/gpu_attn_small_b.sh measured 1-3 % faster steps than 256 at batch 1-16; it only
+    # matters while batch x context < 64k tokens, above that the target unit count sets the chunk)
+    ATTN_MIN_CHUNK = int(os.environ.get("DLLM_ATTN_MIN_CHUNK", "512"))
     # Alternative decode kernel (csrc/kernels/decode_attn.hip, one wave per unit, 1024 workgroups,
     # 4096-unit list): measured equal at best, slower at small batch (profiles/r2_decode_attention_
     # microbench.md), so opt-in only
@@ -849,7 +854,8 @@ class LLMEngine:
             grid = self._attn_grid(bs)
             target = 4096 if self.DECODE_WAVE else self.ATTN_ITEMS_PER_WG * grid
             items_t, items = self._items_bufs[p]
-            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target, out=items)
+            ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target,
+                                  min_chunk=self.ATTN_MIN_CHUNK, out=items)
             n_items = 1 + 2 * int(items[0])
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)

@@ -71,7 +71,8 @@ class _Planner:
     def __init__(self):
         self.plans: Dict[Tuple[int, int, int, bool], Tuple] = {}     # best overall, for linear()
         self.tg_plans: Dict[Tuple[int, int, int], Tuple] = {}        # best tgemm tile, for the fused ops
-        self.fused_core: Dict[Tuple[int, int, int], str] = {}        # "tg" | "blas" per tuned shape
+        self.fused_core: Dict[Tuple[int, int, int], str] = {}        # "tg" | "lin" | "gemvR" per tuned shape
+        self.fused_opts: Dict[Tuple[int, int, int], Dict[str, float]] = {}   # measured us per core choice
         self.ws: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
         self.timings: Dict[Tuple[int, int, int, bool], Dict[str, float]] = {}
 
@@ -465,8 +466,14 @@ def _plan_key(k) -> str:
     return "%d,%d,%d,%d" % (k[0], k[1], k[2], int(k[3]))
 
 
-def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False) -> None:
-    """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest."""
+def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False,
+             fused: Iterable[Tuple[int, int]] = ()) -> None:
+    """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest.
+
+    ``fused``: the (N, K) shapes of one decoder layer's fused ops (QKV, Wo, gate|up, down).  At a
+    given M their fused-GEMV choices are made all-or-nothing: a GEMV residual producer leaves one
+    row-sum slot per workgroup (hundreds), which a GEMV consumer sums in one round trip but a tgemm
+    or standalone-epilogue consumer would walk serially."""
     dev = torch.device(device)
     if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
         return
@@ -485,6 +492,7 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
                     _P.plans[(int(parts[0]), int(parts[1]), int(parts[2]), parts[3] == "1")] = tuple(v)
     shapes = list(shapes)
     _autotune(shapes, list(ms), dev, verbose)
+    _couple_gemv_choices(list(fused), list(ms), verbose)
     if cache:
         import json
         d = {_plan_key(k): list(v) for k, v in _P.plans.items()}
@@ -492,6 +500,20 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
         d.update({"c,%d,%d,%d" % k: v for k, v in _P.fused_core.items()})
         with open(cache, "w") as f:
             json.dump(d, f)
+
+
+def _couple_gemv_choices(fused, ms, verbose: bool) -> None:
+    for M in ms:
+        keys = [(M, N, K) for (N, K) in fused if (M, N, K) in _P.fused_core]
+        gv = [k for k in keys if _P.fused_core[k].startswith("gemv")]
+        if not gv or len(gv) == len(keys):
+            continue
+        for k in gv:
+            opts = {c: t for c, t in _P.fused_opts.get(k, {}).items() if not c.startswith("gemv")}
+            _P.fused_core[k] = min(opts, key=opts.get) if opts else "lin"
+            if verbose:
+                print(f"gemm M={M} N={k[1]} K={k[2]}: fused GEMV dropped (the layer's other fused ops do not "
+                      f"consume its per-workgroup row sums) -> core {_P.fused_core[k]}", flush=True)
 
 
 def _tg_cands(M: int, N: int, K: int):
@@ -587,6 +609,7 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                     for c in gv:
                         opts["gemv%d" % c[1]] = _time(lambda i: ext.gemv_resadd(x, ws[i % copies], rr, sq, c[1]))
                 _P.fused_core[tkey] = min(opts, key=opts.get)
+                _P.fused_opts[tkey] = opts
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
                       for k in ("gemv", "skinny", "lds", "mm", "tg")}

@@ -157,6 +157,14 @@ def bench_decode(eng, B, C):
     h[o[6] + rows] = C
     eng._sync_bt()
     eng.dec_dev.copy_(eng.dec_host_t)
+    if eng._use_worklist(bs):
+        # the persistent attention kernel walks a host-built work list: without it the step's
+        # attention launches would find zero units (rounds before r2-late measured that by mistake)
+        items_t, items = eng._items_bufs[0]
+        ops.decode_work_items(np.full(B, C), eng.model.nkv, eng.max_splits,
+                              eng.ATTN_ITEMS_PER_WG * eng._attn_grid(bs), min_chunk=eng.ATTN_MIN_CHUNK, out=items)
+        n_items = 1 + 2 * int(items[0])
+        eng.items_dev[:n_items].copy_(items_t[:n_items])
     g = eng._graphs.get(bs) or eng._capture(bs)
     ms = timeit(g.replay)
     wbytes = eng.model.weight_bytes()
@@ -333,9 +341,14 @@ if __name__ == "__main__":
         if "decode" in what:
             Bs = [int(x) for x in os.environ.get("MB_DECODE_B", "1,8,32,64,128,256").split(",")]
             Cs = [int(x) for x in os.environ.get("MB_DECODE_C", "512,2048").split(",")]
+            mcs = [int(x) for x in os.environ.get("MB_MIN_CHUNKS", str(eng.ATTN_MIN_CHUNK)).split(",")]
             for B in Bs:
                 for C in Cs:
-                    print(json.dumps(bench_decode(eng, B, C)), flush=True)
+                    for mc in mcs:
+                        eng.ATTN_MIN_CHUNK = mc
+                        print(json.dumps(dict(bench_decode(eng, B, C), min_chunk=mc,
+                                              attn_ch=os.environ.get("DLLM_ATTN_CH", "1"),
+                                              bt_prefetch=os.environ.get("DLLM_ATTN_BT_PREFETCH", "0"))), flush=True)
         if "prefill" in what:
             for B, L in ((1, 512), (8, 1024), (32, 2048)):
                 print(json.dumps(bench_prefill(eng, B, L)), flush=True)

@@ -47,7 +47,7 @@ Published reference rows for comparison (BASELINE.md): general_knowledge @200 ru
 technical_coding @400 runs 75.5 s/query at 8.91 tok/s. personal_health @400 runs 72.9 s/query at 8.32 tok/s.
 Orin energy is 0.37-0.65 J/token.
 
-Single-stream decode of the 1.1B model takes ~0.9 ms per token (scripts/microbench.py --what decode, B=1);
+Single-stream decode of the 1.1B model takes ~0.72 ms per token (scripts/microbench.py --what decode, B=1, fused-epilogue GEMVs);
 that is the latency floor of this sequential protocol. Throughput comes from concurrency (bench.py).
 
 Token counting: "routed tok/s (reference counting)" divides TokenCounter counts of the returned text by the
