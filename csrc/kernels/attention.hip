@@ -65,9 +65,22 @@ struct AttnSmem {
 
 // One work unit: (16-row tile, kv head, split `split` of `nsplit`).  Returns with the LDS free
 // for reuse only after a __syncthreads by the caller.
+// Per-tile metadata: from the tile / sequence arrays, or (extended decode work list) carried in the
+// work item itself, which takes two dependent global round trips off a decode unit's critical path
+// (item -> tile_seq -> seq_qlen/ctx/qstart -> block table -> K/V becomes item -> block table -> K/V).
+struct TileMeta {
+  int seq, tok0, qlen, ctx, qstart;
+};
+
+__device__ __forceinline__ TileMeta load_tile_meta(const AttnArgs& a, int tile) {
+  TileMeta t{a.tile_seq[tile], a.tile_tok0[tile], 0, 0, 0};
+  if (t.seq >= 0) { t.qlen = a.seq_qlen[t.seq]; t.ctx = a.seq_ctx[t.seq]; t.qstart = a.seq_qstart[t.seq]; }
+  return t;
+}
+
 template <int D, int W, int CH, bool PF>
 __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, const int tile, const int kvh,
-                                          const int split, int nsplit) {
+                                          const int split, int nsplit, const TileMeta tm) {
   constexpr int KSTEPS = D / 32;
   constexpr int NT = D / 16;
   auto& s_o = sm.o;
@@ -76,11 +89,9 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   const int splits = a.split_stride;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, rl = lane & 15;
-  const int seq = a.tile_seq[tile];
+  const int seq = tm.seq;
   const int G = a.G, tpt = 16 / G;
-  const int tok0 = a.tile_tok0[tile];
-  int qlen = 0, ctx = 0, qstart = 0;
-  if (seq >= 0) { qlen = a.seq_qlen[seq]; ctx = a.seq_ctx[seq]; qstart = a.seq_qstart[seq]; }
+  const int tok0 = tm.tok0, qlen = tm.qlen, ctx = tm.ctx, qstart = tm.qstart;
 
   // this lane's row
   const int my_tok = tok0 + rl / G, my_head = kvh * G + rl % G;
@@ -365,7 +376,12 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     // key ranges, longest sequences first, so a batch of very different context lengths costs
     // ~(total keys / grid) per workgroup instead of the longest sequence's keys (no surplus
     // early-exit blocks, no tail of one long chain).
-    const int n = a.items[0];
+    // items[0] = n: pairs (tile | kvh << 16, split | nsplit << 8) from items[1]; items[0] = -n:
+    // extended decode list, 16-B units from items[4]: (.., .., seq | qstart << 16, ctx), one token
+    // per tile (qlen 1, tok0 0)
+    const int n0 = a.items[0];
+    const bool ext = n0 < 0;
+    const int n = ext ? -n0 : n0;
     // static: units blockIdx.x, + gridDim.x, ...; dynamic: workgroups take the next unit from an
     // atomic cursor (greedy longest-first scheduling of unequal units) and the last workgroup to
     // leave re-arms cursor and exit count.  (One attn_unit call site: a lambda wrapper here made
@@ -379,11 +395,22 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
       __syncthreads();
     }
     while (it < n) {
-      const int w0 = a.items[1 + 2 * it], w1 = a.items[2 + 2 * it];
+      int w0, w1;
+      TileMeta tm;
+      if (ext) {
+        const int4 u = *reinterpret_cast<const int4*>(a.items + 4 + 4 * it);
+        w0 = u.x;
+        w1 = u.y;
+        tm = TileMeta{u.z & 0xffff, 0, 1, u.w, (int)((unsigned)u.z >> 16)};
+      } else {
+        w0 = a.items[1 + 2 * it];
+        w1 = a.items[2 + 2 * it];
+      }
       const int tile = w0 & 0xffff, kvh = w0 >> 16, split = w1 & 0xff, nsplit = w1 >> 8;
+      if (!ext) tm = load_tile_meta(a, tile < a.num_tiles ? tile : 0);
       // a malformed unit is skipped rather than trusted (it would index past the workspaces)
-      if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.split_stride && split < nsplit)
-        attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, nsplit);
+      if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.split_stride && split < nsplit && tm.ctx >= 0)
+        attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, nsplit, tm);
       __syncthreads();
       if (a.wl_dynamic) {
         if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -421,7 +448,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     kvh = (int)(rest % ny);
     split = (int)(rest / ny);
   }
-  attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, splits);
+  attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, splits, load_tile_meta(a, tile));
 }
 
 template <int D, int W>

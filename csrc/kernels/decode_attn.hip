@@ -235,9 +235,13 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(DecArgs a) {
   if (a.items != nullptr) {
     // persistent: every wave strides over the work list (units longest first, so the round-robin
     // approximates longest-processing-time scheduling); a fixed grid keeps graph replay valid
-    const int n = a.items[0], nw = gridDim.x * 4;
+    // (items[0] < 0: the extended list of attention.hip, 4 ints per unit from items[4]; the
+    // per-unit metadata it carries is not used here)
+    const int n0 = a.items[0], n = n0 < 0 ? -n0 : n0, nw = gridDim.x * 4;
+    const int* base = n0 < 0 ? a.items + 4 : a.items + 1;
+    const int st = n0 < 0 ? 4 : 2;
     for (int it = wid; it < n; it += nw) {
-      const int w0 = a.items[1 + 2 * it], w1 = a.items[2 + 2 * it];
+      const int w0 = base[st * it], w1 = base[st * it + 1];
       const int tile = w0 & 0xffff, kvh = w0 >> 16, split = w1 & 0xff, nsplit = w1 >> 8;
       // a malformed unit is skipped rather than trusted (it would index past the workspaces)
       if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.ns && split < nsplit)

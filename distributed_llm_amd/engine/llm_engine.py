@@ -235,7 +235,7 @@ class LLMEngine:
         # persistent decode attention: host-built work list, copied with the step's metadata
         self.attn_worklist = self.ATTN_WORKLIST and not self.ATTN_DYNAMIC
         if self.attn_worklist:
-            cap = 1 + 2 * mb * nkv * self.max_splits
+            cap = 4 + 4 * mb * nkv * self.max_splits   # extended list (ops.decode_work_items)
             self._items_bufs = []
             for _ in range(2):
                 t = torch.zeros(cap, dtype=torch.int32, pin_memory=pin)
@@ -855,8 +855,8 @@ class LLMEngine:
             target = 4096 if self.DECODE_WAVE else self.ATTN_ITEMS_PER_WG * grid
             items_t, items = self._items_bufs[p]
             ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target,
-                                  min_chunk=self.ATTN_MIN_CHUNK, out=items)
-            n_items = 1 + 2 * int(items[0])
+                                  min_chunk=self.ATTN_MIN_CHUNK, out=items, seq=rows[order], qstart=order)
+            n_items = ops.work_items_len(items)
         h[o[4]:o[6] + R + 1] = 0
         h[o[4] + rows] = np.arange(B)
         h[o[5] + rows] = 1

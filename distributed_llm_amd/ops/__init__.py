@@ -234,7 +234,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
 
 
 def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,
-                      out: Optional[np.ndarray] = None) -> np.ndarray:
+                      out: Optional[np.ndarray] = None, seq=None, qstart=None) -> np.ndarray:
     """Work list for persistent decode attention (one query token per tile, tiles in ``ctx`` order).
 
     Every (tile, kv head) is cut into ``ceil(ctx / chunk)`` splits (at most ``max_splits``) with
@@ -242,6 +242,11 @@ def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chu
     tile, so with tiles sorted longest context first the list runs from the largest units to the
     smallest (round-robin over the grid then approximates longest-processing-time scheduling).
     Returns int32 ``[1 + 2n]``: ``n``, then ``(tile | kvh << 16, split | nsplit << 8)`` pairs.
+
+    With ``seq`` / ``qstart`` (per tile: block-table row and query row) the list is the extended
+    form ``[4 + 4n]``: ``-n``, three pad words, then 16-byte units ``(tile | kvh << 16,
+    split | nsplit << 8, seq | qstart << 16, ctx)``, so the kernel reads a unit's sequence
+    metadata with the unit instead of through two more dependent loads.
     """
     ctx = np.asarray(ctx, dtype=np.int64)
     B = ctx.shape[0]
@@ -255,12 +260,26 @@ def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chu
     j = np.arange(n, dtype=np.int64) - np.repeat(starts, rep)
     ns_r = np.repeat(ns, rep)
     tile = np.repeat(np.arange(B, dtype=np.int64), rep)
-    buf = out if out is not None else np.empty(1 + 2 * n, dtype=np.int32)
-    buf[0] = n
-    w = buf[1:1 + 2 * n].reshape(n, 2)
+    ext = seq is not None
+    head, width = (4, 4) if ext else (1, 2)
+    buf = out if out is not None else np.empty(head + width * n, dtype=np.int32)
+    buf[0] = -n if ext else n
+    w = buf[head:head + width * n].reshape(n, width)
     w[:, 0] = tile | ((j // ns_r) << 16)
     w[:, 1] = (j % ns_r) | (ns_r << 8)
+    if ext:
+        buf[1:4] = 0
+        seq = np.asarray(seq, dtype=np.int64)
+        qstart = np.asarray(qstart, dtype=np.int64)
+        w[:, 2] = np.repeat(seq | (qstart << 16), rep)
+        w[:, 3] = np.repeat(ctx, rep)
     return buf
+
+
+def work_items_len(items: np.ndarray) -> int:
+    """Number of int32 words of a :func:`decode_work_items` list (either form)."""
+    n = int(items[0])
+    return 4 + 4 * (-n) if n < 0 else 1 + 2 * n
 
 
 # ----------------------------------------------------------------------------- activations

@@ -162,8 +162,9 @@ def bench_decode(eng, B, C):
         # attention launches would find zero units (rounds before r2-late measured that by mistake)
         items_t, items = eng._items_bufs[0]
         ops.decode_work_items(np.full(B, C), eng.model.nkv, eng.max_splits,
-                              eng.ATTN_ITEMS_PER_WG * eng._attn_grid(bs), min_chunk=eng.ATTN_MIN_CHUNK, out=items)
-        n_items = 1 + 2 * int(items[0])
+                              eng.ATTN_ITEMS_PER_WG * eng._attn_grid(bs), min_chunk=eng.ATTN_MIN_CHUNK, out=items,
+                              seq=rows, qstart=np.arange(B))
+        n_items = ops.work_items_len(items)
         eng.items_dev[:n_items].copy_(items_t[:n_items])
     g = eng._graphs.get(bs) or eng._capture(bs)
     ms = timeit(g.replay)

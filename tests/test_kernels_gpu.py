@@ -134,9 +134,11 @@ def test_paged_attention_dynamic_split(split_len, z):
 
 @pytest.mark.parametrize("nq,nkv,d", [(32, 4, 64), (32, 8, 128), (64, 8, 128)])
 @pytest.mark.parametrize("grid,target,min_chunk", [(1, 4, 32), (7, 16, 32), (64, 256, 256), (512, 2048, 256)])
-def test_paged_attention_worklist(nq, nkv, d, grid, target, min_chunk):
+@pytest.mark.parametrize("ext", [False, True])
+def test_paged_attention_worklist(nq, nkv, d, grid, target, min_chunk, ext):
     """Persistent decode attention: a fixed grid walks a host-built list of (tile, kv head, split)
-    units (1..16 splits per tile, longest first); repeated launches re-use the ticket counters."""
+    units (1..16 splits per tile, longest first); repeated launches re-use the ticket counters.
+    ``ext``: the extended list whose units carry (sequence, query row, context) themselves."""
     ctxs = [1000, 1, 17, 300, 64, 2047, 33, 512, 129, 5]
     seqs = [(1, c) for c in ctxs]
     q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(nq, nkv, d, seqs, NB=320, spike=True)
@@ -147,9 +149,15 @@ def test_paged_attention_worklist(nq, nkv, d, grid, target, min_chunk):
     nt = ts.numel()
     ws = (torch.empty(nt * nkv * z * 16 * d, device=DEV), torch.empty(nt * nkv * z * 16 * 2, device=DEV),
           torch.zeros(nt * nkv + 2, dtype=torch.int32, device=DEV))
-    items = ops.decode_work_items(np.array(ctxs)[order], nkv, z, target, min_chunk=min_chunk)
-    n = int(items[0])
-    w = items[1:1 + 2 * n].reshape(n, 2)
+    if ext:
+        items = ops.decode_work_items(np.array(ctxs)[order], nkv, z, target, min_chunk=min_chunk, seq=order,
+                                      qstart=qs.cpu().numpy()[order])
+        n = -int(items[0])
+        w = items[4:4 + 4 * n].reshape(n, 4)
+    else:
+        items = ops.decode_work_items(np.array(ctxs)[order], nkv, z, target, min_chunk=min_chunk)
+        n = int(items[0])
+        w = items[1:1 + 2 * n].reshape(n, 2)
     assert ((w[:, 1] & 0xFF) < (w[:, 1] >> 8)).all() and (w[:, 1] >> 8).max() <= z
     it = torch.tensor(items, device=DEV)
     o2 = ref.paged_attention(q, kc, vc, bt, qs, ql, cx, 1 / math.sqrt(d))

@@ -35,3 +35,21 @@ def test_work_items_into_buffer():
     out = np.full(1 + 2 * 64, -7, dtype=np.int32)
     buf = ops.decode_work_items(np.array([100, 40]), 2, 16, 64, min_chunk=32, out=out)
     assert buf is out and int(out[0]) == 2 * (4 + 2)   # ceil(100/32)=4, ceil(40/32)=2 splits
+
+
+def test_work_items_extended_form():
+    """Extended list: -n, 3 pad words, then 16-B units that also carry (seq | qstart << 16, ctx)
+    of their tile; the (tile, head, split) part is identical to the plain list."""
+    ctx = np.array([900, 300, 40, 1])
+    seq = np.array([5, 0, 7, 2])
+    qstart = np.array([1, 3, 0, 2])
+    plain = ops.decode_work_items(ctx, 4, 16, 64, min_chunk=64)
+    ext = ops.decode_work_items(ctx, 4, 16, 64, min_chunk=64, seq=seq, qstart=qstart)
+    n = int(plain[0])
+    assert int(ext[0]) == -n and (ext[1:4] == 0).all() and ops.work_items_len(ext) == 4 + 4 * n == ext.size
+    assert ops.work_items_len(plain) == 1 + 2 * n
+    u = ext[4:].reshape(n, 4).astype(np.int64)
+    assert (u[:, :2] == plain[1:].reshape(n, 2)).all()
+    tile = u[:, 0] & 0xFFFF
+    assert (u[:, 2] & 0xFFFF == seq[tile]).all() and (u[:, 2] >> 16 == qstart[tile]).all()
+    assert (u[:, 3] == ctx[tile]).all()
