@@ -109,6 +109,23 @@ constexpr int SR_CAP = 1024;   // candidate list capacity (only ties AT the thre
 constexpr int SR_MAXN = 512;   // above this many candidates the exact-threshold pass runs
 constexpr int SR_KMAX = 256;
 
+// Visit a row's 16-B logit vectors c = tid, tid + NT, ... four at a time with all four loads
+// issued before the first is used (a row is ~16 vectors per thread: one dependent round trip per
+// vector was most of a batch-1 sampler launch).  f(vec, c) sees every vector exactly once.
+template <int NT, class F>
+static __device__ __forceinline__ void for_each_vec(const u16* __restrict__ l, int nv, int tid, F f) {
+  int c = tid;
+  for (; c + 3 * NT < nv; c += 4 * NT) {
+    const uint4 v0 = ld16(l + (long)c * 8), v1 = ld16(l + (long)(c + NT) * 8);
+    const uint4 v2 = ld16(l + (long)(c + 2 * NT) * 8), v3 = ld16(l + (long)(c + 3 * NT) * 8);
+    f(v0, c);
+    f(v1, c + NT);
+    f(v2, c + 2 * NT);
+    f(v3, c + 3 * NT);
+  }
+  for (; c < nv; c += NT) f(ld16(l + (long)c * 8), c);
+}
+
 static __device__ __forceinline__ unsigned bf_key(u16 b) {
   if ((b & 0x7f80) == 0x7f80 && (b & 0x7f)) return 0u;  // NaN: never selected
   return (b & 0x8000) ? (unsigned)(~b & 0xffff) : (unsigned)(b | 0x8000);
@@ -148,12 +165,12 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
   if (!(t > 0.f)) {  // greedy row: arg-max, ties -> lowest index
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int c = tid; c < nv; c += SR_THREADS) {
+    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
       float f[8];
-      unpack8(ld16(l + c * 8), f);
+      unpack8(v, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) better(bv, bi, f[j], c * 8 + j);
-    }
+    });
     for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) better(bv, bi, bf2f(l[i]), i);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -172,6 +189,57 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
   int k = top_k[row];
   if (k <= 0 || k > SR_KMAX) k = SR_KMAX;
   if (k > V) k = V;
+
+  // ---- 0. fast bound (no histogram): T0 = the k-th largest of the 256 per-thread maximum keys.
+  // At least k logits are >= T0 (one per thread whose maximum is), so every top-k logit is too;
+  // when few logits reach T0 (typical: ~k-3k of 32 K) they are the whole candidate list and the
+  // 4096-bin LDS-atomic histogram (hot bins serialise its atomics: ~40 us for one row) is skipped.
+  // A flat row (> SR_MAXN logits at or above T0) falls through to the histogram path.
+  {
+    unsigned tmax = 0u;
+    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int) {
+      const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tmax = max(tmax, bf_key(e[j]));
+    });
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) tmax = max(tmax, bf_key(l[i]));
+    hist[tid] = tmax;
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    int r = 0;  // rank among the thread maxima (ties -> lower thread first)
+    for (int j = 0; j < SR_THREADS; ++j) {
+      const unsigned o = hist[j];
+      r += (o > tmax || (o == tmax && j < tid)) ? 1 : 0;
+    }
+    if (r == k - 1) s_lo = (int)tmax;
+    __syncthreads();
+    const unsigned t0 = (unsigned)s_lo;
+    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
+      const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned key = bf_key(e[j]);
+        if (key >= t0 && key != 0u) {
+          const int p = atomicAdd(&s_n, 1);
+          if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+        }
+      }
+    });
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
+      const unsigned key = bf_key(l[i]);
+      if (key >= t0 && key != 0u) {
+        const int p = atomicAdd(&s_n, 1);
+        if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(i));
+      }
+    }
+    __syncthreads();
+  }
+  int na, nt;
+  if (s_n >= k && s_n <= SR_MAXN) {
+    na = s_n;
+    nt = 0;
+  } else {
+  __syncthreads();  // every thread has read s_n before the histogram path reuses it
 
   // ---- 1. coarse histogram (12-bit bins) and the bin of the k-th largest
   for (int i = tid; i < 4096; i += SR_THREADS) hist[i] = 0u;
@@ -275,7 +343,9 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
     }
   }
   __syncthreads();
-  const int na = min(s_n, amax), nt = min(s_nt, SR_CAP - amax);
+  na = min(s_n, amax);
+  nt = min(s_nt, SR_CAP - amax);
+  }
   const int n = na + nt;
   // candidate j of the union [0, na) u [SR_CAP - nt, SR_CAP)
   auto cidx = [&](int j) { return j < na ? j : SR_CAP - nt + (j - na); };
