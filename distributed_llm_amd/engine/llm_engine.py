@@ -88,6 +88,7 @@ class _Seq:
     finished: Optional[float] = None
     error: Optional[str] = None
     done: threading.Event = field(default_factory=threading.Event)
+    out_text: Optional[str] = None   # detokenised answer, formed as soon as the sequence stops
 
     @property
     def length(self) -> int:
@@ -1074,6 +1075,12 @@ class LLMEngine:
             self.timers["decode_host_post"] += time.perf_counter() - _t2
             if launched is None:
                 return finished, preempted
+            if done_now:
+                # the next step is already on the GPU: detokenise the stopped answers under it
+                _t3 = time.perf_counter()
+                for s in done_now:
+                    self._finalize_text(s)
+                self.timers["output"] += time.perf_counter() - _t3
             freed = bool(waiting) and bool(done_now or preempted)
             cur, pc, ev = launched
 
@@ -1145,13 +1152,14 @@ class LLMEngine:
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ outputs
-    def _output(self, s: _Seq) -> RequestOutput:
-        end = s.finished or time.perf_counter()
-        lat = (end - s.arrival) * 1000.0
-        ttft = ((s.first_tok or end) - s.arrival) * 1000.0
-        queue = ((s.admitted or end) - s.arrival) * 1000.0
-        n = len(s.out)
-        dec_t = (end - s.first_tok) if s.first_tok else 0.0
+    def _finalize_text(self, s: _Seq) -> str:
+        """Detokenise a stopped sequence's answer and memoise prompt+answer ids for the next turn.
+
+        Called from the decode loop the moment a sequence stops (``_decode_burst``), so with
+        pipelined decode this host work runs while the GPU executes the next step instead of in
+        one serial pass after the whole batch has finished; ``_output`` re-uses the result."""
+        if s.out_text is not None:
+            return s.out_text
         toks = [t for t in s.out if t != self.tok.eos_id] if not s.params.ignore_eos else list(s.out)
         # strip whitespace-only tokens at both ends so that text == decode(ids) exactly (pools strip)
         while toks and not self.tok.decode(toks[:1]).strip():
@@ -1161,5 +1169,16 @@ class LLMEngine:
         text = self.tok.decode(toks)
         if s.text is not None and s.error is None and text:
             self._remember(s.text + text, s.prompt + toks)
+        s.out_text = text
+        return text
+
+    def _output(self, s: _Seq) -> RequestOutput:
+        end = s.finished or time.perf_counter()
+        lat = (end - s.arrival) * 1000.0
+        ttft = ((s.first_tok or end) - s.arrival) * 1000.0
+        queue = ((s.admitted or end) - s.arrival) * 1000.0
+        n = len(s.out)
+        dec_t = (end - s.first_tok) if s.first_tok else 0.0
+        text = self._finalize_text(s)
         return RequestOutput(s.id, text, list(s.out), len(s.prompt), s.num_cached, n, lat, ttft,
                              queue, (n - 1) / dec_t if n > 1 and dec_t > 0 else 0.0, s.error)
