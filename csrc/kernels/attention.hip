@@ -27,6 +27,7 @@
 namespace {
 constexpr int BS = 16;     // tokens per KV block
 constexpr int WAVES = 4;   // LDS combine slots; a workgroup runs W = 4 or 8 waves
+constexpr int COMBINE_MAXS = 16;  // split counts up to this take the parallel last-arriver combine
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct AttnArgs {
@@ -332,6 +333,56 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   }
   if (!ticket_last(&a.counters[tile * a.nkv + kvh], nsplit, &sm.last)) return;
   const long tbase = (((long)tile * a.nkv + kvh) * splits) * 16;
+  if (nsplit <= COMBINE_MAXS) {
+    // Parallel combine: every split's (m, l) pair is loaded by its own thread and every thread's
+    // O partials of all splits are in flight together, so the last arriver pays ~2 memory round
+    // trips instead of 3 x nsplit dependent ones (the write-through loads go past L2; at batch 1
+    // that serial chain was most of a decode attention launch).  sm.o is free scratch here.
+    float* s_pm = &sm.o[0][0][0];               // [nsplit][16] maxima, then [nsplit][16] sums
+    float* s_pl = s_pm + COMBINE_MAXS * 16;
+    if (threadIdx.x < 8 * nsplit) {             // thread (sp, pair): rows 2 pair, 2 pair + 1
+      const int sp = threadIdx.x >> 3, pr = threadIdx.x & 7;
+      const float4 q = ld_wt16(rml, (unsigned)((tbase + sp * 16 + 2 * pr) * 2 * 4));
+      s_pm[sp * 16 + 2 * pr] = q.x;
+      s_pl[sp * 16 + 2 * pr] = q.y;
+      s_pm[sp * 16 + 2 * pr + 1] = q.z;
+      s_pl[sp * 16 + 2 * pr + 1] = q.w;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+      const int row = threadIdx.x;
+      float M = -INFINITY;
+      for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, s_pm[sp * 16 + row]);
+      const float Ms = (M == -INFINITY) ? 0.f : M;
+      float L = 0.f;
+      for (int sp = 0; sp < nsplit; ++sp) L += s_pl[sp * 16 + row] * exp2f(s_pm[sp * 16 + row] - Ms);
+      s_m[0][row] = Ms;
+      s_l[0][row] = L;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x * 4; e < 16 * D; e += blockDim.x * 4) {
+      const int row = e / D, col = e % D;
+      const int tok = tok0 + row / G_, head = kvh * G_ + row % G_;
+      if (seq < 0 || tok >= qlen) continue;
+      float4 q[COMBINE_MAXS];
+#pragma unroll
+      for (int sp = 0; sp < COMBINE_MAXS; ++sp)
+        if (sp < nsplit) q[sp] = ld_wt16(ro, (unsigned)(((tbase + sp * 16 + row) * D + col) * 4));
+      float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < COMBINE_MAXS; ++sp) {
+        if (sp < nsplit) {
+          const float f = exp2f(s_pm[sp * 16 + row] - s_m[0][row]);
+          o[0] += q[sp].x * f; o[1] += q[sp].y * f; o[2] += q[sp].z * f; o[3] += q[sp].w * f;
+        }
+      }
+      const float L = s_l[0][row], inv = L > 0.f ? 1.f / L : 0.f;
+      u16* dst = a.out + ((long)(qstart + tok) * a.nq + head) * D + col;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = f2bf(o[j] * inv);
+    }
+    return;
+  }
   if (threadIdx.x < 16) {
     const int row = threadIdx.x;
     float M = -INFINITY;
