@@ -280,9 +280,10 @@ class LLMEngine:
     # static split grid (a kernel-only sweep had B=16-64 about even)
     ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "1"))
     # shortest key range of one work-list unit (split-K granularity)
-    # (512: scripts/gpu_attn_small_b.sh measured 1-3 % faster steps than 256 at batch 1-16; it only
-    # matters while batch x context < 64k tokens, above that the target unit count sets the chunk)
-    ATTN_MIN_CHUNK = int(os.environ.get("DLLM_ATTN_MIN_CHUNK", "512"))
+    # (256: with the parallel split combine, batch 1-8 steps at 2k context are 2-3 % faster than at
+    # 512 and equal at 8k, microbench decode sweep; it only matters while batch x context < 64k
+    # tokens, above that the target unit count sets the chunk)
+    ATTN_MIN_CHUNK = int(os.environ.get("DLLM_ATTN_MIN_CHUNK", "256"))
     # Alternative decode kernel (csrc/kernels/decode_attn.hip, one wave per unit, 1024 workgroups,
     # 4096-unit list): measured equal at best, slower at small batch (profiles/r2_decode_attention_
     # microbench.md), so opt-in only
