@@ -248,11 +248,18 @@ def main() -> int:
         tracer.enable(a.trace.replace("{rank}", str(rank)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     on_gpu = torch.cuda.is_available() and not a.cpu
+    # DLLM_REHEARSE_ONE_GPU=1: every rank on GPU 0 with gloo collectives — rehearses the N-rank
+    # bench path (process group, per-rank engines and graphs, barriers, cross-rank reduction) on a
+    # one-GPU box; RCCL itself refuses two ranks on one device.  Never used for reported numbers.
+    rehearse = world > 1 and on_gpu and os.environ.get("DLLM_REHEARSE_ONE_GPU") == "1"
+    if rehearse:
+        local = 0
+    coll_dev = "cpu" if (rehearse or not on_gpu) else f"cuda:{local}"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if on_gpu:
             torch.cuda.set_device(local)
-        dist.init_process_group("nccl" if on_gpu else "gloo")
+        dist.init_process_group("nccl" if on_gpu and not rehearse else "gloo")
     dev = f"cuda:{local}" if on_gpu else "cpu"
     if not on_gpu:
         os.environ.setdefault("DLLM_EMBEDDER", "hash")
@@ -389,7 +396,7 @@ def main() -> int:
         tokens = sum(r["tok"] for r in records)
     lats = sorted(r["lat"] for r in records)
     if world > 1:
-        t = torch.tensor([float(tokens), elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([float(tokens), elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t[:1], op=dist.ReduceOp.SUM)
         dist.all_reduce(t[1:], op=dist.ReduceOp.MAX)
         tokens_all, elapsed_max = float(t[0]), float(t[1])
@@ -440,6 +447,8 @@ def main() -> int:
                                     for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
                                               "t_decode_host_post_s", "t_encode_s", "t_admit_s", "t_output_s")},
         }
+        if rehearse:
+            out["rehearsal_one_gpu"] = True   # N ranks shared ONE GPU: plumbing check, not a number
         # rank-0 wall time not inside any engine timer: routing, prompt formatting, orchestration
         out["engine_time_split_s"]["outside_engine_s"] = round(
             elapsed_max - sum(out["engine_time_split_s"].values()), 3) if len(engines) == 1 else None
