@@ -312,13 +312,15 @@ def main() -> int:
         sm = a.small_model if on_gpu else "tiny-llama-test"
         lg = a.large_model if on_gpu else "tiny-moe-test"
         n_small = len(topo.replicas[SMALL])
+        # (a one-GPU rehearsal runs the collectives on gloo, which a hipGraph cannot capture)
+        graphs = not (a.no_graphs or rehearse)
         specs = {SMALL: TierSpec(sm, a.small_new, 0.0, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
-                                 max_num_seqs=max(16, a.convs * world)),
+                                 max_num_seqs=max(16, a.convs * world), graphs=graphs),
                  LARGE: TierSpec(lg, a.large_new, 0.8, 40, 0.9, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
-                                 max_num_seqs=max(16, a.convs * world))}
+                                 max_num_seqs=max(16, a.convs * world), graphs=graphs)}
         cluster = Cluster(topo, specs, device=dev)
         engines = list(cluster.engines.values())
-        if on_gpu:
+        if on_gpu and graphs:
             for e in engines:
                 e.capture_all(max_bs=e._bucket(min(e.R, max(16, a.convs * world))))
         tp = len(topo.replicas[LARGE][0])

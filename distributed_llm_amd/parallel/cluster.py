@@ -37,6 +37,7 @@ class TierSpec:
     top_p: float = 1.0
     kv_cache_gb: Optional[float] = None
     max_num_seqs: int = 256
+    graphs: bool = True          # hipGraph decode (off: eager steps, e.g. gloo collectives)
 
 
 @dataclass
@@ -105,7 +106,7 @@ class Cluster:
             if str(self.device).startswith("cuda"):
                 par.enable_custom_all_reduce(self.device)  # collective over this TP group
             eng = LLMEngine(spec.model, device=self.device, par=par, kv_cache_gb=spec.kv_cache_gb,
-                            max_num_seqs=spec.max_num_seqs)
+                            max_num_seqs=spec.max_num_seqs, use_graphs=spec.graphs)
             if len(ranks) > 1:
                 eng.enable_tp_mirror(self.mirror_groups[tuple(ranks)], ranks[0])
             self.engines[key] = eng

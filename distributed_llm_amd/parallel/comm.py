@@ -117,11 +117,11 @@ class ParallelContext:
         if self.tp_size == 1:
             return t.unsqueeze(0)
         t = t.contiguous()
-        if t.is_cuda:  # RCCL: one fused all-gather into a preallocated tensor
+        if t.is_cuda and dist.get_backend(self.tp_group) == "nccl":  # RCCL: one fused all-gather
             out = torch.empty((self.tp_size, *t.shape), dtype=t.dtype, device=t.device)
             dist.all_gather_into_tensor(out, t, group=self.tp_group)
             return out
-        parts = [torch.empty_like(t) for _ in range(self.tp_size)]  # gloo (CPU tests)
+        parts = [torch.empty_like(t) for _ in range(self.tp_size)]  # gloo (CPU tests, one-GPU rehearsal)
         dist.all_gather(parts, t, group=self.tp_group)
         return torch.stack(parts)
 
