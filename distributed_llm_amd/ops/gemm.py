@@ -470,10 +470,9 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
              fused: Iterable[Tuple[int, int]] = ()) -> None:
     """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest.
 
-    ``fused``: the (N, K) shapes of one decoder layer's fused ops (QKV, Wo, gate|up, down).  At a
-    given M their fused-GEMV choices are made all-or-nothing: a GEMV residual producer leaves one
-    row-sum slot per workgroup (hundreds), which a GEMV consumer sums in one round trip but a tgemm
-    or standalone-epilogue consumer would walk serially."""
+    ``fused``: the (N, K) shapes of one decoder layer's fused ops (QKV, Wo, gate|up, down); a
+    residual producer keeps the fused GEMV only where its consumer runs it too
+    (``_couple_gemv_choices``)."""
     dev = torch.device(device)
     if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
         return
@@ -503,17 +502,25 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
 
 
 def _couple_gemv_choices(fused, ms, verbose: bool) -> None:
+    """A fused-GEMV residual producer leaves one row-sum slot per workgroup (hundreds), which a
+    GEMV consumer sums in one round trip but a tgemm prologue or standalone epilogue walks
+    serially.  ``fused`` = (QKV, Wo, gate|up, down) shapes of a dense layer: Wo feeds gate|up and
+    down feeds the next layer's QKV, so a producer keeps the GEMV only if its consumer runs it too
+    (MoE layers pass (QKV, Wo): their producers feed standalone norms, no constraint)."""
+    fused = list(fused)
+    pairs = [(fused[1], fused[2]), (fused[3], fused[0])] if len(fused) == 4 else []
     for M in ms:
-        keys = [(M, N, K) for (N, K) in fused if (M, N, K) in _P.fused_core]
-        gv = [k for k in keys if _P.fused_core[k].startswith("gemv")]
-        if not gv or len(gv) == len(keys):
-            continue
-        for k in gv:
-            opts = {c: t for c, t in _P.fused_opts.get(k, {}).items() if not c.startswith("gemv")}
-            _P.fused_core[k] = min(opts, key=opts.get) if opts else "lin"
+        for prod, cons in pairs:
+            kp, kc = (M,) + tuple(prod), (M,) + tuple(cons)
+            cp, cc = _P.fused_core.get(kp), _P.fused_core.get(kc)
+            if cp is None or not cp.startswith("gemv") or (cc is not None and cc.startswith("gemv")):
+                continue
+            opts = {c: t for c, t in _P.fused_opts.get(kp, {}).items() if not c.startswith("gemv")}
+            _P.fused_core[kp] = min(opts, key=opts.get) if opts else "lin"
             if verbose:
-                print(f"gemm M={M} N={k[1]} K={k[2]}: fused GEMV dropped (the layer's other fused ops do not "
-                      f"consume its per-workgroup row sums) -> core {_P.fused_core[k]}", flush=True)
+                print(f"gemm M={M} N={kp[1]} K={kp[2]}: fused GEMV dropped (its consumer N={kc[1]} K={kc[2]} "
+                      f"runs {cc}, which would walk the per-workgroup row sums) -> core {_P.fused_core[kp]}",
+                      flush=True)
 
 
 def _tg_cands(M: int, N: int, K: int):

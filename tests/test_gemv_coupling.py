@@ -1,0 +1,32 @@
+"""Fused-GEMV choice coupling (ops.gemm._couple_gemv_choices): a residual producer (Wo, down) keeps
+the fused GEMV only where its consumer (gate|up, next layer's QKV) runs it too, since a GEMV
+producer leaves one row-sum slot per workgroup.  Pure host logic: runs on CPU."""
+from distributed_llm_amd.ops import gemm as G
+
+LAYER = [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632)]   # QKV, Wo, gate|up, down
+
+
+def _set(M, choices):
+    for (N, K), c in zip(LAYER, choices):
+        G._P.fused_core[(M, N, K)] = c
+        G._P.fused_opts[(M, N, K)] = {"tg": 5.0, "lin": 4.0, c: 3.0}
+
+
+def test_producer_drops_gemv_when_consumer_does_not_run_it(monkeypatch):
+    monkeypatch.setattr(G._P, "fused_core", {})
+    monkeypatch.setattr(G._P, "fused_opts", {})
+    _set(1, ("gemv1",) * 4)                          # all GEMV: nothing changes
+    _set(4, ("gemv1", "gemv1", "tg", "gemv1"))       # Wo -> tg gate|up: Wo falls back, down keeps it
+    _set(8, ("lin", "gemv2", "gemv1", "gemv1"))      # down -> lin QKV: down falls back
+    G._couple_gemv_choices(LAYER, [1, 4, 8], verbose=False)
+    fc = G._P.fused_core
+    assert all(fc[(1, N, K)] == "gemv1" for N, K in LAYER)
+    assert fc[(4, 2048, 2048)] == "lin" and fc[(4, 2048, 5632)] == "gemv1" and fc[(4, 2560, 2048)] == "gemv1"
+    assert fc[(8, 2048, 2048)] == "gemv2" and fc[(8, 2048, 5632)] == "lin"
+
+
+def test_moe_layers_have_no_pairs(monkeypatch):
+    monkeypatch.setattr(G._P, "fused_core", {(2, 2560, 2048): "gemv1", (2, 2048, 2048): "gemv1"})
+    monkeypatch.setattr(G._P, "fused_opts", {})
+    G._couple_gemv_choices(LAYER[:2], [2], verbose=False)
+    assert G._P.fused_core[(2, 2048, 2048)] == "gemv1"
