@@ -146,3 +146,22 @@ def test_pipelined_decode_eos_zombie_rows(monkeypatch):
         assert eos not in x[:-1] and len(x) <= 24
     assert any(x and x[-1] == eos for x in a)
     assert ea.bm.check_invariants() == "" and ea.bm.stats()["active_seqs"] == 0
+
+
+def test_pipelined_text_and_turn_memo_match_stepwise(monkeypatch):
+    """Answers detokenised inside the pipelined burst (under the next GPU step) give the same text
+    as the step-by-step loop, and the memoised prompt+answer ids make turn 2 a prefix-cache hit."""
+    sps = [SamplingParams(max_new_tokens=6 + 4 * (i % 3), ignore_eos=True) for i in range(len(PROMPTS))]
+
+    def two_turns():
+        e = _engine(max_num_seqs=8)
+        first = e.generate(PROMPTS, sps)
+        turn2 = [p + first[i].text + "\nuser: go on" for i, p in enumerate(PROMPTS)]
+        second = e.generate(turn2, sps)
+        return [o.text for o in first], [o.token_ids for o in second], [o.num_cached for o in second]
+
+    ta, ia, ca = two_turns()
+    _stepwise(monkeypatch)
+    tb, ib, cb = two_turns()
+    assert ta == tb and ia == ib and ca == cb
+    assert all(c >= 16 for c, p in zip(ca, PROMPTS) if len(p) >= 32)
