@@ -1103,12 +1103,12 @@ class LLMEngine:
         if self._use_worklist(bs):
             return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart,
                             qlen=self.d_qlen, ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
-                            last_idx=self.d_last[:bs], splits=self.max_splits, workspace=self.dec_ws,
+                            last_idx=self.d_last[:bs], all_last=True, splits=self.max_splits, workspace=self.dec_ws,
                             items=self.items_dev, grid_items=1024 if self.DECODE_WAVE else self._attn_grid(bs),
                             wave=self.DECODE_WAVE)
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
                         ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
-                        last_idx=self.d_last[:bs], splits=self._decode_splits(bs), workspace=self.dec_ws,
+                        last_idx=self.d_last[:bs], all_last=True, splits=self._decode_splits(bs), workspace=self.dec_ws,
                         split_len=self.d_split if self.ATTN_DYNAMIC else None)
 
     def _decode_forward(self, bs: int) -> None:

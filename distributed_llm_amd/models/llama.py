@@ -54,6 +54,7 @@ class AttnMeta:
     grid_items: int = 0                        # workgroups walking ``items``
     flash: bool = False                        # prefill: tile_seq/tile_tok0 are 128-row flash tiles
     wave: bool = False                         # decode: wave-per-unit kernel (decode_attn.hip) over ``items``
+    all_last: bool = False                     # decode: every row is its sequence's last token (no gather)
 
 
 def qk_dim_order(d: int) -> torch.Tensor:
@@ -352,8 +353,8 @@ class LlamaModel:
             else:
                 x = ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual)
                 h = self._mlp_out(L, x)
-        last_h = h.index_select(0, meta.last_idx)
-        last_r = residual.index_select(0, meta.last_idx)
+        last_h = h if meta.all_last else h.index_select(0, meta.last_idx)
+        last_r = residual if meta.all_last else residual.index_select(0, meta.last_idx)
         return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)
 
     def _hidden_states_fused(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
@@ -379,7 +380,7 @@ class LlamaModel:
             else:
                 x = ops.rms_norm(r, L["ln2"], eps)
                 n = ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a)
-        return ops.rms_norm(r.index_select(0, meta.last_idx), self.final_norm, eps)
+        return ops.rms_norm(r if meta.all_last else r.index_select(0, meta.last_idx), self.final_norm, eps)
 
     def _hidden_states_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
                           kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:

@@ -497,6 +497,8 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
         d = {_plan_key(k): list(v) for k, v in _P.plans.items()}
         d.update({_plan_key(k): list(v) for k, v in _P.tg_plans.items()})
         d.update({"c,%d,%d,%d" % k: v for k, v in _P.fused_core.items()})
+        if os.path.dirname(cache):
+            os.makedirs(os.path.dirname(cache), exist_ok=True)
         with open(cache, "w") as f:
             json.dump(d, f)
 
