@@ -30,3 +30,22 @@ def test_moe_layers_have_no_pairs(monkeypatch):
     monkeypatch.setattr(G._P, "fused_opts", {})
     G._couple_gemv_choices(LAYER[:2], [2], verbose=False)
     assert G._P.fused_core[(2, 2048, 2048)] == "gemv1"
+
+
+def test_fused_gemv_eligibility(monkeypatch):
+    """fused_gemv_r: only batch 1/2/4/8, X within the 64 KB LDS stage, 16-B aligned rows, N % 32 == 0,
+    and only where the autotuner (or DLLM_FUSED_CORE) picked a gemvR core."""
+    import torch
+    monkeypatch.setattr(G._P, "fused_core", {(1, 2560, 2048): "gemv2", (8, 2560, 2048): "tg"})
+    monkeypatch.delenv("DLLM_FUSED_CORE", raising=False)
+    x1 = torch.zeros(1, 2048, dtype=torch.bfloat16)
+    assert G.fused_gemv_r(x1, 2560) == 2
+    assert G.fused_gemv_r(torch.zeros(8, 2048, dtype=torch.bfloat16), 2560) == 0     # tuned to tgemm
+    assert G.fused_gemv_r(torch.zeros(3, 2048, dtype=torch.bfloat16), 2560) == 0     # not a GEMV batch
+    assert G.fused_gemv_r(x1, 2561) == 0                                             # N % 32
+    assert G.fused_gemv_r(torch.zeros(8, 8192, dtype=torch.bfloat16), 2560) == 0     # 128 KB of X
+    assert G.fused_gemv_r(torch.zeros(1, 4096, dtype=torch.bfloat16)[:, :2048], 2560) == 2   # strided rows ok
+    monkeypatch.setenv("DLLM_FUSED_CORE", "gemv4")
+    assert G.fused_gemv_r(torch.zeros(4, 2048, dtype=torch.bfloat16), 64) == 4
+    monkeypatch.setenv("DLLM_FUSED_CORE", "tg")
+    assert G.fused_gemv_r(x1, 2560) == 0
