@@ -18,7 +18,7 @@ int dllm_paged_attention(const void*, const void*, const void*, const int*, cons
                          const int*, const int*, void*, float*, float*, int*, const int*, const int*, int, int, int,
                          int, int, int, int, int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
-int dllm_embed(const int*, const void*, void*, long, int, long, long, hipStream_t);
+int dllm_embed(const int*, const void*, void*, long, int, long, long, float*, hipStream_t);
 int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, int, const void*, void*, const void*,
               float, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
@@ -256,14 +256,21 @@ void silu_mul(torch::Tensor gu, torch::Tensor out) {
   ok(dllm_silu_mul(gu.data_ptr(), out.data_ptr(), T, I, gu.stride(0), stream()), "silu_mul");
 }
 
-void embed(torch::Tensor ids, torch::Tensor table, torch::Tensor out, int64_t lo) {
+// token-embedding gather; ssq (optional, f32 [>= T]): each row's sum of squares
+void embed(torch::Tensor ids, torch::Tensor table, torch::Tensor out, int64_t lo, c10::optional<torch::Tensor> ssq) {
   TORCH_CHECK(ids.scalar_type() == torch::kInt && ids.is_contiguous() && ids.is_cuda(), "ids: contiguous int32");
   check_bf16(table, "table");
   check_bf16(out, "out");
   TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && out.is_contiguous(), "table [rows, H] contiguous");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == ids.numel() && out.size(1) == table.size(1), "out [T, H]");
+  float* sp = nullptr;
+  if (ssq.has_value()) {
+    check_f32(*ssq, "ssq");
+    TORCH_CHECK(ssq->is_contiguous() && ssq->numel() >= ids.numel(), "ssq [>= T] contiguous");
+    sp = ssq->data_ptr<float>();
+  }
   ok(dllm_embed(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), table.size(1), lo,
-                table.size(0), stream()),
+                table.size(0), sp, stream()),
      "embed");
 }
 
@@ -949,7 +956,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("paged_attention", &paged_attention);
   m.def("flash_prefill", &flash_prefill);
   m.def("silu_mul", &silu_mul);
-  m.def("embed", &embed);
+  m.def("embed", &embed, py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("lo"), py::arg("ssq") = py::none());
   m.def("gelu", &gelu);
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("moe_gate", &moe_gate);

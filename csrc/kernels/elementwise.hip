@@ -28,16 +28,32 @@ __global__ void silu_mul_kernel(const u16* __restrict__ gu, u16* __restrict__ ou
 
 // one wave per token row, 16-B vectors; rows of a 288 GB-resident table are gathered straight to
 // registers (a random-row gather reads at ~5.5 TB/s: MI355X_MICROARCH.md)
+// ssq (optional): the row's sum of squares, ssq[t] — the first decoder layer's folded-RMSNorm row
+// scale then needs no separate res_add_ssq pass over the embeddings (one launch less per step)
 __global__ void __launch_bounds__(256) embed_kernel(const int* __restrict__ ids, const u16* __restrict__ table,
-                                                    u16* __restrict__ out, long T, int H, long lo, long rows) {
+                                                    u16* __restrict__ out, long T, int H, long lo, long rows,
+                                                    float* __restrict__ ssq) {
   const long t = blockIdx.x * 4L + (threadIdx.x >> 6);
   if (t >= T) return;
   const long r = ids[t] - lo;
   const bool ok = r >= 0 && r < rows;
   const u16* src = table + (ok ? r : 0) * (long)H;
   u16* dst = out + t * (long)H;
-  for (int c = (threadIdx.x & 63) * 8; c < H; c += 64 * 8)
-    st16(dst + c, ok ? ld16(src + c) : make_uint4(0, 0, 0, 0));
+  float s = 0.f;
+  for (int c = (threadIdx.x & 63) * 8; c < H; c += 64 * 8) {
+    const uint4 v = ok ? ld16(src + c) : make_uint4(0, 0, 0, 0);
+    st16(dst + c, v);
+    if (ssq) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+    }
+  }
+  if (ssq) {
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) ssq[t] = s;
+  }
 }
 
 __global__ void gelu_kernel(const u16* __restrict__ x, u16* __restrict__ y, long n8) {
@@ -126,11 +142,11 @@ extern "C" int dllm_silu_mul(const void* gu, void* out, long T, int I, long in_s
 }
 
 extern "C" int dllm_embed(const int* ids, const void* table, void* out, long T, int H, long lo, long rows,
-                          hipStream_t stream) {
+                          float* ssq, hipStream_t stream) {
   if (H % 8 != 0) return -1;
   if (T == 0) return 0;
   hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, stream, ids, (const u16*)table,
-                     (u16*)out, T, H, lo, rows);
+                     (u16*)out, T, H, lo, rows, ssq);
   return (int)hipGetLastError();
 }
 

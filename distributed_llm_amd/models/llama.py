@@ -363,11 +363,12 @@ class LlamaModel:
         epilogues; ``ssq``/``n`` = partial row sums of r^2 of the latest residual producer."""
         cfg = self.cfg
         T, H, eps = input_ids.shape[0], cfg.hidden, cfg.rms_eps
-        r = ops.embedding(input_ids, self.embed, self.vocab_shard.start)
         slots_n = ops.gemm.max_slots(H, T)
-        ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
-        ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=r.device)
-        n = ops.gemm.res_add_ssq(None, r, ssq_a)
+        ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=input_ids.device)
+        ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=input_ids.device)
+        # the gather also leaves each row's sum of squares in slot 0 (first layer's row scale)
+        r = ops.embedding(input_ids, self.embed, self.vocab_shard.start, ssq_out=ssq_a[0])
+        n = 1
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,

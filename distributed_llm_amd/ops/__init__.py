@@ -294,15 +294,20 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     return o
 
 
-def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0) -> torch.Tensor:
+def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0,
+              ssq_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Row gather ``table[ids - lo]`` -> [T, H]; ids outside ``[lo, lo + rows)`` give zero rows
-    (vocab-parallel shard of a TP rank: the all-reduce then sums the owners' rows)."""
+    (vocab-parallel shard of a TP rank: the all-reduce then sums the owners' rows).  ``ssq_out``
+    (f32, >= T): also each row's sum of squares, in the same launch."""
     ext = _native(table)
     if ext is None:
-        return ref.embedding(ids, table, lo)
+        out = ref.embedding(ids, table, lo)
+        if ssq_out is not None:
+            ssq_out[:out.shape[0]] = (out.float() ** 2).sum(1)
+        return out
     ids = ids.reshape(-1).to(torch.int32).contiguous()
     out = torch.empty((ids.numel(), table.shape[1]), dtype=table.dtype, device=table.device)
-    ext.embed(ids, table, out, int(lo))
+    ext.embed(ids, table, out, int(lo), ssq_out)
     return out
 
 

@@ -456,6 +456,11 @@ def test_embedding(H, lo, rows):
     got = ops.embedding(ids, table, lo)
     want = ref.embedding(ids.cpu(), table.cpu(), lo).to(DEV)
     assert torch.equal(got, want)
+    ssq = torch.full((300,), float("nan"), device=DEV)      # fused row sums of squares (first layer's scale)
+    got2 = ops.embedding(ids, table, lo, ssq_out=ssq)
+    assert torch.equal(got2, want)
+    torch.testing.assert_close(ssq[:257], (want.float() ** 2).sum(1), rtol=1e-5, atol=1e-4)
+    assert torch.isnan(ssq[257:]).all()
 
 
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
