@@ -1,6 +1,7 @@
-"""Fused-GEMV choice coupling (ops.gemm._couple_gemv_choices): a residual producer (Wo, down) keeps
-the fused GEMV only where its consumer (gate|up, next layer's QKV) runs it too, since a GEMV
-producer leaves one row-sum slot per workgroup.  Pure host logic: runs on CPU."""
+"""Host-side rules of the decode path, on CPU: fused-GEMV choice coupling
+(ops.gemm._couple_gemv_choices: a residual producer (Wo, down) keeps the fused GEMV only where its
+consumer (gate|up, next layer's QKV) runs it too, since a GEMV producer leaves one row-sum slot per
+workgroup), fused-GEMV eligibility, and the embedding gather's row sums (reference path)."""
 from distributed_llm_amd.ops import gemm as G
 
 LAYER = [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632)]   # QKV, Wo, gate|up, down
@@ -49,3 +50,18 @@ def test_fused_gemv_eligibility(monkeypatch):
     assert G.fused_gemv_r(torch.zeros(4, 2048, dtype=torch.bfloat16), 64) == 4
     monkeypatch.setenv("DLLM_FUSED_CORE", "tg")
     assert G.fused_gemv_r(x1, 2560) == 0
+
+
+def test_embedding_row_sums_reference_path():
+    """ops.embedding(ssq_out=...) on CPU: the gathered rows and each row's sum of squares (the
+    first decoder layer's row scale input), zero rows for ids outside the vocab shard."""
+    import torch
+    from distributed_llm_amd import ops
+    table = torch.randn(50, 64).to(torch.bfloat16)
+    ids = torch.tensor([3, 7, 49, 60, 0], dtype=torch.int32)
+    ssq = torch.full((8,), float("nan"))
+    out = ops.embedding(ids, table, 0, ssq_out=ssq)
+    want = torch.stack([table[i] if i < 50 else torch.zeros(64, dtype=torch.bfloat16) for i in ids.tolist()])
+    assert torch.equal(out, want)
+    torch.testing.assert_close(ssq[:5], (want.float() ** 2).sum(1))
+    assert torch.isnan(ssq[5:]).all()
