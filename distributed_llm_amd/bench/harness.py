@@ -53,7 +53,7 @@ PER_QUERY_HEADERS = [
     "energy_mJ", "latency_per_token_ms", "energy_per_token_mJ",
 ]
 PER_QUERY_EXTRA = ["gpus", "small_pool", "large_pool", "ttft_ms", "prefill_tokens", "cached_tokens",
-                   "generated_tokens"]
+                   "generated_tokens", "energy_method", "energy_gpus"]
 
 
 @dataclass
@@ -181,6 +181,7 @@ def run_experiment(items: List[QueryItem], cfg: RunConfig, pools, tier_gpus: Dic
                 rows: List[Dict[str, Any]] = []
                 for i, it in enumerate(items):
                     history.append({"role": "user", "content": it.text})
+                    m0 = sampler.mark() if sampler is not None else None
                     t0 = datetime.now()
                     row = {"query_set": cfg.query_set_name, "strategy": strategy, "cache_mode": cache_mode,
                            "token_threshold": thr, "query_index": i, "query_text": it.text,
@@ -190,6 +191,7 @@ def run_experiment(items: List[QueryItem], cfg: RunConfig, pools, tier_gpus: Dic
                         payload, ntok, dev = router.route_query(history)
                     except Exception as e:
                         t1 = datetime.now()
+                        row["_marks"] = (m0, sampler.mark() if sampler is not None else None)
                         row.update({"device_used": "error", "start_time": t0, "end_time": t1,
                                     "latency_ms": int((t1 - t0).total_seconds() * 1000), "response_tokens": 0,
                                     "energy_mJ": 0.0})
@@ -197,6 +199,7 @@ def run_experiment(items: List[QueryItem], cfg: RunConfig, pools, tier_gpus: Dic
                         log(f"[err] strategy={strategy} i={i}: {e}")
                         continue
                     t1 = datetime.now()
+                    row["_marks"] = (m0, sampler.mark() if sampler is not None else None)
                     text = str(payload.get("response", "")) if isinstance(payload, dict) else str(payload)
                     history.append({"role": "assistant", "content": text})
                     timing = (payload.get("timing") or {}) if isinstance(payload, dict) else {}
@@ -215,11 +218,18 @@ def run_experiment(items: List[QueryItem], cfg: RunConfig, pools, tier_gpus: Dic
                     rows.append(row)
                 for r in rows:
                     dev = r.get("device_used")
-                    if dev in (SMALL, LARGE) and sampler is not None:
-                        e = sampler.energy_mj(tier_gpus.get(dev, []), r["start_time"], r["end_time"])
+                    marks = r.pop("_marks", (None, None))
+                    gl = tier_gpus.get(dev, []) if dev in (SMALL, LARGE) else []
+                    # energy of the serving tier's GPU(s) over the query window: cumulative-counter
+                    # delta (reference: power integrated over the window, routing_chatbot_tester.py
+                    # :239-254); with tiers sharing a GPU this is that GPU's energy, not a tier share
+                    if sampler is not None and gl and marks[0] is not None and marks[1] is not None:
+                        e, method = sampler.energy_between(gl, marks[0], marks[1])
                     else:
-                        e = 0.0
+                        e, method = 0.0, "none"
                     r["energy_mJ"] = round(e, 3)
+                    r["energy_method"] = method
+                    r["energy_gpus"] = " ".join(str(g) for g in gl)
                     toks, lat = int(r.get("response_tokens") or 0), int(r.get("latency_ms") or 0)
                     ok = dev in (SMALL, LARGE) and toks > 0
                     r["latency_per_token_ms"] = lat / toks if ok else ""

@@ -7,8 +7,10 @@ response cache off, failover on; for each threshold ``Router.set_threshold(t)`` 
 conversation over the query set; per threshold and tier: total latency (ms), energy (mJ), average
 power (W = mJ / ms) and generated tokens.
 
-Energy: the reference sums 1 Hz mW samples (= mJ at 1 Hz).  The sampler here runs at ``hz``; the
-sum is scaled by 1/hz so the unit stays mJ.  Note: ``set_threshold`` only
+Energy: the reference sums 1 Hz mW samples (= mJ at 1 Hz) inside each query window.  Here each
+query's energy is the GPU energy-counter delta over its window (``PowerSampler.mark`` /
+``energy_between``; trapezoid over the interpolated power trace where no counter exists), so
+sub-second queries are not read as 0 mJ.  Note: ``set_threshold`` only
 moves the routing-exception fallback, so — as in the reference's current code — the threshold axis
 does not change perf routing; ``--threshold-routing`` instead sweeps the token router's threshold,
 which is what the published table's trend reflects.
@@ -48,21 +50,21 @@ def run_legacy(query_set: str, thresholds: Sequence[int], pools, tier_gpus: Dict
         history = []
         for q in items:
             history.append({"role": "user", "content": q})
+            m0 = sampler.mark() if sampler is not None else None
             t0 = datetime.now()
             payload, ntok, dev = router.route_query(history)
             t1 = datetime.now()
+            m1 = sampler.mark() if sampler is not None else None
             history.append({"role": "assistant", "content": payload.get("response", "")})
-            log.append((thr, dev, t0, t1, int(ntok)))
-    hz = sampler.hz if sampler is not None else 1.0
+            log.append((thr, dev, t0, t1, int(ntok), m0, m1))
     results: Dict[int, Dict[str, List[float]]] = {}
-    for thr, dev, t0, t1, ntok in log:
+    for thr, dev, t0, t1, ntok, m0, m1 in log:
         r = results.setdefault(thr, {SMALL: [0, 0.0, 0.0, 0], LARGE: [0, 0.0, 0.0, 0]})
         if dev not in r:
             continue
         e = 0.0
-        if sampler is not None:
-            for g in tier_gpus.get(dev, []):
-                e += sum(p for t, p in sampler.samples.get(g, []) if t0 <= t <= t1) / hz
+        if sampler is not None and m0 is not None and m1 is not None:
+            e = sampler.energy_between(tier_gpus.get(dev, []), m0, m1)[0]
         r[dev][0] += round((t1 - t0).total_seconds() * 1000)
         r[dev][1] += e
         r[dev][3] += ntok

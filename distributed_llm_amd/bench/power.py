@@ -7,6 +7,16 @@ Reference: ``src/tests/logging_power.py`` (jtop @ 1 Hz, lines ``"%Y-%m-%d %H:%M:
 Here a background thread samples every GPU's socket power through ``amdsmi`` (default 10 Hz) and
 keeps samples in memory; it can also write the reference log format.  When amdsmi or a GPU is
 unavailable the sampler records nothing and every energy reads 0.0 (reported as such).
+
+Per-query energy (the reference integrates power over each query window) is measured from the
+GPU's cumulative energy counter (``amdsmi_get_energy_count``): ``mark()`` snapshots it at a query's
+start and end and ``energy_between`` returns the delta, so a 100 ms query reads its real energy
+instead of the 0 mJ a 1-10 Hz sample sum gives when no sample falls inside the window.  Where the
+counter is unavailable the fallback is a trapezoid integral of the power trace linearly
+interpolated at the window's boundaries (``energy_for_window_trapz``), which also covers windows
+shorter than one sample period.  Energy is a property of a GPU, not of a tier: when tiers share a
+GPU the per-query figure is that GPU's energy during the query (the harness is sequential, so
+windows never overlap).
 """
 from __future__ import annotations
 
@@ -83,8 +93,53 @@ class PowerSampler:
             self._thread.join(timeout=5)
             self._thread = None
 
+    def counter_mj(self, handle) -> Optional[float]:
+        """The GPU's cumulative energy counter in mJ (None if the driver does not expose it)."""
+        try:
+            d = self._amdsmi.amdsmi_get_energy_count(handle)
+            acc, res = d.get("energy_accumulator"), d.get("counter_resolution")
+            if acc is None or not res:
+                return None
+            return float(acc) * float(res) / 1000.0   # counter units x uJ/unit -> mJ
+        except Exception:
+            return None
+
+    def mark(self) -> "EnergyMark":
+        """Snapshot (wall time, energy counter per GPU) at a query boundary."""
+        cnt = {}
+        for i, h in self._handles:
+            cnt[i] = self.counter_mj(h)
+        return EnergyMark(datetime.now(), cnt)
+
+    def energy_between(self, gpus: Sequence[int], m0: "EnergyMark", m1: "EnergyMark") -> Tuple[float, str]:
+        """Energy (mJ) of ``gpus`` between two marks and the method used: ``counter`` (energy
+        counter delta), ``trapz`` (interpolated power trace) or ``none``."""
+        total, method = 0.0, "none"
+        for g in gpus:
+            c0, c1 = m0.counters.get(g), m1.counters.get(g)
+            if c0 is not None and c1 is not None and c1 >= c0:
+                total += c1 - c0
+                method = "counter"
+                continue
+            pts = self.samples.get(g, [])
+            if pts:
+                total += energy_for_window_trapz(pts, m0.time, m1.time)
+                method = "trapz" if method == "none" else method
+        return total, method
+
     def energy_mj(self, gpus: Sequence[int], start: datetime, end: datetime) -> float:
-        return sum(energy_for_window(dict(self.samples.get(g, [])), start, end) for g in gpus)
+        """Energy of ``gpus`` over [start, end] from the sampled power trace (trapezoid over the
+        trace interpolated at the window's boundaries)."""
+        return sum(energy_for_window_trapz(self.samples.get(g, []), start, end) for g in gpus)
+
+
+class EnergyMark:
+    """Wall time plus each GPU's energy counter (mJ, or None) at one instant."""
+    __slots__ = ("time", "counters")
+
+    def __init__(self, time_: datetime, counters: Dict[int, Optional[float]]):
+        self.time = time_
+        self.counters = counters
 
 
 def parse_power_log(path: str) -> Dict[datetime, int]:
@@ -124,6 +179,39 @@ def energy_for_window(power: Dict[datetime, int], start: datetime, end: datetime
         dt = (t1 - t0).total_seconds()
         if dt > 0:
             e += p0 * dt
+    return e
+
+
+def energy_for_window_trapz(samples, start: datetime, end: datetime) -> float:
+    """Integral (mJ) of a mW trace over [start, end]: the trace is linearly interpolated at both
+    boundaries (held constant beyond its first / last sample) and integrated with the trapezoid
+    rule, so the segments that straddle the window's edges count and a window shorter than one
+    sample period still reads power x duration.  ``samples``: (time, mW) pairs or a dict."""
+    pts = sorted(samples.items() if isinstance(samples, dict) else samples)
+    if not pts or end <= start:
+        return 0.0
+
+    def at(t: datetime) -> float:
+        if t <= pts[0][0]:
+            return float(pts[0][1])
+        if t >= pts[-1][0]:
+            return float(pts[-1][1])
+        lo, hi = 0, len(pts) - 1
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if pts[mid][0] <= t:
+                lo = mid
+            else:
+                hi = mid
+        (t0, p0), (t1, p1) = pts[lo], pts[hi]
+        span = (t1 - t0).total_seconds()
+        w = (t - t0).total_seconds() / span if span > 0 else 0.0
+        return p0 + (p1 - p0) * w
+
+    knots = [(start, at(start))] + [(t, float(p)) for t, p in pts if start < t < end] + [(end, at(end))]
+    e = 0.0
+    for (t0, p0), (t1, p1) in zip(knots, knots[1:]):
+        e += 0.5 * (p0 + p1) * (t1 - t0).total_seconds()
     return e
 
 

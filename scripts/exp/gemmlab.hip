@@ -1,0 +1,480 @@
+// Decode-GEMM lab: Y[M, N] = X[M, K] . W[N, K]^T at the serving batch sizes (M = 256-512),
+// timed as hipGraph replays over rotated weight copies (every launch streams W from HBM, as one
+// decode step does).  Compares the production tgemm (csrc/kernels/tgemm.hip, PLAIN epilogue)
+// with the experimental kernel below:
+//
+//   lg_kernel<BM, BN, WGM, WGN, ST, WT>: same LDS ring idea (global_load_lds 16 B/lane, XOR
+//   swizzle, counted vmcnt across a raw s_barrier), but any WGM x WGN wave grid and an optional
+//   TILED weight layout (WT): W repacked once as [N/BN][K/64][BN][64] with the LDS swizzle
+//   pre-applied, so every ring fill of the weight operand is ONE contiguous 1 KB per wave
+//   instruction instead of 8 rows x 128 B at a 2K..11K-byte row stride.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -o scripts/exp/bin/gemmlab scripts/exp/gemmlab.hip
+#include "../../csrc/kernels/tgemm.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include <string>
+#include <functional>
+#include <algorithm>
+#include <math.h>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+namespace lab {
+constexpr int BK = 64, ROWB = 128;
+
+template <int N>
+__device__ __forceinline__ void vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int G, int MAXR>
+__device__ __forceinline__ void wait_r(int r) {
+  if constexpr (MAXR >= 4) { if (r >= 4) { vm<4 * G>(); return; } }
+  if constexpr (MAXR >= 3) { if (r == 3) { vm<3 * G>(); return; } }
+  if constexpr (MAXR >= 2) { if (r == 2) { vm<2 * G>(); return; } }
+  if constexpr (MAXR >= 1) { if (r == 1) { vm<G>(); return; } }
+  vm<0>();
+}
+__device__ __forceinline__ void bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int WGM, int WGN, int ST, bool WT>
+__global__ void __launch_bounds__(64 * WGM * WGN) lg_kernel(const u16* __restrict__ A, long lda, const u16* __restrict__ W,
+                                                            u16* __restrict__ Y, int M, int N, int K) {
+  constexpr int NWV = WGM * WGN, NT = 64 * NWV;
+  constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;
+  constexpr int GL = (BM + BN) / 8;  // 1 KB glds pieces per stage
+  static_assert(GL % NWV == 0, "pieces per wave");
+  constexpr int G = GL / NWV;
+  constexpr int OLD = BN + 8;
+  constexpr int RING = (ST * STAGE > BM * OLD * 2) ? ST * STAGE : BM * OLD * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[RING];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN, nwg = mt * nt;
+  const int bid = blockIdx.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m_tile = wgid % mt, n_tile = wgid / mt;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int nk = K / BK;
+
+  const int srow = lane >> 3, spos = lane & 7;
+  const u16* src[G];
+  long sstep[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = wave * G + j;  // piece index in the stage image: rows 8g .. 8g+7 of [A; B]
+    const int r = 8 * g + srow;
+    if (g < BM / 8) {
+      src[j] = A + (long)min(m0 + r, M - 1) * lda + 8 * (spos ^ ((r >> 1) & 7));
+      sstep[j] = BK;
+    } else {
+      const int rb = r - BM;
+      if constexpr (WT) {
+        src[j] = W + ((long)n_tile * nk * BN + rb) * BK + 8 * spos;  // [nt][kt][BN][64], pre-swizzled
+        sstep[j] = (long)BN * BK;
+      } else {
+        src[j] = W + (long)min(n0 + rb, N - 1) * K + 8 * (spos ^ ((rb >> 1) & 7));
+        sstep[j] = BK;
+      }
+    }
+  }
+  auto issue = [&](int t) {
+    unsigned char* base = smem + (t % ST) * STAGE;
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * sstep[j]), (lds_void*)(base + (wave * G + j) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < ST - 1; ++t)
+    if (t < nk) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    wait_r<G, (ST - 2 < 4 ? ST - 2 : 4)>(min(ST - 2, nk - 1 - t));
+    bar();
+    if (t + ST - 1 < nk) issue(t + ST - 1);
+    const unsigned char* base = smem + (t % ST) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[FM], bw[FN];
+      const int c = 4 * s + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * WM + 16 * i + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(base + r * ROWB + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * WN + 16 * j + (lane & 15);
+        bw[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + r * ROWB + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  u16* so = reinterpret_cast<u16*>(smem);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        so[(wm * WM + 16 * i + 4 * (lane >> 4) + e) * OLD + wn * WN + 16 * j + (lane & 15)] = f2bf(acc[i][j][e]);
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+    const int rl = e / CPR, c0 = (e % CPR) * 8, m = m0 + rl, n = n0 + c0;
+    if (m < M && n < N) st16(Y + (long)m * N + n, *reinterpret_cast<const uint4*>(so + rl * OLD + c0));
+  }
+}
+
+// Loader / consumer split: NL loader waves only issue global_load_lds (and wait for it), the
+// WGM x WGN consumer waves only read LDS fragments and issue MFMAs; one raw s_barrier per 64-deep
+// k-step hands a ring slot from the loaders (data landed: counted vmcnt before the barrier) to the
+// consumers (fragments read: lgkmcnt(0) before the barrier) and back.  Split-K over gridDim:
+// S k-chunks per output tile, write-through f32 slabs + relaxed ticket, the last arriver sums
+// the slabs in split order (Guideline 16 R1, as tgemm).
+template <int BM, int BN, int WGM, int WGN, int NL, int ST>
+__global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __restrict__ A, long lda,
+                                                                     const u16* __restrict__ W, u16* __restrict__ Y,
+                                                                     int M, int N, int K, int S, float* part,
+                                                                     int* counters) {
+  constexpr int NC = WGM * WGN, NT = 64 * (NC + NL);
+  constexpr int WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;
+  constexpr int GL = (BM + BN) / 8;
+  static_assert(GL % NL == 0, "pieces per loader");
+  constexpr int G = GL / NL;
+  constexpr int OLD = BN + 8;
+  constexpr int RING = (ST * STAGE > BM * OLD * 2) ? ST * STAGE : BM * OLD * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[RING + 16];
+  int* s_last = reinterpret_cast<int*>(smem + RING);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool loader = wave >= NC;
+  const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN, nwg = mt * nt * S;
+  const int bid = blockIdx.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = wgid % S, rest = wgid / S;
+  const int m_tile = rest % mt, n_tile = rest / mt;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int kc = K / S;  // host: K % (64 S) == 0
+  const int kbeg = split * kc, nk = kc / BK;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (loader) {
+    const int lw = wave - NC, srow = lane >> 3, spos = lane & 7;
+    const u16* src[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int g = lw + NL * j;
+      const int r = 8 * g + srow;
+      if (g < BM / 8) {
+        src[j] = A + (long)min(m0 + r, M - 1) * lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+      } else {
+        const int rb = r - BM;
+        src[j] = W + (long)min(n0 + rb, N - 1) * K + kbeg + 8 * (spos ^ ((rb >> 1) & 7));
+      }
+    }
+    auto issue = [&](int t) {
+      unsigned char* base = smem + (t % ST) * STAGE;
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * BK), (lds_void*)(base + (lw + NL * j) * 1024), 16, 0, 0);
+    };
+#pragma unroll
+    for (int t = 0; t < ST - 1; ++t)
+      if (t < nk) issue(t);
+    for (int t = 0; t < nk; ++t) {
+      wait_r<G, (ST - 2 < 4 ? ST - 2 : 4)>(min(ST - 2, nk - 1 - t));
+      bar();
+      if (t + ST - 1 < nk) issue(t + ST - 1);
+    }
+  } else {
+    const int wm = wave / WGN, wn = wave % WGN;
+    for (int t = 0; t < nk; ++t) {
+      bar();
+      const unsigned char* base = smem + (t % ST) * STAGE;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[FM], bw[FN];
+        const int c = 4 * s + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r = wm * WM + 16 * i + (lane & 15);
+          af[i] = *reinterpret_cast<const bf16x8*>(base + r * ROWB + ((c ^ ((r >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * WN + 16 * j + (lane & 15);
+          bw[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + r * ROWB + ((c ^ ((r >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  const int wm = wave / WGN, wn = wave % WGN;
+  if (S > 1) {
+    const int tile_id = n_tile * mt + m_tile;
+    const long slab = (long)BM * BN;
+    const __amdgpu_buffer_rsrc_t pr = make_rsrc(part, 0x7fffffff);
+    if (!loader) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
+          st_wt16(pr, (unsigned)((((long)tile_id * S + split) * slab + (long)c * BM + r) * 4),
+                  make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
+        }
+    }
+    if (!ticket_last(&counters[tile_id], S, s_last)) return;
+    if (!loader) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          for (int sp = 0; sp < S; ++sp) {
+            const float4 q = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
+            v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+          }
+          acc[i][j] = v;
+        }
+    }
+  }
+  __syncthreads();
+  u16* so = reinterpret_cast<u16*>(smem);
+  if (!loader) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          so[(wm * WM + 16 * i + 4 * (lane >> 4) + e) * OLD + wn * WN + 16 * j + (lane & 15)] = f2bf(acc[i][j][e]);
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int e = threadIdx.x; e < BM * CPR; e += NT) {
+    const int rl = e / CPR, c0 = (e % CPR) * 8, m = m0 + rl, n = n0 + c0;
+    if (m < M && n < N) st16(Y + (long)m * N + n, *reinterpret_cast<const uint4*>(so + rl * OLD + c0));
+  }
+}
+
+// naive f32 reference: one thread per output
+__global__ void ref_kernel(const u16* A, const u16* W, float* Y, int M, int N, int K) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x, m = blockIdx.y;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += bf2f(A[(long)m * K + k]) * bf2f(W[(long)n * K + k]);
+  Y[(long)m * N + n] = s;
+}
+
+// repack W [N, K] -> [N/BN][K/64][BN][64] with the LDS swizzle pre-applied (rows past N clamp)
+__global__ void tile_kernel(const u16* W, u16* Wt, int N, int K, int BN) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;  // one 16-B chunk of Wt
+  const int nk = K / 64, ntile = (N + BN - 1) / BN;
+  const long chunks = (long)ntile * nk * BN * 8;
+  if (i >= chunks) return;
+  const int p = i & 7;
+  const long row_id = i >> 3;  // (nt, kt, r)
+  const int r = row_id % BN;
+  const long tk = row_id / BN;
+  const int kt = tk % nk, ntl = tk / nk;
+  const int n = min(ntl * BN + r, N - 1);
+  const int c = p ^ ((r >> 1) & 7);
+  st16(Wt + i * 8, ld16(W + (long)n * K + kt * 64 + c * 8));
+}
+}  // namespace lab
+
+static float* g_part = nullptr;
+static int* g_cnt = nullptr;
+
+struct Var {
+  std::string name;
+  int bm, bn, S;
+  bool wt;
+  std::function<void(const u16*, const u16*, u16*, int, int, int, hipStream_t)> launch;
+};
+
+template <int BM, int BN, int WGM, int WGN, int ST, bool WT>
+Var lgv() {
+  char nm[96];
+  snprintf(nm, sizeof nm, "lg<%d,%d,%dx%d,st%d,%s>", BM, BN, WGM, WGN, ST, WT ? "wt" : "rm");
+  return Var{nm, BM, BN, 1, WT, [](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
+               const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+               hipLaunchKernelGGL((lab::lg_kernel<BM, BN, WGM, WGN, ST, WT>), dim3(g), dim3(64 * WGM * WGN), 0, s, A,
+                                  (long)K, W, Y, M, N, K);
+             }};
+}
+
+template <int BM, int BN, int WGM, int WGN, int NL, int ST>
+Var rgv(int S) {
+  char nm[96];
+  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>", BM, BN, WGM, WGN, NL, ST, S);
+  return Var{nm, BM, BN, S, false, [S](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
+               const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
+               hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST>), dim3(g), dim3(64 * (WGM * WGN + NL)), 0, s,
+                                  A, (long)K, W, Y, M, N, K, S, g_part, g_cnt);
+             }};
+}
+
+static float hbf(u16 h) { uint32_t u = ((uint32_t)h) << 16; float f; memcpy(&f, &u, 4); return f; }
+
+int main(int argc, char** argv) {
+  std::vector<Var> vars = {
+      lgv<64, 64, 2, 2, 3, false>(), lgv<128, 128, 2, 4, 3, false>(),
+      rgv<64, 64, 2, 2, 2, 4>(1),     rgv<64, 64, 2, 2, 2, 4>(2),     rgv<64, 64, 2, 2, 4, 4>(2),
+      rgv<128, 64, 2, 2, 4, 4>(1),    rgv<128, 64, 2, 2, 4, 4>(2),    rgv<128, 64, 2, 2, 4, 4>(4),
+      rgv<128, 128, 2, 2, 4, 4>(1),   rgv<128, 128, 2, 2, 4, 4>(2),   rgv<128, 128, 2, 2, 4, 4>(4),
+      rgv<128, 128, 2, 4, 4, 4>(2),   rgv<160, 64, 2, 2, 4, 4>(2),    rgv<160, 64, 2, 2, 4, 4>(4),
+      rgv<80, 64, 1, 4, 2, 4>(2),     rgv<80, 64, 1, 4, 3, 4>(1),     rgv<160, 128, 2, 4, 4, 3>(1),
+      rgv<160, 128, 2, 4, 4, 3>(2),   rgv<256, 128, 4, 2, 4, 3>(1),   rgv<256, 128, 4, 2, 4, 3>(2),
+      rgv<320, 128, 4, 2, 4, 2>(1),   rgv<320, 64, 4, 2, 4, 3>(1),    rgv<320, 64, 4, 2, 4, 3>(2),
+  };
+  struct Shape { int N, K; };
+  std::vector<Shape> shapes = {{2560, 2048}, {2048, 2048}, {11264, 2048}, {2048, 5632}};
+  std::vector<int> ms = {320, 512};
+  if (argc > 1) ms = {atoi(argv[1])};
+  hipStream_t s;
+  CHECK(hipStreamCreate(&s));
+  CHECK(hipMalloc(&g_part, (256L << 20) * 4));
+  CHECK(hipMalloc(&g_cnt, 1 << 20));
+  CHECK(hipMemset(g_cnt, 0, 1 << 20));
+  const int MAXM = 512;
+  for (auto sh : shapes) {
+    const int N = sh.N, K = sh.K;
+    const long wel = (long)N * K;
+    const int copies = std::max(2L, std::min(48L, (640L << 20) / (wel * 2)));
+    std::vector<u16*> ws(copies), wts(copies);
+    std::vector<u16> hw(wel);
+    u16 *A, *Y, *Wt_scratch;
+    float* Yr;
+    CHECK(hipMalloc(&A, (long)MAXM * K * 2));
+    CHECK(hipMalloc(&Y, (long)MAXM * N * 2));
+    CHECK(hipMalloc(&Yr, (long)MAXM * N * 4));
+    {
+      std::vector<u16> ha((long)MAXM * K);
+      srand(1);
+      for (auto& x : ha) { float f = (rand() / (float)RAND_MAX - 0.5f); uint32_t u; memcpy(&u, &f, 4); x = u >> 16; }
+      CHECK(hipMemcpy(A, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+      for (auto& x : hw) { float f = (rand() / (float)RAND_MAX - 0.5f) * 0.05f; uint32_t u; memcpy(&u, &f, 4); x = u >> 16; }
+    }
+    for (int c = 0; c < copies; ++c) {
+      CHECK(hipMalloc(&ws[c], wel * 2));
+      CHECK(hipMemcpy(ws[c], hw.data(), wel * 2, hipMemcpyHostToDevice));
+    }
+    // tiled copies are re-made per BN (largest tiled footprint: N rounded up to BN)
+    const long wt_el = (long)(N + 256) * K;
+    for (int c = 0; c < copies; ++c) CHECK(hipMalloc(&wts[c], wt_el * 2));
+    (void)Wt_scratch;
+    for (int M : ms) {
+      hipLaunchKernelGGL(lab::ref_kernel, dim3((N + 255) / 256, M), dim3(256), 0, s, A, ws[0], Yr, M, N, K);
+      std::vector<float> yr((long)M * N);
+      CHECK(hipMemcpy(yr.data(), Yr, yr.size() * 4, hipMemcpyDeviceToHost));
+      std::vector<u16> y((long)M * N);
+      auto check = [&](const char* name) {
+        CHECK(hipMemcpy(y.data(), Y, y.size() * 2, hipMemcpyDeviceToHost));
+        double md = 0, mr = 0;
+        for (long i = 0; i < (long)M * N; ++i) {
+          md = std::max(md, (double)fabsf(hbf(y[i]) - yr[i]));
+          mr = std::max(mr, (double)fabsf(yr[i]));
+        }
+        if (md > 0.02 * mr + 1e-3) printf("  !! %s wrong: max diff %.4g (max |ref| %.4g)\n", name, md, mr);
+        return md;
+      };
+      auto time_graph = [&](auto&& body) -> double {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+        for (int i = 0; i < copies; ++i) body(i);
+        CHECK(hipStreamEndCapture(s, &g));
+        CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        CHECK(hipGraphLaunch(ge, s));
+        CHECK(hipStreamSynchronize(s));
+        hipEvent_t e0, e1;
+        CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+        const int reps = 4;
+        CHECK(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; ++r) CHECK(hipGraphLaunch(ge, s));
+        CHECK(hipEventRecord(e1, s));
+        CHECK(hipEventSynchronize(e1));
+        float ms_;
+        CHECK(hipEventElapsedTime(&ms_, e0, e1));
+        CHECK(hipGraphExecDestroy(ge));
+        CHECK(hipGraphDestroy(g));
+        return ms_ * 1000.0 / (reps * copies);
+      };
+      const double flops = 2.0 * M * N * K, wbytes = wel * 2.0;
+      auto report = [&](const char* name, double us, double err) {
+        printf("{\"M\": %d, \"N\": %d, \"K\": %d, \"kernel\": \"%s\", \"us\": %.2f, \"TFs\": %.0f, \"WTBs\": %.2f, \"err\": %.3g}\n",
+               M, N, K, name, us, flops / us / 1e6, wbytes / us / 1e6, err);
+        fflush(stdout);
+      };
+      // production tgemm, a few plans from profiles/r2_tgemm_tune_tinyllama_shapes.log
+      const int tplans[][6] = {{64, 64, 3, 1, 1, 4}, {64, 64, 4, 1, 1, 4}, {64, 128, 3, 1, 1, 8}, {128, 128, 2, 1, 1, 8},
+                               {128, 64, 2, 1, 1, 4}, {256, 128, 3, 1, 1, 8}};
+      for (auto& p : tplans) {
+        dllm::GemmArgs a{};
+        a.A = A; a.lda = K; a.W = nullptr; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.kchunk = K; a.splits = 1;
+        a.W = ws[0];
+        if (dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s) != 0) continue;
+        CHECK(hipStreamSynchronize(s));
+        const double err = check("tgemm");
+        const double us = time_graph([&](int i) { a.W = ws[i]; dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s); });
+        char nm[96];
+        snprintf(nm, sizeof nm, "tgemm<%d,%d,st%d,nw%d>", p[0], p[1], p[2], p[5]);
+        report(nm, us, err);
+      }
+      int tiled_bn = -1;
+      for (auto& v : vars) {
+        if (v.wt && v.bn != tiled_bn) {
+          for (int c = 0; c < copies; ++c) {
+            const long chunks = (long)((N + v.bn - 1) / v.bn) * (K / 64) * v.bn * 8;
+            hipLaunchKernelGGL(lab::tile_kernel, dim3((chunks + 255) / 256), dim3(256), 0, s, ws[c], wts[c], N, K, v.bn);
+          }
+          CHECK(hipStreamSynchronize(s));
+          tiled_bn = v.bn;
+        }
+        auto& wsel = v.wt ? wts : ws;
+        if (K % (64 * v.S)) continue;
+        if ((long)((M + v.bm - 1) / v.bm) * ((N + v.bn - 1) / v.bn) * v.S * v.bm * v.bn > (256L << 20)) continue;
+        v.launch(A, wsel[0], Y, M, N, K, s);
+        CHECK(hipStreamSynchronize(s));
+        const double err = check(v.name.c_str());
+        const double us = time_graph([&](int i) { v.launch(A, wsel[i], Y, M, N, K, s); });
+        report(v.name.c_str(), us, err);
+      }
+    }
+    for (int c = 0; c < copies; ++c) { CHECK(hipFree(ws[c])); CHECK(hipFree(wts[c])); }
+    CHECK(hipFree(A)); CHECK(hipFree(Y)); CHECK(hipFree(Yr));
+  }
+  return 0;
+}

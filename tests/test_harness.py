@@ -104,6 +104,54 @@ def test_power_sampler_degrades_without_gpu():
     s = power.PowerSampler(gpus=[0], hz=5).start()
     s.stop()
     assert s.energy_mj([0], datetime.now(), datetime.now()) == 0.0
+    m0, m1 = s.mark(), s.mark()
+    assert s.energy_between([0], m0, m1) == (0.0, "none")
+
+
+def test_trapezoid_energy_sub_sample_windows():
+    """A window shorter than the sample period reads interpolated power x duration (the old
+    in-window sample sum read 0 mJ: profiles/r2_harness_1gpu/benchmark_results.csv)."""
+    t0 = datetime(2026, 1, 1, 12, 0, 0)
+    trace = [(t0 + timedelta(seconds=i), 100_000 + 10_000 * i) for i in range(6)]   # mW, 1 Hz ramp
+    # 100 ms window between two samples: power 105,000 -> 106,000 mW
+    w0, w1 = t0 + timedelta(seconds=0.5), t0 + timedelta(seconds=0.6)
+    e = power.energy_for_window_trapz(trace, w0, w1)
+    assert abs(e - 0.1 * 105_500) < 1e-6
+    assert power.energy_for_window(dict(trace), w0, w1) == 0.0          # the reference's left-Riemann
+    # window spanning samples: exact integral of the linear ramp (boundary segments included)
+    e = power.energy_for_window_trapz(trace, t0 + timedelta(seconds=0.25), t0 + timedelta(seconds=3.75))
+    exact = 3.5 * 100_000 + 10_000 * (3.75 ** 2 - 0.25 ** 2) / 2
+    assert abs(e - exact) < 1e-6
+    # outside the trace: held at the edge value
+    e = power.energy_for_window_trapz(trace, t0 - timedelta(seconds=1), t0)
+    assert abs(e - 100_000) < 1e-6
+    assert power.energy_for_window_trapz([], w0, w1) == 0.0
+
+
+def test_energy_counter_marks_preferred_over_trace():
+    """With an energy counter the per-query energy is the counter delta; a GPU without one falls
+    back to the interpolated trace."""
+    class Fake(power.PowerSampler):
+        def __init__(self):
+            self.hz, self.log_path, self.available = 10.0, None, True
+            self._handles = [(0, "h0"), (1, "h1")]
+            t0 = datetime(2026, 1, 1)
+            self.samples = {0: [], 1: [(t0, 200_000), (t0 + timedelta(seconds=10), 200_000)]}
+            self.counter = 1_000.0
+
+        def counter_mj(self, handle):
+            return self.counter if handle == "h0" else None
+
+    s = Fake()
+    m0 = power.EnergyMark(datetime(2026, 1, 1, 0, 0, 1), {0: 1_000.0, 1: None})
+    m1 = power.EnergyMark(datetime(2026, 1, 1, 0, 0, 1, 250_000), {0: 1_230.5, 1: None})
+    assert s.energy_between([0], m0, m1) == (230.5, "counter")
+    e, how = s.energy_between([1], m0, m1)
+    assert how == "trapz" and abs(e - 0.25 * 200_000) < 1e-6
+    e, how = s.energy_between([0, 1], m0, m1)
+    assert how == "counter" and abs(e - (230.5 + 50_000)) < 1e-6
+    mk = s.mark()
+    assert mk.counters == {0: 1_000.0, 1: None}
 
 
 def test_cli_repl():
