@@ -402,8 +402,10 @@ class LLMEngine:
             pending, self._inbox = self._inbox, []
             self._driving = self._bg is not None
         for s in pending + list(self._active):
-            if not s.done.is_set():
-                s.error = s.error or why
+            # early-completed rows (_complete_early) are done but still own blocks and a row
+            if not s.done.is_set() or s.row >= 0:
+                if not s.done.is_set():
+                    s.error = s.error or why
                 try:
                     self.bm.free(s.id)
                 except Exception:  # noqa: BLE001 - best effort cleanup
@@ -483,7 +485,13 @@ class LLMEngine:
                 continue
             self._mirror_pending = msg
             with self._lock:
-                self._run([])
+                try:
+                    self._run([])
+                except BaseException as e:  # noqa: BLE001 - same recovery as the leader's loop
+                    # the leader catches the same step failure (every rank raises it on the same
+                    # step, e.g. a custom all-reduce trip) and aborts its batch; a member that
+                    # exited here would leave the leader's next collective waiting forever
+                    self._abort_all(f"engine step failed: {e!r}")
 
     # ------------------------------------------------------------------ background serving loop
     def start(self) -> "LLMEngine":
@@ -631,7 +639,8 @@ class LLMEngine:
 
     def _release(self, s: _Seq, keep: bool = True) -> None:
         if keep:
-            s.finished = time.perf_counter()
+            if s.finished is None:    # _complete_early may have set it when the row stopped
+                s.finished = time.perf_counter()
             if tracer.enabled:
                 self._trace_request(s)
         self.bm.free(s.id)
@@ -1080,13 +1089,24 @@ class LLMEngine:
             if launched is None:
                 return finished, preempted
             if done_now:
-                # the next step is already on the GPU: detokenise the stopped answers under it
+                # the next step is already on the GPU: detokenise the stopped answers under it and
+                # hand them to their callers now: a short answer must not wait for the
+                # longest row of the burst.  Only the KV-block free is deferred to the caller of
+                # the burst (the in-flight step may still write the stopped row's reserved slot;
+                # nothing allocates blocks before the burst has drained).
                 _t3 = time.perf_counter()
                 for s in done_now:
-                    self._finalize_text(s)
+                    self._complete_early(s)
                 self.timers["output"] += time.perf_counter() - _t3
             freed = bool(waiting) and bool(done_now or preempted)
             cur, pc, ev = launched
+
+    def _complete_early(self, s: _Seq) -> None:
+        """A sequence stopped inside a pipelined burst: record its finish time, form its text and
+        wake its caller; ``_release`` (after the burst) frees its blocks and row."""
+        s.finished = time.perf_counter()
+        self._finalize_text(s)
+        s.done.set()
 
     def _check_collectives(self) -> None:
         """TP: a one-shot all-reduce that timed out on any rank fails this step (every rank the

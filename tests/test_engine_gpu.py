@@ -165,3 +165,32 @@ def test_pipelined_text_and_turn_memo_match_stepwise(monkeypatch):
     tb, ib, cb = two_turns()
     assert ta == tb and ia == ib and ca == cb
     assert all(c >= 16 for c, p in zip(ca, PROMPTS) if len(p) >= 32)
+
+
+def test_pipelined_short_request_completes_before_long_one():
+    """a row that stops inside a pipelined burst is handed back at once (its caller
+    wakes, its latency ends) instead of waiting for the longest row of the batch; its KV blocks
+    are released after the burst and the block accounting stays clean."""
+    import threading
+    import time as _time
+    e = _engine(max_num_seqs=8).start()
+    try:
+        done = {}
+
+        def run(name, prompt, n):
+            o = e.generate([prompt], SamplingParams(max_new_tokens=n, ignore_eos=True))[0]
+            done[name] = (_time.perf_counter(), o)
+
+        ts = [threading.Thread(target=run, args=("long", PROMPTS[1], 200)),
+              threading.Thread(target=run, args=("short", PROMPTS[0], 4))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        (t_short, o_short), (t_long, o_long) = done["short"], done["long"]
+        assert o_short.num_generated == 4 and o_long.num_generated == 200
+        assert t_short < t_long
+        assert o_short.latency_ms < 0.5 * o_long.latency_ms, (o_short.latency_ms, o_long.latency_ms)
+    finally:
+        e.stop()
+    assert e.bm.check_invariants() == "" and e.bm.stats()["active_seqs"] == 0
