@@ -46,6 +46,10 @@ int dllm_car_open_handle(const char*, void**);
 int dllm_car_close_handle(void*);
 int dllm_car_free(void*);
 int dllm_car_allreduce(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
+int dllm_car_resadd_slots(int);
+int dllm_car_resadd(const void*, void*, long, float*, long, int, int, int, void* const*, int, int, long, unsigned*, int*,
+                    long, hipStream_t);
+int dllm_car_allgather(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t);
 int dllm_decode_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*, void*,
                           float*, float*, int*, const int*, const int*, int, int, int, int, int, int, int, float,
@@ -672,6 +676,49 @@ void car_allreduce(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
      "car_allreduce");
 }
 
+// r = bf16(sum_p y_p) + r (add) or r = bf16(sum_p y_p), in place, and the new r's partial row sums
+// of squares per column slice into ssq [slots, >= T]; returns the slot count (one-shot all-reduce
+// with the fused residual / RMSNorm-statistics epilogue, csrc/kernels/custom_ar.hip)
+int64_t car_resadd(torch::Tensor y, torch::Tensor r, torch::Tensor ssq, bool add, std::vector<int64_t> bases,
+                   int64_t rank, int64_t data_bytes, torch::Tensor counters, torch::Tensor err, int64_t spin_limit) {
+  check_bf16(y, "y");
+  check_bf16(r, "r");
+  check_f32(ssq, "ssq");
+  check_i32(counters, "counters");
+  check_i32(err, "err");
+  TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && r.dim() == 2 && r.stride(1) == 1 && r.sizes() == y.sizes(),
+              "y [T, H] contiguous, r like y (row stride may differ)");
+  const int H = (int)y.size(1), T = (int)y.size(0);
+  const int slots = dllm_car_resadd_slots(H);
+  TORCH_CHECK(slots >= 1, "hidden size has no column-slice split");
+  TORCH_CHECK(ssq.dim() == 2 && ssq.size(0) >= slots && ssq.size(1) >= T && ssq.stride(1) == 1, "ssq [>= slots, >= T]");
+  TORCH_CHECK((int64_t)T * H * 2 <= data_bytes, "message must fit the buffer");
+  TORCH_CHECK(!bases.empty() && bases.size() <= 8 && rank >= 0 && rank < (int64_t)bases.size(), "bad ranks");
+  void* b[8];
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = (void*)bases[i];
+  const int n = dllm_car_resadd(y.data_ptr(), r.data_ptr(), r.stride(0), ssq.data_ptr<float>(), ssq.stride(0), T, H,
+                                add ? 1 : 0, b, (int)bases.size(), (int)rank, data_bytes,
+                                (unsigned*)counters.data_ptr<int>(), err.data_ptr<int>(), spin_limit, stream());
+  TORCH_CHECK(n >= 1, "car_resadd failed (", n, ")");
+  return n;
+}
+int64_t car_resadd_slots(int64_t H) { return dllm_car_resadd_slots((int)H); }
+void car_allgather(torch::Tensor x, torch::Tensor out, std::vector<int64_t> bases, int64_t rank, int64_t data_bytes,
+                   torch::Tensor counters, torch::Tensor err, int64_t spin_limit) {
+  check_i32(counters, "counters");
+  check_i32(err, "err");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.scalar_type() == out.scalar_type(), "contiguous, same dtype");
+  TORCH_CHECK(out.numel() == x.numel() * (int64_t)bases.size(), "out = world x input");
+  const int64_t nbytes = x.numel() * x.element_size();
+  TORCH_CHECK(nbytes % 16 == 0 && nbytes <= data_bytes, "message must be a multiple of 16 B and fit the buffer");
+  TORCH_CHECK(!bases.empty() && bases.size() <= 8 && rank >= 0 && rank < (int64_t)bases.size(), "bad ranks");
+  void* b[8];
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = (void*)bases[i];
+  ok(dllm_car_allgather(x.data_ptr(), out.data_ptr(), nbytes, b, (int)bases.size(), (int)rank, data_bytes,
+                        (unsigned*)counters.data_ptr<int>(), err.data_ptr<int>(), spin_limit, stream()),
+     "car_allgather");
+}
+
 // ---- fused-epilogue LDS-tiled GEMM (csrc/kernels/tgemm.hip).  epi: 0 plain y = x.w^T (optionally
 // row-scaled by rinv from ssq_in), 1 residual add (y = residual, in place; ssq_out partial row
 // sums), 2 QKV (RoPE + q_out + paged K/V writes), 3 SwiGLU (y = [M, N/2]), 4 GELU (y = gelu(x.w^T +
@@ -949,6 +996,9 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("car_close", &car_close);
   m.def("car_free", &car_free);
   m.def("car_allreduce", &car_allreduce);
+  m.def("car_resadd", &car_resadd);
+  m.def("car_resadd_slots", &car_resadd_slots);
+  m.def("car_allgather", &car_allgather);
   m.doc() = "gfx950 HIP kernels for distributed_llm_amd";
   m.def("norm", &norm);
   m.def("rope_kv", &rope_kv);

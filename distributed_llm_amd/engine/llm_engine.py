@@ -149,10 +149,12 @@ class LLMEngine:
         self._gen.manual_seed(seed + 1)
         self._seed_base = (seed * 0x9E3779B1 + 0x5851F42D) & 0x7FFFFFFF
         self._init_rows()
-        if self.on_gpu:
-            self._autotune()
+        if self.on_gpu and os.environ.get("DLLM_AUTOTUNE", "1") == "1":
+            self._autotune()      # DLLM_AUTOTUNE=0: heuristic GEMM plans (multi-process tests on one GPU)
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
+        self.collective_trips = 0
+        self._check_graph_collectives()
         self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
         self.timers = {"prefill": 0.0, "decode_host_pre": 0.0, "decode_gpu_wait": 0.0, "decode_host_post": 0.0,
                        "encode": 0.0, "admit": 0.0, "output": 0.0}
@@ -221,7 +223,8 @@ class LLMEngine:
         self.d_qstart, self.d_qlen, self.d_ctx = d[o[4]:o[5]], d[o[5]:o[6]], d[o[6]:o[6] + R + 1]
         self.d_tok0 = torch.zeros(mb, dtype=torch.int32, device=self.device)
         self.d_last = torch.arange(mb, dtype=torch.int64, device=self.device)
-        self.d_out = torch.zeros(mb, dtype=torch.int32, device=self.device)
+        # sampled tokens; slot [bucket] of a TP decode step holds the collectives' health vote
+        self.d_out = torch.zeros(mb + 1, dtype=torch.int32, device=self.device)
         self.d_src = torch.zeros(mb, dtype=torch.int64, device=self.device)   # pipelined: id gather rows
         self._out_bufs = [torch.zeros(mb, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         # numpy views of the pinned read-back buffers: ndarray.tolist() of a step's tokens costs a few
@@ -772,9 +775,12 @@ class LLMEngine:
                         ctx=ctx_d, tile_seq=tseq_d, tile_tok0=ttok_d, last_idx=last_d,
                         splits=splits, xcd_remap=True, flash=flash)
         hidden = self.model.hidden_states(ids_d, pos_d, meta, self.kv_caches)
+        if not self._collectives_ok():
+            # a one-shot all-reduce timed out on some rank: every rank re-runs the chunk on RCCL
+            # (same inputs, the K/V slot writes are idempotent)
+            hidden = self.model.hidden_states(ids_d, pos_d, meta, self.kv_caches)
         self.steps["prefill"] += 1
         self.steps["prefill_tokens"] += t
-        self._check_collectives()
         done_seqs = [s for (s, a, b) in chunk if b == len(s.fill)]
         for s, a, b in chunk:
             s.num_computed = b
@@ -896,6 +902,9 @@ class LLMEngine:
         last = np.fromiter((s.out[-1] for s in running), dtype=np.int64, count=B)
         bs = self._prep_decode(running, lens, last, 0)
         _t1 = time.perf_counter()
+        if self.FAULT_TRIP_DECODE >= 0 and self.steps["decode"] == self.FAULT_TRIP_DECODE \
+                and self.par.custom_ar is not None:
+            self.par.custom_ar.err.fill_(1)     # fault injection: as if an all-reduce timed out
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=self.use_graphs):
             if self.use_graphs:
                 g = self._graphs.get(bs)
@@ -906,10 +915,19 @@ class LLMEngine:
                 self._decode_forward(bs)
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
-        self._check_collectives()
-        if self.fused_sampler:
+        if self.fused_sampler and self.par.custom_ar is not None:
+            # tokens and the in-graph health vote of the one-shot all-reduces in ONE read-back
+            vals = self.d_out[:bs + 1].tolist()
+            if vals[bs]:
+                self._collective_trip("decode step")
+                self._decode_forward(bs)    # re-run on RCCL: same inputs, idempotent K/V writes
+                vals = self.d_out[:bs + 1].tolist()
+            toks = vals[:B]
+        elif self.fused_sampler:
             toks = self.d_out[:B].tolist()
         else:
+            if not self._collectives_ok():
+                self._decode_forward(bs)
             toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
         _t2 = time.perf_counter()
         self.timers["decode_host_pre"] += _t1 - _t0
@@ -1108,16 +1126,41 @@ class LLMEngine:
         self._finalize_text(s)
         s.done.set()
 
-    def _check_collectives(self) -> None:
-        """TP: a one-shot all-reduce that timed out on any rank fails this step (every rank the
-        same way) and switches the group to RCCL; captured graphs embed the old collective, so
-        they are dropped and re-captured on demand."""
-        if self.par.custom_ar is None:
+    # fault injection (tests): force a collective trip on the Nth decode / prefill step of every rank
+    FAULT_TRIP_DECODE = int(os.environ.get("DLLM_FAULT_CAR_TRIP_DECODE", "-1"))
+    FAULT_TRIP_PREFILL = int(os.environ.get("DLLM_FAULT_CAR_TRIP_PREFILL", "-1"))
+
+    def _collective_trip(self, where: str) -> None:
+        """Every TP rank sees the same trip on the same step: drop the one-shot all-reduce (its
+        epochs are out of step), drop the graphs that embed it (re-captured on demand), and let
+        the caller re-run the step on RCCL."""
+        self.par.drop_custom_ar(f"timed out on a peer during a {where}")
+        self._graphs.clear()
+        self._check_graph_collectives()
+        self.collective_trips = getattr(self, "collective_trips", 0) + 1
+
+    def _check_graph_collectives(self) -> None:
+        """A TP decode graph can only capture device collectives: the one-shot IPC kernels or RCCL.
+        A group on gloo (one-GPU multi-process tests) without the one-shot all-reduce runs eager."""
+        if not self.par.enabled or not self.use_graphs or self.par.custom_ar is not None:
             return
-        if not self.par.check_collectives():
-            self._graphs.clear()
-            raise RuntimeError("tensor-parallel all-reduce timed out on a peer; step discarded, "
-                               "group switched to RCCL")
+        import torch.distributed as dist
+        if self.par.tp_group is None or dist.get_backend(self.par.tp_group) != "nccl":
+            self.use_graphs = False
+
+    def _collectives_ok(self) -> bool:
+        """Prefill / unfused-sampler steps: MAX-reduce the one-shot all-reduce's error flag over
+        the group (one small collective + host read); False = the caller re-runs the step."""
+        if self.par.custom_ar is None:
+            return True
+        if self.FAULT_TRIP_PREFILL >= 0 and self.steps["prefill"] == self.FAULT_TRIP_PREFILL:
+            self.par.custom_ar.err.fill_(1)
+        if self.par.check_collectives():
+            return True
+        self._graphs.clear()
+        self._check_graph_collectives()
+        self.collective_trips = getattr(self, "collective_trips", 0) + 1
+        return False
 
     def _decode_meta(self, bs: int) -> AttnMeta:
         if self._use_worklist(bs):
@@ -1141,6 +1184,8 @@ class LLMEngine:
         if self.fused_sampler:
             self.model.sample(hid, self.d_temp[:bs], self.d_topp[:bs], self.d_topk[:bs], self.d_seed,
                               self.d_out[:bs])
+            if self.par.custom_ar is not None:
+                self.par.graph_error_flag(self.d_out[bs:bs + 1])
             return
         self.d_hidden[:bs].copy_(hid)
         self.d_out[:bs].copy_(self.model.greedy(hid))

@@ -13,12 +13,17 @@ tied embeddings and dense-vs-MoE MLP (models.configs).  MI355X-first layout deci
     all-reduce) and LM head (distributed arg-max / top-k; parallel.comm).
 Weights: random init with a fixed seed (no checkpoints in this environment) or HF safetensors.
 
-Fused decoder layer (GPU, tensor-parallel size 1; ``DLLM_FUSED=0`` disables): the residual stream
+Fused decoder layer (GPU, any tensor-parallel size; ``DLLM_FUSED=0`` disables): the residual stream
 ``r`` is updated in place by GEMM epilogues (csrc/kernels/tgemm.hip) and every RMSNorm is folded
 into the GEMM that consumes it (gamma into the weight columns, rinv from the producer's partial
 row sums of squares), so a dense layer is five launches: QKV+RoPE+KV-write, attention,
-o_proj+residual, gate|up+SwiGLU, down+residual.  The fused weights are stored instead of the plain
-ones (same bytes); ``reference_layers()`` reconstructs the plain layout for reference checks.
+o_proj+residual, gate|up+SwiGLU, down+residual.  Under tensor parallelism the column-parallel QKV and
+gate|up keep their fused epilogues on this rank's heads / intermediate shard, and each row-parallel
+projection (o_proj, down) writes its partial sums, which ONE collective all-reduces with the
+residual add and the next RMSNorm's row statistics fused in (ParallelContext.all_reduce_resadd:
+the one-shot IPC kernel for decode-size messages): seven launches per layer, no standalone norm,
+RoPE or SiLU kernels.  The fused weights are stored instead of the plain ones (same bytes);
+``reference_layers()`` reconstructs the plain layout for reference checks.
 """
 from __future__ import annotations
 
@@ -147,7 +152,7 @@ class LlamaModel:
     # ------------------------------------------------------------------ fused layout
     def _fusable(self) -> bool:
         cfg = self.cfg
-        if self.device.type != "cuda" or self.par.tp_size != 1 or os.environ.get("DLLM_FUSED", "1") != "1":
+        if self.device.type != "cuda" or os.environ.get("DLLM_FUSED", "1") != "1":
             return False
         if not ops.native_available():
             return False
@@ -361,26 +366,46 @@ class LlamaModel:
                              kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Fused layer path (module docstring): residual stream ``r`` updated in place by GEMM
         epilogues; ``ssq``/``n`` = partial row sums of r^2 of the latest residual producer."""
-        cfg = self.cfg
+        cfg, par = self.cfg, self.par
         T, H, eps = input_ids.shape[0], cfg.hidden, cfg.rms_eps
-        slots_n = ops.gemm.max_slots(H, T)
+        slots_n = max(ops.gemm.max_slots(H, T), 32)   # >= the one-shot all-reduce's column slices
         ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=input_ids.device)
         ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=input_ids.device)
-        # the gather also leaves each row's sum of squares in slot 0 (first layer's row scale)
-        r = ops.embedding(input_ids, self.embed, self.vocab_shard.start, ssq_out=ssq_a[0])
-        n = 1
+        tp = par.tp_size > 1
+        if not tp:
+            # the gather also leaves each row's sum of squares in slot 0 (first layer's row scale)
+            r = ops.embedding(input_ids, self.embed, self.vocab_shard.start, ssq_out=ssq_a[0])
+            n = 1
+        else:
+            # vocab-parallel rows (zero outside this rank's shard) summed by the all-reduce, which
+            # also leaves the row statistics of the first RMSNorm
+            r = torch.empty((T, H), dtype=self.dtype, device=input_ids.device)
+            n = par.all_reduce_resadd(ops.embedding(input_ids, self.embed, self.vocab_shard.start), r, ssq_a,
+                                      add=False)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
+            # column-parallel QKV (this rank's heads) with RMSNorm folded + RoPE + paged K/V write
             q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,
                                         self.nq, self.nkv, self.d)
             o = self._attention(q, kc, vc, meta)
-            nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b)
+            if not tp:
+                nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b)
+            else:   # row-parallel o_proj: partial sums -> all-reduce + residual add + row statistics
+                nb = par.all_reduce_resadd(ops.linear(o.view(T, -1), L["wo"]), r, ssq_b)
             if not cfg.is_moe:
                 act = ops.gemm.swiglu_matmul(r, L["wgu_f"], ssq_b, nb, eps)
-                n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a)
+                if not tp:
+                    n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a)
+                else:
+                    n = par.all_reduce_resadd(ops.linear(act, L["wd"]), r, ssq_a)
             else:
                 x = ops.rms_norm(r, L["ln2"], eps)
-                n = ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a)
+                if not tp:
+                    n = ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a)
+                elif self.moe_ep:   # expert parallel: the combined output is already replicated
+                    n = ops.gemm.res_add_ssq(self._mlp_out(L, x), r, ssq_a)
+                else:               # TP-within-expert partial sums
+                    n = par.all_reduce_resadd(self._mlp(L, x), r, ssq_a)
         return ops.rms_norm(r if meta.all_last else r.index_select(0, meta.last_idx), self.final_norm, eps)
 
     def _hidden_states_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,

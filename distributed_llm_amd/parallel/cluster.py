@@ -76,7 +76,10 @@ class Cluster:
         # --- groups (collective: every rank creates every group in the same order)
         #   tp_groups:     RCCL (default backend) per TP replica: model all-reduces
         #   mirror_groups: gloo per TP replica: the leader's scheduler broadcast (engine mirror)
-        #   pair_groups:   router <-> remote leader, default backend: data plane (token ids, pings)
+        #   pair_groups:   router <-> remote leader: data plane (token ids, pings); gloo unless
+        #                  DLLM_DATA_PLANE=rccl (a dead peer is then an exception in the calling
+        #                  thread, never an RCCL watchdog abort of the router process), so RCCL
+        #                  carries only the TP collectives
         #   ctrl_groups:   router <-> remote leader, gloo: tagged control messages (pools.remote)
         self.tp_groups: Dict[tuple, Any] = {}
         self.mirror_groups: Dict[tuple, Any] = {}
@@ -89,8 +92,10 @@ class Cluster:
                 self.tp_groups[key] = dist.new_group(list(ranks))
                 self.mirror_groups[key] = dist.new_group(list(ranks), backend="gloo")
         leaders = sorted({ranks[0] for _, ranks in topo.all_groups() if ranks[0] != 0})
+        import os
+        data_backend = None if os.environ.get("DLLM_DATA_PLANE", "gloo") == "rccl" else "gloo"
         for ld in leaders:
-            self.pair_groups[ld] = dist.new_group([0, ld]) if init else None
+            self.pair_groups[ld] = dist.new_group([0, ld], backend=data_backend) if init else None
             self.ctrl_groups[ld] = dist.new_group([0, ld], backend="gloo") if init else None
         # --- this rank's replica(s): a rank serves exactly one replica (both tiers only if shared)
         self.my: List[tuple] = [(tier, ranks) for tier, ranks in topo.all_groups() if self.rank in ranks]

@@ -49,6 +49,23 @@ class ParallelContext:
                 dist.all_reduce(t, group=self.tp_group)
         return t
 
+    def all_reduce_resadd(self, y: torch.Tensor, r: torch.Tensor, ssq: torch.Tensor, add: bool = True) -> int:
+        """Row-parallel output epilogue of the fused tensor-parallel layer: ``r += sum over the TP
+        group of y`` (``r = sum`` when not ``add``: the vocab-parallel embedding) in place, plus the
+        new residual's partial row sums of squares in ``ssq`` for the next fused RMSNorm-folding
+        GEMM.  One kernel when the one-shot all-reduce takes the message (decode), else RCCL
+        all-reduce + the res_add_ssq kernel.  Returns the number of ssq slots written."""
+        from .. import ops
+        car = self.custom_ar
+        if self.tp_size > 1 and car is not None and car.eligible_resadd(y, r):
+            return car.all_reduce_resadd(y, r, ssq, add)
+        if self.tp_size > 1:
+            dist.all_reduce(y, group=self.tp_group)
+        if add:
+            return ops.gemm.res_add_ssq(y, r, ssq)
+        r.copy_(y)
+        return ops.gemm.res_add_ssq(None, r, ssq)
+
     def enable_custom_all_reduce(self, device, max_bytes: Optional[int] = None) -> bool:
         """Collective over the TP group.  Returns False (RCCL only) when not applicable."""
         if self.tp_size <= 1 or self.tp_size > 8 or torch.device(device).type != "cuda":
@@ -63,6 +80,30 @@ class ParallelContext:
             logging.getLogger(__name__).warning("custom all-reduce disabled: %s", e)
             return False
         return True
+
+    def graph_error_flag(self, out: torch.Tensor) -> None:
+        """In-graph health vote of the one-shot all-reduce, appended to a decode step: every rank
+        contributes (its error flag != 0) to one more 16-byte one-shot all-reduce and writes
+        ``sum > 0 or own flag`` into ``out`` (an int32 slot read back WITH the step's tokens), so
+        live ranks agree on a trip without a per-step host all-reduce: a rank that timed out on a
+        peer still published its own data, so every rank that completes the vote sees its 1, and
+        a rank whose vote itself timed out sees its own flag."""
+        car = self.custom_ar
+        if car is None:
+            out.zero_()
+            return
+        v = car.flag_vec
+        v.zero_()
+        v[:1].copy_((car.err != 0).to(v.dtype))
+        car.all_reduce(v)
+        out.copy_(((v[:1] > 0) | (car.err != 0)).to(out.dtype))
+
+    def drop_custom_ar(self, why: str) -> None:
+        """Every rank of the group calls this on the same step (agreed trip): RCCL carries every
+        later all-reduce; the one-shot buffers stay mapped until process exit."""
+        import logging
+        logging.getLogger(__name__).error("custom all-reduce dropped: %s; continuing on RCCL", why)
+        self.custom_ar = None
 
     def check_collectives(self) -> bool:
         """After a step: did any rank's one-shot all-reduce time out waiting for a peer (its error
@@ -117,13 +158,19 @@ class ParallelContext:
         if self.tp_size == 1:
             return t.unsqueeze(0)
         t = t.contiguous()
+        car = self.custom_ar
+        if car is not None and car.eligible_gather(t):   # one-shot IPC gather (decode candidates)
+            return car.all_gather(t)
         if t.is_cuda and dist.get_backend(self.tp_group) == "nccl":  # RCCL: one fused all-gather
             out = torch.empty((self.tp_size, *t.shape), dtype=t.dtype, device=t.device)
             dist.all_gather_into_tensor(out, t, group=self.tp_group)
             return out
-        parts = [torch.empty_like(t) for _ in range(self.tp_size)]  # gloo (CPU tests, one-GPU rehearsal)
-        dist.all_gather(parts, t, group=self.tp_group)
-        return torch.stack(parts)
+        # gloo (CPU tests, one-GPU rehearsal): stage device tensors through the host
+        src = t.cpu() if t.is_cuda else t
+        parts = [torch.empty_like(src) for _ in range(self.tp_size)]
+        dist.all_gather(parts, src, group=self.tp_group)
+        out = torch.stack(parts)
+        return out.to(t.device) if t.is_cuda else out
 
 
 SINGLE = ParallelContext()

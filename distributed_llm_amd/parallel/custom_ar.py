@@ -85,6 +85,7 @@ class CustomAllReduce:
         self.bases = bases
         self.counters = torch.zeros(2, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.flag_vec = torch.zeros(8, dtype=torch.bfloat16, device=self.device)   # in-graph health vote
         dist.barrier(group=group)  # every region zeroed + mapped before the first flag is written
         self.calls = 0
 
@@ -98,6 +99,33 @@ class CustomAllReduce:
         out = t if out is None else out
         _ext().car_allreduce(t, out, self.bases, self.rank, self.max_bytes, self.counters, self.err,
                              self.spin_limit)
+        self.calls += 1
+        return out
+
+    def resadd_slots(self, H: int) -> int:
+        return int(_ext().car_resadd_slots(int(H)))
+
+    def eligible_resadd(self, y: torch.Tensor, r: torch.Tensor) -> bool:
+        return (self.eligible(y) and y.dim() == 2 and r.dtype == torch.bfloat16 and r.stride(1) == 1
+                and r.stride(0) % 8 == 0 and self.resadd_slots(y.shape[1]) >= 1)
+
+    def all_reduce_resadd(self, y: torch.Tensor, r: torch.Tensor, ssq: torch.Tensor, add: bool = True) -> int:
+        """``r += sum_p y_p`` (``r = sum`` when not ``add``) in place with the new r's partial row
+        sums of squares in ``ssq[:slots]``; one launch (csrc/kernels/custom_ar.hip car_resadd_kernel).
+        Returns the slot count."""
+        n = _ext().car_resadd(y, r, ssq, bool(add), self.bases, self.rank, self.max_bytes, self.counters, self.err,
+                              self.spin_limit)
+        self.calls += 1
+        return int(n)
+
+    def eligible_gather(self, t: torch.Tensor) -> bool:
+        n = t.numel() * t.element_size()
+        return t.is_cuda and t.is_contiguous() and n % 16 == 0 and 0 < n <= self.max_bytes
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape] of every rank's ``t`` (one launch, graph-capturable)."""
+        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        _ext().car_allgather(t, out, self.bases, self.rank, self.max_bytes, self.counters, self.err, self.spin_limit)
         self.calls += 1
         return out
 

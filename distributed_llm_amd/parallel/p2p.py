@@ -11,8 +11,11 @@ On one MI355X node, pools are process groups and the router talks to a pool lead
   * ``send_tokens`` / ``recv_tokens``: int32 token-id tensors (failover hand-off of a prompt);
   * ``bcast_obj``: leader -> TP group fan-out of a work item;
   * ``ping``: 4 KiB ping-pong health probe, timed.
-Calls made from a side thread run on a dedicated HIP stream (``side_stream``) so transfers
-never queue behind the local engine's kernels on the default stream.
+Every data-plane wait can be bounded (``timeout_s``: isend / irecv + ``Work.wait(timeout)``); a
+transfer past its deadline raises ``DataPlaneTimeout`` and the caller retires that pair group.
+The data plane defaults to gloo (parallel.cluster): token ids and pings are tiny, and on gloo a
+dead peer is a timeout exception in the calling thread rather than an RCCL watchdog abort of the
+whole router process.
 """
 from __future__ import annotations
 
@@ -77,46 +80,63 @@ def bcast_obj(obj: Any, src: int, group=None) -> Any:
     return obj if me == src else json.loads(bytes(buf.cpu().numpy().tobytes()).decode("utf-8"))
 
 
-def send_tokens(ids, dst: int, group=None) -> None:
+class DataPlaneTimeout(RuntimeError):
+    """A data-plane transfer did not complete within its deadline.  The pair group may still hold
+    a posted receive, so callers stop using it (RemotePool falls back to the control plane)."""
+
+
+def _wait(work, timeout_s: Optional[float], what: str) -> None:
+    if timeout_s is None:
+        work.wait()
+        return
+    from datetime import timedelta
+    try:
+        done = work.wait(timeout=timedelta(seconds=float(timeout_s)))
+    except RuntimeError as e:   # gloo raises on its deadline
+        raise DataPlaneTimeout(f"{what} timed out after {timeout_s}s: {e}") from e
+    if done is False:
+        raise DataPlaneTimeout(f"{what} timed out after {timeout_s}s")
+
+
+def _send(t: torch.Tensor, dst: int, group, timeout_s: Optional[float], what: str) -> None:
+    _wait(dist.isend(t, dst, group=group), timeout_s, what)
+
+
+def _recv(t: torch.Tensor, src: int, group, timeout_s: Optional[float], what: str) -> None:
+    _wait(dist.irecv(t, src, group=group), timeout_s, what)
+
+
+def send_tokens(ids, dst: int, group=None, timeout_s: Optional[float] = None) -> None:
+    """Ship int32 token ids (length header + payload); every wait is bounded by ``timeout_s``."""
     dev = _dev(group)
     t = torch.as_tensor(ids, dtype=torch.int32).to(dev)
-    dist.send(torch.tensor([t.numel()], dtype=torch.int64, device=dev), dst, group=group)
-    dist.send(t, dst, group=group)
+    _send(torch.tensor([t.numel()], dtype=torch.int64, device=dev), dst, group, timeout_s, "token header send")
+    if t.numel():
+        _send(t, dst, group, timeout_s, "token send")
 
 
-def recv_tokens(src: int, group=None) -> torch.Tensor:
+def recv_tokens(src: int, group=None, timeout_s: Optional[float] = None) -> torch.Tensor:
     dev = _dev(group)
     hdr = torch.empty(1, dtype=torch.int64, device=dev)
-    dist.recv(hdr, src, group=group)
+    _recv(hdr, src, group, timeout_s, "token header receive")
     t = torch.empty(int(hdr.item()), dtype=torch.int32, device=dev)
-    dist.recv(t, src, group=group)
+    if t.numel():
+        _recv(t, src, group, timeout_s, "token receive")
     return t
 
 
-def ping(peer: int, group=None, nbytes: int = 4096, initiator: bool = True) -> float:
+def ping(peer: int, group=None, nbytes: int = 4096, initiator: bool = True,
+         timeout_s: Optional[float] = None) -> float:
     """4 KiB ping-pong; returns the round-trip time in microseconds on the initiator."""
     dev = _dev(group)
     buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
     t0 = time.perf_counter()
     if initiator:
-        dist.send(buf, peer, group=group)
-        dist.recv(buf, peer, group=group)
+        _send(buf, peer, group, timeout_s, "ping send")
+        _recv(buf, peer, group, timeout_s, "ping receive")
     else:
-        dist.recv(buf, peer, group=group)
-        dist.send(buf, peer, group=group)
+        _recv(buf, peer, group, timeout_s, "ping receive")
+        _send(buf, peer, group, timeout_s, "ping send")
     if dev.type == "cuda":
         torch.cuda.current_stream().synchronize()
     return (time.perf_counter() - t0) * 1e6
-
-
-_side = {}
-
-
-def side_stream(device: Optional[torch.device] = None):
-    """A per-device side stream for pool-to-pool transfers (None on CPU)."""
-    if not torch.cuda.is_available():
-        return None
-    d = torch.cuda.current_device() if device is None else torch.device(device).index
-    if d not in _side:
-        _side[d] = torch.cuda.Stream(device=d)
-    return _side[d]

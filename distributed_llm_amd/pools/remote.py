@@ -11,17 +11,27 @@ src/router.py:277-282); liveness is a TCP connect and readiness a ``/health`` po
   then gets an error payload (the orchestrator fails over); a pool process that dies closes its
   sockets, which fails every in-flight request at once.  The router never blocks on a dead or
   hung pool.
-* **data plane** — the router<->leader pair group (RCCL over xGMI on GPU ranks, gloo on CPU):
-  prompt token ids for a failover hand-off (``process_failover``: the router tokenises with the
-  target pool's tokenizer and ships int32 ids, so the surviving pool prefills ids directly) and
-  the periodic 4 KiB data-plane ping.
+* **data plane** — the router<->leader pair group (gloo by default, RCCL with
+  ``DLLM_DATA_PLANE=rccl``): prompt token ids for a failover hand-off (``process_failover``: the
+  router tokenises with the target pool's tokenizer and ships int32 ids, so the surviving pool
+  prefills ids directly) and the periodic 4 KiB data-plane ping.  Every transfer and the lock
+  that orders them have deadlines (``data_timeout_s``); a data-plane failure retires the data
+  plane of that pool (the hand-off falls back to the text prompt on the control plane) instead
+  of blocking a caller.
 * **health** — a probe thread pings every ``probe_interval_s`` on the control plane (answered by
   the leader's receiver thread immediately, never queued behind generation) and every
-  ``data_probe_every``-th time on the data plane; two consecutive failures mark the pool dead;
-  every probe result is reported to ``on_health`` (the orchestrator feeds the perf router).
+  ``data_probe_every``-th time on the data plane; two consecutive control-plane failures mark
+  the pool dead; every probe result is reported to ``on_health`` (the orchestrator feeds the
+  perf router).  Recovery: a pool marked dead by probes while its transport is intact (a hung
+  engine, a long GC pause) is probed on, and ``revive_after`` consecutive good probes put it back
+  in service — the reference's lazy restart-on-next-call (src/models/nano.py:19-21) for a pool
+  that cannot be respawned inside one torch.distributed job; a pool whose process died (transport
+  closed) stays out (restartable pools are the supervised HTTP workers, pools.supervisor).
 * **pool side** (``PoolLeader``) — the receiver thread answers pings inline and hands each
-  generate request to a worker thread that calls ``engine.generate``; the engine runs its
-  background step loop, so concurrent requests from the router JOIN ONE continuous batch.
+  generate request to a worker thread that calls ``engine.generate``; data-plane operations
+  (token receives, data pings) run in order on a dedicated data thread with deadlines, so a
+  router that dies mid-transfer never wedges the receiver loop; the engine runs its background
+  step loop, so concurrent requests from the router JOIN ONE continuous batch.
   Tensor-parallel pools keep their members in lockstep with the engine's mirror channel
   (``LLMEngine.enable_tp_mirror``), not per request.
 * ``ReplicatedPool`` — several replicas of one tier (data parallel), least-loaded dispatch.
@@ -29,6 +39,7 @@ src/router.py:277-282); liveness is a TCP connect and readiness a ``/health`` po
 from __future__ import annotations
 
 import itertools
+import os
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -61,7 +72,8 @@ class RemotePool(PoolClient):
     def __init__(self, name: str, leader: int, ctrl_group, data_group=None, max_new_tokens: int = 256,
                  temperature: float = 0.0, top_k: int = 0, top_p: float = 1.0,
                  generation_prompt: str = EnginePool.GENERATION_PROMPT, timeout_s: float = 180.0,
-                 tokenizer=None, on_health: Optional[Callable[[str, bool, Optional[float]], None]] = None):
+                 tokenizer=None, on_health: Optional[Callable[[str, bool, Optional[float]], None]] = None,
+                 data_timeout_s: float = 10.0, revive_after: int = 3):
         super().__init__()
         self.name = name
         self.leader = leader
@@ -73,6 +85,12 @@ class RemotePool(PoolClient):
         self.tokenizer = tokenizer          # the pool's tokenizer (token-id hand-off), optional
         self.on_health = on_health
         self.alive = True
+        self.transport_ok = True            # False once the control-plane receiver has died
+        self.data_timeout_s = data_timeout_s
+        self.data_error: Optional[str] = None   # set when the data plane was retired
+        self.revive_after = revive_after
+        self._good_probes = 0
+        self.revivals = 0
         self.server_manager = RemoteServerManager(self)
         self._send_lock = threading.Lock()
         self._data_lock = threading.Lock()
@@ -98,9 +116,11 @@ class RemotePool(PoolClient):
             try:
                 msg = p2p.recv_obj(self.leader, self.ctrl, tag=TAG_REP)
             except Exception as e:  # peer died / transport closed: fail everything in flight
+                self.transport_ok = False
                 self._fail_all(f"pool {self.name} transport failed: {e}")
                 return
             if msg.get("op") == "bye":
+                self.transport_ok = False
                 self._fail_all(f"pool {self.name} stopped")
                 return
             with self._plock:
@@ -121,9 +141,18 @@ class RemotePool(PoolClient):
         with self._send_lock:
             p2p.send_obj(msg, self.leader, self.ctrl, tag=TAG_REQ)
 
-    def _call(self, msg: Dict[str, Any], timeout: Optional[float] = None, data_fn=None) -> Dict[str, Any]:
+    def data_ok(self) -> bool:
+        return self.data is not None and self.data_error is None and self.alive
+
+    def _retire_data(self, why: str) -> None:
+        """Stop using the data plane of this pool (a pending transfer may still be posted on it)."""
+        if self.data_error is None:
+            self.data_error = why
+
+    def _call(self, msg: Dict[str, Any], timeout: Optional[float] = None, data_fn=None,
+              probe: bool = False) -> Dict[str, Any]:
         """Send one tagged request and wait for its reply at most ``timeout`` seconds."""
-        if not self.alive:
+        if not self.alive and not (probe and self.transport_ok):
             return {"error": f"pool {self.name} unavailable"}
         rid = next(self._ids)
         msg["id"] = rid
@@ -134,9 +163,18 @@ class RemotePool(PoolClient):
             if data_fn is None:
                 self._send(msg)
             else:  # control message + its data-plane payload, in order w.r.t. other data ops
-                with self._data_lock:
+                if not self._data_lock.acquire(timeout=self.data_timeout_s):
+                    raise p2p.DataPlaneTimeout("data plane busy (a transfer is stuck)")
+                try:
                     self._send(msg)
                     data_fn()
+                finally:
+                    self._data_lock.release()
+        except p2p.DataPlaneTimeout as e:
+            with self._plock:
+                self._pending.pop(rid, None)
+            self._retire_data(str(e))
+            return {"error": f"pool {self.name} data plane: {e}", "data_plane_failed": True}
         except Exception as e:
             with self._plock:
                 self._pending.pop(rid, None)
@@ -165,15 +203,18 @@ class RemotePool(PoolClient):
 
         def ship():
             for p in ids:
-                p2p.send_tokens(p, self.leader, self.data)
+                p2p.send_tokens(p, self.leader, self.data, timeout_s=self.data_timeout_s)
         rep = self._call({"op": "generate_ids", "n": len(ids), "params": params}, data_fn=ship)
         return self._results(rep, len(ids))
 
     def process_failover(self, history: Any) -> Dict[str, Any]:
         """Failover entry (orchestrator): hand the prompt over as token ids when this router has
-        the pool's tokenizer and a data plane, else as text."""
-        if self.tokenizer is not None and self.data is not None:
-            return self.process_ids([self.tokenizer.encode(self.prompt_for(history))])[0]
+        the pool's tokenizer and a live data plane, else (or if the hand-off fails on the data
+        plane) as text on the control plane."""
+        if self.tokenizer is not None and self.data_ok():
+            r = self.process_ids([self.tokenizer.encode(self.prompt_for(history))])[0]
+            if not (isinstance(r, dict) and "data plane" in str(r.get("error", ""))):
+                return r
         return self.process(history)
 
     @staticmethod
@@ -185,9 +226,10 @@ class RemotePool(PoolClient):
 
     # ------------------------------------------------------------------ health
     def probe(self, timeout: float = 5.0) -> Dict[str, Any]:
-        """Control-plane round trip + the pool's engine statistics (never queued behind work)."""
+        """Control-plane round trip + the pool's engine statistics (never queued behind work).
+        Also sent to a pool marked dead while its transport is intact (revival)."""
         t0 = time.perf_counter()
-        rep = self._call({"op": "ping"}, timeout=timeout)
+        rep = self._call({"op": "ping"}, timeout=timeout, probe=True)
         if "error" in rep:
             return {"ok": False, "error": rep["error"]}
         self.last_rtt_us = (time.perf_counter() - t0) * 1e6
@@ -195,26 +237,23 @@ class RemotePool(PoolClient):
         return {"ok": True, "rtt_us": self.last_rtt_us, **self.last_stats}
 
     def probe_data(self, timeout: float = 5.0) -> Dict[str, Any]:
-        """4 KiB ping-pong on the data plane (RCCL over xGMI between GPU ranks).  Runs in a helper
-        thread so a peer that never answers cannot hang the caller past ``timeout``."""
-        if self.data is None or not self.alive:
-            return {"ok": False, "error": "no data plane"}
-        out: Dict[str, Any] = {}
-
-        def run():
-            try:
-                with self._data_lock:
-                    self._send({"op": "ping_data", "id": 0})
-                    out["rtt_us"] = p2p.ping(self.leader, self.data, initiator=True)
-            except Exception as e:  # noqa: BLE001
-                out["error"] = str(e)
-        t = threading.Thread(target=run, daemon=True)
-        t.start()
-        t.join(timeout)
-        if t.is_alive() or "error" in out:
-            return {"ok": False, "error": out.get("error", f"data-plane ping timed out after {timeout}s")}
-        self.last_data_rtt_us = out["rtt_us"]
-        return {"ok": True, "rtt_us": out["rtt_us"]}
+        """4 KiB ping-pong on the data plane.  Every wait (the ordering lock, each transfer) is
+        bounded by ``timeout``; a failure retires the data plane (failover then ships text)."""
+        if not self.data_ok():
+            return {"ok": False, "error": self.data_error or "no data plane"}
+        if not self._data_lock.acquire(timeout=timeout):
+            self._retire_data(f"data plane busy for {timeout}s")
+            return {"ok": False, "error": self.data_error}
+        try:
+            self._send({"op": "ping_data", "id": 0, "timeout_s": timeout})
+            rtt = p2p.ping(self.leader, self.data, initiator=True, timeout_s=timeout)
+        except Exception as e:  # noqa: BLE001 - DataPlaneTimeout or transport error
+            self._retire_data(f"data-plane ping failed: {e}")
+            return {"ok": False, "error": self.data_error}
+        finally:
+            self._data_lock.release()
+        self.last_data_rtt_us = rtt
+        return {"ok": True, "rtt_us": rtt}
 
     def start_probes(self, interval_s: float = 2.0, timeout_s: float = 5.0, data_probe_every: int = 5) -> None:
         """Periodic health probes on their own thread; two consecutive failures mark the pool dead."""
@@ -224,15 +263,24 @@ class RemotePool(PoolClient):
         def loop():
             k = 0
             while not self._probe_stop.wait(interval_s):
-                if not self.alive:
-                    self._report(False, None)
+                if not self.alive and not self.transport_ok:
+                    self._report(False, None)   # the pool process is gone: stays out of service
                     continue
                 k += 1
                 r = self.probe(timeout_s)
-                if r["ok"] and data_probe_every and k % data_probe_every == 0 and self.data is not None:
-                    d = self.probe_data(timeout_s)
-                    if not d["ok"]:
-                        r = d
+                if not self.alive:
+                    # dead by probes, transport intact: revive after enough consecutive good probes
+                    self._good_probes = self._good_probes + 1 if r["ok"] else 0
+                    if self._good_probes >= self.revive_after:
+                        self.alive, self.probe_failures, self._good_probes = True, 0, 0
+                        self.revivals += 1
+                        self._report(True, r.get("rtt_us"))
+                    else:
+                        self._report(False, None)
+                    continue
+                if r["ok"] and data_probe_every and k % data_probe_every == 0 and self.data_ok():
+                    # a data-plane failure retires the data plane; the pool stays in service
+                    self.probe_data(timeout_s)
                 if r["ok"]:
                     self.probe_failures = 0
                     self._report(True, r.get("rtt_us"))
@@ -274,14 +322,52 @@ class PoolLeader:
     """Pool-side server of one pool leader rank (see module docstring)."""
 
     def __init__(self, engine, ctrl_group, data_group=None, router_rank: int = 0, on_sync=None,
-                 max_workers: int = 64):
+                 max_workers: int = 64, data_timeout_s: float = 10.0):
+        import queue
         self.engine = engine
         self.ctrl = ctrl_group
         self.data = data_group
         self.router = router_rank
         self.on_sync = on_sync
+        self.data_timeout_s = data_timeout_s
+        self.data_error: Optional[str] = None
         self._send_lock = threading.Lock()
         self._ex = ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="dllm-pool")
+        # data-plane operations, in arrival order, off the receiver loop (bounded waits)
+        self._dq: "queue.Queue" = queue.Queue()
+        self._dthread = threading.Thread(target=self._data_loop, name="dllm-pool-data", daemon=True)
+        self._dthread.start()
+
+    def _data_loop(self) -> None:
+        while True:
+            msg = self._dq.get()
+            if msg is None:
+                return
+            op = msg.get("op")
+            if self.data_error is not None:   # retired: answer what needs an answer, move nothing
+                if op == "generate_ids":
+                    self._safe_reply({"id": msg["id"], "error": f"data plane retired: {self.data_error}"})
+                continue
+            try:
+                if op == "ping_data" and os.environ.get("DLLM_FAULT_DIE_ON_DATA_PING") == "1":
+                    os._exit(17)   # fault injection (tests): the leader dies during a data-plane ping
+                if op == "ping_data":
+                    p2p.ping(self.router, self.data, initiator=False,
+                             timeout_s=float(msg.get("timeout_s") or self.data_timeout_s))
+                elif op == "generate_ids":
+                    prompts = [p2p.recv_tokens(self.router, self.data, timeout_s=self.data_timeout_s).tolist()
+                               for _ in range(int(msg["n"]))]
+                    self._ex.submit(self._generate, msg["id"], prompts, msg.get("params"))
+            except Exception as e:  # noqa: BLE001 - DataPlaneTimeout / transport: retire, report
+                self.data_error = str(e)
+                if op == "generate_ids":
+                    self._safe_reply({"id": msg["id"], "error": f"data plane: {e}"})
+
+    def _safe_reply(self, msg: Dict[str, Any]) -> None:
+        try:
+            self._reply(msg)
+        except Exception:  # noqa: BLE001 - router gone
+            pass
 
     def _reply(self, msg: Dict[str, Any]) -> None:
         with self._send_lock:
@@ -316,15 +402,21 @@ class PoolLeader:
                     return
                 op = msg.get("op")
                 if op == "stop":
+                    self._dq.put(None)
                     self._ex.shutdown(wait=True)
                     self._reply({"op": "bye"})
                     return
                 if op == "ping":
+                    nd = int(os.environ.get("DLLM_FAULT_PING_DELAY_N", "0"))
+                    if nd > 0:   # fault injection (tests): the first pings stall the receiver loop
+                        self._pings_seen = getattr(self, "_pings_seen", 0) + 1
+                        if self._pings_seen <= nd:
+                            time.sleep(float(os.environ.get("DLLM_FAULT_PING_DELAY_S", "1")))
                     self._reply({"id": msg["id"], "op": "pong",
                                  "stats": {k: v for k, v in self.engine.stats().items()
                                            if isinstance(v, (int, float, str))}})
                 elif op == "ping_data":
-                    p2p.ping(self.router, self.data, initiator=False)
+                    self._dq.put(msg)
                 elif op == "sync":
                     self.engine.mirror_control({"sync": True})
                     if self.on_sync is not None:
@@ -335,9 +427,9 @@ class PoolLeader:
                         os._exit(17)   # fault injection (tests): the pool process dies mid-request
                     self._ex.submit(self._generate, msg["id"], msg["prompts"], msg.get("params"))
                 elif op == "generate_ids":
-                    prompts = [p2p.recv_tokens(self.router, self.data).tolist() for _ in range(int(msg["n"]))]
-                    self._ex.submit(self._generate, msg["id"], prompts, msg.get("params"))
+                    self._dq.put(msg)
         finally:
+            self._dq.put(None)
             self.engine.stop()
 
 

@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) lg_kernel(const u16* __restric
 // consumers (fragments read: lgkmcnt(0) before the barrier) and back.  Split-K over gridDim:
 // S k-chunks per output tile, write-through f32 slabs + relaxed ticket, the last arriver sums
 // the slabs in split order (Guideline 16 R1, as tgemm).
-template <int BM, int BN, int WGM, int WGN, int NL, int ST>
+template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0>
 __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __restrict__ A, long lda,
                                                                      const u16* __restrict__ W, u16* __restrict__ Y,
                                                                      int M, int N, int K, int S, float* part,
@@ -206,16 +206,17 @@ __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __
     };
 #pragma unroll
     for (int t = 0; t < ST - 1; ++t)
-      if (t < nk) issue(t);
+      if (PROBE != 2 && t < nk) issue(t);
     for (int t = 0; t < nk; ++t) {
-      wait_r<G, (ST - 2 < 4 ? ST - 2 : 4)>(min(ST - 2, nk - 1 - t));
+      if (PROBE != 2) wait_r<G, (ST - 2 < 4 ? ST - 2 : 4)>(min(ST - 2, nk - 1 - t));
       bar();
-      if (t + ST - 1 < nk) issue(t + ST - 1);
+      if (PROBE != 2 && t + ST - 1 < nk) issue(t + ST - 1);
     }
   } else {
     const int wm = wave / WGN, wn = wave % WGN;
     for (int t = 0; t < nk; ++t) {
       bar();
+      if (PROBE == 1) continue;
       const unsigned char* base = smem + (t % ST) * STAGE;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -258,15 +259,23 @@ __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
-          f32x4 v = {0.f, 0.f, 0.f, 0.f};
-          for (int sp = 0; sp < S; ++sp) {
-            const float4 q = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
-            v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < S; ++sp) {  // one round trip per split: all fragments of a slab at once
+        float4 q[FM][FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
+            q[i][j] = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
           }
-          acc[i][j] = v;
-        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            acc[i][j][0] += q[i][j].x; acc[i][j][1] += q[i][j].y; acc[i][j][2] += q[i][j].z; acc[i][j][3] += q[i][j].w;
+          }
+      }
     }
   }
   __syncthreads();
@@ -335,13 +344,14 @@ Var lgv() {
              }};
 }
 
-template <int BM, int BN, int WGM, int WGN, int NL, int ST>
+template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0>
 Var rgv(int S) {
   char nm[96];
-  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>", BM, BN, WGM, WGN, NL, ST, S);
+  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s", BM, BN, WGM, WGN, NL, ST, S,
+           PROBE == 1 ? " LOADERS-ONLY" : PROBE == 2 ? " CONSUMERS-ONLY" : "");
   return Var{nm, BM, BN, S, false, [S](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
                const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
-               hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST>), dim3(g), dim3(64 * (WGM * WGN + NL)), 0, s,
+               hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE>), dim3(g), dim3(64 * (WGM * WGN + NL)), 0, s,
                                   A, (long)K, W, Y, M, N, K, S, g_part, g_cnt);
              }};
 }
@@ -358,11 +368,19 @@ int main(int argc, char** argv) {
       rgv<80, 64, 1, 4, 2, 4>(2),     rgv<80, 64, 1, 4, 3, 4>(1),     rgv<160, 128, 2, 4, 4, 3>(1),
       rgv<160, 128, 2, 4, 4, 3>(2),   rgv<256, 128, 4, 2, 4, 3>(1),   rgv<256, 128, 4, 2, 4, 3>(2),
       rgv<320, 128, 4, 2, 4, 2>(1),   rgv<320, 64, 4, 2, 4, 3>(1),    rgv<320, 64, 4, 2, 4, 3>(2),
+      rgv<128, 128, 2, 2, 4, 4, 1>(1), rgv<128, 128, 2, 2, 4, 4, 2>(1), rgv<64, 64, 2, 2, 2, 4, 1>(1),
+      rgv<64, 64, 2, 2, 2, 4, 2>(1),   rgv<128, 64, 2, 2, 4, 6>(1),  rgv<64, 64, 2, 2, 2, 8>(1),
+      rgv<64, 64, 2, 2, 4, 8>(1),
   };
   struct Shape { int N, K; };
   std::vector<Shape> shapes = {{2560, 2048}, {2048, 2048}, {11264, 2048}, {2048, 5632}};
   std::vector<int> ms = {320, 512};
   if (argc > 1) ms = {atoi(argv[1])};
+  // optional filters: argv[2] = N (0: all), argv[3] = substring of the variant name ("-": all),
+  // argv[4] = "notg" to skip the production tgemm plans
+  const int only_n = argc > 2 ? atoi(argv[2]) : 0;
+  const char* only_v = (argc > 3 && strcmp(argv[3], "-") != 0) ? argv[3] : nullptr;
+  const bool skip_tg = argc > 4 && strcmp(argv[4], "notg") == 0;
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   CHECK(hipMalloc(&g_part, (256L << 20) * 4));
@@ -370,6 +388,7 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(g_cnt, 0, 1 << 20));
   const int MAXM = 512;
   for (auto sh : shapes) {
+    if (only_n && sh.N != only_n) continue;
     const int N = sh.N, K = sh.K;
     const long wel = (long)N * K;
     const int copies = std::max(2L, std::min(48L, (640L << 20) / (wel * 2)));
@@ -442,6 +461,7 @@ int main(int argc, char** argv) {
       const int tplans[][6] = {{64, 64, 3, 1, 1, 4}, {64, 64, 4, 1, 1, 4}, {64, 128, 3, 1, 1, 8}, {128, 128, 2, 1, 1, 8},
                                {128, 64, 2, 1, 1, 4}, {256, 128, 3, 1, 1, 8}};
       for (auto& p : tplans) {
+        if (skip_tg) break;
         dllm::GemmArgs a{};
         a.A = A; a.lda = K; a.W = nullptr; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.kchunk = K; a.splits = 1;
         a.W = ws[0];
@@ -455,6 +475,7 @@ int main(int argc, char** argv) {
       }
       int tiled_bn = -1;
       for (auto& v : vars) {
+        if (only_v && v.name.find(only_v) == std::string::npos) continue;
         if (v.wt && v.bn != tiled_bn) {
           for (int c = 0; c < copies; ++c) {
             const long chunks = (long)((N + v.bn - 1) / v.bn) * (K / 64) * v.bn * 8;

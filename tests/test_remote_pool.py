@@ -58,7 +58,7 @@ def _worker(rank, world, port, scenario, q, env):
         import traceback
         q.put({"rank": rank, "error": f"{e!r}\n{traceback.format_exc()}"})
     finally:
-        if scenario in ("concurrent", "handoff"):
+        if scenario in ("concurrent", "handoff", "revive", "stuck_lock"):
             dist.destroy_process_group()
         else:
             q.close()
@@ -145,8 +145,85 @@ def _router_handoff(ctrl, data):
     return {"ids": via_ids.get("response"), "text": via_text.get("response"), "data_ping": data_ping["ok"]}
 
 
+def _router_die_in_data_ping(ctrl, data):
+    """The pool leader dies while a data-plane ping is in flight and a request is routed to it:
+    the ping returns an error within its deadline (the data plane is retired, nothing blocks on
+    its lock), the request fails over to the other tier well inside the request deadline."""
+    import threading
+    from distributed_llm_amd.config import LARGE, SMALL
+    from distributed_llm_amd.orchestrator import Router
+    from distributed_llm_amd.pools.base import EnginePool
+    from distributed_llm_amd.pools.remote import RemotePool
+    rp = RemotePool(LARGE, 1, ctrl, data, max_new_tokens=6, timeout_s=60, data_timeout_s=3.0)
+    r = Router("heuristic", config={"cache_enabled": False}, pools={SMALL: EnginePool(SMALL, _engine(), 5),
+                                                                   LARGE: rp})
+    ping = {}
+
+    def do_ping():
+        t = time.perf_counter()
+        ping["res"] = rp.probe_data(timeout=3.0)
+        ping["dt"] = time.perf_counter() - t
+    th = threading.Thread(target=do_ping)
+    th.start()
+    time.sleep(0.2)
+    t0 = time.perf_counter()
+    payload, ntok, dev = r.route_query([{"role": "user", "content":
+                                         "Write a Python function with recursion and explain it step by step"}])
+    dt = time.perf_counter() - t0
+    th.join(30)
+    # a later failover hand-off to this pool must not block on the data-plane lock either
+    t1 = time.perf_counter()
+    fo = rp.process_failover([{"role": "user", "content": "hello"}])
+    return {"dev": dev, "ok": payload["ok"], "dt": dt, "ping_ok": ping["res"]["ok"], "ping_dt": ping["dt"],
+            "fo_err": "error" in fo, "fo_dt": time.perf_counter() - t1, "alive": rp.alive}
+
+
+def _router_revive(ctrl, data):
+    """A pool whose receiver loop stalls (its first pings take 1.5 s against a 0.4 s probe
+    deadline) is marked dead by the probes, but its transport is intact: after the stall the
+    probes succeed again and the pool is put back in service."""
+    from distributed_llm_amd.pools.remote import RemotePool
+    health = []
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=4, timeout_s=30, revive_after=2)
+    rp.on_health = lambda name, ok, rtt: health.append(ok)
+    rp.start_probes(interval_s=0.1, timeout_s=0.4, data_probe_every=0)
+    t0 = time.perf_counter()
+    dead_seen = False
+    while time.perf_counter() - t0 < 20:
+        if not rp.alive:
+            dead_seen = True
+        if dead_seen and rp.alive:
+            break
+        time.sleep(0.05)
+    alive = rp.alive
+    after = rp.process([{"role": "user", "content": "are you back?"}])
+    rp._probe_stop.set()
+    rp.stop()
+    return {"dead_seen": dead_seen, "alive": alive, "revivals": rp.revivals, "after": "response" in after,
+            "health": health}
+
+
+def _router_stuck_data_lock(ctrl, data):
+    """A data-plane transfer that never finishes holds the ordering lock: the failover hand-off
+    gives up on the data plane after its deadline and ships the prompt as text instead."""
+    from distributed_llm_amd.engine.tokenizer import get_tokenizer
+    from distributed_llm_amd.models.configs import get_model_config
+    from distributed_llm_amd.pools.remote import RemotePool
+    cfg = get_model_config("tiny-llama-test")
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=5, timeout_s=60, data_timeout_s=1.0,
+                    tokenizer=get_tokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id))
+    rp._data_lock.acquire()             # as if a transfer were stuck forever
+    t0 = time.perf_counter()
+    r = rp.process_failover([{"role": "user", "content": "hand me over"}])
+    dt = time.perf_counter() - t0
+    ping = rp.probe_data(timeout=1.0)
+    rp.stop()
+    return {"ok": "response" in r, "dt": dt, "retired": rp.data_error is not None, "ping_ok": ping["ok"]}
+
+
 _ROUTER = {"concurrent": _router_concurrent, "kill": _router_kill, "hang": _router_hang,
-           "handoff": _router_handoff}
+           "handoff": _router_handoff, "data_die": _router_die_in_data_ping, "revive": _router_revive,
+           "stuck_lock": _router_stuck_data_lock}
 
 
 def _run(scenario, env=None, timeout=240):
@@ -158,7 +235,7 @@ def _run(scenario, env=None, timeout=240):
         p.start()
     outs = []
     try:
-        for _ in range(2 if scenario in ("concurrent", "handoff") else 1):
+        for _ in range(2 if scenario in ("concurrent", "handoff", "revive", "stuck_lock") else 1):
             outs.append(q.get(timeout=timeout))
     finally:
         for p in procs:
@@ -196,3 +273,24 @@ def test_failover_token_id_handoff_matches_text():
     out = _run("handoff")
     assert out["ids"] and out["ids"] == out["text"]
     assert out["data_ping"]
+
+
+def test_leader_dies_during_data_ping_while_request_fails_over():
+    out = _run("data_die", env={"DLLM_FAULT_DIE_ON_DATA_PING": "1"})
+    assert out["ok"] and out["dev"] == "nano", out
+    assert out["dt"] < 30.0, out
+    assert out["ping_ok"] is False and out["ping_dt"] < 8.0, out
+    assert out["fo_err"] and out["fo_dt"] < 8.0 and out["alive"] is False, out
+
+
+def test_pool_dead_by_probes_is_revived_when_probes_recover():
+    out = _run("revive", env={"DLLM_FAULT_PING_DELAY_N": "3", "DLLM_FAULT_PING_DELAY_S": "1.5"})
+    assert out["dead_seen"] and out["alive"] and out["revivals"] == 1, out
+    assert out["after"], out
+    assert False in out["health"] and out["health"][-1] is True
+
+
+def test_stuck_data_plane_lock_falls_back_to_text():
+    out = _run("stuck_lock")
+    assert out["ok"] and out["dt"] < 20.0, out
+    assert out["retired"] and out["ping_ok"] is False, out

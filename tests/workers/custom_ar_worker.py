@@ -56,6 +56,35 @@ def main():
         if not torch.equal(xs.cpu(), want):
             fails.append(f"graph replay {it}")
     car.check()
+    # fused residual add + row statistics (car_resadd) and the one-shot all-gather
+    for T, H in ((1, 2048), (5, 4096), (64, 8192), (37, 3072), (3, 64)):
+        ys = [inputs(r, T * H, salt=7).view(T, H) for r in range(world)]
+        r0 = inputs(99, T * H, salt=3).view(T, H)
+        tot = sum(y.float() for y in ys).to(torch.bfloat16)           # all-reduce output (bf16)
+        for add in (True, False):
+            want = (tot.float() + r0.float()).to(torch.bfloat16) if add else tot
+            rr = r0.clone().cuda()
+            ssq = torch.full((40, T), -1.0, device="cuda")
+            n = car.all_reduce_resadd(ys[rank].cuda(), rr, ssq, add)
+            torch.cuda.synchronize()
+            if not torch.equal(rr.cpu(), want):
+                fails.append(f"resadd T={T} H={H} add={add}: max err {(rr.cpu().float() - want.float()).abs().max()}")
+            got = ssq[:n].sum(0).cpu()
+            ref = want.float().pow(2).sum(1)
+            if not torch.allclose(got, ref, rtol=1e-4, atol=1e-3) or n != car.resadd_slots(H):
+                fails.append(f"resadd ssq T={T} H={H} n={n}")
+    for n in (8, 256 * 3, 8 * 512):
+        x = inputs(rank, n, salt=11).cuda()
+        got = car.all_gather(x)
+        torch.cuda.synchronize()
+        want = torch.stack([inputs(r, n, salt=11) for r in range(world)])
+        if not torch.equal(got.cpu(), want):
+            fails.append(f"all_gather n={n}")
+    xi = torch.arange(64, dtype=torch.int32, device="cuda") + 1000 * rank
+    gi = car.all_gather(xi).cpu()
+    if not torch.equal(gi, torch.stack([torch.arange(64, dtype=torch.int32) + 1000 * r for r in range(world)])):
+        fails.append("all_gather int32")
+    car.check()
     # a peer that never arrives: rank 1 skips one all-reduce while rank 0 spins out (bounded);
     # the error flag trips on rank 0 only, and the consensus check drops the custom all-reduce on
     # BOTH ranks (ParallelContext.check_collectives), so neither deadlocks nor diverges

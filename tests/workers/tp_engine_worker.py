@@ -1,0 +1,98 @@
+"""Worker for tests/test_tp_gpu.py: one rank of a TP=N serving engine, all N ranks on ONE GPU.
+
+The tensor-parallel decode path is the production one (models.llama fused layer: column-parallel
+QKV / gate|up with their fused epilogues, row-parallel o_proj / down whose partial sums go through
+the one-shot IPC all-reduce with the residual add + RMSNorm statistics fused in, vocab-parallel
+sampling over the one-shot all-gather, the in-graph health vote); IPC mapping works between
+processes on one device, so only the process group is gloo (RCCL refuses two ranks on one GPU).
+
+argv: rank world port repo model out_dir
+Writes out_dir/rank{r}.pt: greedy tokens from graph replay, from eager decode, after an injected
+collective trip, and (rank 0) the final hidden states of a direct prefill.
+"""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, sys.argv[4])
+
+PROMPTS = ["user: hello there", "user: explain paged attention step by step", "x" * 70,
+           "user: what does tensor parallelism split?"]
+
+
+def main():
+    rank, world, port, model, out = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[5],
+                                      sys.argv[6])
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from distributed_llm_amd import ops
+    from distributed_llm_amd.engine.llm_engine import LLMEngine
+    from distributed_llm_amd.engine.sampling import SamplingParams
+    from distributed_llm_amd.models.configs import get_model_config
+    from distributed_llm_amd.models.llama import AttnMeta
+    from distributed_llm_amd.parallel.comm import make_tp_groups
+
+    log = lambda *a: print(f"[rank {rank}]", *a, flush=True)
+    log("process group up")
+    par = make_tp_groups(world)
+    assert par.enable_custom_all_reduce("cuda:0", max_bytes=4 << 20), "one-shot all-reduce unavailable"
+    cfg = get_model_config(model, n_layers=2)
+    eng = LLMEngine(cfg, device="cuda:0", par=par, kv_cache_gb=0.25, max_num_seqs=8, max_model_len=1024,
+                    prefix_cache=False, seed=0)
+    log("engine built")
+    assert eng.model.fused, "the fused tensor-parallel layer must be active"
+    assert eng.use_graphs, "decode graphs must be capturable over the one-shot collectives"
+    sp = SamplingParams(max_new_tokens=8)
+    res = {"graph": [o.token_ids for o in eng.generate(PROMPTS, sp)]}
+    assert eng._graphs, "no decode graph was replayed"
+    log("graph decode done", res["graph"][0])
+    eng.use_graphs = False
+    res["eager"] = [o.token_ids for o in eng.generate(PROMPTS, sp)]
+    # sampled decode: every rank must draw the same tokens (shared seed, merged candidates)
+    eng.use_graphs = True
+    res["sampled"] = [o.token_ids for o in eng.generate(
+        PROMPTS, SamplingParams(max_new_tokens=6, temperature=0.9, top_k=40, top_p=0.95))]
+    # final hidden states of one prompt through a direct prefill (TP vs TP=1 numerics)
+    ids = eng.tok.encode(PROMPTS[1])
+    T = len(ids)
+    table, _ = eng.bm.allocate(7777, ids)
+    dev = torch.device("cuda:0")
+    I = lambda x, dt=torch.int32: torch.tensor(x, dtype=dt, device=dev)
+    m = eng.model
+    ts, tt = ops.build_tiles([T], m.nq // m.nkv)
+    meta = AttnMeta(I(eng.bm.slots(7777, 0, T)), I([table]), I([0]), I([T]), I([T]), I(ts), I(tt),
+                    I([T - 1], torch.int64))
+    res["hidden"] = m.hidden_states(I(ids), I(list(range(T))), meta, eng.kv_caches).float().cpu()
+    eng.bm.free(7777)
+    # an injected one-shot all-reduce trip on the 3rd decode step: every rank agrees through the
+    # in-graph vote, drops the one-shot kernel, re-runs the step on the fallback collectives and
+    # keeps serving (same tokens as before)
+    if os.environ.get("TP_WORKER_DEBUG") == "1":   # per-step sync + log (find a faulting step)
+        orig = eng._decode_step
+
+        def step(running):
+            log("decode step", eng.steps["decode"], "graphs", eng.use_graphs, "car", par.custom_ar is not None)
+            out_ = orig(running)
+            torch.cuda.synchronize()
+            log("  ok")
+            return out_
+        eng._decode_step = step
+        if os.environ.get("TP_WORKER_EAGER_TRIP") == "1":
+            eng.use_graphs = False
+    torch.cuda.synchronize()
+    log("trip phase")
+    eng.FAULT_TRIP_DECODE = eng.steps["decode"] + 2
+    res["after_trip"] = [o.token_ids for o in eng.generate(PROMPTS, sp)]
+    log("after-trip decode done", res["after_trip"][0])
+    res["trips"] = eng.collective_trips
+    res["custom_ar_left"] = par.custom_ar is not None
+    torch.save(res, os.path.join(out, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+    print("OK", flush=True)
+
+
+if __name__ == "__main__":
+    main()
