@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) lg_kernel(const u16* __restric
 // consumers (fragments read: lgkmcnt(0) before the barrier) and back.  Split-K over gridDim:
 // S k-chunks per output tile, write-through f32 slabs + relaxed ticket, the last arriver sums
 // the slabs in split order (Guideline 16 R1, as tgemm).
-template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0>
+template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false>
 __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __restrict__ A, long lda,
                                                                      const u16* __restrict__ W, u16* __restrict__ Y,
                                                                      int M, int N, int K, int S, float* part,
@@ -198,11 +198,17 @@ __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __
         src[j] = W + (long)min(n0 + rb, N - 1) * K + kbeg + 8 * (spos ^ ((rb >> 1) & 7));
       }
     }
+    // ROT: each output tile walks K from its own offset, so the many tiles that stream the SAME
+    // activation rows at once are spread over different K columns (L2 channels) instead of all
+    // hitting one line together
+    const int rot = ROT ? (int)(((unsigned)(n_tile * 7 + m_tile * 3)) % (unsigned)nk) : 0;
     auto issue = [&](int t) {
       unsigned char* base = smem + (t % ST) * STAGE;
+      int tt = t + rot;
+      if (tt >= nk) tt -= nk;
 #pragma unroll
       for (int j = 0; j < G; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * BK), (lds_void*)(base + (lw + NL * j) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(src[j] + tt * BK), (lds_void*)(base + (lw + NL * j) * 1024), 16, 0, 0);
     };
 #pragma unroll
     for (int t = 0; t < ST - 1; ++t)
@@ -344,14 +350,14 @@ Var lgv() {
              }};
 }
 
-template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0>
+template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false>
 Var rgv(int S) {
   char nm[96];
-  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s", BM, BN, WGM, WGN, NL, ST, S,
+  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s%s", BM, BN, WGM, WGN, NL, ST, S, ROT ? " ROT" : "",
            PROBE == 1 ? " LOADERS-ONLY" : PROBE == 2 ? " CONSUMERS-ONLY" : "");
   return Var{nm, BM, BN, S, false, [S](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
                const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
-               hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE>), dim3(g), dim3(64 * (WGM * WGN + NL)), 0, s,
+               hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE, ROT>), dim3(g), dim3(64 * (WGM * WGN + NL)), 0, s,
                                   A, (long)K, W, Y, M, N, K, S, g_part, g_cnt);
              }};
 }
@@ -360,17 +366,15 @@ static float hbf(u16 h) { uint32_t u = ((uint32_t)h) << 16; float f; memcpy(&f, 
 
 int main(int argc, char** argv) {
   std::vector<Var> vars = {
-      lgv<64, 64, 2, 2, 3, false>(), lgv<128, 128, 2, 4, 3, false>(),
-      rgv<64, 64, 2, 2, 2, 4>(1),     rgv<64, 64, 2, 2, 2, 4>(2),     rgv<64, 64, 2, 2, 4, 4>(2),
-      rgv<128, 64, 2, 2, 4, 4>(1),    rgv<128, 64, 2, 2, 4, 4>(2),    rgv<128, 64, 2, 2, 4, 4>(4),
-      rgv<128, 128, 2, 2, 4, 4>(1),   rgv<128, 128, 2, 2, 4, 4>(2),   rgv<128, 128, 2, 2, 4, 4>(4),
-      rgv<128, 128, 2, 4, 4, 4>(2),   rgv<160, 64, 2, 2, 4, 4>(2),    rgv<160, 64, 2, 2, 4, 4>(4),
-      rgv<80, 64, 1, 4, 2, 4>(2),     rgv<80, 64, 1, 4, 3, 4>(1),     rgv<160, 128, 2, 4, 4, 3>(1),
-      rgv<160, 128, 2, 4, 4, 3>(2),   rgv<256, 128, 4, 2, 4, 3>(1),   rgv<256, 128, 4, 2, 4, 3>(2),
-      rgv<320, 128, 4, 2, 4, 2>(1),   rgv<320, 64, 4, 2, 4, 3>(1),    rgv<320, 64, 4, 2, 4, 3>(2),
-      rgv<128, 128, 2, 2, 4, 4, 1>(1), rgv<128, 128, 2, 2, 4, 4, 2>(1), rgv<64, 64, 2, 2, 2, 4, 1>(1),
-      rgv<64, 64, 2, 2, 2, 4, 2>(1),   rgv<128, 64, 2, 2, 4, 6>(1),  rgv<64, 64, 2, 2, 2, 8>(1),
-      rgv<64, 64, 2, 2, 4, 8>(1),
+      rgv<64, 64, 2, 2, 2, 4>(1),              rgv<64, 64, 2, 2, 2, 4, 0, true>(1),
+      rgv<64, 64, 2, 2, 2, 4, 1, true>(1),     rgv<64, 64, 2, 2, 4, 8, 0, true>(1),
+      rgv<128, 64, 2, 2, 4, 4>(1),             rgv<128, 64, 2, 2, 4, 4, 0, true>(1),
+      rgv<128, 128, 2, 2, 4, 4>(1),            rgv<128, 128, 2, 2, 4, 4, 0, true>(1),
+      rgv<128, 128, 2, 2, 4, 4, 1, true>(1),   rgv<80, 64, 1, 4, 2, 4, 0, true>(2),
+      rgv<80, 64, 1, 4, 3, 4, 0, true>(1),     rgv<160, 128, 2, 4, 4, 3, 0, true>(1),
+      rgv<160, 128, 2, 4, 4, 3>(1),            rgv<256, 128, 4, 2, 4, 3, 0, true>(1),
+      rgv<256, 128, 4, 2, 4, 3>(1),            rgv<160, 64, 2, 2, 4, 4, 0, true>(2),
+      rgv<128, 64, 2, 2, 4, 4, 0, true>(2),    rgv<64, 64, 2, 2, 4, 4, 0, true>(2),
   };
   struct Shape { int N, K; };
   std::vector<Shape> shapes = {{2560, 2048}, {2048, 2048}, {11264, 2048}, {2048, 5632}};
