@@ -19,7 +19,12 @@ answers = skipped work); small tier greedy (reference Nano), large tier Ollama-d
 ``--topology pools`` (BASELINE configs 3-5): the tiers live on disjoint GPU subsets
 (parallel.cluster.default_topology: 2 GPUs small|large, 4 GPUs 2 small replicas + large TP=2,
 8 GPUs 4 small replicas + large TP=4); rank 0 hosts the router and drives
-``--convs x N`` conversations; requests reach remote pools over RCCL point-to-point messages.
+``--convs x N`` conversations; requests reach remote pools over the gloo control/data planes,
+RCCL carries only the large pool's tensor-parallel collectives.  Without ``--baseline-config``
+2-4 GPUs run config 3 (Llama-3.2-1B | Llama-3-8B), 8 GPUs config 4 (Llama-3-8B x4 | Llama-3-70B
+TP=4, perf router); ``--baseline-config 5`` puts Mixtral-8x7B on the large half (TP = N/2, not
+co-located with the small pool as in the reference's config).  The JSON line names the config
+it ran in ``baseline_config``.
 
 ``value`` = total generated tokens over all ranks / max rank wall time of the timed steps.
 """
@@ -46,12 +51,15 @@ def parse():
                     help="replicated: both tiers on one engine per GPU (BASELINE config 2); pools: tiers on "
                          "disjoint GPU subsets (configs 3-5, N>1); tiers: --small-model and --large-model "
                          "co-located as two engines on every GPU")
+    ap.add_argument("--baseline-config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="BASELINE.json config to run (default: 2 replicated; --topology pools: 3 at 2-4 GPUs, "
+                         "4 at 8 GPUs); sets topology and models")
     ap.add_argument("--model", default="tinyllama-1.1b")
-    ap.add_argument("--small-model", default="llama-3.2-1b")
-    ap.add_argument("--large-model", default="llama-3-8b")
+    ap.add_argument("--small-model", default=None, help="pools/tiers small tier (default per baseline config)")
+    ap.add_argument("--large-model", default=None, help="pools/tiers large tier (default per baseline config)")
     ap.add_argument("--large-tp", type=int, default=None)
     ap.add_argument("--convs", type=int, default=512, help="concurrent conversations per GPU")
-    ap.add_argument("--strategy", default="hybrid")
+    ap.add_argument("--strategy", default=None, help="routing strategy (default: perf for config 4, else hybrid)")
     ap.add_argument("--threshold", type=int, default=1000)
     ap.add_argument("--small-new", type=int, default=128)
     ap.add_argument("--large-new", type=int, default=384)
@@ -68,6 +76,35 @@ def parse():
                     help="write a Chrome trace (router/pool/engine spans, GPU decode time) to this path; "
                          "'{rank}' is replaced by the rank")
     return ap.parse_args()
+
+
+# BASELINE.json "configs" (1-based) -> (topology, small model, large model, large TP or None = default)
+BASELINE_CONFIGS = {
+    2: ("replicated", None, None, None),
+    3: ("pools", "llama-3.2-1b", "llama-3-8b", None),         # 1B | 8B, one GPU each (2 GPUs)
+    4: ("pools", "llama-3-8b", "llama-3-70b", 4),             # 8B replicas | 70B TP=4 over xGMI
+    5: ("pools", "llama-3.2-1b", "mixtral-8x7b", None),       # 1B replicas | Mixtral TP=N/2 (MoE)
+}
+
+
+def resolve_config(a, world: int) -> int:
+    """Fill topology / models from ``--baseline-config`` (or infer it) and return the config id
+    tagged on the JSON line."""
+    cfg = a.baseline_config
+    if cfg is None:
+        if a.topology == "pools" and world > 1:
+            cfg = 4 if world >= 8 else 3
+        else:
+            cfg = 2
+    topo, sm, lg, tp = BASELINE_CONFIGS[cfg]
+    if a.baseline_config is not None:
+        a.topology = topo
+    a.small_model = a.small_model or sm or "llama-3.2-1b"
+    a.large_model = a.large_model or lg or "llama-3-8b"
+    if a.large_tp is None and tp is not None and world >= 2 * tp:
+        a.large_tp = tp
+    a.strategy = a.strategy or ("perf" if cfg == 4 else "hybrid")   # config 4: perf-router failover
+    return cfg
 
 
 class Conversations:
@@ -266,7 +303,10 @@ def main() -> int:
     if a.no_encoder_memo:
         os.environ["DLLM_ENCODER_MEMO"] = "0"
     from distributed_llm_amd.router.embedder import encoder_stats
+    baseline_config = resolve_config(a, world)
     topology = a.topology if (world > 1 or a.topology == "tiers") else "replicated"
+    if topology == "replicated":
+        baseline_config = 2
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
 
@@ -409,6 +449,8 @@ def main() -> int:
         tokens_all, elapsed_max = float(tokens), elapsed
     if rank == 0:
         value = tokens_all / max(elapsed_max, 1e-9)
+        rates = sorted(r["tok"] * 1000.0 / r["lat"] for r in records if r["lat"] > 0 and r["tok"] > 0)
+        per_stream = rates[len(rates) // 2] if rates else None   # one request's own decode rate (reference protocol)
         pct = lambda p: lats[min(len(lats) - 1, int(p * len(lats)))] if lats else 0.0
         n_small = sum(1 for r in records if r["dev"] == SMALL)
         hits = sum(b["prefix_hit_tokens"] - a_["prefix_hit_tokens"] for a_, b in zip(st0, st1))
@@ -424,6 +466,13 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_TOK_S, 2),
+            # vs_baseline divides this whole-job aggregate (all conversations, all GPUs) by the
+            # reference's single-stream 10.57 tok/s; the like-for-like ratio is per stream:
+            "vs_baseline_basis": "aggregate tokens/s over all concurrent conversations / reference single-stream "
+                                 "10.57 tok/s (BASELINE.md)",
+            "per_stream_tok_s_p50": round(per_stream, 1) if per_stream else None,
+            "per_stream_vs_baseline": round(per_stream / BASELINE_TOK_S, 2) if per_stream else None,
+            "baseline_config": baseline_config,
             "dtype": "bf16",
             "data": "synthetic: reference query sets replayed as growing conversations; random-init weights",
             "config": {"model": model_desc, "global_batch": a.convs * world,

@@ -50,7 +50,7 @@ int dllm_car_resadd_slots(int);
 int dllm_car_resadd(const void*, void*, long, float*, long, int, int, int, void* const*, int, int, long, unsigned*, int*,
                     long, hipStream_t);
 int dllm_car_allgather(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
-int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t);
+int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t, int);
 int dllm_decode_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*, void*,
                           float*, float*, int*, const int*, const int*, int, int, int, int, int, int, int, float,
                           hipStream_t);
@@ -729,9 +729,18 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
            c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> pos,
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
-           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk) {
+           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk, int64_t nl) {
   check_bf16(x, "x");
   check_bf16(w, "w");
+  if (nl > 0) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
+    const bool known = ks == 1 && wk == 1 &&
+                       ((bm == 64 && bn == 64 && nw == 4 && ((nl == 2 && stages == 4) || (nl == 4 && (stages == 4 || stages == 8)))) ||
+                        (bm == 128 && bn == 64 && nw == 4 && nl == 4 && stages == 4) ||
+                        (bm == 128 && bn == 128 && nw == 4 && nl == 4 && stages == 4) ||
+                        (bm == 160 && bn == 128 && nw == 8 && nl == 4 && stages == 3) ||
+                        (bm == 256 && bn == 128 && nw == 8 && nl == 4 && stages == 3));
+    TORCH_CHECK(known, "tgemm: no loader-wave plan (", bm, "x", bn, ", ", stages, " stages, ", nw, "+", nl, " waves)");
+  }
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
   TORCH_CHECK(epi >= 0 && epi <= 4, "epi");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
@@ -740,9 +749,9 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK(wk == 1 || (wk == 2 && nw == 4 && ks == 2 && stages <= 3 && bm <= 128 && bn <= 128),
               "wk 2: two k-groups of 4 waves, ks 2, 2-3 stages, tiles up to 128 x 128");
   TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
-  TORCH_CHECK((bm == 64 || bm == 128 || ((bm == 192 || bm == 256) && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
+  TORCH_CHECK(nl > 0 || ((bm == 64 || bm == 128 || ((bm == 192 || bm == 256) && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
                   (stages == 2 || stages == 3 || ((stages == 4 || stages == 6) && ks == 1 && bm <= 128)) &&
-                  (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024,
+                  (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024),
               "tile / ring size");
   TORCH_CHECK(splits >= 1 && splits <= 64, "splits");
   const int kq = 64 * (int)ks;
@@ -823,7 +832,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
     a.vc = (uint16_t*)vc->data_ptr();
     a.nq = nq; a.nkv = nkv; a.d = d;
   }
-  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)wk, (int)epi, stream()), "tgemm");
+  ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)wk, (int)epi, stream(), (int)nl), "tgemm");
 }
 
 // standalone EPI_QKV / EPI_SWIGLU for a vendor-GEMM output y (prefill)

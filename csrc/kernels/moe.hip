@@ -24,7 +24,7 @@
 #include "tgemm_args.h"
 
 extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, int nw, int wk, int epi,
-                          hipStream_t stream);
+                          hipStream_t stream, int nl);
 
 namespace {
 constexpr int MT = 32;
@@ -294,13 +294,13 @@ extern "C" int dllm_moe_ffn_tg(const void* x, long x_stride, long T, int H, cons
   g.A = (const uint16_t*)x; g.lda = x_stride; g.W = (const uint16_t*)w13; g.Y = (uint16_t*)act; g.ldy = I;
   g.M = max_tiles * bm; g.N = 2 * I; g.K = H; g.kchunk = H; g.splits = 1;
   g.g_tiles = tiles; g.g_max = max_tiles; g.g_perm = perm; g.g_k = k; g.g_wstride = 2L * I * H;
-  int rc = dllm_tgemm(&g, bm, plan[1], plan[2], plan[3], plan[4], 1, dllm::EPI_SWIGLU, stream);
+  int rc = dllm_tgemm(&g, bm, plan[1], plan[2], plan[3], plan[4], 1, dllm::EPI_SWIGLU, stream, 0);
   if (rc) return 1000 + rc;
   dllm::GemmArgs d{};
   d.A = (const uint16_t*)act; d.lda = I; d.W = (const uint16_t*)w2; d.Y = (uint16_t*)y; d.ldy = H;
   d.M = max_tiles * bm; d.N = H; d.K = I; d.kchunk = I; d.splits = 1;
   d.g_tiles = tiles; d.g_max = max_tiles; d.g_perm = nullptr; d.g_k = 1; d.g_wstride = (long)H * I;
-  rc = dllm_tgemm(&d, bm, plan[5], plan[6], plan[7], plan[8], 1, dllm::EPI_PLAIN, stream);
+  rc = dllm_tgemm(&d, bm, plan[5], plan[6], plan[7], plan[8], 1, dllm::EPI_PLAIN, stream, 0);
   if (rc) return 2000 + rc;
   long n8 = T * (H / 8);
   long gr = (n8 + 255) / 256;

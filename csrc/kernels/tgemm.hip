@@ -54,6 +54,8 @@ __device__ __forceinline__ void wait_vm() {
 // wait until at most r stages of ring loads (G per stage per wave) are still in flight, r <= MAXR
 template <int G, int MAXR>
 __device__ __forceinline__ void wait_stages(int r) {
+  if constexpr (MAXR >= 6) { if (r >= 6) { wait_vm<6 * G>(); return; } }
+  if constexpr (MAXR >= 5) { if (r == 5) { wait_vm<5 * G>(); return; } }
   if constexpr (MAXR >= 4) { if (r >= 4) { wait_vm<4 * G>(); return; } }
   if constexpr (MAXR >= 3) { if (r == 3) { wait_vm<3 * G>(); return; } }
   if constexpr (MAXR >= 2) { if (r == 2) { wait_vm<2 * G>(); return; } }
@@ -72,22 +74,33 @@ __device__ __forceinline__ float bfr(float x) { return bf2f(f2bf(x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // KS: 64-deep k sub-tiles per ring stage (one barrier per stage); NW: waves per k-group, laid out
-// 2 (M) x NW/2 (N), each wave a (BM/2) x (BN/(NW/2)) tile; WK: k-groups (1, or 2 with KS = 2): group g
-// stages and multiplies sub-tile g of every stage, and group 1's accumulators are added into group
-// 0's through LDS after the loop.  WK = 2 doubles the waves of a small output tile (decode-size M
-// has few tiles: 1 wave per SIMD leaves every LDS-read -> MFMA chain exposed) and halves each
-// wave's serial k chain without a global split-K combine.
-template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1>
-__global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
+// WGM (M) x NW/WGM (N), each wave a (BM/WGM) x (BN/(NW/WGM)) tile; WK: k-groups (1, or 2 with
+// KS = 2): group g stages and multiplies sub-tile g of every stage, and group 1's accumulators are
+// added into group 0's through LDS after the loop.  WK = 2 doubles the waves of a small output tile
+// (decode-size M has few tiles: 1 wave per SIMD leaves every LDS-read -> MFMA chain exposed) and
+// halves each wave's serial k chain without a global split-K combine.
+// NL > 0: NL extra LOADER waves issue (and wait for) every global_load_lds of the ring while the NW
+// compute waves only read LDS fragments and issue MFMAs; one raw barrier per stage hands a slot
+// from the loaders (counted vmcnt before it) to the computers (lgkmcnt(0) before it) and back.
+// At decode-size M a stage's fill and its MFMA chain then overlap instead of alternating inside
+// each wave (profiles/r3_decode_gemm_lab.md: 5-30 % faster on the TinyLlama / Llama-3-8B decode
+// projections at M = 320-512).
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
+__global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) {
   static_assert(WK == 1 || (WK == 2 && KS == 2), "k-groups split the KS sub-tiles of a stage");
-  constexpr int NT = 64 * NW * WK, NWN = NW / 2;  // NT: threads of the block
-  constexpr int WM = BM / 2, WN = BN / NWN;
+  static_assert(NL == 0 || WK == 1, "loader waves or k-groups, not both");
+  constexpr int NC = NW * WK, NT = 64 * (NC + NL), NWN = NW / WGM;  // NT: threads of the block
+  constexpr int WM = BM / WGM, WN = BN / NWN;
   constexpr int FM = WM / 16, FN = WN / 16;
-  static_assert(FN % 2 == 0 && FM >= 1, "wave tile: >= 16 rows, a multiple of 32 columns");
+  static_assert(FN % 2 == 0 && FM >= 1 && WM % 16 == 0 && NW % WGM == 0, "wave tile: >= 16 rows, a multiple of 32 columns");
   constexpr int A_BYTES = BM * ROWB, SUB_BYTES = (BM + BN) * ROWB, STAGE_BYTES = KS * SUB_BYTES;
-  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // global_load_lds per wave per sub-tile
-  constexpr int G = (KS / WK) * (GA + GB);               // ... per stage
-  static_assert(GA >= 1 && GB >= 1, "tile too small for the wave count");
+  constexpr int GA = NL ? 1 : BM / (8 * NW), GB = NL ? 1 : BN / (8 * NW);  // global_load_lds per wave per sub-tile
+  constexpr int PPS = KS * (BM + BN) / 8;                                  // 1 KB pieces per stage
+  constexpr int GL = NL ? PPS / NL : 1;                                    // ... per loader wave
+  static_assert(NL == 0 || PPS % NL == 0, "stage pieces must split evenly over the loader waves");
+  constexpr int G = NL ? GL : (KS / WK) * (GA + GB);     // ring loads per (issuing) wave per stage
+  static_assert(NL > 0 || (GA >= 1 && GB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0),
+                "tile too small for the wave count");
   constexpr int KSTEP = BK * KS;
   constexpr int OW = (EPI == EPI_SWIGLU) ? BN / 2 : BN;  // staged output columns per row
   constexpr int OLD = OW + 8;                             // staged row stride (bf16)
@@ -100,9 +113,11 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   float* s_red = s_rsp + TPR * BM;
   int* s_last = reinterpret_cast<int*>(s_red + 2 * BM);
 
-  const int lane = threadIdx.x & 63, kg = (threadIdx.x >> 6) / NW, wave = (threadIdx.x >> 6) % NW;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool loader = NL > 0 && wid >= NC;
+  const int kg = loader ? 0 : wid / NW, wave = loader ? 0 : wid % NW;
   const int wm = wave / NWN, wn = wave % NWN;
-  const bool fw = (WK == 1) || kg == 0;  // this wave owns the final accumulators
+  const bool fw = ((WK == 1) || kg == 0) && !loader;  // this wave owns the final accumulators
   const int N = a.N, K = a.K, S = a.splits;
   int M = a.M;
   const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
@@ -143,21 +158,40 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   // ---- staging: wave w owns ring rows [8 (w*GA + j), +8) of A and [8 (w*GB + j), +8) of B;
   // lane -> row + lane/8, LDS chunk lane%8 <- source chunk (lane%8) ^ ((row >> 1) & 7)
   const int srow = lane >> 3, spos = lane & 7;
-  const u16* a_src[GA];
-  const u16* b_src[GB];
-#pragma unroll
-  for (int j = 0; j < GA; ++j) {
-    const int r = 8 * (wave * GA + j) + srow;
+  auto a_row = [&](int r) -> const u16* {  // A source of tile row r (k offset 0 of this split)
     const int row = min(m0 + r, M - 1);
     const long arow = a.g_perm != nullptr ? (long)(a.g_perm[row] / a.g_k) : (long)row;  // MoE: gathered rows
-    a_src[j] = a.A + arow * a.lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
-  }
+    return a.A + arow * a.lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+  };
+  auto b_row = [&](int r) -> const u16* {
+    return Wb + (long)min(n0 + r, N - 1) * K + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+  };
+  const u16* a_src[GA];
+  const u16* b_src[GB];
+  const u16* l_src[GL];   // loader waves: piece lw + NL j of the stage image ([A; B] per sub-tile)
+  int l_off[GL];
+  if constexpr (NL == 0) {
 #pragma unroll
-  for (int j = 0; j < GB; ++j) {
-    const int r = 8 * (wave * GB + j) + srow;
-    b_src[j] = Wb + (long)min(n0 + r, N - 1) * K + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+    for (int j = 0; j < GA; ++j) a_src[j] = a_row(8 * (wave * GA + j) + srow);
+#pragma unroll
+    for (int j = 0; j < GB; ++j) b_src[j] = b_row(8 * (wave * GB + j) + srow);
+  } else if (loader) {
+    const int lw = wid - NC;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) {
+      const int g = lw + NL * j, ks = g / ((BM + BN) / 8), p = g % ((BM + BN) / 8);
+      l_src[j] = (p < BM / 8 ? a_row(8 * p + srow) : b_row(8 * (p - BM / 8) + srow)) + ks * BK;
+      l_off[j] = ks * SUB_BYTES + p * 1024;
+    }
   }
   auto issue = [&](int t) {
+    if constexpr (NL > 0) {
+      unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
+#pragma unroll
+      for (int j = 0; j < GL; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + t * KSTEP), (lds_void*)(base + l_off[j]), 16, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (WK == 2 && ks != kg) continue;  // each k-group stages its own sub-tile
@@ -180,9 +214,11 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if (NL == 0 || loader) {
 #pragma unroll
-  for (int t = 0; t < STAGES - 1; ++t)
-    if (t < nk) issue(t);
+    for (int t = 0; t < STAGES - 1; ++t)
+      if (t < nk) issue(t);
+  }
 
   if (has_rs && rs_on) {
     float s = 0.f;
@@ -199,11 +235,17 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   }
 
   // ---- main loop: wait for tile t, barrier, refill the slot read at t-1, compute tile t
+  // (NL > 0: the loader waves do the waits and refills, the compute waves only the MFMA part)
   for (int t = 0; t < nk; ++t) {
-    // tile t landed once at most min(STAGES - 2, nk - 1 - t) later stages are still in flight
-    wait_stages<G, (STAGES - 2 < 4 ? STAGES - 2 : 4)>(min(STAGES - 2, nk - 1 - t));
+    if (NL == 0 || loader) {
+      // tile t landed once at most min(STAGES - 2, nk - 1 - t) later stages are still in flight
+      wait_stages<G, (STAGES - 2 < 6 ? STAGES - 2 : 6)>(min(STAGES - 2, nk - 1 - t));
+    }
     block_sync_lds();
-    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    if (NL == 0 || loader) {
+      if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    }
+    if (loader) continue;
 #pragma unroll
     for (int s = 0; s < 2 * KS; ++s) {
       if (WK == 2 && (s >> 1) != kg) continue;
@@ -269,19 +311,42 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
                 make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
       }
     if (!ticket_last(&a.counters[tile_id], S, s_last)) return;
+    if (fw && FM * FN > 16) {   // big wave tiles: no registers to spare for a slab's fragments
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if (!fw) continue;
-        const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        for (int sp = 0; sp < S; ++sp) {
-          const float4 q = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
-          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+        for (int j = 0; j < FN; ++j) {
+          const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          for (int sp = 0; sp < S; ++sp) {
+            const float4 q = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
+            v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+          }
+          acc[i][j] = v;
         }
-        acc[i][j] = v;
+    } else if (fw) {
+      // one round trip per split: every fragment of a slab is loaded before any is added
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < S; ++sp) {
+        float4 q[FM][FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
+            q[i][j] = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
+          }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            acc[i][j][0] += q[i][j].x; acc[i][j][1] += q[i][j].y; acc[i][j][2] += q[i][j].z; acc[i][j][3] += q[i][j].w;
+          }
       }
+    }
   }
 
   // ---- epilogue.  Lane's elements: row m0 + wm*WM + 16 i + 4 (lane>>4) + e, col n0 + wn*WN + 16 j + (lane&15)
@@ -406,10 +471,11 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   if constexpr (EPI == EPI_RESADD) {
     // each thread owns chunks of one row per pass; CPR consecutive lanes share a row -> the row's
     // sum of squares is reduced with shuffles and written once per (n-tile, row)
-    constexpr int RPP = NT / CPR;  // rows per pass
+    constexpr int RPP = NT / CPR;  // rows per pass (need not divide BM with loader waves)
     const int c0 = (threadIdx.x % CPR) * 8;
     for (int r0 = 0; r0 < BM; r0 += RPP) {
-      const int rl = r0 + threadIdx.x / CPR, m = m0 + rl, n = ncol0 + c0;
+      const int rl = r0 + threadIdx.x / CPR, n = ncol0 + c0;
+      const int m = rl < BM ? m0 + rl : M;  // past the tile: not this workgroup's rows
       float ss = 0.f;
       if (m < M && (full_n || n < nlim)) {
         u16* yp = a.Y + (long)m * a.ldy + n;
@@ -436,21 +502,37 @@ __global__ void __launch_bounds__(64 * NW * WK) tgemm_kernel(GemmArgs a) {
   }
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
 int launch_t(const GemmArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK>), dim3(mt * nt * a.splits), dim3(64 * NW * WK), 0, st,
-                     a);
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>), dim3(mt * nt * a.splits),
+                     dim3(64 * (NW * WK + NL)), 0, st, a);
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
 int launch_fit(const GemmArgs& a, hipStream_t st) {
   if constexpr (ST * KS * (BM + BN) * ROWB > 150 * 1024) {
     return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
   } else {
-    return launch_t<BM, BN, EPI, ST, KS, NW, WK>(a, st);
+    return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>(a, st);
   }
+}
+
+// loader-wave tiles (NL > 0; KS 1): the decode-size plans the lab measured fastest
+template <int EPI>
+int by_tile_nl(int bm, int bn, int stages, int nw, int nl, const GemmArgs& a, hipStream_t st) {
+  if (bm == 64 && bn == 64 && nw == 4) {
+    if (nl == 2 && stages == 4) return launch_fit<64, 64, EPI, 4, 1, 4, 1, 2>(a, st);
+    if (nl == 4 && stages == 4) return launch_fit<64, 64, EPI, 4, 1, 4, 1, 4>(a, st);
+    if (nl == 4 && stages == 8) return launch_fit<64, 64, EPI, 8, 1, 4, 1, 4>(a, st);
+  }
+  if (bm == 128 && bn == 64 && nw == 4 && nl == 4 && stages == 4) return launch_fit<128, 64, EPI, 4, 1, 4, 1, 4>(a, st);
+  if (bm == 128 && bn == 128 && nw == 4 && nl == 4 && stages == 4) return launch_fit<128, 128, EPI, 4, 1, 4, 1, 4>(a, st);
+  if (bm == 160 && bn == 128 && nw == 8 && nl == 4 && stages == 3) return launch_fit<160, 128, EPI, 3, 1, 8, 1, 4>(a, st);
+  if (bm == 256 && bn == 128 && nw == 8 && nl == 4 && stages == 3)
+    return launch_fit<256, 128, EPI, 3, 1, 8, 1, 4, 4>(a, st);   // 4 x 2 compute waves of 64 x 64
+  return -22;
 }
 
 template <int BM, int BN, int EPI, int NW>
@@ -660,9 +742,25 @@ extern "C" int dllm_tgemm_sizeof_args() { return (int)sizeof(GemmArgs); }
 // splits >= 1 with kchunk % 64 == 0, part >= splits * tiles * bm * bn floats and counters >= tiles
 // (zeroed) when splits > 1; QKV/SWIGLU need N % 32 == 0 (and d % 32 == 0).
 extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, int nw, int wk, int epi,
-                          hipStream_t stream) {
+                          hipStream_t stream, int nl) {
   const GemmArgs& a = *reinterpret_cast<const GemmArgs*>(args);
   if (a.M <= 0 || a.N <= 0) return 0;
+  if (nl > 0) {   // loader-wave plans: KS 1, one k-group, no MoE gather
+    if (ks != 1 || wk != 1 || a.g_tiles != nullptr || a.K % BK || a.kchunk % BK || a.kchunk <= 0 || a.splits < 1 ||
+        a.lda % 8 || a.N % 8 || (a.Y && a.ldy % 8))
+      return -23;
+    if (a.splits > 1 && (!a.part || !a.counters)) return -2;
+    if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
+    if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
+    switch (epi) {
+      case EPI_PLAIN: return by_tile_nl<EPI_PLAIN>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_RESADD: return by_tile_nl<EPI_RESADD>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_QKV: return by_tile_nl<EPI_QKV>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_SWIGLU: return by_tile_nl<EPI_SWIGLU>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_GELU: return by_tile_nl<EPI_GELU>(bm, bn, stages, nw, nl, a, stream);
+      default: return -6;
+    }
+  }
   if ((ks != 1 && ks != 2) || (nw != 4 && nw != 8) || (wk != 1 && wk != 2)) return -8;
   if (a.K % (BK * ks) || a.kchunk % (BK * ks) || a.kchunk <= 0 || a.splits < 1 || a.lda % 8) return -1;
   if (a.splits > 1 && (!a.part || !a.counters)) return -2;

@@ -49,6 +49,10 @@ _TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8
              (256, 128, 8),
              (256, 256, 8))
 _TG_SPLITS = (1, 2, 3, 4, 6, 8)
+# loader-wave plans (csrc/kernels/tgemm.hip by_tile_nl): (bm, bn, compute waves, stages, loader waves);
+# M is the smallest batch each is tried at (larger tiles only pay once M fills them)
+_TG_NL = ((64, 64, 4, 4, 2, 1), (64, 64, 4, 4, 4, 1), (64, 64, 4, 8, 4, 1), (128, 64, 4, 4, 4, 65),
+          (128, 128, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129))
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
 WS_COUNTERS = 1 << 16
 
@@ -204,10 +208,11 @@ def _run_plan(plan, x, w, swiglu, out):
 
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
            pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None):
-    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups]])"""
+    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves]]])"""
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     wk = plan[6] if len(plan) >= 7 else 1
+    nl = plan[7] if len(plan) >= 8 else 0
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if K % (64 * ks):
         ks, wk = 1, 1
@@ -216,7 +221,7 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
         floats, tiles = _need_tg(M, N, K, bm, bn, sp, ks)
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
-              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk))
+              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl))
 
 
 def ref_silu_mul(gu):
@@ -549,6 +554,17 @@ def _tg_cands(M: int, N: int, K: int):
                     out.append((bm, bn, st, sp, ks, nw))
                     if ks == 2 and nw == 4 and st <= 3 and bm <= 128 and bn <= 128:
                         out.append((bm, bn, st, sp, ks, nw, 2))   # two k-groups of 4 waves
+    if N % 8 == 0 and os.environ.get("DLLM_TG_NL", "1") == "1":
+        for bm, bn, nw, st, nl, m_min in _TG_NL:
+            if M < m_min:
+                continue
+            tiles = -(-M // bm) * -(-N // bn)
+            for sp in (1, 2, 3, 4):
+                if sp > 1 and (K // sp < 256 or tiles * sp > 2048 or _tg_splits(K, sp) != sp):
+                    continue
+                if _need_tg(M, N, K, bm, bn, sp)[0] > WS_FLOATS:
+                    continue
+                out.append((bm, bn, st, sp, 1, nw, 1, nl))
     return out
 
 

@@ -469,10 +469,10 @@ int main(int argc, char** argv) {
         dllm::GemmArgs a{};
         a.A = A; a.lda = K; a.W = nullptr; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.kchunk = K; a.splits = 1;
         a.W = ws[0];
-        if (dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s) != 0) continue;
+        if (dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s, 0) != 0) continue;
         CHECK(hipStreamSynchronize(s));
         const double err = check("tgemm");
-        const double us = time_graph([&](int i) { a.W = ws[i]; dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s); });
+        const double us = time_graph([&](int i) { a.W = ws[i]; dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s, 0); });
         char nm[96];
         snprintf(nm, sizeof nm, "tgemm<%d,%d,st%d,nw%d>", p[0], p[1], p[2], p[5]);
         report(nm, us, err);

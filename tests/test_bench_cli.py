@@ -19,9 +19,11 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n,extra,par", [(1, [], "dp1"), (2, [], "dp2"), (4, ["--topology", "pools"], "pools:"),
-                                         (1, ["--topology", "tiers"], "dp1-colocated")])
-def test_bench_json_line(n, extra, par):
+@pytest.mark.parametrize("n,extra,par,cfg", [(1, [], "dp1", 2), (2, [], "dp2", 2),
+                                             (4, ["--topology", "pools"], "pools:", 3),
+                                             (4, ["--baseline-config", "4"], "pools:small2xtp1+large1xtp2", 4),
+                                             (1, ["--topology", "tiers"], "dp1-colocated", 2)])
+def test_bench_json_line(n, extra, par, cfg):
     args = ["bench.py", "--cpu", "--gpus", str(n), "--steps", "1", "--warmup", "1", "--convs", "2",
             "--small-new", "4", "--large-new", "6"] + extra
     if n > 1:
@@ -40,3 +42,5 @@ def test_bench_json_line(n, extra, par):
     assert out["value"] > 0 and out["higher_is_better"] is True and out["scaling"] == "weak"
     assert out["config"]["parallelism"].startswith(par)
     assert out["requests"] == 2 * n and out["p50_latency_ms"] > 0
+    assert out["baseline_config"] == cfg
+    assert out["per_stream_vs_baseline"] is None or out["per_stream_vs_baseline"] > 0

@@ -20,7 +20,9 @@ PLANS = [p for p in ([(bm, bn, st, sp, 1, nw) for bm, bn, nw in G._TG_TILES for 
                          for st in (4, 6) for sp in (1, 3)]
                       # two k-groups of 4 waves (KS = 2)
                       + [(bm, bn, st, sp, 2, 4, 2) for bm, bn in ((64, 64), (64, 128), (128, 64), (128, 128))
-                         for st in (2, 3) for sp in (1, 2)])
+                         for st in (2, 3) for sp in (1, 2)]
+                      # loader-wave plans (NL extra waves stream the ring, the rest only compute)
+                      + [(bm, bn, st, sp, 1, nw, 1, nl) for bm, bn, nw, st, nl, _ in G._TG_NL for sp in (1, 3)])
          if p[2] * p[4] * (p[0] + p[1]) * 128 <= 150 * 1024]
 
 

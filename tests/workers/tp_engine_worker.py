@@ -37,7 +37,8 @@ def main():
     log = lambda *a: print(f"[rank {rank}]", *a, flush=True)
     log("process group up")
     par = make_tp_groups(world)
-    assert par.enable_custom_all_reduce("cuda:0", max_bytes=4 << 20), "one-shot all-reduce unavailable"
+    if world > 1:
+        assert par.enable_custom_all_reduce("cuda:0", max_bytes=4 << 20), "one-shot all-reduce unavailable"
     cfg = get_model_config(model, n_layers=2)
     eng = LLMEngine(cfg, device="cuda:0", par=par, kv_cache_gb=0.25, max_num_seqs=8, max_model_len=1024,
                     prefix_cache=False, seed=0)
@@ -45,6 +46,18 @@ def main():
     assert eng.model.fused, "the fused tensor-parallel layer must be active"
     assert eng.use_graphs, "decode graphs must be capturable over the one-shot collectives"
     sp = SamplingParams(max_new_tokens=8)
+    mode = os.environ.get("TP_WORKER_MODE", "full")
+    if mode != "full":   # diagnostics: "graph" / "eager" = 3 gens in that mode, "alt" = graph, eager, graph
+        seq = {"graph": [True] * 3, "eager": [False] * 3, "alt": [True, False, True, True]}[mode]
+        for k, g in enumerate(seq):
+            eng.use_graphs = g
+            toks = [o.token_ids for o in eng.generate(PROMPTS, sp)]
+            torch.cuda.synchronize()
+            log(f"gen {k} graphs={g} ok", toks[0])
+        dist.barrier()
+        dist.destroy_process_group()
+        print("OK", flush=True)
+        return
     res = {"graph": [o.token_ids for o in eng.generate(PROMPTS, sp)]}
     assert eng._graphs, "no decode graph was replayed"
     log("graph decode done", res["graph"][0])
