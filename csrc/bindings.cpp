@@ -30,6 +30,9 @@ int dllm_sample_topp(const float*, const long*, int, int, const float*, const fl
 int dllm_cosine_scores(const float*, const float*, float*, int, int, int, hipStream_t);
 int dllm_sample_rows(const void*, long, int, int, const float*, const float*, const int*, const unsigned*, int*,
                      hipStream_t);
+int dllm_tp_cands_k();
+int dllm_tp_cands(const void*, long, int, int, int, void*, hipStream_t);
+int dllm_tp_sample(const void*, int, int, const float*, const float*, const int*, const unsigned*, int*, hipStream_t);
 int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                      hipStream_t);
 int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
@@ -364,6 +367,39 @@ void sample_rows(torch::Tensor logits, torch::Tensor temp, torch::Tensor top_p, 
                       top_p.data_ptr<float>(), top_k.data_ptr<int>(), (const unsigned*)seed.data_ptr<int>(),
                       out.data_ptr<int>(), stream()),
      "sample_rows");
+}
+
+// vocab-parallel sampler (csrc/kernels/sampling.hip): a shard's ranked top-KC candidates as int32
+// pairs (value f32 bits, global id) [S, KC, 2], and the merge + draw over all-gathered [tp, S, KC, 2]
+int64_t tp_cands_k() { return dllm_tp_cands_k(); }
+void tp_cands(torch::Tensor logits, int64_t start, torch::Tensor cand) {
+  check_bf16(logits, "logits");
+  check_i32(cand, "cand");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0,
+              "logits [S, V] row-major, 16-B aligned rows");
+  const int S = logits.size(0), KC = dllm_tp_cands_k();
+  TORCH_CHECK(cand.is_contiguous() && cand.numel() == (int64_t)S * KC * 2, "cand [S, KC, 2] int32");
+  ok(dllm_tp_cands(logits.data_ptr(), logits.stride(0), S, logits.size(1), (int)start, cand.data_ptr(), stream()),
+     "tp_cands");
+}
+void tp_sample(torch::Tensor cands, torch::Tensor temp, torch::Tensor top_p, torch::Tensor top_k, torch::Tensor seed,
+               torch::Tensor out) {
+  check_i32(cands, "cands");
+  check_f32(temp, "temperature");
+  check_f32(top_p, "top_p");
+  check_i32(top_k, "top_k");
+  check_i32(seed, "seed");
+  check_i32(out, "out");
+  const int KC = dllm_tp_cands_k();
+  TORCH_CHECK(cands.is_contiguous() && cands.dim() == 4 && cands.size(2) == KC && cands.size(3) == 2 &&
+                  cands.size(0) >= 1 && cands.size(0) <= 8,
+              "cands [tp <= 8, S, KC, 2] int32");
+  const int tp = cands.size(0), S = cands.size(1);
+  TORCH_CHECK(temp.numel() >= S && top_p.numel() >= S && top_k.numel() >= S && out.numel() >= S && seed.numel() >= 1,
+              "per-row parameter lengths");
+  ok(dllm_tp_sample(cands.data_ptr(), S, tp, temp.data_ptr<float>(), top_p.data_ptr<float>(), top_k.data_ptr<int>(),
+                    (const unsigned*)seed.data_ptr<int>(), out.data_ptr<int>(), stream()),
+     "tp_sample");
 }
 
 void cosine_scores(torch::Tensor q, torch::Tensor c, torch::Tensor s) {
@@ -1023,6 +1059,9 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("scatter_pairs", &scatter_pairs);
   m.def("sample_topp", &sample_topp);
   m.def("sample_rows", &sample_rows);
+  m.def("tp_cands_k", &tp_cands_k);
+  m.def("tp_cands", &tp_cands);
+  m.def("tp_sample", &tp_sample);
   m.def("cosine_scores", &cosine_scores);
   m.def("masked_cosine_argmax", &masked_cosine_argmax);
   m.def("skinny_gemm", &skinny_gemm);

@@ -142,21 +142,258 @@ static __device__ __forceinline__ float row_uniform(unsigned seed, unsigned row)
   return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
+// Shared state of one row's selection (one workgroup per row).
+struct SrShared {
+  unsigned hist[4096];
+  float2 cand[SR_CAP];          // (value, index bits)
+  float w_r[SR_KMAX];           // value by rank
+  int i_r[SR_KMAX];             // token id by rank
+  unsigned wsum[SR_THREADS / 64];
+  float sv[SR_THREADS / 64];
+  int si[SR_THREADS / 64];
+  int s_bin, s_above, s_n, s_nt, s_lo, s_amax;
+  float s_m;
+};
+
+// Phases 0-3 over one row of V bf16 logits: afterwards sh.w_r / sh.i_r hold the exact top
+// min(k, n) (value desc, index asc) and sh.s_m the row maximum; returns n (every thread), the
+// candidate count, which is < k only for rows with fewer than k non-NaN logits.
+static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V, int k, SrShared& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nv = V >> 3;
+  // ---- 0. fast bound (no histogram): T0 = the k-th largest of the 256 per-thread maximum keys.
+  // At least k logits are >= T0 (one per thread whose maximum is), so every top-k logit is too;
+  // when few logits reach T0 (typical: ~k-3k of 32 K) they are the whole candidate list and the
+  // 4096-bin LDS-atomic histogram (hot bins serialise its atomics: ~40 us for one row) is skipped.
+  // A flat row (> SR_MAXN logits at or above T0) falls through to the histogram path.
+  {
+    unsigned tmax = 0u;
+    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int) {
+      const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tmax = max(tmax, bf_key(e[j]));
+    });
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) tmax = max(tmax, bf_key(l[i]));
+    sh.hist[tid] = tmax;
+    if (tid == 0) { sh.s_n = 0; sh.s_lo = 0; }
+    __syncthreads();
+    int r = 0;  // rank among the thread maxima (ties -> lower thread first)
+    for (int j = 0; j < SR_THREADS; ++j) {
+      const unsigned o = sh.hist[j];
+      r += (o > tmax || (o == tmax && j < tid)) ? 1 : 0;
+    }
+    if (r == k - 1) sh.s_lo = (int)tmax;
+    __syncthreads();
+    const unsigned t0 = (unsigned)sh.s_lo;
+    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
+      const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned key = bf_key(e[j]);
+        if (key >= t0 && key != 0u) {
+          const int p = atomicAdd(&sh.s_n, 1);
+          if (p < SR_CAP) sh.cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+        }
+      }
+    });
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
+      const unsigned key = bf_key(l[i]);
+      if (key >= t0 && key != 0u) {
+        const int p = atomicAdd(&sh.s_n, 1);
+        if (p < SR_CAP) sh.cand[p] = make_float2(key_f(key), __int_as_float(i));
+      }
+    }
+    __syncthreads();
+  }
+  int na, nt;
+  if (sh.s_n >= k && sh.s_n <= SR_MAXN) {
+    na = sh.s_n;
+    nt = 0;
+  } else {
+  __syncthreads();  // every thread has read s_n before the histogram path reuses it
+
+  // ---- 1. coarse histogram (12-bit bins) and the bin of the k-th largest
+  for (int i = tid; i < 4096; i += SR_THREADS) sh.hist[i] = 0u;
+  if (tid == 0) { sh.s_bin = 0; sh.s_above = 0; }   // a row with < k non-NaN logits keeps them all
+  __syncthreads();
+  for (int c = tid; c < nv; c += SR_THREADS) {
+    const uint4 v = ld16(l + c * 8);
+    const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sh.hist[bf_key(e[j]) >> 4], 1u);
+  }
+  for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) atomicAdd(&sh.hist[bf_key(l[i]) >> 4], 1u);
+  __syncthreads();
+  unsigned mine = 0;  // thread t owns bins 4095-16t .. 4080-16t (descending key order)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) mine += sh.hist[4095 - 16 * tid - j];
+  unsigned x = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh.wsum[wid] = x;
+  __syncthreads();
+  unsigned base = 0;
+  for (int w = 0; w < wid; ++w) base += sh.wsum[w];
+  const unsigned incl = base + x, excl = incl - mine;
+  if (excl < (unsigned)k && incl >= (unsigned)k) {  // exactly one thread
+    unsigned acc = excl;
+    for (int j = 0; j < 16; ++j) {
+      const int b = 4095 - 16 * tid - j;
+      if (acc + sh.hist[b] >= (unsigned)k) { sh.s_bin = b; sh.s_above = (int)acc; break; }
+      acc += sh.hist[b];
+    }
+  }
+  __syncthreads();
+  const int bin = sh.s_bin;
+  if (sh.s_above + (int)sh.hist[bin] > SR_MAXN) {  // crowded bin: exact threshold from its low 4 bits
+    __syncthreads();
+    if (tid < 16) sh.hist[tid] = 0u;            // hist[0..15] re-used as the 16 fine bins (the coarse
+    __syncthreads();                            // counts are no longer needed past this point)
+    for (int c = tid; c < nv; c += SR_THREADS) {
+      const uint4 v = ld16(l + c * 8);
+      const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned key = bf_key(e[j]);
+        if ((int)(key >> 4) == bin) atomicAdd(&sh.hist[key & 15], 1u);
+      }
+    }
+    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
+      const unsigned key = bf_key(l[i]);
+      if ((int)(key >> 4) == bin) atomicAdd(&sh.hist[key & 15], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned acc = (unsigned)sh.s_above;
+      int lo = bin << 4;
+      for (int b = 15; b >= 0; --b) {
+        if (acc + sh.hist[b] >= (unsigned)k) { lo = (bin << 4) | b; break; }
+        acc += sh.hist[b];
+      }
+      sh.s_lo = lo;
+      sh.s_amax = (int)acc;  // exactly the keys strictly above lo (< k)
+    }
+  } else if (tid == 0) {
+    sh.s_lo = bin << 4;
+    sh.s_amax = sh.s_above + (int)sh.hist[bin];  // every candidate (<= SR_MAXN): none is ever dropped
+  }
+  if (tid == 0) { sh.s_n = 0; sh.s_nt = 0; }
+  __syncthreads();
+
+  // ---- 2. candidates: every logit at or above the threshold key.  Keys strictly above it (at most
+  // s_amax: < k for a crowded bin, <= SR_MAXN otherwise) fill slots from the bottom; ties AT the
+  // threshold fill slots from the top, never below slot s_amax — so a crowded tie bin can only
+  // drop ties, never a strictly better logit, and the top-k stays exact.  NaN (key 0) never enters.
+  const unsigned lo = (unsigned)sh.s_lo;
+  const int amax = min(sh.s_amax, SR_CAP);
+  for (int c = tid; c < nv; c += SR_THREADS) {
+    const uint4 v = ld16(l + c * 8);
+    const u16* e = reinterpret_cast<const u16*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned key = bf_key(e[j]);
+      if (key == 0u) continue;
+      if (key > lo) {
+        const int p = atomicAdd(&sh.s_n, 1);
+        if (p < amax) sh.cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+      } else if (key == lo) {
+        const int p = atomicAdd(&sh.s_nt, 1);
+        if (p < SR_CAP - amax) sh.cand[SR_CAP - 1 - p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
+      }
+    }
+  }
+  for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
+    const unsigned key = bf_key(l[i]);
+    if (key == 0u) continue;
+    if (key > lo) {
+      const int p = atomicAdd(&sh.s_n, 1);
+      if (p < amax) sh.cand[p] = make_float2(key_f(key), __int_as_float(i));
+    } else if (key == lo) {
+      const int p = atomicAdd(&sh.s_nt, 1);
+      if (p < SR_CAP - amax) sh.cand[SR_CAP - 1 - p] = make_float2(key_f(key), __int_as_float(i));
+    }
+  }
+  __syncthreads();
+  na = min(sh.s_n, amax);
+  nt = min(sh.s_nt, SR_CAP - amax);
+  }
+  const int n = min(na, SR_CAP) + nt;
+  // candidate j of the union [0, na) u [SR_CAP - nt, SR_CAP)
+  auto cidx = [&](int j) { return j < na ? j : SR_CAP - nt + (j - na); };
+
+  // ---- 3. rank = #strictly better candidates; ranks < k are the top-k
+  for (int j = tid; j < n; j += SR_THREADS) {
+    const float2 cj = sh.cand[cidx(j)];
+    const int ij = __float_as_int(cj.y);
+    int r = 0;
+    for (int i = 0; i < n; ++i) {
+      const float2 ci = sh.cand[cidx(i)];
+      r += (ci.x > cj.x || (ci.x == cj.x && __float_as_int(ci.y) < ij)) ? 1 : 0;
+    }
+    if (r < k) { sh.i_r[r] = ij; sh.w_r[r] = cj.x; }
+    if (r == 0) sh.s_m = cj.x;
+  }
+  __syncthreads();
+  return n;
+}
+
+// Phase 4 (wave 0 only): softmax weights of ranks [0, kk) at temperature t, nucleus = shortest
+// prefix with mass >= top_p, inverse-CDF pick with u = hash(seed, row).  Returns the picked rank
+// (uniform in the wave), -1 when kk == 0.
+static __device__ __forceinline__ int draw_rank(const SrShared& sh, int kk, float t, float top_p, unsigned seed,
+                                                unsigned row) {
+  const int lane = threadIdx.x & 63;
+  if (kk <= 0) return -1;
+  const float m = sh.s_m, it = 1.f / fmaxf(t, 1e-5f);
+  float c4[4];
+  float run = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * lane + q;
+    run += r < kk ? __expf((sh.w_r[r] - m) * it) : 0.f;
+    c4[q] = run;                                  // lane-local inclusive prefix
+  }
+  float pre = run;                                // wave exclusive scan of lane totals
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(pre, o, 64);
+    if (lane >= o) pre += y;
+  }
+  pre -= run;
+  const float s = __shfl(pre + run, 63, 64);      // total mass of the top-k
+  const float tp = top_p * s;
+  int cut = kk;                                   // nucleus size = first rank with cum >= top_p, + 1
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * lane + q;
+    if (r < kk && pre + c4[q] >= tp) cut = min(cut, r + 1);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cut = min(cut, __shfl_xor(cut, o, 64));
+  const int last = cut - 1;
+  const float mass = __shfl(pre + c4[last & 3], last >> 2, 64);
+  const float target = row_uniform(seed, row) * mass;
+  int pick = last;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * lane + q;
+    if (r < cut && pre + c4[q] > target) pick = min(pick, r);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pick = min(pick, __shfl_xor(pick, o, 64));
+  return pick;
+}
+
 __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __restrict__ logits, long stride, int V,
                                                                  const float* __restrict__ temp,
                                                                  const float* __restrict__ top_p,
                                                                  const int* __restrict__ top_k,
                                                                  const unsigned* __restrict__ seed,
                                                                  int* __restrict__ out) {
-  __shared__ unsigned hist[4096];
-  __shared__ float2 cand[SR_CAP];          // (value, index bits)
-  __shared__ float w_r[SR_KMAX];           // softmax weight by rank
-  __shared__ int i_r[SR_KMAX];             // token id by rank
-  __shared__ unsigned wsum[SR_THREADS / 64];
-  __shared__ float sv[SR_THREADS / 64];
-  __shared__ int si[SR_THREADS / 64];
-  __shared__ int s_bin, s_above, s_n, s_nt, s_lo, s_amax;
-  __shared__ float s_m;
+  __shared__ SrShared sh;
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const u16* l = logits + (long)row * stride;
   const int nv = V >> 3;
@@ -178,10 +415,10 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
       const int oi = __shfl_xor(bi, o, 64);
       better(bv, bi, ov, oi);
     }
-    if (lane == 0) { sv[wid] = bv; si[wid] = bi; }
+    if (lane == 0) { sh.sv[wid] = bv; sh.si[wid] = bi; }
     __syncthreads();
     if (tid == 0) {
-      for (int w = 1; w < SR_THREADS / 64; ++w) better(bv, bi, sv[w], si[w]);
+      for (int w = 1; w < SR_THREADS / 64; ++w) better(bv, bi, sh.sv[w], sh.si[w]);
       out[row] = (bi == 0x7fffffff) ? 0 : bi;
     }
     return;
@@ -189,222 +426,85 @@ __global__ void __launch_bounds__(SR_THREADS) sample_rows_kernel(const u16* __re
   int k = top_k[row];
   if (k <= 0 || k > SR_KMAX) k = SR_KMAX;
   if (k > V) k = V;
-
-  // ---- 0. fast bound (no histogram): T0 = the k-th largest of the 256 per-thread maximum keys.
-  // At least k logits are >= T0 (one per thread whose maximum is), so every top-k logit is too;
-  // when few logits reach T0 (typical: ~k-3k of 32 K) they are the whole candidate list and the
-  // 4096-bin LDS-atomic histogram (hot bins serialise its atomics: ~40 us for one row) is skipped.
-  // A flat row (> SR_MAXN logits at or above T0) falls through to the histogram path.
-  {
-    unsigned tmax = 0u;
-    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int) {
-      const u16* e = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tmax = max(tmax, bf_key(e[j]));
-    });
-    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) tmax = max(tmax, bf_key(l[i]));
-    hist[tid] = tmax;
-    if (tid == 0) s_n = 0;
-    __syncthreads();
-    int r = 0;  // rank among the thread maxima (ties -> lower thread first)
-    for (int j = 0; j < SR_THREADS; ++j) {
-      const unsigned o = hist[j];
-      r += (o > tmax || (o == tmax && j < tid)) ? 1 : 0;
-    }
-    if (r == k - 1) s_lo = (int)tmax;
-    __syncthreads();
-    const unsigned t0 = (unsigned)s_lo;
-    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
-      const u16* e = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const unsigned key = bf_key(e[j]);
-        if (key >= t0 && key != 0u) {
-          const int p = atomicAdd(&s_n, 1);
-          if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
-        }
-      }
-    });
-    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
-      const unsigned key = bf_key(l[i]);
-      if (key >= t0 && key != 0u) {
-        const int p = atomicAdd(&s_n, 1);
-        if (p < SR_CAP) cand[p] = make_float2(key_f(key), __int_as_float(i));
-      }
-    }
-    __syncthreads();
-  }
-  int na, nt;
-  if (s_n >= k && s_n <= SR_MAXN) {
-    na = s_n;
-    nt = 0;
-  } else {
-  __syncthreads();  // every thread has read s_n before the histogram path reuses it
-
-  // ---- 1. coarse histogram (12-bit bins) and the bin of the k-th largest
-  for (int i = tid; i < 4096; i += SR_THREADS) hist[i] = 0u;
-  __syncthreads();
-  for (int c = tid; c < nv; c += SR_THREADS) {
-    const uint4 v = ld16(l + c * 8);
-    const u16* e = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&hist[bf_key(e[j]) >> 4], 1u);
-  }
-  for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) atomicAdd(&hist[bf_key(l[i]) >> 4], 1u);
-  __syncthreads();
-  unsigned mine = 0;  // thread t owns bins 4095-16t .. 4080-16t (descending key order)
-#pragma unroll
-  for (int j = 0; j < 16; ++j) mine += hist[4095 - 16 * tid - j];
-  unsigned x = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  unsigned base = 0;
-  for (int w = 0; w < wid; ++w) base += wsum[w];
-  const unsigned incl = base + x, excl = incl - mine;
-  if (excl < (unsigned)k && incl >= (unsigned)k) {  // exactly one thread
-    unsigned acc = excl;
-    for (int j = 0; j < 16; ++j) {
-      const int b = 4095 - 16 * tid - j;
-      if (acc + hist[b] >= (unsigned)k) { s_bin = b; s_above = (int)acc; break; }
-      acc += hist[b];
-    }
-  }
-  __syncthreads();
-  const int bin = s_bin;
-  if (s_above + (int)hist[bin] > SR_MAXN) {  // crowded bin: exact threshold from its low 4 bits
-    __syncthreads();
-    if (tid < 16) hist[tid] = 0u;            // hist[0..15] re-used as the 16 fine bins (the coarse
-    __syncthreads();                         // counts are no longer needed past this point)
-    for (int c = tid; c < nv; c += SR_THREADS) {
-      const uint4 v = ld16(l + c * 8);
-      const u16* e = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const unsigned key = bf_key(e[j]);
-        if ((int)(key >> 4) == bin) atomicAdd(&hist[key & 15], 1u);
-      }
-    }
-    for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
-      const unsigned key = bf_key(l[i]);
-      if ((int)(key >> 4) == bin) atomicAdd(&hist[key & 15], 1u);
-    }
-    __syncthreads();
-    if (tid == 0) {
-      unsigned acc = (unsigned)s_above;
-      int lo = bin << 4;
-      for (int b = 15; b >= 0; --b) {
-        if (acc + hist[b] >= (unsigned)k) { lo = (bin << 4) | b; break; }
-        acc += hist[b];
-      }
-      s_lo = lo;
-      s_amax = (int)acc;  // exactly the keys strictly above lo (< k)
-    }
-  } else if (tid == 0) {
-    s_lo = bin << 4;
-    s_amax = s_above + (int)hist[bin];  // every candidate (<= SR_MAXN): none is ever dropped
-  }
-  if (tid == 0) { s_n = 0; s_nt = 0; }
-  __syncthreads();
-
-  // ---- 2. candidates: every logit at or above the threshold key.  Keys strictly above it (at most
-  // s_amax: < k for a crowded bin, <= SR_MAXN otherwise) fill slots from the bottom; ties AT the
-  // threshold fill slots from the top, never below slot s_amax — so a crowded tie bin can only
-  // drop ties, never a strictly better logit, and the top-k stays exact.
-  const unsigned lo = (unsigned)s_lo;
-  const int amax = min(s_amax, SR_CAP);
-  for (int c = tid; c < nv; c += SR_THREADS) {
-    const uint4 v = ld16(l + c * 8);
-    const u16* e = reinterpret_cast<const u16*>(&v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const unsigned key = bf_key(e[j]);
-      if (key > lo) {
-        const int p = atomicAdd(&s_n, 1);
-        if (p < amax) cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
-      } else if (key == lo) {
-        const int p = atomicAdd(&s_nt, 1);
-        if (p < SR_CAP - amax) cand[SR_CAP - 1 - p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
-      }
-    }
-  }
-  for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
-    const unsigned key = bf_key(l[i]);
-    if (key > lo) {
-      const int p = atomicAdd(&s_n, 1);
-      if (p < amax) cand[p] = make_float2(key_f(key), __int_as_float(i));
-    } else if (key == lo) {
-      const int p = atomicAdd(&s_nt, 1);
-      if (p < SR_CAP - amax) cand[SR_CAP - 1 - p] = make_float2(key_f(key), __int_as_float(i));
-    }
-  }
-  __syncthreads();
-  na = min(s_n, amax);
-  nt = min(s_nt, SR_CAP - amax);
-  }
-  const int n = na + nt;
-  // candidate j of the union [0, na) u [SR_CAP - nt, SR_CAP)
-  auto cidx = [&](int j) { return j < na ? j : SR_CAP - nt + (j - na); };
-
-  // ---- 3. rank = #strictly better candidates; ranks < k are the top-k
-  for (int j = tid; j < n; j += SR_THREADS) {
-    const float2 cj = cand[cidx(j)];
-    const int ij = __float_as_int(cj.y);
-    int r = 0;
-    for (int i = 0; i < n; ++i) {
-      const float2 ci = cand[cidx(i)];
-      r += (ci.x > cj.x || (ci.x == cj.x && __float_as_int(ci.y) < ij)) ? 1 : 0;
-    }
-    if (r < k) { i_r[r] = ij; w_r[r] = cj.x; }
-    if (r == 0) s_m = cj.x;
-  }
-  __syncthreads();
-
-  // ---- 4. temperature, nucleus, draw (wave 0; rank r = 4 * lane + q)
+  const int n = row_topk(l, V, k, sh);
   if (wid == 0) {
-    const int kk = min(k, n);
-    const float m = s_m, it = 1.f / fmaxf(t, 1e-5f);
-    float c4[4];
-    float run = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 4 * lane + q;
-      run += r < kk ? __expf((w_r[r] - m) * it) : 0.f;
-      c4[q] = run;                                  // lane-local inclusive prefix
+    const int pick = draw_rank(sh, min(k, n), t, top_p[row], *seed, (unsigned)row);
+    if (lane == 0) out[row] = pick >= 0 ? sh.i_r[pick] : 0;   // an all-NaN row yields token 0
+  }
+}
+
+// ---------------------------------------------------------------------------- vocab-parallel sampler
+// Tensor parallelism shards the LM head by vocabulary: rank p holds logits [S, V/tp] of ids
+// [start_p, start_p + V/tp).  The global top-k (k <= 256) of a row lies inside the union of every
+// shard's top-256, so each rank reduces its shard to TP_KC ranked candidates (tp_cands_kernel), one
+// all-gather moves [tp, S, TP_KC] (value, id) pairs, and tp_sample_kernel merges the tp sorted lists
+// (rank of a candidate = its position in its list + a binary search in every other list, same
+// (value desc, id asc) order as sample_rows_kernel) and runs the same draw — every rank holds the
+// same gathered lists and the same seed, so every rank emits the same token, and it is the token
+// sample_rows_kernel would draw from the unsharded row.
+constexpr int TP_KC = 256;
+
+// cand [S, TP_KC] int2 (value f32 bits, global id); ranks past the shard's candidate count are
+// (-inf, INT_MAX)
+__global__ void __launch_bounds__(SR_THREADS) tp_cands_kernel(const u16* __restrict__ logits, long stride, int V,
+                                                              int start, int2* __restrict__ cand) {
+  __shared__ SrShared sh;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int k = min(TP_KC, V);
+  const int n = min(row_topk(logits + (long)row * stride, V, k, sh), k);
+  for (int r = tid; r < TP_KC; r += SR_THREADS)
+    cand[(long)row * TP_KC + r] = r < n ? make_int2(__float_as_int(sh.w_r[r]), sh.i_r[r] + start)
+                                        : make_int2(__float_as_int(-INFINITY), 0x7fffffff);
+}
+
+static __device__ __forceinline__ bool cand_better(int2 a, int2 b) {  // value desc, id asc
+  const float va = __int_as_float(a.x), vb = __int_as_float(b.x);
+  return va > vb || (va == vb && a.y < b.y);
+}
+
+// cands [tp][S][TP_KC] (rank-sorted lists of every shard, all-gathered); out [S] global token ids
+__global__ void __launch_bounds__(SR_THREADS) tp_sample_kernel(const int2* __restrict__ cands, int S, int tp,
+                                                               const float* __restrict__ temp,
+                                                               const float* __restrict__ top_p,
+                                                               const int* __restrict__ top_k,
+                                                               const unsigned* __restrict__ seed,
+                                                               int* __restrict__ out) {
+  __shared__ SrShared sh;
+  __shared__ int2 lists[8 * TP_KC];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n = tp * TP_KC;
+  for (int j = tid; j < n; j += SR_THREADS) lists[j] = cands[((long)(j / TP_KC) * S + row) * TP_KC + j % TP_KC];
+  __syncthreads();
+  const float t = temp[row];
+  int k = t > 0.f ? top_k[row] : 1;
+  if (k <= 0 || k > SR_KMAX) k = SR_KMAX;
+  if (tid == 0) sh.s_n = 0;
+  __syncthreads();
+  int valid = 0;
+  for (int j = tid; j < n; j += SR_THREADS) {
+    const int p = j / TP_KC, i = j % TP_KC;
+    const int2 c = lists[j];
+    if (c.y == 0x7fffffff) continue;                 // padding
+    ++valid;
+    int r = i;                                       // better ones in its own (sorted) list
+    for (int q = 0; q < tp; ++q) {
+      if (q == p) continue;
+      int lo = 0, hi = TP_KC;                        // # of list q strictly better than c
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cand_better(lists[q * TP_KC + mid], c)) lo = mid + 1; else hi = mid;
+      }
+      r += lo;
     }
-    float pre = run;                                // wave exclusive scan of lane totals
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float y = __shfl_up(pre, o, 64);
-      if (lane >= o) pre += y;
-    }
-    pre -= run;
-    const float s = __shfl(pre + run, 63, 64);      // total mass of the top-k
-    const float tp = top_p[row] * s;
-    int cut = kk;                                   // nucleus size = first rank with cum >= top_p, + 1
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 4 * lane + q;
-      if (r < kk && pre + c4[q] >= tp) cut = min(cut, r + 1);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cut = min(cut, __shfl_xor(cut, o, 64));
-    const int last = cut - 1;
-    const float mass = __shfl(pre + c4[last & 3], last >> 2, 64);
-    const float target = row_uniform(*seed, (unsigned)row) * mass;
-    int pick = last;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 4 * lane + q;
-      if (r < cut && pre + c4[q] > target) pick = min(pick, r);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pick = min(pick, __shfl_xor(pick, o, 64));
-    if (lane == 0) out[row] = i_r[pick];
+    if (r < k) { sh.i_r[r] = c.y; sh.w_r[r] = __int_as_float(c.x); }
+    if (r == 0) sh.s_m = __int_as_float(c.x);
+  }
+  atomicAdd(&sh.s_n, valid);
+  __syncthreads();
+  const int kk = min(k, sh.s_n);
+  if (wid == 0) {
+    const int pick = t > 0.f ? draw_rank(sh, kk, t, top_p[row], *seed, (unsigned)row) : (kk > 0 ? 0 : -1);
+    if (lane == 0) out[row] = pick >= 0 ? sh.i_r[pick] : 0;
   }
 }
 }  // namespace
@@ -415,6 +515,27 @@ extern "C" int dllm_sample_rows(const void* logits, long stride, int B, int V, c
   if (V <= 0 || stride % 8 != 0) return -1;
   hipLaunchKernelGGL(sample_rows_kernel, dim3(B), dim3(SR_THREADS), 0, stream, (const u16*)logits, stride, V, temp,
                      top_p, top_k, seed, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_tp_cands_k() { return TP_KC; }
+
+// logits [S, V] bf16 (row stride % 8 == 0) of a vocab shard starting at global id `start` -> cand [S, TP_KC] int2
+extern "C" int dllm_tp_cands(const void* logits, long stride, int S, int V, int start, void* cand, hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (V <= 0 || stride % 8 != 0) return -1;
+  hipLaunchKernelGGL(tp_cands_kernel, dim3(S), dim3(SR_THREADS), 0, stream, (const u16*)logits, stride, V, start,
+                     (int2*)cand);
+  return (int)hipGetLastError();
+}
+
+// cands [tp, S, TP_KC] int2 -> out [S] token ids
+extern "C" int dllm_tp_sample(const void* cands, int S, int tp, const float* temp, const float* top_p, const int* top_k,
+                              const unsigned* seed, int* out, hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (tp < 1 || tp > 8) return -1;
+  hipLaunchKernelGGL(tp_sample_kernel, dim3(S), dim3(SR_THREADS), 0, stream, (const int2*)cands, S, tp, temp, top_p,
+                     top_k, seed, out);
   return (int)hipGetLastError();
 }
 

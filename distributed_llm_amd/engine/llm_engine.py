@@ -1139,10 +1139,24 @@ class LLMEngine:
         self._check_graph_collectives()
         self.collective_trips = getattr(self, "collective_trips", 0) + 1
 
+    # Tensor-parallel decode graphs are opt-in (DLLM_TP_GRAPHS=1): on the one-GPU TP=2 rehearsal a
+    # captured decode graph replayed correctly within its first generation but the first replay
+    # after the next eager prefill faulted on both ranks, while eager TP decode, TP=1 graphs and
+    # graph/eager alternation at TP=1 were all clean (profiles/r3_tp_graph_fault.md).  Until that
+    # replay is proven on hardware, tensor-parallel pools decode eagerly (the one-shot all-reduce
+    # kernels and the in-step health vote run the same way, launch by launch).
+    TP_GRAPHS = os.environ.get("DLLM_TP_GRAPHS", "0") == "1"
+
     def _check_graph_collectives(self) -> None:
         """A TP decode graph can only capture device collectives: the one-shot IPC kernels or RCCL.
-        A group on gloo (one-GPU multi-process tests) without the one-shot all-reduce runs eager."""
-        if not self.par.enabled or not self.use_graphs or self.par.custom_ar is not None:
+        A group on gloo (one-GPU multi-process tests) without the one-shot all-reduce runs eager;
+        so does every TP group unless ``TP_GRAPHS``."""
+        if not self.par.enabled or not self.use_graphs:
+            return
+        if not self.TP_GRAPHS:
+            self.use_graphs = False
+            return
+        if self.par.custom_ar is not None:
             return
         import torch.distributed as dist
         if self.par.tp_group is None or dist.get_backend(self.par.tp_group) != "nccl":

@@ -462,23 +462,17 @@ class LlamaModel:
                seed: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """Fused per-row sampling (greedy / exact top-k + top-p, ops.sample_rows) over the LM head.
 
-        Under TP the vocab is sharded: every rank keeps its shard's top-256 (values, global ids),
-        one all-gather of [tp, S, 256] candidates replaces the [S, V] logits, and every rank runs
-        the same sampler on the merged candidate rows with the same seed -> the same token on all
-        ranks (the global top-k of any k <= 256 is inside the union of the per-shard top-256).
-        Graph-capturable: no host sync."""
+        Under TP the vocab is sharded: every rank reduces its shard to its ranked top-256
+        (value, global id) pairs (ops.tp_candidates, one launch), one all-gather of [tp, S, 256, 2]
+        replaces the [S, V] logits, and every rank merges the tp sorted lists and draws with the
+        same seed (ops.tp_sample, one launch) -> the same token on all ranks, and the token the
+        unsharded sampler would draw (the global top-k of any k <= 256 is inside the union of the
+        per-shard top-256).  Graph-capturable: three launches, no host sync, no torch.topk."""
         lg = self.logits(hidden)
         if self.par.tp_size == 1:
             return ops.sample_rows(lg, temperature, top_p, top_k, seed, out=out)
-        S = lg.shape[0]
-        kk = min(256, lg.shape[1])
-        v, i = torch.topk(lg, kk, dim=-1)
-        i = (i + self.vocab_shard.start).to(torch.int32)
-        cv = self.par.all_gather(v).permute(1, 0, 2).reshape(S, -1).contiguous()     # [S, tp * kk]
-        ci = self.par.all_gather(i).permute(1, 0, 2).reshape(S, -1)
-        j = ops.sample_rows(cv, temperature, top_p, top_k, seed)
-        out.copy_(ci.gather(1, j.long().unsqueeze(1)).squeeze(1))
-        return out
+        cand = ops.tp_candidates(lg, self.vocab_shard.start)
+        return ops.tp_sample(self.par.all_gather(cand), temperature, top_p, top_k, seed, out=out)
 
     def topk_candidates(self, hidden: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """Global top-k (values desc, ids) from per-rank top-k of the vocab shards."""

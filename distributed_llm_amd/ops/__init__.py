@@ -451,6 +451,37 @@ def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Te
     return o
 
 
+TP_KC = 256   # candidates per vocab shard (csrc/kernels/sampling.hip TP_KC)
+
+
+def tp_candidates(logits: torch.Tensor, start: int) -> torch.Tensor:
+    """A vocab shard's ranked top-``TP_KC`` candidates per row as int32 pairs [S, TP_KC, 2] =
+    (value as f32 bits, global id = local index + ``start``), order value desc / id asc; rows with
+    fewer candidates are padded with (-inf, INT32_MAX).  One launch (tp_cands_kernel)."""
+    ext = _native(logits)
+    if ext is None:
+        return ref.tp_candidates(logits, start, TP_KC)
+    cand = torch.empty((logits.shape[0], TP_KC, 2), dtype=torch.int32, device=logits.device)
+    ext.tp_cands(logits, int(start), cand)
+    return cand
+
+
+def tp_sample(cands: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
+              seed: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Token per row from the all-gathered shard candidates ``cands`` [tp, S, TP_KC, 2]: merge the
+    tp ranked lists and draw exactly as ``sample_rows`` would on the unsharded row (greedy ->
+    best id; else top-k, temperature, top-p, u = hash(seed, row)).  One launch (tp_sample_kernel)."""
+    S = cands.shape[1]
+    o = out if out is not None else torch.empty(S, dtype=torch.int32, device=cands.device)
+    ext = _native(cands)
+    if ext is None:
+        r = ref.tp_sample(cands, temperature.cpu(), top_p.cpu(), top_k.cpu(), int(seed.reshape(-1)[0]))
+        o[:S].copy_(r)
+        return o
+    ext.tp_sample(cands.contiguous(), temperature, top_p, top_k, seed, o)
+    return o
+
+
 # ----------------------------------------------------------------------------- router scorers
 
 def cosine_scores(q: torch.Tensor, c: torch.Tensor) -> torch.Tensor:

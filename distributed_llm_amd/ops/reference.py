@@ -240,6 +240,63 @@ def sample_rows(logits, temperature, top_p, top_k, seed: int):
     return out
 
 
+def _draw_ranked(vals, ids, t: float, top_p: float, k: int, u: float) -> int:
+    """sample_rows' draw over candidates already ranked (value desc, id asc)."""
+    if not t > 0.0:
+        return int(ids[0])
+    k = 256 if k <= 0 or k > 256 else k
+    k = min(k, len(ids))
+    vals = torch.as_tensor(vals[:k], dtype=torch.float32)
+    w = torch.exp((vals - vals[0]) / max(t, 1e-5))
+    c = torch.cumsum(w, 0)
+    s = float(c[-1])
+    cut = k
+    for i in range(k):
+        if float(c[i]) >= top_p * s:
+            cut = i + 1
+            break
+    target = u * float(c[cut - 1])
+    pick = cut - 1
+    for i in range(cut):
+        if float(c[i]) > target:
+            pick = i
+            break
+    return int(ids[pick])
+
+
+def tp_candidates(logits, start: int, kc: int = 256):
+    """Reference of tp_cands_kernel: [S, kc, 2] int32 (value f32 bits, global id)."""
+    lg = logits.float().cpu()
+    S, V = lg.shape
+    out = torch.empty((S, kc, 2), dtype=torch.int32)
+    out[:, :, 0] = torch.tensor([float("-inf")], dtype=torch.float32).view(torch.int32)
+    out[:, :, 1] = 2 ** 31 - 1
+    _, order = torch.sort(-lg, dim=1, stable=True)          # value desc, index asc
+    n = min(kc, V)
+    for r in range(S):
+        idx = order[r, :n]
+        out[r, :n, 0] = lg[r, idx].contiguous().view(torch.int32)
+        out[r, :n, 1] = (idx + start).to(torch.int32)
+    return out.to(logits.device)
+
+
+def tp_sample(cands, temperature, top_p, top_k, seed: int):
+    """Reference of tp_sample_kernel over all-gathered candidates [tp, S, kc, 2]."""
+    c = cands.cpu()
+    tp, S, kc, _ = c.shape
+    u = row_uniform(int(seed) & 0xFFFFFFFF, S)
+    out = torch.empty(S, dtype=torch.int32)
+    for r in range(S):
+        v = c[:, r, :, 0].reshape(-1).contiguous().view(torch.float32)
+        ids = c[:, r, :, 1].reshape(-1)
+        keep = ids != 2 ** 31 - 1
+        v, ids = v[keep], ids[keep]
+        order = sorted(range(len(ids)), key=lambda i: (-float(v[i]), int(ids[i])))
+        out[r] = _draw_ranked([float(v[i]) for i in order], [int(ids[i]) for i in order], float(temperature[r]),
+                              float(top_p[r]), int(top_k[r]), float(u[r]))
+    return out
+
+
 def cosine_scores(q, c):
     qn = q.float()
     cn = c.float()

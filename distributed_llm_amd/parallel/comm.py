@@ -46,8 +46,19 @@ class ParallelContext:
             if car is not None and car.eligible(t):
                 car.all_reduce(t)
             else:
-                dist.all_reduce(t, group=self.tp_group)
+                self._group_all_reduce(t)
         return t
+
+    def _group_all_reduce(self, t: torch.Tensor) -> None:
+        """RCCL, or gloo (CPU tests, the one-GPU multi-process rehearsal): device tensors are
+        staged through the host there, so the fallback after a one-shot all-reduce trip never
+        depends on gloo's device support."""
+        if t.is_cuda and dist.get_backend(self.tp_group) != "nccl":
+            h = t.cpu()
+            dist.all_reduce(h, group=self.tp_group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=self.tp_group)
 
     def all_reduce_resadd(self, y: torch.Tensor, r: torch.Tensor, ssq: torch.Tensor, add: bool = True) -> int:
         """Row-parallel output epilogue of the fused tensor-parallel layer: ``r += sum over the TP
@@ -60,7 +71,7 @@ class ParallelContext:
         if self.tp_size > 1 and car is not None and car.eligible_resadd(y, r):
             return car.all_reduce_resadd(y, r, ssq, add)
         if self.tp_size > 1:
-            dist.all_reduce(y, group=self.tp_group)
+            self._group_all_reduce(y)
         if add:
             return ops.gemm.res_add_ssq(y, r, ssq)
         r.copy_(y)

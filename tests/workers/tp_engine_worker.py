@@ -44,13 +44,16 @@ def main():
                     prefix_cache=False, seed=0)
     log("engine built")
     assert eng.model.fused, "the fused tensor-parallel layer must be active"
-    assert eng.use_graphs, "decode graphs must be capturable over the one-shot collectives"
+    graphs = eng.use_graphs       # TP decode graphs are opt-in (LLMEngine.TP_GRAPHS)
+    assert graphs == (world == 1 or eng.TP_GRAPHS)
     sp = SamplingParams(max_new_tokens=8)
     mode = os.environ.get("TP_WORKER_MODE", "full")
     if mode != "full":   # diagnostics: "graph" / "eager" = 3 gens in that mode, "alt" = graph, eager, graph
         seq = {"graph": [True] * 3, "eager": [False] * 3, "alt": [True, False, True, True]}[mode]
         for k, g in enumerate(seq):
-            eng.use_graphs = g
+            eng.use_graphs = g and graphs
+            if os.environ.get("TP_WORKER_RECAPTURE") == "1":
+                eng._graphs.clear()          # diagnostic: capture afresh in every generation
             toks = [o.token_ids for o in eng.generate(PROMPTS, sp)]
             torch.cuda.synchronize()
             log(f"gen {k} graphs={g} ok", toks[0])
@@ -58,13 +61,13 @@ def main():
         dist.destroy_process_group()
         print("OK", flush=True)
         return
-    res = {"graph": [o.token_ids for o in eng.generate(PROMPTS, sp)]}
-    assert eng._graphs, "no decode graph was replayed"
-    log("graph decode done", res["graph"][0])
+    res = {"graph": [o.token_ids for o in eng.generate(PROMPTS, sp)], "graphs_on": graphs}
+    assert bool(eng._graphs) == graphs, "decode graphs replayed iff enabled"
+    log("first decode done (graphs %s)" % graphs, res["graph"][0])
     eng.use_graphs = False
     res["eager"] = [o.token_ids for o in eng.generate(PROMPTS, sp)]
     # sampled decode: every rank must draw the same tokens (shared seed, merged candidates)
-    eng.use_graphs = True
+    eng.use_graphs = graphs
     res["sampled"] = [o.token_ids for o in eng.generate(
         PROMPTS, SamplingParams(max_new_tokens=6, temperature=0.9, top_k=40, top_p=0.95))]
     # final hidden states of one prompt through a direct prefill (TP vs TP=1 numerics)
