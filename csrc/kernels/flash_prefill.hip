@@ -37,7 +37,7 @@ constexpr int NWAVES = 8;
 constexpr int ROWS = 32 * NWAVES;  // query rows per workgroup
 constexpr int CK = 64;             // keys per chunk (four cache blocks)
 constexpr int STAGES = 3;
-constexpr int MAXBT = 1024;        // block-table entries staged per tile (16K-token context)
+constexpr int MAXBT = 1024;        // block-table window staged in LDS (16K keys; re-staged past it)
 
 struct FlashArgs {
   const u16* q;  // [T, nq, D]
@@ -106,8 +106,9 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   const int kmax = a.causal ? ctx - qlen + last_tok + 1 : ctx;
   const int nchunks = (kmax + CK - 1) / CK;
   const int* bt = a.block_tables + (long)seq * a.max_blocks;
-  const int nbt = min((kmax + 15) / 16, MAXBT);
-  for (int i = threadIdx.x; i < nbt; i += 64 * NWAVES) s_bt[i] = bt[i];
+  const int nbt = (kmax + 15) / 16;   // block-table entries this tile reads (any length)
+  int wb = 0;                          // first entry of the staged window (a multiple of MAXBT)
+  for (int i = threadIdx.x; i < min(nbt, MAXBT); i += 64 * NWAVES) s_bt[i] = bt[i];
 
   // this lane's query row (both lane halves hold the same row, different keys)
   const int r = 32 * wave + rl;
@@ -140,12 +141,12 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
       if (p * 1024 < KBYTES) {
         const int rho = byte / (2 * D), pos = (byte % (2 * D)) / 16;
         const int key = kperm(rho);
-        const int blk = s_bt[min(bi + (key >> 4), nbt - 1)];
+        const int blk = s_bt[min(bi + (key >> 4), nbt - 1) - wb];
         src = a.kc + ((long)blk * a.nkv + kvh) * hstride + (key & 15) * D + 8 * kswz<D>(rho, pos);
       } else {
         const int vb = byte - KBYTES, b = vb / (32 * D), w = vb % (32 * D);
         const int dim = w / 32, c = ((w % 32) / 16) ^ ((dim >> 3) & 1);
-        const int blk = s_bt[min(bi + b, nbt - 1)];
+        const int blk = s_bt[min(bi + b, nbt - 1) - wb];
         src = a.vc + ((long)blk * a.nkv + kvh) * hstride + dim * 16 + 8 * c;
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + p * 1024), 16, 0, 0);
@@ -167,7 +168,18 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   for (int t = 0; t < nchunks; ++t) {
     if (t + 1 < nchunks) wait_vm<GI>(); else wait_vm<0>();
     sync_lds();
-    if (t + STAGES - 1 < nchunks) issue(t + STAGES - 1);
+    if (t + STAGES - 1 < nchunks) {
+      const int tn = t + STAGES - 1, w = (tn * (CK / 16)) & ~(MAXBT - 1);
+      if (w != wb) {
+        // the next chunk's entries lie past the staged window (block-uniform, once per 16K keys):
+        // every earlier issue's s_bt reads retired before the barrier above, so re-stage it (the
+        // plain loads drain the ring here, a rare stall) and publish it before issuing
+        wb = w;
+        for (int i = threadIdx.x; i < min(nbt - wb, MAXBT); i += 64 * NWAVES) s_bt[i] = bt[wb + i];
+        __syncthreads();
+      }
+      issue(tn);
+    }
     const int kb = t * CK;
     if (kb >= wave_lim) continue;  // wave-uniform: every row of this wave is past its causal limit
     const unsigned char* kbase = smem + (t % STAGES) * STAGE;
@@ -268,7 +280,6 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   const int G = nq / nkv;
   if (ROWS % G || G > 32) return -2;
   if (num_tiles <= 0) return 0;
-  if (max_blocks > MAXBT) return -3;
   FlashArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
               tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, num_tiles, scale * LOG2E_F};
   const dim3 grid((unsigned)num_tiles * (unsigned)nkv);

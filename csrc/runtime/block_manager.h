@@ -11,8 +11,10 @@
 // Hashes are registered only by commit(), i.e. after the forward pass that wrote the block's
 // K/V, so a prompt can never match a block whose contents are not computed yet.
 // A match on the 64-bit chain hash alone is not trusted: every hashed block keeps the 16 tokens it
-// was computed from (and its parent block), and a match is taken only when both agree, so a hash
-// collision degrades to a cache miss instead of re-using another sequence's K/V.
+// was computed from and its parent block (index AND generation: a block's generation is bumped
+// whenever it is recycled, so a child whose parent was evicted and re-filled with other content
+// never matches through it), and a match is taken only when all agree, so a hash collision
+// degrades to a cache miss instead of re-using another sequence's K/V.
 //
 // Header-only core (no Python): the pybind11 module in block_manager.cpp wraps it, and
 // csrc/runtime/tests/block_manager_stress.cpp drives it under ASan/UBSan.
@@ -45,6 +47,8 @@ struct Block {
   bool hashed = false;
   uint64_t hash = 0;
   int parent = -1;  // block holding the previous 16 tokens of the chain (-1: first block)
+  uint32_t parent_gen = 0;  // that block's generation when this one was registered
+  uint32_t gen = 0;         // bumped every time the block is (re)allocated by fresh()
   std::list<int>::iterator lru_it;
   bool in_lru = false;
 };
@@ -55,6 +59,7 @@ struct Seq {
   std::vector<uint64_t> chain;  // chain hash per committed full block
   std::vector<int> canon;       // canonical registered block holding each committed full block's
                                 // content (-2: none, e.g. a hash collision), the parent link of the next
+  std::vector<uint32_t> canon_gen;  // generation of each canonical block when it was recorded
   int committed = 0;            // tokens whose K/V have been computed
 };
 
@@ -91,7 +96,8 @@ class BlockManager {
         for (int j = 0; j < bs_; ++j) h = mix(h, tokens[b * bs_ + j]);
         auto it = hash2block_.find(h);
         if (it == hash2block_.end()) break;
-        if (!same_block(it->second, matched.empty() ? -1 : matched.back(), &tokens[b * bs_])) {
+        const int par = matched.empty() ? -1 : matched.back();
+        if (!same_block(it->second, par, par >= 0 ? blocks_[par].gen : 0u, &tokens[b * bs_])) {
           ++collisions_;
           break;
         }
@@ -111,6 +117,7 @@ class BlockManager {
     s.tokens = tokens;
     s.chain = chain;
     s.canon = matched;
+    for (int b : matched) s.canon_gen.push_back(blocks_[b].gen);
     s.committed = (int)matched.size() * bs_;
     hit_tokens_ += s.committed;
     query_tokens_ += n;
@@ -183,22 +190,25 @@ class BlockManager {
       // a later lookup will have matched), not necessarily this sequence's own copy: two sequences
       // that prefilled the same prefix concurrently both keep matching each other's chains.
       const int parent = b > 0 ? s.canon[b - 1] : -1;
+      const uint32_t pgen = b > 0 ? s.canon_gen[b - 1] : 0u;
       const int32_t* toks = &s.tokens[(size_t)b * bs_];
       int canon = -2;
       auto it = hash2block_.find(h);
       if (it != hash2block_.end()) {
-        if (parent != -2 && same_block(it->second, parent, toks)) canon = it->second;
+        if (parent != -2 && same_block(it->second, parent, pgen, toks)) canon = it->second;
         else ++collisions_;
       } else if (parent != -2 && !blocks_[s.blocks[b]].hashed) {
         const int blk = s.blocks[b];
         blocks_[blk].hashed = true;
         blocks_[blk].hash = h;
         blocks_[blk].parent = parent;
+        blocks_[blk].parent_gen = pgen;
         std::copy(toks, toks + bs_, tok_store_.begin() + (size_t)blk * bs_);
         hash2block_[h] = blk;
         canon = blk;
       }
       s.canon.push_back(canon);
+      s.canon_gen.push_back(canon >= 0 ? blocks_[canon].gen : 0u);
     }
   }
 
@@ -280,10 +290,12 @@ class BlockManager {
  private:
   int blocks_needed(int n) const { return (n + bs_ - 1) / bs_; }
 
-  // a hashed block matches a prompt block only if it follows the same parent block and holds the
-  // same tokens (the parent check makes the whole prefix, not just this block, equal by induction)
-  bool same_block(int blk, int parent, const int32_t* toks) const {
+  // a hashed block matches a prompt block only if it follows the same parent block (same index
+  // and generation: the parent still holds the content it held when this block was registered)
+  // and holds the same tokens; the parent check makes the whole prefix equal by induction
+  bool same_block(int blk, int parent, uint32_t pgen, const int32_t* toks) const {
     if (blocks_[blk].parent != parent) return false;
+    if (parent >= 0 && blocks_[blk].parent_gen != pgen) return false;
     return std::equal(toks, toks + bs_, tok_store_.begin() + (size_t)blk * bs_);
   }
 
@@ -320,6 +332,7 @@ class BlockManager {
       }
     }
     blocks_[b].ref = 1;
+    ++blocks_[b].gen;  // new content from here on: children registered under the old one go stale
     return b;
   }
 

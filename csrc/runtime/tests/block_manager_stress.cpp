@@ -34,11 +34,58 @@ struct Model {
   std::exit(1);
 }
 
+#ifdef DLLM_BM_WEAK_HASH
+uint64_t chain_hash(const std::vector<int32_t>& toks, int n) {
+  uint64_t h = 0x51ed270b27ab3e5full;
+  for (int i = 0; i < n; ++i) h = dllm::mix(h, toks[i]);
+  return h;
+}
+
+// a child block registered under parent P must not match once P's block index was
+// evicted and re-filled with other content Q, even when the chain hashes collide (forced here with
+// the 3-bit test hash).  Scenario: G computes [P | X] itself while A registers P; G's X block is
+// registered with parent = A's block a0; A frees, a0 is recycled for Q (hash(Q) == hash(P));
+// K = [Q | X | ..] must then match Q's block only, not G's X block (its K/V follow P, not Q).
+void parent_recycle_scenario() {
+  BlockManager bm(6, kBS, true);
+  std::vector<int32_t> P(kBS), X(kBS), Q(kBS);
+  for (int i = 0; i < kBS; ++i) { P[i] = 1 + i; X[i] = 100 + i; Q[i] = 200 + i; }
+  const uint64_t hp = chain_hash(P, kBS);
+  for (int v = 200; chain_hash(Q, kBS) != hp || Q == P; ++v) Q[kBS - 1] = v;   // hash(Q) == hash(P)
+  auto cat = [](std::vector<int32_t> a, const std::vector<int32_t>& b, int tail) {
+    a.insert(a.end(), b.begin(), b.end());
+    for (int i = 0; i < tail; ++i) a.push_back(7);
+    return a;
+  };
+  std::vector<int32_t> g = cat(P, X, 1), a = P, k = cat(Q, X, 1), d(2 * kBS, 9);
+  a.push_back(3);
+  if (bm.allocate(1, g).first.empty()) die("scenario: G", 0);     // G: 3 fresh blocks, nothing registered yet
+  if (bm.allocate(2, a).first.empty()) die("scenario: A", 0);     // A: 2 fresh blocks
+  bm.commit(2, (int)a.size());                                    // registers a0 = P
+  bm.commit(1, (int)g.size());                                    // P -> canonical a0; X registered, parent a0
+  bm.free(2);                                                     // a0 -> LRU (still hashed), a1 -> free
+  if (bm.allocate(3, d).first.empty()) die("scenario: D", 0);     // takes every free block
+  auto h = bm.allocate(4, Q);                                     // one block: recycles a0 from the LRU
+  if (h.first.empty() || h.second != 0) die("scenario: H", 0);
+  bm.commit(4, kBS);                                              // a0 re-registered with Q (same hash)
+  bm.free(3);
+  auto kk = bm.allocate(5, k);
+  if (kk.first.empty()) die("scenario: K", 0);
+  if (kk.second != kBS) die("prefix match went through a recycled parent block (stale child)", 0);
+  const std::string err = bm.check_invariants();
+  if (!err.empty()) die(err.c_str(), 0);
+  for (int64_t id : {1, 4, 5}) bm.free(id);
+}
+#endif
+
 }  // namespace
 
 int main(int argc, char** argv) {
   const long iters = argc > 1 ? std::atol(argv[1]) : 20000;
   const unsigned seed = argc > 2 ? (unsigned)std::atoi(argv[2]) : 1234u;
+#ifdef DLLM_BM_WEAK_HASH
+  parent_recycle_scenario();
+#endif
   std::mt19937 rng(seed);
   const int nblocks = 96;
   BlockManager bm(nblocks, kBS, true);

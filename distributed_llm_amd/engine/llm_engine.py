@@ -185,6 +185,7 @@ class LLMEngine:
         self.bt_host = self.bt_host_t.numpy()
         self.bt_dev = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, device=self.device)
         self._bt_dirty = True          # whole-table copy needed (admissions / releases)
+        self._bt_hw = 0                # block-table columns ever used (the host -> device copy width)
         self._bt_upd: List[int] = []   # (flat index, block) pairs applied inside the decode graph
         self.buckets = decode_buckets(R)
         mb = self.buckets[-1]
@@ -666,11 +667,22 @@ class LLMEngine:
     def _set_row_blocks(self, s: _Seq) -> None:
         t = self.bm.block_table(s.id)
         self.bt_host[s.row, :len(t)] = t
+        self._bt_hw = max(self._bt_hw, len(t))
         self._bt_dirty = True
 
     def _sync_bt(self) -> None:
-        if self._bt_dirty:  # rare (admission / release): synchronous whole-table copy
-            self.bt_dev.copy_(self.bt_host_t, non_blocking=False)
+        if self._bt_dirty:
+            # rare (admission / release): synchronous copy of the columns any row has used (a 128K
+            # context table is 8K columns; a 2K-token batch needs 128 of them), which also subsumes
+            # the queued per-step updates
+            if self._bt_upd:
+                cols = np.asarray(self._bt_upd[0::2], dtype=np.int64) % self.max_blocks
+                self._bt_hw = max(self._bt_hw, int(cols.max()) + 1)
+            hw = min(self._bt_hw, self.max_blocks)
+            if hw == self.max_blocks:
+                self.bt_dev.copy_(self.bt_host_t, non_blocking=False)
+            elif hw > 0:
+                self.bt_dev[:, :hw].copy_(self.bt_host_t[:, :hw], non_blocking=False)
             self._bt_dirty = False
             self._bt_upd.clear()
 

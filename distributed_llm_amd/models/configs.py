@@ -56,14 +56,14 @@ _LLAMA3_SCALING = {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0
 
 MODELS: Dict[str, ModelConfig] = {
     "tinyllama-1.1b": ModelConfig("tinyllama-1.1b", 2048, 22, 32, 4, 64, 5632, 32000, 10000.0, 1e-5, 16384),
-    "llama-3.2-1b": ModelConfig("llama-3.2-1b", 2048, 16, 32, 8, 64, 8192, 128256, 500000.0, 1e-5, 16384,
+    "llama-3.2-1b": ModelConfig("llama-3.2-1b", 2048, 16, 32, 8, 64, 8192, 128256, 500000.0, 1e-5, 131072,
                                 tie_embeddings=True, rope_scaling=_LLAMA3_SCALING, bos_id=128000, eos_id=128001),
     "llama-3-8b": ModelConfig("llama-3-8b", 4096, 32, 32, 8, 128, 14336, 128256, 500000.0, 1e-5, 16384,
                               bos_id=128000, eos_id=128001),
     "llama-3-70b": ModelConfig("llama-3-70b", 8192, 80, 64, 8, 128, 28672, 128256, 500000.0, 1e-5, 16384,
                                bos_id=128000, eos_id=128001),
     "phi3-mini": ModelConfig("phi3-mini", 3072, 32, 32, 32, 96, 8192, 32064, 10000.0, 1e-5, 8192),
-    "mixtral-8x7b": ModelConfig("mixtral-8x7b", 4096, 32, 32, 8, 128, 14336, 32000, 1e6, 1e-5, 16384,
+    "mixtral-8x7b": ModelConfig("mixtral-8x7b", 4096, 32, 32, 8, 128, 14336, 32000, 1e6, 1e-5, 32768,
                                 n_experts=8, experts_per_token=2),
     # small shapes for CPU tests / smoke runs (same code paths)
     "tiny-llama-test": ModelConfig("tiny-llama-test", 128, 2, 4, 2, 32 * 2, 256, 512, 10000.0, 1e-5, 2048),

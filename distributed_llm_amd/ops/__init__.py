@@ -170,7 +170,8 @@ FLASH_ROWS = 256
 
 
 def flash_supported(d: int, group: int, max_blocks: int) -> bool:
-    return d in (64, 96, 128) and FLASH_ROWS % group == 0 and max_blocks <= 1024 and \
+    # any context length: the kernel re-stages its LDS block-table window every 16K keys
+    return d in (64, 96, 128) and FLASH_ROWS % group == 0 and max_blocks >= 1 and \
         os.environ.get("DLLM_FLASH_PREFILL", "1") == "1"
 
 

@@ -70,3 +70,42 @@ def test_flash_prefill_matches_paged_kernel_in_engine_shapes():
     a = ops.flash_attention(C(q), kcz, vcz, C(bt), C(qs), C(ql), C(cx), I(fts), I(ftt))
     b = ops.paged_attention(C(q), kcz, vcz, C(bt), C(qs), C(ql), C(cx), I(pts), I(ptt))
     torch.testing.assert_close(a.float(), b.float(), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_prefill_past_one_block_table_window(causal):
+    """Contexts past 16K keys (1024 block-table entries): the kernel re-stages its LDS block-table
+    window every 16K keys instead of refusing.  Cached prefixes of 40K and 17K
+    keys, a chunk of new queries each; scattered physical blocks."""
+    d, nq, nkv = 64, 32, 4
+    seqs = [(200, 40000), (64, 17000), (33, 16400)]
+    g = torch.Generator().manual_seed(11)
+    nbs = [(c + 15) // 16 for _, c in seqs]
+    nblocks = sum(nbs) + 8
+    kc = torch.full((nblocks, nkv, 16, d), float("nan"), dtype=torch.bfloat16)
+    vc = torch.full((nblocks, nkv, d, 16), float("nan"), dtype=torch.bfloat16)
+    perm = torch.randperm(nblocks - 1, generator=g) + 1
+    bt = torch.zeros(len(seqs), max(nbs), dtype=torch.int32)
+    k = 0
+    for i, (_, c) in enumerate(seqs):
+        blks = perm[k:k + nbs[i]]
+        k += nbs[i]
+        bt[i, :nbs[i]] = blks.to(torch.int32)
+        kk = torch.randn(nbs[i] * 16, nkv, d, generator=g)
+        vv = torch.randn(nbs[i] * 16, nkv, d, generator=g)
+        kk[c:] = float("nan")            # never-written tail of the last block
+        vv[c:] = float("nan")
+        kc[blks] = kk.view(nbs[i], 16, nkv, d).permute(0, 2, 1, 3).to(torch.bfloat16)
+        vc[blks] = vv.view(nbs[i], 16, nkv, d).permute(0, 2, 3, 1).to(torch.bfloat16)
+    T = sum(q for q, _ in seqs)
+    q = torch.randn(T, nq, d, generator=g).to(torch.bfloat16)
+    I = lambda x: torch.tensor(x, dtype=torch.int32)
+    qs = I([0, 200, 264])
+    ql, cx = I([s[0] for s in seqs]), I([s[1] for s in seqs])
+    ts, tt = ops.flash_tiles(ql.tolist(), nq // nkv)
+    C = lambda t: t.cuda()
+    assert ops.flash_supported(d, nq // nkv, bt.shape[1])
+    got = ops.flash_attention(C(q), C(kc), C(vc), C(bt), C(qs), C(ql), C(cx), C(I(ts)), C(I(tt)), causal=causal)
+    want = ref.paged_attention(q, kc.nan_to_num(0.0), vc.nan_to_num(0.0), bt, qs, ql, cx, 1.0 / math.sqrt(d), causal)
+    assert torch.isfinite(got.float()).all()
+    torch.testing.assert_close(got.cpu().float(), want.float(), atol=2e-2, rtol=2e-2)
