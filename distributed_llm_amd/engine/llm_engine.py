@@ -422,9 +422,19 @@ class LLMEngine:
         self._active = []
         self._bt_dirty = True
 
+    # TP mirror: admissions are exchanged every MIRROR_EVERY scheduler iterations (and whenever the
+    # batch is empty), not every decode step: leader and members call _take_inbox at the same points
+    # of the same deterministic schedule, so both sides know when a broadcast comes
+    MIRROR_EVERY = max(1, int(os.environ.get("DLLM_TP_ADMIT_EVERY", "8")))
+
     def _take_inbox(self, final: bool) -> List[_Seq]:
-        if self._mirror is not None and not self._mirror[2]:
-            return self._mirror_take()
+        if self._mirror is not None:
+            self._mirror_iter += 1
+            poll = final or self._mirror_iter % self.MIRROR_EVERY == 0
+            if not poll:
+                return []
+            if not self._mirror[2]:
+                return self._mirror_take()
         with self._inbox_lock:
             new, self._inbox = self._inbox, []
             if final and not new and self._bg is None:
@@ -438,14 +448,15 @@ class LLMEngine:
         """Continuous batching for a tensor-parallel pool.
 
         Every TP rank must run identical scheduler decisions (same admissions, same batch, same
-        collectives).  The leader (the rank that receives requests) broadcasts, once per scheduler
-        iteration, the requests it takes from its inbox — sequence id, prompt token ids, sampling
-        parameters — over ``group`` (a CPU/gloo group of the TP ranks); members replay them in
-        ``follow()``.  Scheduling is deterministic given those inputs (block manager, stop rules,
+        collectives).  The leader (the rank that receives requests) broadcasts, every
+        ``MIRROR_EVERY`` scheduler iterations (and whenever the batch is empty), the requests it
+        takes from its inbox — sequence id, prompt token ids, sampling parameters — over
+        ``group`` (a CPU/gloo group of the TP ranks); members replay them in ``follow()``.  Scheduling is deterministic given those inputs (block manager, stop rules,
         seeded sampling), so the members' engines stay in step while concurrent callers keep
         joining the leader's running batch (instead of one lockstep batch at a time)."""
         import torch.distributed as dist
         self._mirror = (group, leader, dist.get_rank() == leader)
+        self._mirror_iter = 0
         return self
 
     def _mirror_send(self, msg) -> None:
