@@ -118,6 +118,10 @@ class LLMEngine:
                  seed: int = 0, weights: Optional[str] = None, tokenizer: Optional[str] = None):
         self.cfg = get_model_config(model) if isinstance(model, str) else model
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None and torch.cuda.is_available():
+            # an explicit index: worker threads call torch.cuda.set_device(self.device), which
+            # rejects a bare "cuda" (the background loop died on it before serving anything)
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.par = par
         self.model = LlamaModel(self.cfg, device=self.device, par=par, seed=seed, weights=weights)
         self.tok = get_tokenizer(self.cfg.vocab, self.cfg.bos_id, self.cfg.eos_id, tokenizer)
