@@ -35,10 +35,6 @@ int dllm_tp_cands(const void*, long, int, int, int, void*, hipStream_t);
 int dllm_tp_sample(const void*, int, int, const float*, const float*, const int*, const unsigned*, int*, hipStream_t);
 int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                      hipStream_t);
-int dllm_skinny_lds_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
-                         hipStream_t);
-int dllm_mm_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
-                 hipStream_t);
 int dllm_moe_max_tiles(int, int);
 int dllm_moe_ffn(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int, int*,
                  int*, void*, float*, void*, hipStream_t);
@@ -54,9 +50,6 @@ int dllm_car_resadd(const void*, void*, long, float*, long, int, int, int, void*
                     long, hipStream_t);
 int dllm_car_allgather(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t, int);
-int dllm_decode_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*, void*,
-                          float*, float*, int*, const int*, const int*, int, int, int, int, int, int, int, float,
-                          hipStream_t);
 int dllm_moe_max_tiles_bm(int, int, int);
 int dllm_moe_ffn_tg(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int,
                     int*, int*, int*, void*, void*, void*, const int*, hipStream_t);
@@ -242,7 +235,7 @@ void flash_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::T
               "cache layout");
   const int nkv = kc.size(1);
   TORCH_CHECK(nq % nkv == 0 && 128 % (nq / nkv) == 0, "GQA group must divide 128");
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(1) <= 1024, "block_tables [S, <= 1024] (16K context)");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(1) >= 1, "block_tables [S, max_blocks]");
   const int S = block_tables.size(0);
   TORCH_CHECK(qstart.numel() == S && qlen.numel() == S && ctx.numel() == S, "seq metadata len");
   TORCH_CHECK(tile_tok0.numel() == tile_seq.numel(), "tile metadata len");
@@ -431,7 +424,7 @@ void masked_cosine_argmax(torch::Tensor q, torch::Tensor table, torch::Tensor no
 }
 // y[M, N] = x[M, K] . w[N, K]^T   (swiglu: x is [M, 2K] gate|up, silu(gate)*up computed on load)
 void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw, int64_t splits, bool swiglu,
-                 torch::Tensor part, torch::Tensor counters, int64_t variant) {
+                 torch::Tensor part, torch::Tensor counters) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_bf16(y, "y");
@@ -445,17 +438,14 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
   TORCH_CHECK(y.size(0) == M && y.size(1) == N, "y shape");
   TORCH_CHECK(M >= 1 && M <= 128 && K % 32 == 0, "M in [1,128], K % 32 == 0");
   TORCH_CHECK(ntw == 1 || ntw == 2 || ntw == 4, "ntw in {1,2,4}");
-  TORCH_CHECK(variant == 0 || ntw <= 2, "LDS variant: ntw in {1,2}");
-  TORCH_CHECK(variant == 0 || M <= 64 || ntw == 1, "LDS variant: M > 64 needs ntw 1");
   // slab rows = the kernel's row-tile height (MT x 16, MT in {1, 2, 4, 8}), not ceil(M / 16) x 16
-  const int nc = (variant == 0 ? 16 : 64) * ntw, tiles = (N + nc - 1) / nc,
+  const int nc = 16 * ntw, tiles = (N + nc - 1) / nc,
             mp = 16 * (M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : 8);
   if (splits > 1) {
     TORCH_CHECK(part.numel() >= (int64_t)splits * tiles * nc * mp, "split-K workspace too small");
     TORCH_CHECK(counters.numel() >= tiles, "counter buffer too small");
   }
-  auto fn = variant == 0 ? dllm_skinny_gemm : dllm_skinny_lds_gemm;
-  ok(fn(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, ntw, splits, swiglu ? 1 : 0,
+  ok(dllm_skinny_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, ntw, splits, swiglu ? 1 : 0,
         part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
      "skinny_gemm");
 }
@@ -572,32 +562,6 @@ void gemv_swiglu(torch::Tensor x, torch::Tensor w, torch::Tensor ssq, int64_t ss
                    0, nullptr, 0, ssq.data_ptr<float>(), (int)ssq_n, ssq.stride(0), (float)scale, (float)eps, nullptr,
                    nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, stream()),
      "gemv_swiglu");
-}
-
-// Mid-size decode GEMM (64 < M <= 256; csrc/kernels/mm_gemm.hip): y = x . w^T (x = silu(g)*u if swiglu).
-void mm_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t nt, int64_t splits, bool swiglu,
-             torch::Tensor part, torch::Tensor counters) {
-  check_bf16(x, "x");
-  check_bf16(w, "w");
-  check_bf16(y, "y");
-  check_f32(part, "part");
-  check_i32(counters, "counters");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.is_contiguous() && y.dim() == 2 &&
-                  y.stride(1) == 1 && y.stride(0) % 8 == 0,
-              "2-D row-major operands");
-  const int M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(x.size(1) == (swiglu ? 2 * K : K), "x inner dim");
-  TORCH_CHECK(y.size(0) == M && y.size(1) == N, "y shape");
-  TORCH_CHECK(M >= 1 && M <= 256 && K % 64 == 0 && N % 8 == 0, "M in [1,256], K % 64 == 0, N % 8 == 0");
-  TORCH_CHECK(nt == 2 || nt == 4, "nt in {2,4}");
-  const int bn = 16 * nt, tiles = (N + bn - 1) / bn, bm = M <= 64 ? 64 : M <= 128 ? 128 : 256;
-  if (splits > 1) {
-    TORCH_CHECK(part.numel() >= (int64_t)splits * tiles * bn * bm, "split-K workspace too small");
-    TORCH_CHECK(counters.numel() >= tiles, "counter buffer too small");
-  }
-  ok(dllm_mm_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), y.stride(0), M, N, K, (int)nt, (int)splits,
-                  swiglu ? 1 : 0, part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
-     "mm_gemm");
 }
 
 // Mixtral-style MoE FFN: x [T, H] bf16, ids [T, k] int32, wts [T, k] f32, w13 [E, 2I, H], w2 [E, H, I]
@@ -779,8 +743,11 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   }
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");
   TORCH_CHECK(epi >= 0 && epi <= 4, "epi");
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w: [N, K] contiguous");
-  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  // w: [N, K] row-major, or the K-panel-major copy [K / 64, N, 64] (models.llama.panel_weight)
+  const bool panel = w.dim() == 3;
+  TORCH_CHECK(((w.dim() == 2) || (panel && w.size(2) == 64)) && w.is_contiguous(),
+              "w: [N, K] or [K / 64, N, 64] contiguous");
+  const int M = x.size(0), N = panel ? w.size(1) : w.size(0), K = panel ? w.size(0) * 64 : w.size(1);
   TORCH_CHECK((ks == 1 || ks == 2) && (nw == 4 || (nw == 8 && bn >= 128)), "ks in {1,2}; nw 4, or 8 with bn >= 128");
   TORCH_CHECK(wk == 1 || (wk == 2 && nw == 4 && ks == 2 && stages <= 3 && bm <= 128 && bn <= 128),
               "wk 2: two k-groups of 4 waves, ks 2, 2-3 stages, tiles up to 128 x 128");
@@ -800,6 +767,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   a.lda = x.stride(0);
   a.W = (const uint16_t*)w.data_ptr();
   a.M = M; a.N = N; a.K = K; a.kchunk = kchunk; a.splits = S;
+  a.w_panel = panel ? 1 : 0;
   if (S > 1) {
     TORCH_CHECK(part.has_value() && counters.has_value(), "split-K needs part/counters workspaces");
     check_f32(*part, "part");
@@ -933,63 +901,6 @@ int64_t res_add_ssq(c10::optional<torch::Tensor> h, torch::Tensor r, torch::Tens
   return n;
 }
 
-// decode attention, wave-per-unit (csrc/kernels/decode_attn.hip): one query token per sequence
-void decode_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
-                      torch::Tensor qstart, torch::Tensor ctx, torch::Tensor tile_seq, torch::Tensor out,
-                      c10::optional<torch::Tensor> part_o, c10::optional<torch::Tensor> part_ml,
-                      c10::optional<torch::Tensor> counters, int64_t splits, double scale,
-                      c10::optional<torch::Tensor> split_len, c10::optional<torch::Tensor> items, int64_t grid_wgs) {
-  check_bf16(q, "q");
-  check_bf16(kc, "k_cache");
-  check_bf16(vc, "v_cache");
-  check_bf16(out, "out");
-  for (auto* t : {&block_tables, &qstart, &ctx, &tile_seq}) check_i32(*t, "attention metadata");
-  TORCH_CHECK(q.dim() == 3 && q.is_contiguous() && out.is_contiguous() && out.sizes() == q.sizes(), "q/out [T, nq, d]");
-  const int nq = q.size(1), d = q.size(2);
-  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && kc.size(2) == 16 && kc.size(3) == d &&
-                  vc.size(1) == kc.size(1) && vc.size(2) == d && vc.size(3) == 16,
-              "cache layout: K [blocks, nkv, 16, d], V [blocks, nkv, d, 16]");
-  const int nkv = kc.size(1);
-  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group <= 16");
-  TORCH_CHECK(d == 64 || d == 96 || d == 128, "head_dim must be 64, 96 or 128");
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.is_contiguous(), "block_tables [num_seqs, max_blocks]");
-  const int num_seqs = block_tables.size(0);
-  TORCH_CHECK(qstart.numel() == num_seqs && ctx.numel() == num_seqs, "seq metadata len");
-  const int num_tiles = tile_seq.numel();
-  TORCH_CHECK(splits >= 1 && splits <= 255, "splits");
-  float* po = nullptr;
-  float* pml = nullptr;
-  int* cnt = nullptr;
-  if (splits > 1) {
-    TORCH_CHECK(counters.has_value() && part_o.has_value() && part_ml.has_value(), "split-K needs workspaces");
-    check_i32(*counters, "counters");
-    check_f32(*part_o, "part_o");
-    check_f32(*part_ml, "part_ml");
-    TORCH_CHECK(counters->numel() >= (int64_t)num_tiles * nkv &&
-                    part_o->numel() >= (int64_t)num_tiles * nkv * splits * 16 * d &&
-                    part_ml->numel() >= (int64_t)num_tiles * nkv * splits * 16 * 2,
-                "workspace too small");
-    po = part_o->data_ptr<float>();
-    pml = part_ml->data_ptr<float>();
-    cnt = counters->data_ptr<int>();
-  }
-  const int* sl = nullptr;
-  if (split_len.has_value()) {
-    check_i32(*split_len, "split_len");
-    sl = split_len->data_ptr<int>();
-  }
-  const int* it = nullptr;
-  if (items.has_value()) {
-    check_i32(*items, "items");
-    TORCH_CHECK(items->numel() >= 1 && grid_wgs >= 1, "items: work list and a grid");
-    it = items->data_ptr<int>();
-  }
-  ok(dllm_decode_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
-                           qstart.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(), out.data_ptr(), po,
-                           pml, cnt, sl, it, (int)grid_wgs, num_tiles, nq, nkv, d, block_tables.size(1), (int)splits,
-                           (float)scale, stream()),
-     "decode_attention");
-}
 
 // router encoder (csrc/kernels/encoder.hip): bidirectional attention over a padded batch
 void encoder_attention(torch::Tensor qkv, torch::Tensor lens, torch::Tensor out, int64_t B, int64_t S, int64_t nh,
@@ -1026,7 +937,6 @@ void embed_ln(torch::Tensor ids, torch::Tensor word, torch::Tensor pos, torch::T
 
 PYBIND11_MODULE(_hip_kernels, m) {
   m.def("encoder_attention", &encoder_attention);
-  m.def("decode_attention", &decode_attention);
   m.def("embed_ln", &embed_ln);
   m.def("moe_ffn", &moe_ffn);
   m.def("moe_ffn_tg", &moe_ffn_tg);
@@ -1034,7 +944,6 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("res_add_ssq", &res_add_ssq);
   m.def("qkv_post", &qkv_post);
   m.def("swiglu_post", &swiglu_post);
-  m.def("mm_gemm", &mm_gemm);
   m.def("car_alloc", &car_alloc);
   m.def("car_handle", &car_handle);
   m.def("car_open", &car_open);

@@ -23,7 +23,9 @@
 // Staging: global_load_lds_dwordx4 into a 3-deep ring (counted vmcnt across a raw barrier, as in
 // tgemm.hip).  Both LDS images are XOR-swizzled through the per-lane source address so the
 // 16-lane row reads are conflict-free.  The chunk's block-table entries come from an LDS copy of
-// the tile's block-table row (an ordinary global load there would make hipcc drain the ring).
+// the tile's block-table row (an ordinary global load there would make hipcc drain the ring); the
+// LDS image is sized at launch for the table width, so any context length runs here (re-staging a
+// 16K-key window inside the loop instead spilled the d = 64 variant's issue path to scratch).
 // Keys past the context tail (never written) get P = 0 AND a zeroed V element (0 * NaN).
 // Grid order: consecutive workgroups (dealt round-robin to the 8 XCDs) take consecutive kv heads,
 // so the tiles sharing a head's K/V meet in one XCD's L2; the last (heaviest causal) tiles go first.
@@ -37,7 +39,6 @@ constexpr int NWAVES = 8;
 constexpr int ROWS = 32 * NWAVES;  // query rows per workgroup
 constexpr int CK = 64;             // keys per chunk (four cache blocks)
 constexpr int STAGES = 3;
-constexpr int MAXBT = 1024;        // block-table window staged in LDS (16K keys; re-staged past it)
 
 struct FlashArgs {
   const u16* q;  // [T, nq, D]
@@ -89,7 +90,8 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   constexpr int GI = STAGE / 1024 / NWAVES;  // 1-KB global_load_lds pieces per wave per chunk
   static_assert(STAGE % (1024 * NWAVES) == 0, "whole 1-KB pieces per wave");
   static_assert(KBYTES % 1024 == 0, "K and V^T pieces do not share a 1-KB piece");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + MAXBT * 4];
+  // ONE dynamic LDS array: [ring STAGES x STAGE][block-table row, max_blocks entries]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* s_bt = reinterpret_cast<int*>(smem + STAGES * STAGE);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -106,9 +108,8 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   const int kmax = a.causal ? ctx - qlen + last_tok + 1 : ctx;
   const int nchunks = (kmax + CK - 1) / CK;
   const int* bt = a.block_tables + (long)seq * a.max_blocks;
-  const int nbt = (kmax + 15) / 16;   // block-table entries this tile reads (any length)
-  int wb = 0;                          // first entry of the staged window (a multiple of MAXBT)
-  for (int i = threadIdx.x; i < min(nbt, MAXBT); i += 64 * NWAVES) s_bt[i] = bt[i];
+  const int nbt = min((kmax + 15) / 16, a.max_blocks);
+  for (int i = threadIdx.x; i < nbt; i += 64 * NWAVES) s_bt[i] = bt[i];
 
   // this lane's query row (both lane halves hold the same row, different keys)
   const int r = 32 * wave + rl;
@@ -141,12 +142,12 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
       if (p * 1024 < KBYTES) {
         const int rho = byte / (2 * D), pos = (byte % (2 * D)) / 16;
         const int key = kperm(rho);
-        const int blk = s_bt[min(bi + (key >> 4), nbt - 1) - wb];
+        const int blk = s_bt[min(bi + (key >> 4), nbt - 1)];
         src = a.kc + ((long)blk * a.nkv + kvh) * hstride + (key & 15) * D + 8 * kswz<D>(rho, pos);
       } else {
         const int vb = byte - KBYTES, b = vb / (32 * D), w = vb % (32 * D);
         const int dim = w / 32, c = ((w % 32) / 16) ^ ((dim >> 3) & 1);
-        const int blk = s_bt[min(bi + b, nbt - 1) - wb];
+        const int blk = s_bt[min(bi + b, nbt - 1)];
         src = a.vc + ((long)blk * a.nkv + kvh) * hstride + dim * 16 + 8 * c;
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + p * 1024), 16, 0, 0);
@@ -168,18 +169,7 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   for (int t = 0; t < nchunks; ++t) {
     if (t + 1 < nchunks) wait_vm<GI>(); else wait_vm<0>();
     sync_lds();
-    if (t + STAGES - 1 < nchunks) {
-      const int tn = t + STAGES - 1, w = (tn * (CK / 16)) & ~(MAXBT - 1);
-      if (w != wb) {
-        // the next chunk's entries lie past the staged window (block-uniform, once per 16K keys):
-        // every earlier issue's s_bt reads retired before the barrier above, so re-stage it (the
-        // plain loads drain the ring here, a rare stall) and publish it before issuing
-        wb = w;
-        for (int i = threadIdx.x; i < min(nbt - wb, MAXBT); i += 64 * NWAVES) s_bt[i] = bt[wb + i];
-        __syncthreads();
-      }
-      issue(tn);
-    }
+    if (t + STAGES - 1 < nchunks) issue(t + STAGES - 1);
     const int kb = t * CK;
     if (kb >= wave_lim) continue;  // wave-uniform: every row of this wave is past its causal limit
     const unsigned char* kbase = smem + (t % STAGES) * STAGE;
@@ -283,13 +273,22 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   FlashArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
               tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, num_tiles, scale * LOG2E_F};
   const dim3 grid((unsigned)num_tiles * (unsigned)nkv);
-  // d=64: 4 waves per SIMD (<= 128 VGPRs, 52 KB LDS) = two workgroups per CU; measured 1.14-1.17x
-  // over one at 2k-16k tokens (profiles/r2_flash_prefill_microbench.md)
+  // d=64: 4 waves per SIMD (<= 128 VGPRs, 52 KB LDS at a 16K context) = two workgroups per CU;
+  // measured 1.14-1.17x over one at 2k-16k tokens (profiles/r2_flash_prefill_microbench.md)
+  auto go = [&](auto kern, int dd) -> int {
+    const size_t lds = (size_t)STAGES * (2 * CK * dd * 2) + ((size_t)max_blocks * 4 + 15) / 16 * 16;
+    if (lds > 160 * 1024) return -3;
+    if (lds > 64 * 1024) {   // past the default dynamic-LDS cap (d = 64: contexts beyond ~128K keys)
+      const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(64 * NWAVES), lds, stream, a);
+    return (int)hipGetLastError();
+  };
   switch (d) {
-    case 64: hipLaunchKernelGGL((flash_prefill_kernel<64, 4>), grid, dim3(64 * NWAVES), 0, stream, a); break;
-    case 96: hipLaunchKernelGGL((flash_prefill_kernel<96, 2>), grid, dim3(64 * NWAVES), 0, stream, a); break;
-    case 128: hipLaunchKernelGGL((flash_prefill_kernel<128, 2>), grid, dim3(64 * NWAVES), 0, stream, a); break;
+    case 64: return go(flash_prefill_kernel<64, 4>, 64);
+    case 96: return go(flash_prefill_kernel<96, 2>, 96);
+    case 128: return go(flash_prefill_kernel<128, 2>, 128);
     default: return -4;
   }
-  return (int)hipGetLastError();
 }

@@ -163,12 +163,17 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
     const long arow = a.g_perm != nullptr ? (long)(a.g_perm[row] / a.g_k) : (long)row;  // MoE: gathered rows
     return a.A + arow * a.lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
   };
+  // weight source of tile row r at k offset kbeg (row-major, or panel-major: row n of k panel p
+  // at (p N + n) 64); wstep = elements between consecutive 64-deep k sub-tiles of one row
+  const long wstep = a.w_panel ? 64L * N : 64L;
   auto b_row = [&](int r) -> const u16* {
-    return Wb + (long)min(n0 + r, N - 1) * K + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+    const long n = min(n0 + r, N - 1);
+    return Wb + (a.w_panel ? ((long)(kbeg / BK) * N + n) * BK : n * K + kbeg) + 8 * (spos ^ ((r >> 1) & 7));
   };
   const u16* a_src[GA];
   const u16* b_src[GB];
   const u16* l_src[GL];   // loader waves: piece lw + NL j of the stage image ([A; B] per sub-tile)
+  long l_step[GL];        // ... and its source advance per ring stage (KS sub-tiles)
   int l_off[GL];
   if constexpr (NL == 0) {
 #pragma unroll
@@ -180,7 +185,10 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
 #pragma unroll
     for (int j = 0; j < GL; ++j) {
       const int g = lw + NL * j, ks = g / ((BM + BN) / 8), p = g % ((BM + BN) / 8);
-      l_src[j] = (p < BM / 8 ? a_row(8 * p + srow) : b_row(8 * (p - BM / 8) + srow)) + ks * BK;
+      const bool isa = p < BM / 8;
+      const long st = isa ? (long)BK : wstep;
+      l_src[j] = (isa ? a_row(8 * p + srow) : b_row(8 * (p - BM / 8) + srow)) + ks * st;
+      l_step[j] = st * KS;
       l_off[j] = ks * SUB_BYTES + p * 1024;
     }
   }
@@ -189,7 +197,7 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
 #pragma unroll
       for (int j = 0; j < GL; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + t * KSTEP), (lds_void*)(base + l_off[j]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + t * l_step[j]), (lds_void*)(base + l_off[j]), 16, 0, 0);
       return;
     }
 #pragma unroll
@@ -197,13 +205,14 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
       if (WK == 2 && ks != kg) continue;  // each k-group stages its own sub-tile
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + ks * SUB_BYTES;
       const int ko = t * KSTEP + ks * BK;
+      const long kw = (long)(t * KS + ks) * wstep;
 #pragma unroll
       for (int j = 0; j < GA; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + ko), (lds_void*)(base + (wave * GA + j) * 1024),
                                          16, 0, 0);
 #pragma unroll
       for (int j = 0; j < GB; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + ko),
+        __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + kw),
                                          (lds_void*)(base + A_BYTES + (wave * GB + j) * 1024), 16, 0, 0);
     }
   };
@@ -767,7 +776,8 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
   if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
   if (a.N % 8 || (a.Y && a.ldy % 8)) return -7;  // 16-B output row vectors
   if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
-  if (a.g_tiles != nullptr && (a.splits != 1 || a.M != a.g_max * bm || epi == EPI_QKV || a.ssq_in)) return -10;
+  if (a.g_tiles != nullptr && (a.splits != 1 || a.M != a.g_max * bm || epi == EPI_QKV || a.ssq_in || a.w_panel))
+    return -10;
   if (stages < 2 || stages > 6 || stages == 5 || (stages > 3 && (ks != 1 || bm > 128))) return -5;
   switch (epi) {
     case EPI_PLAIN: return by_tile<EPI_PLAIN>(bm, bn, stages, ks, nw, wk, a, stream);

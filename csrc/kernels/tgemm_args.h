@@ -41,6 +41,11 @@ struct GemmArgs {
   const int* g_perm;
   int g_k;
   long g_wstride;
+  // 1: W is stored K-PANEL-MAJOR, [K / 64][N][64] (element (n, k) at ((k / 64) N + n) 64 + k % 64):
+  // every ring fill of the weight operand (8 rows x 128 B) is then ONE contiguous 1 KB of the
+  // weight stream instead of eight 128-B pieces 2K-11K bytes apart (HBM pages / L2 channels);
+  // repacked once at load time (models/llama.py).  Not with the grouped (MoE) mode.
+  int w_panel;
 };
 enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_GELU = 4 };
 }  // namespace dllm

@@ -295,11 +295,6 @@ class LLMEngine:
     # 512 and equal at 8k, microbench decode sweep; it only matters while batch x context < 64k
     # tokens, above that the target unit count sets the chunk)
     ATTN_MIN_CHUNK = int(os.environ.get("DLLM_ATTN_MIN_CHUNK", "256"))
-    # Alternative decode kernel (csrc/kernels/decode_attn.hip, one wave per unit, 1024 workgroups,
-    # 4096-unit list): measured equal at best, slower at small batch (profiles/r2_decode_attention_
-    # microbench.md), so opt-in only
-    DECODE_WAVE = os.environ.get("DLLM_DECODE_ATTN", "paged") == "wave"
-
     def _use_worklist(self, bs: int) -> bool:
         return self.attn_worklist and bs >= self.ATTN_WL_MIN_BS
 
@@ -899,7 +894,7 @@ class LLMEngine:
         n_items = 0
         if self._use_worklist(bs):
             grid = self._attn_grid(bs)
-            target = 4096 if self.DECODE_WAVE else self.ATTN_ITEMS_PER_WG * grid
+            target = self.ATTN_ITEMS_PER_WG * grid
             items_t, items = self._items_bufs[p]
             ops.decode_work_items(lens[order], self.model.nkv, self.max_splits, target,
                                   min_chunk=self.ATTN_MIN_CHUNK, out=items, seq=rows[order], qstart=order)
@@ -1208,8 +1203,7 @@ class LLMEngine:
             return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart,
                             qlen=self.d_qlen, ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
                             last_idx=self.d_last[:bs], all_last=True, splits=self.max_splits, workspace=self.dec_ws,
-                            items=self.items_dev, grid_items=1024 if self.DECODE_WAVE else self._attn_grid(bs),
-                            wave=self.DECODE_WAVE)
+                            items=self.items_dev, grid_items=self._attn_grid(bs))
         return AttnMeta(slots=self.d_slots[:bs], block_tables=self.bt_dev, qstart=self.d_qstart, qlen=self.d_qlen,
                         ctx=self.d_ctx, tile_seq=self.d_tseq[:bs], tile_tok0=self.d_tok0[:bs],
                         last_idx=self.d_last[:bs], all_last=True, splits=self._decode_splits(bs), workspace=self.dec_ws,

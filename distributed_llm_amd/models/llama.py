@@ -58,7 +58,6 @@ class AttnMeta:
     items: Optional[torch.Tensor] = None       # decode: persistent attention work list (ops.decode_work_items)
     grid_items: int = 0                        # workgroups walking ``items``
     flash: bool = False                        # prefill: tile_seq/tile_tok0 are 128-row flash tiles
-    wave: bool = False                         # decode: wave-per-unit kernel (decode_attn.hip) over ``items``
     all_last: bool = False                     # decode: every row is its sequence's last token (no gather)
 
 
@@ -159,11 +158,27 @@ class LlamaModel:
         return (self.d % 32 == 0 and cfg.hidden % 64 == 0 and (self.nq * self.d) % 64 == 0
                 and (cfg.is_moe or (self.I % 64 == 0)))
 
+    PANEL_NAMES = ("wqkv_f", "wo", "wgu_f", "wd")
+
     def _fuse_weights(self) -> None:
         for L in self.layers:
             L["wqkv_f"] = fuse_qkv_weight(L.pop("wqkv"), L["ln1"], self.nq, self.nkv, self.d)
             if "wgu" in L:
                 L["wgu_f"] = fuse_gate_up_weight(L.pop("wgu"), L["ln2"])
+        # K-panel-major copies of the fused decoder GEMM weights (ops.gemm.panel_weight): the tgemm
+        # plans stream them; the row-major weights stay for the GEMV / skinny / hipBLASLt paths.  Kept
+        # only while both layouts fit in a quarter of the device's memory (e.g. not Llama-3-70B at
+        # TP=1: 141 GB of weights on a 288 GB part)
+        if not ops.gemm.W_PANEL or self.device.type != "cuda":
+            return
+        names = [n for n in self.PANEL_NAMES if n in self.layers[0] and self.layers[0][n].shape[1] % 64 == 0]
+        extra = sum(L[n].numel() * L[n].element_size() for L in self.layers for n in names)
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        if extra > 0.25 * total:
+            return
+        for L in self.layers:
+            for n in names:
+                L[n + "_p"] = ops.gemm.panel_weight(L[n])
 
     def reference_layers(self) -> List[Dict[str, torch.Tensor]]:
         """Layer weights in the plain (unfused) layout, e.g. for a CPU reference forward."""
@@ -171,7 +186,7 @@ class LlamaModel:
             return self.layers
         out = []
         for L in self.layers:
-            R = {k: v for k, v in L.items() if k not in ("wqkv_f", "wgu_f")}
+            R = {k: v for k, v in L.items() if k not in ("wqkv_f", "wgu_f") and not k.endswith("_p")}
             if "wqkv_f" in L:
                 R["wqkv"] = unfuse_qkv_weight(L["wqkv_f"], L["ln1"], self.nq, self.nkv, self.d)
             if "wgu_f" in L:
@@ -324,10 +339,6 @@ class LlamaModel:
         if meta.flash:   # prefill: 128-row tiles, K/V staged once per workgroup (flash_prefill.hip)
             return ops.flash_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                        meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True)
-        if meta.wave:    # decode alternative: one wave per (sequence, kv head, split) unit
-            return ops.decode_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.ctx, meta.tile_seq,
-                                        scale=self.scale, splits=meta.splits, workspace=meta.workspace,
-                                        items=meta.items, grid_wgs=meta.grid_items)
         return ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
@@ -386,18 +397,18 @@ class LlamaModel:
             kc, vc = kv_caches[li]
             # column-parallel QKV (this rank's heads) with RMSNorm folded + RoPE + paged K/V write
             q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,
-                                        self.nq, self.nkv, self.d)
+                                        self.nq, self.nkv, self.d, wp=L.get("wqkv_f_p"))
             o = self._attention(q, kc, vc, meta)
             if not tp:
-                nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b)
+                nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b, wp=L.get("wo_p"))
             else:   # row-parallel o_proj: partial sums -> all-reduce + residual add + row statistics
-                nb = par.all_reduce_resadd(ops.linear(o.view(T, -1), L["wo"]), r, ssq_b)
+                nb = par.all_reduce_resadd(ops.linear(o.view(T, -1), L["wo"], wp=L.get("wo_p")), r, ssq_b)
             if not cfg.is_moe:
-                act = ops.gemm.swiglu_matmul(r, L["wgu_f"], ssq_b, nb, eps)
+                act = ops.gemm.swiglu_matmul(r, L["wgu_f"], ssq_b, nb, eps, wp=L.get("wgu_f_p"))
                 if not tp:
-                    n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a)
+                    n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a, wp=L.get("wd_p"))
                 else:
-                    n = par.all_reduce_resadd(ops.linear(act, L["wd"]), r, ssq_a)
+                    n = par.all_reduce_resadd(ops.linear(act, L["wd"], wp=L.get("wd_p")), r, ssq_a)
             else:
                 x = ops.rms_norm(r, L["ln2"], eps)
                 if not tp:

@@ -203,37 +203,6 @@ def flash_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return o
 
 
-def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
-                     seq_qstart: torch.Tensor, seq_ctx: torch.Tensor, tile_seq: torch.Tensor,
-                     scale: Optional[float] = None, splits: int = 1,
-                     workspace: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                     items: Optional[torch.Tensor] = None, grid_wgs: int = 0,
-                     split_len: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Decode attention, one query token per sequence (csrc/kernels/decode_attn.hip): every wave
-    owns a (tile, kv head, key split) unit — a static grid of ``tiles x nkv x splits`` units, or
-    with ``items`` (:func:`decode_work_items`) a fixed grid of ``grid_wgs`` 4-wave workgroups
-    striding over the list.  Splits merge in-launch (last wave per (tile, kv head))."""
-    d = q.shape[-1]
-    scale = (1.0 / math.sqrt(d)) if scale is None else scale
-    ext = _native(q)
-    if ext is None:   # sequences named by a tile carry one query token, the others none
-        ql = torch.zeros_like(seq_ctx)
-        ts = tile_seq[tile_seq >= 0].long()
-        ql[ts] = 1
-        o = ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, ql, seq_ctx, scale, True)
-        if out is not None:
-            out.copy_(o)
-            return out
-        return o
-    o = out if out is not None else torch.empty_like(q)
-    po = pml = cnt = None
-    if splits > 1:
-        po, pml, cnt = workspace
-    ext.decode_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_ctx, tile_seq, o, po, pml, cnt,
-                         int(splits), float(scale), split_len, items, int(grid_wgs))
-    return o
-
-
 def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,
                       out: Optional[np.ndarray] = None, seq=None, qstart=None) -> np.ndarray:
     """Work list for persistent decode attention (one query token per tile, tiles in ``ctx`` order).

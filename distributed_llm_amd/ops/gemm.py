@@ -8,8 +8,8 @@ Kernels (csrc/kernels):
     block order, optional in-launch split-K) with the transformer epilogues used by the fused
     decoder layer (models/llama.py): QKV + RoPE + paged-KV write, residual add + row sums of
     squares (RMSNorm folded into the next GEMM), SwiGLU.  Any M (decode buckets and prefill).
-  * ``gemv.hip`` (M <= 8), ``skinny_gemm.hip`` / ``skinny_lds.hip`` (M <= 128), ``mm_gemm.hip``
-    (M <= 256): register-streaming decode GEMMs without LDS tiling.
+  * ``gemv.hip`` (M <= 8), ``skinny_gemm.hip`` (M <= 128): register-streaming decode GEMMs without
+    LDS tiling.
   * hipBLASLt via ``F.linear`` stays a candidate, so a custom kernel is used only where it wins.
 
 Plans are measured once per (M, N, K) OUTSIDE graph capture (``autotune``, called by the engine
@@ -38,11 +38,8 @@ from . import _native, reference as ref
 
 MAX_M = 1024       # decode buckets up to this size are autotuned
 SKINNY_MAX_M = 128
-MM_MAX_M = 256
 _SPLITS = (1, 2, 4, 8, 16)
 _NTWS = (1, 2, 4)
-_MM_NTS = (2, 4)
-_MM_SPLITS = (1, 2, 4, 8)
 _GEMV_MS = (1, 2, 4, 8)   # csrc/kernels/gemv.hip instantiations (decode buckets below 16)
 _GEMV_RS = (1, 2, 4)
 _TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8), (128, 128, 8), (192, 128, 8),
@@ -57,6 +54,23 @@ WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
 WS_COUNTERS = 1 << 16
 
 EPI_PLAIN, EPI_RESADD, EPI_QKV, EPI_SWIGLU, EPI_GELU = 0, 1, 2, 3, 4
+
+# K-panel-major weight copies for the fused decoder GEMMs (GemmArgs.w_panel): every tgemm ring fill
+# of the weight operand is one contiguous 1 KB instead of eight 128-B row pieces 4-11 KB apart
+# (profiles/r3_decode_gemm_panel.md).  The row-major weight stays for the GEMV / skinny / hipBLASLt
+# paths; models.llama keeps the panel copy only while both fit comfortably in HBM.
+W_PANEL = os.environ.get("DLLM_W_PANEL", "1") == "1"
+
+
+def panel_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> [K / 64, N, 64] (element (n, k) at ((k // 64) N + n) 64 + k % 64)."""
+    N, K = w.shape
+    return w.view(N, K // 64, 64).transpose(0, 1).contiguous()
+
+
+def _nk(w: torch.Tensor) -> Tuple[int, int]:
+    """(N, K) of a row-major [N, K] or panel [K / 64, N, 64] weight."""
+    return (w.shape[1], w.shape[0] * 64) if w.dim() == 3 else (w.shape[0], w.shape[1])
 
 _OWNER: contextvars.ContextVar = contextvars.ContextVar("dllm_gemm_ws_owner", default=None)
 
@@ -106,17 +120,8 @@ def reserve(device) -> None:
 
 # ----------------------------------------------------------------------------- workspace needs
 
-def _need_mm(M: int, N: int, K: int, nt: int, splits: int) -> Tuple[int, int]:
-    bn = 16 * nt
-    tiles = (N + bn - 1) // bn
-    kchunk = ((K + splits - 1) // splits + 63) // 64 * 64
-    S = (K + kchunk - 1) // kchunk
-    bm = 64 if M <= 64 else 128 if M <= 128 else 256
-    return (S * tiles * bn * bm if S > 1 else 0), tiles
-
-
-def _need(M: int, N: int, K: int, ntw: int, splits: int, variant: int = 0) -> Tuple[int, int]:
-    nc = (16 if variant == 0 else 64) * ntw
+def _need(M: int, N: int, K: int, ntw: int, splits: int) -> Tuple[int, int]:
+    nc = 16 * ntw
     tiles = (N + nc - 1) // nc
     kchunk = ((K + splits - 1) // splits + 31) // 32 * 32
     S = (K + kchunk - 1) // kchunk
@@ -175,7 +180,7 @@ def tg_slots(M: int, N: int, K: int) -> int:
     return -(-N // tg_plan(M, N, K)[1])
 
 
-def _run_plan(plan, x, w, swiglu, out):
+def _run_plan(plan, x, w, swiglu, out, wp=None):
     if plan[0] == "blas":
         if swiglu:
             x = ref_silu_mul(x)
@@ -185,7 +190,7 @@ def _run_plan(plan, x, w, swiglu, out):
         if swiglu:
             x = ref_silu_mul(x)
         y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-        _tgemm(ext, x, w, EPI_PLAIN, plan[1:], y=y)
+        _tgemm(ext, x, wp if wp is not None else w, EPI_PLAIN, plan[1:], y=y)
         return y
     if plan[0] == "gemv":
         y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
@@ -194,15 +199,9 @@ def _run_plan(plan, x, w, swiglu, out):
     kind, ntw, splits = plan
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
-    if kind == "mm":
-        floats, tiles = _need_mm(M, N, K, ntw, splits)
-        part, cnt = _P.workspace(x.device, floats, tiles)
-        ext.mm_gemm(x, w, y, ntw, splits, swiglu, part, cnt)
-        return y
-    variant = 0 if kind == "skinny" else 1
-    floats, tiles = _need(M, N, K, ntw, splits, variant)
+    floats, tiles = _need(M, N, K, ntw, splits)
     part, cnt = _P.workspace(x.device, floats, tiles)
-    ext.skinny_gemm(x, w, y, ntw, splits, swiglu, part, cnt, variant)
+    ext.skinny_gemm(x, w, y, ntw, splits, swiglu, part, cnt)
     return y
 
 
@@ -213,7 +212,8 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     wk = plan[6] if len(plan) >= 7 else 1
     nl = plan[7] if len(plan) >= 8 else 0
-    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    M = x.shape[0]
+    N, K = _nk(w)
     if K % (64 * ks):
         ks, wk = 1, 1
     part = cnt = None
@@ -233,7 +233,9 @@ def _key(x, w, swiglu):
     return (x.shape[0], w.shape[0], w.shape[1], bool(swiglu))
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
+           wp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x @ w.T`` on the shape's tuned plan; ``wp``: the panel copy a tgemm plan streams."""
     if not x.is_cuda or os.environ.get("DLLM_GEMM") == "blas":
         return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
     plan = _P.plans.get(_key(x, w, False))
@@ -245,7 +247,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             plan = ("blas",)
         else:
             plan = _heuristic(x.shape[0], w.shape[0], w.shape[1])
-    return _run_plan(plan, x, w, False, out)
+    return _run_plan(plan, x, w, False, out, wp)
 
 
 def norm_linear(h: torch.Tensor, residual: torch.Tensor, spare: torch.Tensor, norm_w: torch.Tensor, eps: float,
@@ -292,7 +294,7 @@ POST_US = 3.0
 
 
 def use_vendor_core(M: int, N: int, K: int) -> bool:
-    """True: run the fused op as ``linear()`` (the shape's best plain plan — GEMV / skinny / mm /
+    """True: run the fused op as ``linear()`` (the shape's best plain plan — GEMV / skinny /
     hipBLASLt / plain tgemm) followed by the standalone epilogue kernel; False: one tgemm launch
     with the epilogue fused.  (A ``gemvR`` choice is taken before this by ``fused_gemv_r``.)"""
     env = os.environ.get("DLLM_FUSED_CORE")
@@ -319,14 +321,14 @@ def fused_gemv_r(x: torch.Tensor, N: int) -> int:
     return 0
 
 
-def _core(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def _core(x: torch.Tensor, w: torch.Tensor, wp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Plain product for the split (core + epilogue) form of a fused op: the tuned plan of this
     shape (M <= MAX_M), hipBLASLt above."""
-    return linear(x, w) if x.shape[0] <= MAX_M else F.linear(x, w)
+    return linear(x, w, wp=wp) if x.shape[0] <= MAX_M else F.linear(x, w)
 
 def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float,
                    positions: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
-                   v_cache: torch.Tensor, nq: int, nkv: int, d: int) -> torch.Tensor:
+                   v_cache: torch.Tensor, nq: int, nkv: int, d: int, wp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [T, nq, d] of ``rope(rmsnorm(r) . Wqkv^T)``, K/V written to the paged caches, one launch.
 
     ``w`` is the folded/permuted weight of models.llama.fuse_qkv_weight; ``ssq[:ssq_n]`` holds
@@ -341,16 +343,17 @@ def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: i
                             v_cache, nq, nkv, d, R)
         return q
     if use_vendor_core(T, w.shape[0], H):
-        _native(r).qkv_post(_core(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
+        _native(r).qkv_post(_core(r, w, wp), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
                             k_cache, v_cache, nq, nkv, d)
         return q
-    _tgemm(_native(r), r, w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
+    _tgemm(_native(r), r, wp if wp is not None else w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
            eps=eps, pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv,
            d=d)
     return q
 
 
-def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_out: torch.Tensor) -> int:
+def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_out: torch.Tensor,
+                  wp: Optional[torch.Tensor] = None) -> int:
     """``residual += x . w^T`` (bf16 rounding as ``rms_norm``'s residual add) and the partial row
     sums of the new residual's squares into ``ssq_out[:slots]``; returns ``slots``."""
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
@@ -358,14 +361,15 @@ def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_
     if R:
         return int(_native(x).gemv_resadd(x, w, residual, ssq_out, R))
     if M and use_vendor_core(M, N, K):
-        return int(_native(x).res_add_ssq(_core(x, w), residual, ssq_out))
+        return int(_native(x).res_add_ssq(_core(x, w, wp), residual, ssq_out))
     plan = tg_plan(M, N, K)
     if M:
-        _tgemm(_native(x), x, w, EPI_RESADD, plan, y=residual, ssq_out=ssq_out)
+        _tgemm(_native(x), x, wp if wp is not None else w, EPI_RESADD, plan, y=residual, ssq_out=ssq_out)
     return -(-N // plan[1])
 
 
-def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float) -> torch.Tensor:
+def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float,
+                  wp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``silu(g) * u`` with ``[g | u] = rmsnorm(r) . Wgu^T`` (interleaved rows, models.llama
     .fuse_gate_up_weight) -> [T, I]."""
     T, H = r.shape
@@ -375,10 +379,10 @@ def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: in
         _native(r).gemv_swiglu(r, w, ssq, int(ssq_n), 1.0 / H, float(eps), act, R)
         return act
     if T and use_vendor_core(T, w.shape[0], H):
-        _native(r).swiglu_post(_core(r, w), ssq, int(ssq_n), 1.0 / H, float(eps), act)
+        _native(r).swiglu_post(_core(r, w, wp), ssq, int(ssq_n), 1.0 / H, float(eps), act)
         return act
     if T:
-        _tgemm(_native(r), r, w, EPI_SWIGLU, tg_plan(T, w.shape[0], H), y=act, ssq_in=ssq, ssq_n=ssq_n,
+        _tgemm(_native(r), r, wp if wp is not None else w, EPI_SWIGLU, tg_plan(T, w.shape[0], H), y=act, ssq_in=ssq, ssq_n=ssq_n,
                norm_scale=1.0 / H, eps=eps)
     return act
 
@@ -495,8 +499,10 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
                 else:
                     _P.plans[(int(parts[0]), int(parts[1]), int(parts[2]), parts[3] == "1")] = tuple(v)
     shapes = list(shapes)
-    _autotune(shapes, list(ms), dev, verbose)
-    _couple_gemv_choices(list(fused), list(ms), verbose)
+    fused = list(fused)
+    # the fused ops' tgemm plans stream the panel weight copies: time them in that layout
+    _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set())
+    _couple_gemv_choices(fused, list(ms), verbose)
     if cache:
         import json
         d = {_plan_key(k): list(v) for k, v in _P.plans.items()}
@@ -568,11 +574,12 @@ def _tg_cands(M: int, N: int, K: int):
     return out
 
 
-def _autotune(shapes, ms, dev, verbose: bool) -> None:
+def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
     use_tg = os.environ.get("DLLM_GEMM_NO_TG") != "1"
     for (N, K, sw) in shapes:
         copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
         ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        wps = [panel_weight(w) for w in ws] if (N, K) in panel_shapes and K % 64 == 0 and not sw else None
         for M in ms:
             if M > MAX_M:
                 continue
@@ -584,33 +591,24 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 continue
             x = torch.randn(M, 2 * K if sw else K, device=dev).to(torch.bfloat16)
             cands = [("blas",)]
-            if M <= MM_MAX_M and M > 16 and K % 64 == 0 and N % 8 == 0 and os.environ.get("DLLM_GEMM_NO_MM") != "1":
-                for nt in _MM_NTS:
-                    for s in _MM_SPLITS:
-                        if s > 1 and K // s < 256:
-                            continue
-                        floats, tiles = _need_mm(M, N, K, nt, s)
-                        if floats > WS_FLOATS or tiles > WS_COUNTERS:
-                            continue
-                        cands.append(("mm", nt, s))
             if M in _GEMV_MS and K % 8 == 0 and M * K * 2 <= 64 * 1024 and os.environ.get("DLLM_GEMM_NO_GEMV") != "1":
                 cands.extend(("gemv", r) for r in _GEMV_RS)
-            for kind, ntws in ((("skinny", _NTWS), ("lds", (1, 2))) if M <= SKINNY_MAX_M else ()):
-                for ntw in ntws:
-                    if M > 64 and (ntw == 4 or (kind == "lds" and ntw == 2)):
+            for ntw in (_NTWS if M <= SKINNY_MAX_M else ()):
+                if M > 64 and ntw == 4:
+                    continue
+                for s in _SPLITS:
+                    if s > 1 and K // s < 128:
                         continue
-                    for s in _SPLITS:
-                        if s > 1 and K // s < 128:
-                            continue
-                        floats, tiles = _need(M, N, K, ntw, s, 0 if kind == "skinny" else 1)
-                        if floats > WS_FLOATS or tiles > WS_COUNTERS:
-                            continue
-                        cands.append((kind, ntw, s))
+                    floats, tiles = _need(M, N, K, ntw, s)
+                    if floats > WS_FLOATS or tiles > WS_COUNTERS:
+                        continue
+                    cands.append(("skinny", ntw, s))
             if use_tg and not sw:
                 cands.extend(("tg",) + c for c in _tg_cands(M, N, K))
             res = {}
             for c in cands:
-                res[c] = _time(lambda i: _run_plan(c, x, ws[i % copies], sw, None))
+                res[c] = _time(lambda i: _run_plan(c, x, ws[i % copies], sw, None,
+                                                   wps[i % copies] if wps is not None else None))
             best = min(res, key=res.get)
             if need_plain:
                 _P.plans[key] = best
@@ -637,7 +635,7 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 _P.fused_opts[tkey] = opts
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)
-                      for k in ("gemv", "skinny", "lds", "mm", "tg")}
+                      for k in ("gemv", "skinny", "tg")}
                 extra = " ".join(f"{k}={c[1:]}:{res[c]:.1f}us" for k, c in bk.items() if c)
                 top = sorted(tgc, key=res.get)[:4]
                 extra += " | tg top: " + " ".join(f"{c[1:]}:{res[c]:.1f}" for c in top)
@@ -646,7 +644,7 @@ def _autotune(shapes, ms, dev, verbose: bool) -> None:
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
                       f"({N * K * 2 / res[best] / 1e3:.0f} GB/s, {2 * M * N * K / res[best] / 1e6:.0f} TF/s; "
                       f"blas {res[('blas',)]:.1f}us; {extra})", flush=True)
-        del ws
+        del ws, wps
 
 
 def plans() -> Dict:

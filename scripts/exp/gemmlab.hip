@@ -313,6 +313,14 @@ __global__ void ref_kernel(const u16* A, const u16* W, float* Y, int M, int N, i
 }
 
 // repack W [N, K] -> [N/BN][K/64][BN][64] with the LDS swizzle pre-applied (rows past N clamp)
+// K-panel-major weight copy for the production tgemm's w_panel mode: Wp[(k/64) N + n][k%64] = W[n][k]
+__global__ void panel_kernel(const u16* W, u16* Wp, int N, int K) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;   // one 16-B chunk
+  if (i >= (long)N * K / 8) return;
+  const long n = i / (K / 8), k = (i % (K / 8)) * 8;
+  *reinterpret_cast<uint4*>(Wp + ((k / 64) * N + n) * 64 + k % 64) = *reinterpret_cast<const uint4*>(W + n * K + k);
+}
+
 __global__ void tile_kernel(const u16* W, u16* Wt, int N, int K, int BN) {
   const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;  // one 16-B chunk of Wt
   const int nk = K / 64, ntile = (N + BN - 1) / BN;
@@ -461,23 +469,41 @@ int main(int argc, char** argv) {
                M, N, K, name, us, flops / us / 1e6, wbytes / us / 1e6, err);
         fflush(stdout);
       };
-      // production tgemm, a few plans from profiles/r2_tgemm_tune_tinyllama_shapes.log
-      const int tplans[][6] = {{64, 64, 3, 1, 1, 4}, {64, 64, 4, 1, 1, 4}, {64, 128, 3, 1, 1, 8}, {128, 128, 2, 1, 1, 8},
-                               {128, 64, 2, 1, 1, 4}, {256, 128, 3, 1, 1, 8}};
-      for (auto& p : tplans) {
-        if (skip_tg) break;
-        dllm::GemmArgs a{};
-        a.A = A; a.lda = K; a.W = nullptr; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.kchunk = K; a.splits = 1;
-        a.W = ws[0];
-        if (dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s, 0) != 0) continue;
+      // production tgemm: plans {bm, bn, stages, splits, ks, waves, loader waves}, row-major W and
+      // the K-panel-major copy (w_panel)
+      const int tplans[][7] = {{64, 64, 3, 1, 1, 4, 0}, {64, 64, 4, 1, 1, 4, 0}, {64, 128, 3, 1, 1, 8, 0},
+                               {128, 128, 2, 1, 1, 8, 0}, {128, 64, 2, 1, 1, 4, 0}, {256, 128, 3, 1, 1, 8, 0},
+                               {64, 64, 3, 2, 2, 4, 0}, {64, 128, 3, 1, 2, 8, 0}, {64, 64, 4, 1, 1, 4, 2},
+                               {64, 64, 4, 1, 1, 4, 4}, {64, 64, 8, 1, 1, 4, 4}, {128, 64, 4, 1, 1, 4, 4},
+                               {128, 128, 4, 1, 1, 4, 4}, {160, 128, 3, 1, 1, 8, 4}, {256, 128, 3, 1, 1, 8, 4},
+                               {64, 64, 4, 2, 1, 4, 4}, {128, 64, 4, 2, 1, 4, 4}, {64, 64, 4, 3, 1, 4, 4}};
+      if (!skip_tg) {
+        for (int c = 0; c < copies; ++c) {
+          const long chunks = wel / 8;
+          hipLaunchKernelGGL(lab::panel_kernel, dim3((chunks + 255) / 256), dim3(256), 0, s, ws[c], wts[c], N, K);
+        }
         CHECK(hipStreamSynchronize(s));
-        const double err = check("tgemm");
-        const double us = time_graph([&](int i) { a.W = ws[i]; dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s, 0); });
-        char nm[96];
-        snprintf(nm, sizeof nm, "tgemm<%d,%d,st%d,nw%d>", p[0], p[1], p[2], p[5]);
-        report(nm, us, err);
       }
-      int tiled_bn = -1;
+      for (int pw = 0; pw < 2 && !skip_tg; ++pw) {
+        for (auto& p : tplans) {
+          dllm::GemmArgs a{};
+          a.A = A; a.lda = K; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.splits = p[3];
+          a.kchunk = (K / p[3] + 63) / 64 * 64;
+          if (a.kchunk * (p[3] - 1) >= K) continue;
+          a.part = g_part; a.counters = g_cnt; a.w_panel = pw;
+          auto& wsrc = pw ? wts : ws;
+          a.W = wsrc[0];
+          if (dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s, p[6]) != 0) continue;
+          CHECK(hipStreamSynchronize(s));
+          const double err = check("tgemm");
+          const double us = time_graph([&](int i) { a.W = wsrc[i]; dllm_tgemm(&a, p[0], p[1], p[2], p[4], p[5], 1, dllm::EPI_PLAIN, s, p[6]); });
+          char nm[128];
+          snprintf(nm, sizeof nm, "tgemm<%d,%d,st%d,S%d,ks%d,nw%d,nl%d>%s", p[0], p[1], p[2], p[3], p[4], p[5], p[6],
+                   pw ? " PANEL" : "");
+          report(nm, us, err);
+        }
+      }
+      int tiled_bn = -1;   // (wts now holds the panel copies: re-tiled on the first WT variant)
       for (auto& v : vars) {
         if (only_v && v.name.find(only_v) == std::string::npos) continue;
         if (v.wt && v.bn != tiled_bn) {

@@ -304,10 +304,10 @@ def test_cosine_kernels():
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 100, 128])
 @pytest.mark.parametrize("N,K", [(2560, 2048), (2048, 5632), (200, 96)])
 @pytest.mark.parametrize("ntw,splits", [(1, 1), (2, 4), (4, 8), (1, 16)])
-@pytest.mark.parametrize("kind", ["skinny", "lds"])
-def test_skinny_gemm(M, N, K, ntw, splits, kind):
+def test_skinny_gemm(M, N, K, ntw, splits):
     from distributed_llm_amd.ops import gemm
-    if (M > 64 and ntw == 4) or (kind == "lds" and (ntw == 4 or (M > 64 and ntw == 2))):
+    kind = "skinny"
+    if M > 64 and ntw == 4:
         pytest.skip("unsupported tile")
     torch.manual_seed(10)
     x, w = bf(M, K, scale=0.5), bf(N, K, scale=0.05)
@@ -320,9 +320,9 @@ def test_skinny_gemm(M, N, K, ntw, splits, kind):
 
 
 @pytest.mark.parametrize("M", [1, 64, 128])
-@pytest.mark.parametrize("kind", ["skinny", "lds"])
-def test_skinny_gemm_swiglu(M, kind):
+def test_skinny_gemm_swiglu(M):
     from distributed_llm_amd.ops import gemm
+    kind = "skinny"
     torch.manual_seed(11)
     I, H = 1024, 512
     gu, w = bf(M, 2 * I), bf(H, I, scale=0.05)
@@ -428,23 +428,6 @@ def test_moe_ffn_graph_capture():
         i2, w2_ = ref.moe_gate(logits, k)
         want = ref.moe_ffn(x, i2, w2_, w13, w2).float()
         assert (out.float() - want).abs().max().item() < 2e-2
-
-
-@pytest.mark.parametrize("M", [17, 64, 100, 128, 200, 256])
-@pytest.mark.parametrize("N,K,swiglu", [(2560, 2048, False), (2048, 1024, True), (200, 128, False)])
-@pytest.mark.parametrize("nt,splits", [(2, 1), (4, 1), (4, 2), (2, 8)])
-def test_mm_gemm(M, N, K, swiglu, nt, splits):
-    """Mid-size decode GEMM (csrc/kernels/mm_gemm.hip) vs fp32 reference, incl. split-K + SwiGLU."""
-    from distributed_llm_amd.ops import gemm
-    torch.manual_seed(12)
-    x = bf(M, 2 * K if swiglu else K, scale=0.5)
-    w = bf(N, K, scale=0.05)
-    y = gemm._run_plan(("mm", nt, splits), x, w, swiglu, None)
-    xa = ref.silu_mul(x).float() if swiglu else x.float()
-    yr = xa @ w.float().T
-    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
-    y2 = gemm._run_plan(("mm", nt, splits), x, w, swiglu, None)   # counters re-armed
-    assert torch.equal(y, y2)
 
 
 @pytest.mark.parametrize("H,lo,rows", [(2048, 0, 1000), (4096, 500, 300), (384, 0, 77)])
