@@ -72,6 +72,11 @@ def parse():
                     help="1: turn pipelining (replicated topology): conversations advance independently")
     ap.add_argument("--no-encoder-memo", action="store_true",
                     help="encode every routed query with the GPU MiniLM encoder (no per-text memo)")
+    ap.add_argument("--greedy", action="store_true",
+                    help="both tiers greedy (the large tier samples top-k 40 / top-p 0.9 at T 0.8 otherwise); "
+                         "for token-exact cross-topology checks")
+    ap.add_argument("--dump-responses", default=None,
+                    help="rank 0 writes every timed turn's (conversation, turn, tier, response text) as JSON here")
     ap.add_argument("--trace", default=None,
                     help="write a Chrome trace (router/pool/engine spans, GPU decode time) to this path; "
                          "'{rank}' is replaced by the rank")
@@ -118,7 +123,7 @@ class Conversations:
     def _new(self, i):
         return {"set": self.sets[i % 3], "turn": 0, "hist": [], "tag": f"[session r{self.rank}-{next(self._ids)}] "}
 
-    def step(self, router, records=None):
+    def step(self, router, records=None, dump=None):
         hs = []
         for c in self.convs:
             q = c["set"][c["turn"]].text
@@ -129,6 +134,8 @@ class Conversations:
         res = router.route_batch(hs)
         for i, (c, (payload, ntok, device)) in enumerate(zip(self.convs, res)):
             c["hist"].append({"role": "assistant", "content": payload["response"]})
+            if dump is not None:
+                dump.append([i, c["turn"], device, payload["response"]])
             if records is not None:
                 raw = payload.get("raw") or {}
                 records.append({"lat": float(raw.get("latency_ms", 0.0)) if isinstance(raw, dict) else 0.0,
@@ -310,6 +317,9 @@ def main() -> int:
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
 
+    # reference Orin defaults (Ollama: T 0.8, top-k 40, top-p 0.9); --greedy for exact comparisons
+    large_sampling = (dict(temperature=0.0, top_k=0, top_p=1.0) if a.greedy
+                      else dict(temperature=0.8, top_k=40, top_p=0.9))
     cluster = None
     if topology == "tiers":
         # heterogeneous tiers co-located on each GPU: a small-model engine and a large-model engine
@@ -322,10 +332,9 @@ def main() -> int:
         e_small = LLMEngine(sm, device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
                             use_graphs=not a.no_graphs, seed=0)
         e_large = LLMEngine(lg, device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
-                            use_graphs=not a.no_graphs, seed=1)
+                            use_graphs=not a.no_graphs, seed=0)   # seed 0 like the pools' engines
         pools = {SMALL: EnginePool(SMALL, e_small, max_new_tokens=a.small_new, temperature=0.0),
-                 LARGE: EnginePool(LARGE, e_large, max_new_tokens=a.large_new, temperature=0.8, top_k=40,
-                                   top_p=0.9)}
+                 LARGE: EnginePool(LARGE, e_large, max_new_tokens=a.large_new, **large_sampling)}
         if on_gpu:
             for e in (e_small, e_large):
                 e.capture_all(max_bs=e._bucket(max(16, a.convs)))
@@ -339,8 +348,7 @@ def main() -> int:
         engine = LLMEngine(model, device=dev, kv_cache_gb=a.kv_gb if on_gpu else 0.2,
                            max_num_seqs=max(16, a.convs), use_graphs=not a.no_graphs, seed=0)
         pools = {SMALL: EnginePool(SMALL, engine, max_new_tokens=a.small_new, temperature=0.0),
-                 LARGE: EnginePool(LARGE, engine, max_new_tokens=a.large_new, temperature=0.8, top_k=40,
-                                   top_p=0.9)}
+                 LARGE: EnginePool(LARGE, engine, max_new_tokens=a.large_new, **large_sampling)}
         if on_gpu:
             engine.capture_all(max_bs=engine._bucket(max(16, a.convs)))
         engines = [engine]
@@ -356,7 +364,8 @@ def main() -> int:
         graphs = not (a.no_graphs or rehearse)
         specs = {SMALL: TierSpec(sm, a.small_new, 0.0, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
                                  max_num_seqs=max(16, a.convs * world), graphs=graphs),
-                 LARGE: TierSpec(lg, a.large_new, 0.8, 40, 0.9, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
+                 LARGE: TierSpec(lg, a.large_new, large_sampling["temperature"], large_sampling["top_k"],
+                                 large_sampling["top_p"], kv_cache_gb=a.kv_gb if on_gpu else 0.1,
                                  max_num_seqs=max(16, a.convs * world), graphs=graphs)}
         cluster = Cluster(topo, specs, device=dev)
         engines = list(cluster.engines.values())
@@ -425,8 +434,12 @@ def main() -> int:
             enc0 = encoder_stats()
             sync()
             t0 = time.perf_counter()
+            dump = [] if a.dump_responses else None
             for _ in range(a.steps):
-                convs.step(router, records)
+                convs.step(router, records, dump)
+            if dump is not None:
+                with open(a.dump_responses, "w") as f:
+                    json.dump(dump, f)
             sync()
             elapsed = time.perf_counter() - t0
             st1 = [dict(e.stats()) for e in engines]

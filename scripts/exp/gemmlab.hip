@@ -406,7 +406,8 @@ int main(int argc, char** argv) {
     const int copies = std::max(2L, std::min(48L, (640L << 20) / (wel * 2)));
     std::vector<u16*> ws(copies), wts(copies);
     std::vector<u16> hw(wel);
-    u16 *A, *Y, *Wt_scratch;
+    u16 *A, *Y, *Wt_scratch, *Ap;
+    int apad = 0;
     float* Yr;
     CHECK(hipMalloc(&A, (long)MAXM * K * 2));
     CHECK(hipMalloc(&Y, (long)MAXM * N * 2));
@@ -416,6 +417,15 @@ int main(int argc, char** argv) {
       srand(1);
       for (auto& x : ha) { float f = (rand() / (float)RAND_MAX - 0.5f); uint32_t u; memcpy(&u, &f, 4); x = u >> 16; }
       CHECK(hipMemcpy(A, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+      // LAB_APAD: a row-padded copy of A (lda = K + pad elements) for the production tgemm runs
+      const char* ep = getenv("LAB_APAD");
+      apad = ep ? atoi(ep) : 0;
+      if (apad > 0) {
+        CHECK(hipMalloc(&Ap, (long)MAXM * (K + apad) * 2));
+        CHECK(hipMemcpy2D(Ap, (K + apad) * 2, A, K * 2, K * 2, MAXM, hipMemcpyDeviceToDevice));
+      } else {
+        Ap = A;
+      }
       for (auto& x : hw) { float f = (rand() / (float)RAND_MAX - 0.5f) * 0.05f; uint32_t u; memcpy(&u, &f, 4); x = u >> 16; }
     }
     for (int c = 0; c < copies; ++c) {
@@ -487,7 +497,7 @@ int main(int argc, char** argv) {
       for (int pw = 0; pw < 2 && !skip_tg; ++pw) {
         for (auto& p : tplans) {
           dllm::GemmArgs a{};
-          a.A = A; a.lda = K; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.splits = p[3];
+          a.A = Ap; a.lda = K + apad; a.Y = Y; a.ldy = N; a.M = M; a.N = N; a.K = K; a.splits = p[3];
           a.kchunk = (K / p[3] + 63) / 64 * 64;
           if (a.kchunk * (p[3] - 1) >= K) continue;
           a.part = g_part; a.counters = g_cnt; a.w_panel = pw;

@@ -123,7 +123,7 @@ int main(int argc, char** argv) {
       char* buf;
       CHECK(hipMalloc(&buf, bytes + (1 << 20)));
       CHECK(hipMemset(buf, 1, bytes + (1 << 20)));
-      for (long stride : {4096L, 11264L}) {
+      for (long stride : {4096L, 4352L, 4224L, 11264L, 11520L}) {
         run_rows<4, 8, 8>(buf, bytes, stride, out);
         run_rows<4, 8, 4>(buf, bytes, stride, out);
         run_rows<4, 8, 2>(buf, bytes, stride, out);

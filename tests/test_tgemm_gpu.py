@@ -285,3 +285,42 @@ def test_gemv_swiglu(M, R, H, I):
     want = ref.silu_mul((x.float() @ wgu.cpu().float().t()).to(torch.bfloat16))
     tol = max(3e-2, 8e-3 * want.abs().max().item())   # about 1 bf16 ulp of the largest output (test_gemv_qkv)
     torch.testing.assert_close(act.cpu().float(), want.float(), atol=tol, rtol=3e-2)
+
+
+@pytest.mark.parametrize("plan", PLANS)
+@pytest.mark.parametrize("M,N,K", [(37, 200, 384), (320, 2048, 2048)])
+def test_panel_weight_matches_row_major(plan, M, N, K):
+    """The K-panel-major weight copy (GemmArgs.w_panel) streams the same tiles in the same k order:
+    bit-identical outputs to the row-major weight for every plan, split-K included."""
+    torch.manual_seed(M * 7 + N)
+    G.reserve("cuda")
+    x, w = _rnd(M, K), _rnd(N, K, scale=0.05)
+    wp = G.panel_weight(w)
+    assert G._nk(wp) == (N, K)
+    a = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    b = torch.empty_like(a)
+    G._tgemm(_ext(), x, w, G.EPI_PLAIN, plan, y=a)
+    G._tgemm(_ext(), x, wp, G.EPI_PLAIN, plan, y=b)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M", [5, 200])
+def test_panel_weight_fused_epilogues(M):
+    """RESADD / SWIGLU / QKV through the fused ops with the panel copy (wp=) equal the row-major run."""
+    torch.manual_seed(21 + M)
+    G.reserve("cuda")
+    H, I, nq, nkv, d = 512, 768, 8, 2, 64
+    plan = G.tg_plan(M, 2 * I, H)
+    r0 = _rnd(M, H)
+    w_gu, w_o = _rnd(2 * I, H, scale=0.05), _rnd(H, I, scale=0.05)
+    ssq = torch.rand(3, M, device="cuda") * 10 + 1
+    outs = []
+    for panel in (False, True):
+        act = G.swiglu_matmul(r0, w_gu, ssq, 3, 1e-5, wp=G.panel_weight(w_gu) if panel else None)
+        r = r0.clone()
+        so = torch.zeros(64, M, device="cuda")
+        n = G.matmul_resadd(act, w_o, r, so, wp=G.panel_weight(w_o) if panel else None)
+        outs.append((act, r, so[:n]))
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    assert plan
