@@ -734,11 +734,12 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   check_bf16(w, "w");
   if (nl > 0) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
     const bool known = ks == 1 && wk == 1 &&
-                       ((bm == 64 && bn == 64 && nw == 4 && ((nl == 2 && stages == 4) || (nl == 4 && (stages == 4 || stages == 8)))) ||
-                        (bm == 128 && bn == 64 && nw == 4 && nl == 4 && stages == 4) ||
-                        (bm == 128 && bn == 128 && nw == 4 && nl == 4 && stages == 4) ||
-                        (bm == 160 && bn == 128 && nw == 8 && nl == 4 && stages == 3) ||
-                        (bm == 256 && bn == 128 && nw == 8 && nl == 4 && stages == 3));
+                       ((bm == 64 && bn == 64 && nw == 4 &&
+                         ((nl == 2 && stages == 4) || ((nl == 4 || nl == 8) && (stages == 4 || stages == 8)))) ||
+                        (bm == 128 && bn == 64 && nw == 4 && (nl == 4 || nl == 8) && stages == 4) ||
+                        (bm == 128 && bn == 128 && nw == 4 && (nl == 4 || nl == 8) && stages == 4) ||
+                        (bm == 160 && bn == 128 && nw == 8 && (nl == 4 || nl == 6) && stages == 3) ||
+                        (bm == 256 && bn == 128 && nw == 8 && (nl == 4 || nl == 8) && stages == 3));
     TORCH_CHECK(known, "tgemm: no loader-wave plan (", bm, "x", bn, ", ", stages, " stages, ", nw, "+", nl, " waves)");
   }
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x: 2-D row-major, 16-B aligned rows");

@@ -536,11 +536,26 @@ int by_tile_nl(int bm, int bn, int stages, int nw, int nl, const GemmArgs& a, hi
     if (nl == 4 && stages == 4) return launch_fit<64, 64, EPI, 4, 1, 4, 1, 4>(a, st);
     if (nl == 4 && stages == 8) return launch_fit<64, 64, EPI, 8, 1, 4, 1, 4>(a, st);
   }
-  if (bm == 128 && bn == 64 && nw == 4 && nl == 4 && stages == 4) return launch_fit<128, 64, EPI, 4, 1, 4, 1, 4>(a, st);
-  if (bm == 128 && bn == 128 && nw == 4 && nl == 4 && stages == 4) return launch_fit<128, 128, EPI, 4, 1, 4, 1, 4>(a, st);
-  if (bm == 160 && bn == 128 && nw == 8 && nl == 4 && stages == 3) return launch_fit<160, 128, EPI, 3, 1, 8, 1, 4>(a, st);
-  if (bm == 256 && bn == 128 && nw == 8 && nl == 4 && stages == 3)
-    return launch_fit<256, 128, EPI, 3, 1, 8, 1, 4, 4>(a, st);   // 4 x 2 compute waves of 64 x 64
+  if (bm == 64 && bn == 64 && nw == 4 && nl == 8) {   // 8 loader waves: ~2x a 4-loader CU's intake
+    if (stages == 4) return launch_fit<64, 64, EPI, 4, 1, 4, 1, 8>(a, st);
+    if (stages == 8) return launch_fit<64, 64, EPI, 8, 1, 4, 1, 8>(a, st);
+  }
+  if (bm == 128 && bn == 64 && nw == 4 && stages == 4) {
+    if (nl == 4) return launch_fit<128, 64, EPI, 4, 1, 4, 1, 4>(a, st);
+    if (nl == 8) return launch_fit<128, 64, EPI, 4, 1, 4, 1, 8>(a, st);
+  }
+  if (bm == 128 && bn == 128 && nw == 4 && stages == 4) {
+    if (nl == 4) return launch_fit<128, 128, EPI, 4, 1, 4, 1, 4>(a, st);
+    if (nl == 8) return launch_fit<128, 128, EPI, 4, 1, 4, 1, 8>(a, st);
+  }
+  if (bm == 160 && bn == 128 && nw == 8 && stages == 3) {
+    if (nl == 4) return launch_fit<160, 128, EPI, 3, 1, 8, 1, 4>(a, st);
+    if (nl == 6) return launch_fit<160, 128, EPI, 3, 1, 8, 1, 6>(a, st);
+  }
+  if (bm == 256 && bn == 128 && nw == 8 && stages == 3) {   // 4 x 2 compute waves of 64 x 64
+    if (nl == 4) return launch_fit<256, 128, EPI, 3, 1, 8, 1, 4, 4>(a, st);
+    if (nl == 8) return launch_fit<256, 128, EPI, 3, 1, 8, 1, 8, 4>(a, st);
+  }
   return -22;
 }
 

@@ -48,8 +48,12 @@ _TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8
 _TG_SPLITS = (1, 2, 3, 4, 6, 8)
 # loader-wave plans (csrc/kernels/tgemm.hip by_tile_nl): (bm, bn, compute waves, stages, loader waves);
 # M is the smallest batch each is tried at (larger tiles only pay once M fills them)
+# (8 loader waves: a CU's LDS-DMA intake grows with the waves issuing it, ~75 GB/s at 4 and ~140 GB/s
+# at 8 on contiguous pieces, scripts/exp/intake.hip; profiles/r3_decode_gemm_panel.md)
 _TG_NL = ((64, 64, 4, 4, 2, 1), (64, 64, 4, 4, 4, 1), (64, 64, 4, 8, 4, 1), (128, 64, 4, 4, 4, 65),
-          (128, 128, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129))
+          (128, 128, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
+          (64, 64, 4, 4, 8, 1), (64, 64, 4, 8, 8, 1), (128, 64, 4, 4, 8, 65), (128, 128, 4, 4, 8, 65),
+          (160, 128, 8, 3, 6, 129), (256, 128, 8, 3, 8, 129))
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
 WS_COUNTERS = 1 << 16
 

@@ -486,7 +486,10 @@ int main(int argc, char** argv) {
                                {64, 64, 3, 2, 2, 4, 0}, {64, 128, 3, 1, 2, 8, 0}, {64, 64, 4, 1, 1, 4, 2},
                                {64, 64, 4, 1, 1, 4, 4}, {64, 64, 8, 1, 1, 4, 4}, {128, 64, 4, 1, 1, 4, 4},
                                {128, 128, 4, 1, 1, 4, 4}, {160, 128, 3, 1, 1, 8, 4}, {256, 128, 3, 1, 1, 8, 4},
-                               {64, 64, 4, 2, 1, 4, 4}, {128, 64, 4, 2, 1, 4, 4}, {64, 64, 4, 3, 1, 4, 4}};
+                               {64, 64, 4, 2, 1, 4, 4}, {128, 64, 4, 2, 1, 4, 4}, {64, 64, 4, 3, 1, 4, 4},
+                               {64, 64, 4, 1, 1, 4, 8}, {64, 64, 8, 1, 1, 4, 8}, {128, 64, 4, 1, 1, 4, 8},
+                               {128, 128, 4, 1, 1, 4, 8}, {160, 128, 3, 1, 1, 8, 6}, {256, 128, 3, 1, 1, 8, 8},
+                               {64, 64, 4, 2, 1, 4, 8}, {128, 64, 4, 2, 1, 4, 8}, {64, 64, 8, 2, 1, 4, 8}};
       if (!skip_tg) {
         for (int c = 0; c < copies; ++c) {
           const long chunks = wel / 8;
