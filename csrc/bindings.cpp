@@ -729,7 +729,8 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
            c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> pos,
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
-           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk, int64_t nl) {
+           int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk, int64_t nl,
+           c10::optional<torch::Tensor> sk_table, int64_t sk_cmax) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   if (nl > 0) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
@@ -769,7 +770,23 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   a.W = (const uint16_t*)w.data_ptr();
   a.M = M; a.N = N; a.K = K; a.kchunk = kchunk; a.splits = S;
   a.w_panel = panel ? 1 : 0;
-  if (S > 1) {
+  if (sk_table.has_value()) {   // stream-K: the host-built segment lists (ops.gemm.stream_k_table)
+    check_i32(*sk_table, "sk_table");
+    TORCH_CHECK(sk_table->dim() == 3 && sk_table->size(2) == 4 && sk_table->is_contiguous() &&
+                    sk_table->size(0) >= 1 && sk_table->size(1) >= 1 && sk_cmax >= 1 && splits == 1,
+                "sk_table [grid, segments, 4] int32, splits 1");
+    TORCH_CHECK(part.has_value() && counters.has_value(), "stream-K needs part/counters workspaces");
+    check_f32(*part, "part");
+    check_i32(*counters, "counters");
+    TORCH_CHECK(part->numel() >= sk_cmax * tiles * bm * bn && counters->numel() >= tiles,
+                "stream-K workspace too small");
+    a.part = part->data_ptr<float>();
+    a.counters = counters->data_ptr<int>();
+    a.sk_table = sk_table->data_ptr<int>();
+    a.sk_grid = (int)sk_table->size(0);
+    a.sk_segmax = (int)sk_table->size(1);
+    a.sk_cmax = (int)sk_cmax;
+  } else if (S > 1) {
     TORCH_CHECK(part.has_value() && counters.has_value(), "split-K needs part/counters workspaces");
     check_f32(*part, "part");
     check_i32(*counters, "counters");

@@ -85,8 +85,12 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + er
 // At decode-size M a stage's fill and its MFMA chain then overlap instead of alternating inside
 // each wave (profiles/r3_decode_gemm_lab.md: 5-30 % faster on the TinyLlama / Llama-3-8B decode
 // projections at M = 320-512).
-template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
-__global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) {
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK, int NL, int WGM>
+__device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* smem, int M, const int S,
+                                           const int SC, const int split, const int m_tile,
+                                           const int n_tile, const int kbeg, const int nk) {
+  // one (tile, k range) unit: the whole body of a one-unit workgroup, or one segment of a
+  // stream-K workgroup (SC: slab slots per tile in the split-K workspace)
   static_assert(WK == 1 || (WK == 2 && KS == 2), "k-groups split the KS sub-tiles of a stage");
   static_assert(NL == 0 || WK == 1, "loader waves or k-groups, not both");
   constexpr int NC = NW * WK, NT = 64 * (NC + NL), NWN = NW / WGM;  // NT: threads of the block
@@ -108,7 +112,6 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
   constexpr int TPR = NT >= BM ? NT / BM : 1;  // threads per row in the rinv reduction
   // one LDS array (a second __shared__ object can make hipcc drain the ring: §5 trap 4(a))
   //   [ring][rinv partials TPR x BM][row-sum partials 2 x BM][flag]
-  __shared__ __attribute__((aligned(16))) unsigned char smem[RING + TPR * BM * 4 + 2 * BM * 4 + 16];
   float* s_rsp = reinterpret_cast<float*>(smem + RING);
   float* s_red = s_rsp + TPR * BM;
   int* s_last = reinterpret_cast<int*>(s_red + 2 * BM);
@@ -118,15 +121,8 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
   const int kg = loader ? 0 : wid / NW, wave = loader ? 0 : wid % NW;
   const int wm = wave / NWN, wn = wave % NWN;
   const bool fw = ((WK == 1) || kg == 0) && !loader;  // this wave owns the final accumulators
-  const int N = a.N, K = a.K, S = a.splits;
-  int M = a.M;
-  const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
-  const int nwg = mt * nt * S;
-  // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD -> contiguous logical ids)
-  const int bid = blockIdx.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = wgid % S, rest = wgid / S;
-  const int m_tile = rest % mt, n_tile = rest / mt;
+  const int N = a.N, K = a.K;
+  const int mt = (a.M + BM - 1) / BM, nt = (N + BN - 1) / BN;
   int m0 = m_tile * BM;
   const int n0 = n_tile * BN;
   const u16* Wb = a.W;
@@ -136,8 +132,6 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
     M = m0 + a.g_tiles[2 * a.g_max + m_tile];
     Wb = a.W + (long)a.g_tiles[m_tile] * a.g_wstride;
   }
-  const int kbeg = split * a.kchunk;
-  const int nk = max(0, (min(K, kbeg + a.kchunk) - kbeg) / KSTEP);
 
   // ---- row-scale prologue: the partial-sum loads are issued before the ring so they retire at
   // the ring's first wait; their sums go to LDS and are combined per row in the epilogue
@@ -307,9 +301,9 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
   if (S > 1) {
     const int tile_id = n_tile * mt + m_tile;
     const long slab = (long)BM * BN;
-    const unsigned bytes = (unsigned)min((long)mt * nt * S * slab * 4, 0x7fffffffL);
+    const unsigned bytes = (unsigned)min((long)mt * nt * SC * slab * 4, 0x7fffffffL);
     const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.part, bytes);
-    const long my = ((long)tile_id * S + split) * slab;
+    const long my = ((long)tile_id * SC + split) * slab;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -328,7 +322,7 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
           const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           for (int sp = 0; sp < S; ++sp) {
-            const float4 q = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
+            const float4 q = ld_wt16(pr, (unsigned)((((long)tile_id * SC + sp) * slab + (long)c * BM + r) * 4));
             v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
           }
           acc[i][j] = v;
@@ -346,7 +340,7 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             const int r = wm * WM + 16 * i + 4 * (lane >> 4), c = wn * WN + 16 * j + (lane & 15);
-            q[i][j] = ld_wt16(pr, (unsigned)((((long)tile_id * S + sp) * slab + (long)c * BM + r) * 4));
+            q[i][j] = ld_wt16(pr, (unsigned)((((long)tile_id * SC + sp) * slab + (long)c * BM + r) * 4));
           }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -511,12 +505,76 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
   }
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false>
+__global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) {
+  static_assert(WK == 1 || (WK == 2 && KS == 2), "k-groups split the KS sub-tiles of a stage");
+  static_assert(NL == 0 || WK == 1, "loader waves or k-groups, not both");
+  constexpr int NC = NW * WK, NT = 64 * (NC + NL), NWN = NW / WGM;  // NT: threads of the block
+  constexpr int WM = BM / WGM, WN = BN / NWN;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  static_assert(FN % 2 == 0 && FM >= 1 && WM % 16 == 0 && NW % WGM == 0, "wave tile: >= 16 rows, a multiple of 32 columns");
+  constexpr int A_BYTES = BM * ROWB, SUB_BYTES = (BM + BN) * ROWB, STAGE_BYTES = KS * SUB_BYTES;
+  constexpr int GA = NL ? 1 : BM / (8 * NW), GB = NL ? 1 : BN / (8 * NW);  // global_load_lds per wave per sub-tile
+  constexpr int PPS = KS * (BM + BN) / 8;                                  // 1 KB pieces per stage
+  constexpr int GL = NL ? PPS / NL : 1;                                    // ... per loader wave
+  static_assert(NL == 0 || PPS % NL == 0, "stage pieces must split evenly over the loader waves");
+  constexpr int G = NL ? GL : (KS / WK) * (GA + GB);     // ring loads per (issuing) wave per stage
+  static_assert(NL > 0 || (GA >= 1 && GB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0),
+                "tile too small for the wave count");
+  constexpr int KSTEP = BK * KS;
+  constexpr int OW = (EPI == EPI_SWIGLU) ? BN / 2 : BN;  // staged output columns per row
+  constexpr int OLD = OW + 8;                             // staged row stride (bf16)
+  constexpr int RING = (STAGES * STAGE_BYTES > BM * OLD * 2) ? STAGES * STAGE_BYTES : BM * OLD * 2;
+  constexpr int TPR = NT >= BM ? NT / BM : 1;  // threads per row in the rinv reduction
+  // one LDS array (a second __shared__ object can make hipcc drain the ring: §5 trap 4(a))
+  //   [ring][rinv partials TPR x BM][row-sum partials 2 x BM][flag]
+  __shared__ __attribute__((aligned(16))) unsigned char smem[RING + TPR * BM * 4 + 2 * BM * 4 + 16];
+  const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
+  const int bid = blockIdx.x;
+  // Stream-K (SK, a.sk_table): a grid of about one workgroup per CU, each walking its host-built
+  // list of (tile, k-step range) segments, so an output-tile count that is not a multiple of the CU
+  // count (M = 320: 160 tiles of 64 x 64 for N = 2048) no longer idles the rest of the chip; a tile
+  // split over several workgroups is combined by its last arriver from the write-through slabs in a
+  // fixed order (ops.gemm.stream_k_table).  Otherwise exactly one (tile, split) unit per workgroup.
+  if constexpr (!SK) {
+    const int S = a.splits;
+    // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD -> contiguous logical ids)
+    const int nwg = mt * nt * S, q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int split = wgid % S, rest = wgid / S;
+    const int kbeg = split * a.kchunk;
+    tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM>(a, smem, a.M, S, S, split, rest % mt, rest / mt, kbeg,
+                                                        max(0, (min(a.K, kbeg + a.kchunk) - kbeg) / KSTEP));
+  } else {
+    const int ng = gridDim.x, q8 = ng >> 3, r8 = ng & 7, xcd = bid & 7;
+    const int wl = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    for (int sg = 0; sg < a.sk_segmax; ++sg) {
+      const int4 e = *reinterpret_cast<const int4*>(a.sk_table + ((long)wl * a.sk_segmax + sg) * 4);
+      if (e.x < 0) break;   // block-uniform: this workgroup's list ended
+      tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM>(a, smem, a.M, e.w >> 16, a.sk_cmax, e.w & 0xffff, e.x % mt,
+                                                          e.x / mt, e.y * KSTEP, e.z - e.y);
+      __syncthreads();   // the next segment re-uses the ring, the row-scale partials and the flag
+    }
+  }
+}
+
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false>
 int launch_t(const GemmArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>), dim3(mt * nt * a.splits),
+  const int grid = SK ? a.sk_grid : mt * nt * a.splits;
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, SK>), dim3(grid),
                      dim3(64 * (NW * WK + NL)), 0, st, a);
   return (int)hipGetLastError();
+}
+
+// the stream-K instantiations: the one-split plans the autotuner pairs with a stream-K table
+// (ops.gemm._tg_cands); any other plan asked for in stream-K mode is refused (-25)
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK, int NL, int WGM>
+constexpr bool sk_plan() {
+  return WK == 1 && ((BM == 64 && BN == 64 && ((NL == 0 && NW == 4 && ((ST == 3 && KS == 2) || (ST == 4 && KS == 1))) ||
+                                              (NL == 4 && ST == 4) || (NL == 8 && ST == 4))) ||
+                     (BM == 64 && BN == 128 && NL == 0 && NW == 8 && ST == 3 && KS == 1) ||
+                     (BM == 128 && BN == 64 && NL == 4 && ST == 4));   // (160 x 128 spilled in the segment loop)
 }
 
 template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
@@ -524,6 +582,12 @@ int launch_fit(const GemmArgs& a, hipStream_t st) {
   if constexpr (ST * KS * (BM + BN) * ROWB > 150 * 1024) {
     return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
   } else {
+    if (a.sk_table != nullptr) {
+      if constexpr (sk_plan<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>())
+        return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, true>(a, st);
+      else
+        return -25;
+    }
     return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>(a, st);
   }
 }
@@ -769,6 +833,9 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
                           hipStream_t stream, int nl) {
   const GemmArgs& a = *reinterpret_cast<const GemmArgs*>(args);
   if (a.M <= 0 || a.N <= 0) return 0;
+  if (a.sk_table != nullptr && (!a.part || !a.counters || a.sk_grid < 1 || a.sk_segmax < 1 || a.sk_cmax < 1 ||
+                                a.g_tiles != nullptr || a.splits != 1))
+    return -24;
   if (nl > 0) {   // loader-wave plans: KS 1, one k-group, no MoE gather
     if (ks != 1 || wk != 1 || a.g_tiles != nullptr || a.K % BK || a.kchunk % BK || a.kchunk <= 0 || a.splits < 1 ||
         a.lda % 8 || a.N % 8 || (a.Y && a.ldy % 8))

@@ -46,6 +46,12 @@ struct GemmArgs {
   // weight stream instead of eight 128-B pieces 2K-11K bytes apart (HBM pages / L2 channels);
   // repacked once at load time (models/llama.py).  Not with the grouped (MoE) mode.
   int w_panel;
+  // Stream-K decomposition (ops.gemm.stream_k_table): sk_grid workgroups, workgroup L (the
+  // XCD-remapped block id) walks sk_table[L][0 .. sk_segmax) = int4 (tile, first k-step, end
+  // k-step, slab index | contributors << 16), tile < 0 ends its list; split-K slabs hold sk_cmax
+  // slots per tile.  Null: one (tile, split) unit per workgroup.
+  const int* sk_table;
+  int sk_grid, sk_segmax, sk_cmax;
 };
 enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_GELU = 4 };
 }  // namespace dllm

@@ -54,6 +54,9 @@ _TG_NL = ((64, 64, 4, 4, 2, 1), (64, 64, 4, 4, 4, 1), (64, 64, 4, 8, 4, 1), (128
           (128, 128, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
           (64, 64, 4, 4, 8, 1), (64, 64, 4, 8, 8, 1), (128, 64, 4, 4, 8, 65), (128, 128, 4, 4, 8, 65),
           (160, 128, 8, 3, 6, 129), (256, 128, 8, 3, 8, 129))
+# one-split plans with a stream-K instantiation (csrc/kernels/tgemm.hip sk_plan): (bm, bn, stages, ks, waves, loaders)
+_SK_PLANS = {(64, 64, 3, 2, 4, 0), (64, 64, 4, 1, 4, 0), (64, 64, 4, 1, 4, 4), (64, 64, 4, 1, 4, 8),
+             (64, 128, 3, 1, 8, 0), (128, 64, 4, 1, 4, 4)}
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
 WS_COUNTERS = 1 << 16
 
@@ -96,6 +99,7 @@ class _Planner:
         self.fused_core: Dict[Tuple[int, int, int], str] = {}        # "tg" | "lin" | "gemvR" per tuned shape
         self.fused_opts: Dict[Tuple[int, int, int], Dict[str, float]] = {}   # measured us per core choice
         self.ws: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self.sk_tables: Dict[Tuple, Tuple[torch.Tensor, int]] = {}   # stream-K segment lists per shape
         self.timings: Dict[Tuple[int, int, int, bool], Dict[str, float]] = {}
 
     def workspace(self, dev: torch.device, floats: int, tiles: int):
@@ -209,23 +213,81 @@ def _run_plan(plan, x, w, swiglu, out, wp=None):
     return y
 
 
+def stream_k_table(M: int, N: int, K: int, bm: int, bn: int, ks: int, grid: int):
+    """Stream-K work split of an (M, N, K) GEMM over ``grid`` workgroups (csrc/kernels/tgemm.hip,
+    GemmArgs.sk_table): the tiles x k-steps iteration space is cut into ``grid`` equal contiguous
+    ranges; workgroup w walks its range as segments (tile, first k-step, end k-step, slab index |
+    contributors << 16).  A tile covered by c workgroups gets slab indices 0..c-1 in k order, so its
+    last arriver sums the partials in the same order every time.  Returns (int32 [grid, segmax, 4]
+    array padded with tile -1, cmax = the largest contributor count)."""
+    import numpy as np
+    mt, nt = -(-M // bm), -(-N // bn)
+    tiles, nkt = mt * nt, K // (64 * ks)
+    total = tiles * nkt
+    segs = [[] for _ in range(grid)]
+    contrib: Dict[int, list] = {}
+    for w in range(grid):
+        it, hi = w * total // grid, (w + 1) * total // grid
+        while it < hi:
+            t, kb = divmod(it, nkt)
+            ke = min(nkt, kb + hi - it)
+            segs[w].append([t, kb, ke, 0])
+            contrib.setdefault(t, []).append((w, len(segs[w]) - 1))
+            it += ke - kb
+    cmax = max(len(v) for v in contrib.values())
+    for t, lst in contrib.items():
+        for idx, (w, j) in enumerate(lst):
+            segs[w][j][3] = idx | (len(lst) << 16)
+    segmax = max(1, max(len(s_) for s_ in segs))
+    tab = np.full((grid, segmax, 4), -1, dtype=np.int32)
+    for w, sl in enumerate(segs):
+        if sl:
+            tab[w, :len(sl)] = np.asarray(sl, dtype=np.int32)
+    return tab, cmax
+
+
+def _sk_grid(dev) -> int:
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def _sk_tensor(dev, M, N, K, bm, bn, ks):
+    """The device copy of a stream-K table, created once per shape outside graph capture (the
+    engine's capture warm-up runs every step eagerly first) and kept for the process lifetime."""
+    key = (str(dev), M, N, K, bm, bn, ks)
+    hit = _P.sk_tables.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("stream-K table first needed during graph capture (run the step eagerly first)")
+        tab, cmax = stream_k_table(M, N, K, bm, bn, ks, _sk_grid(dev))
+        hit = (torch.from_numpy(tab).to(dev), cmax)
+        _P.sk_tables[key] = hit
+    return hit
+
+
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
            pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None):
-    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves]]])"""
+    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves[, stream-K]]]])"""
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     wk = plan[6] if len(plan) >= 7 else 1
     nl = plan[7] if len(plan) >= 8 else 0
+    sk = len(plan) >= 9 and plan[8] == 1
     M = x.shape[0]
     N, K = _nk(w)
     if K % (64 * ks):
         ks, wk = 1, 1
-    part = cnt = None
-    if _tg_splits(K, sp, ks) > 1:
+    part = cnt = tab = None
+    cmax = 0
+    if sk:
+        tab, cmax = _sk_tensor(x.device, M, N, K, bm, bn, ks)
+        tiles = -(-M // bm) * -(-N // bn)
+        part, cnt = _P.workspace(x.device, tiles * cmax * bm * bn, tiles)
+        sp = 1
+    elif _tg_splits(K, sp, ks) > 1:
         floats, tiles = _need_tg(M, N, K, bm, bn, sp, ks)
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
-              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl))
+              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl), tab, int(cmax))
 
 
 def ref_silu_mul(gu):
@@ -575,6 +637,21 @@ def _tg_cands(M: int, N: int, K: int):
                 if _need_tg(M, N, K, bm, bn, sp)[0] > WS_FLOATS:
                     continue
                 out.append((bm, bn, st, sp, 1, nw, 1, nl))
+    # stream-K forms (one workgroup per CU walking equal shares of tiles x k-steps) of the one-split
+    # plans whose tile count leaves CUs idle: M = 320 gives a 64 x 64 grid 160 tiles for N = 2048
+    if torch.cuda.is_available() and os.environ.get("DLLM_TG_SK", "1") == "1":
+        g = _sk_grid(torch.cuda.current_device())
+        for c in list(out):
+            bm, bn, st, sp, ks, nw = c[:6]
+            if sp != 1 or (len(c) >= 7 and c[6] != 1):
+                continue
+            tiles = -(-M // bm) * -(-N // bn)
+            if tiles % g == 0 or tiles >= 2 * g or tiles * (K // (64 * ks)) < 2 * g:
+                continue
+            nl = c[7] if len(c) >= 8 else 0
+            if (bm, bn, st, ks, nw, nl) not in _SK_PLANS:
+                continue
+            out.append((bm, bn, st, 1, ks, nw, 1, nl, 1))
     return out
 
 

@@ -324,3 +324,60 @@ def test_panel_weight_fused_epilogues(M):
     for u, v in zip(*outs):
         assert torch.equal(u, v)
     assert plan
+
+
+SK_PLANS = sorted((bm, bn, st, 1, ks, nw, 1, nl, 1) for bm, bn, st, ks, nw, nl in G._SK_PLANS)
+
+
+@pytest.mark.parametrize("plan", SK_PLANS)
+@pytest.mark.parametrize("M,N,K", [(320, 2048, 2048), (37, 200, 384), (130, 320, 1024), (300, 2560, 5632)])
+def test_stream_k_plain(plan, M, N, K):
+    """Stream-K (one workgroup per CU walking equal shares of tiles x k-steps, tiles split over
+    workgroups combined by their last arriver) against the fp32 reference; deterministic sums."""
+    torch.manual_seed(M + 3 * N + K)
+    G.reserve("cuda")
+    x, w = _rnd(M, K), _rnd(N, K, scale=0.05)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    G._tgemm(_ext(), x, w, G.EPI_PLAIN, plan, y=y)
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), want, atol=2e-2 * want.abs().max().item(), rtol=2e-2)
+    y2 = torch.empty_like(y)
+    G._tgemm(_ext(), x, G.panel_weight(w), G.EPI_PLAIN, plan, y=y2)   # tickets re-armed, panel weights
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("plan", SK_PLANS)
+def test_stream_k_fused_epilogues(plan, monkeypatch):
+    """RESADD (+ row sums), SwiGLU and QKV (+ RoPE, paged K/V) epilogues under a stream-K plan
+    equal the same ops under a one-unit plan up to the fp32 summation order."""
+    torch.manual_seed(77)
+    G.reserve("cuda")
+    M, H, I = 320, 512, 1024
+    nq, nkv, d = 8, 2, 64
+    base = (plan[0], plan[1], plan[2], 1, plan[4], plan[5], 1, plan[7])
+    r0, w_gu, w_d = _rnd(M, H), _rnd(2 * I, H, scale=0.05), _rnd(H, I, scale=0.05)
+    wqkv = _rnd((nq + 2 * nkv) * d, H, scale=0.05)
+    ssq = torch.rand(4, M, device="cuda") * 10 + 1
+    pos = torch.randint(0, 1000, (M,), dtype=torch.int32, device="cuda")
+    cos_sin = ops.rope_cos_sin(2048, d, 10000.0, torch.device("cuda"))
+    nb = M // 16 + 2
+    slots = torch.randperm(nb * 16, device="cuda")[:M].to(torch.int32)
+    outs = []
+    for p in (base, plan):
+        for key in ((M, 2 * I, H), (M, H, I), (M, wqkv.shape[0], H)):
+            G._P.tg_plans[key] = p
+            G._P.fused_core[key] = "tg"
+        act = G.swiglu_matmul(r0, w_gu, ssq, 4, 1e-5)
+        r = r0.clone()
+        so = torch.zeros(64, M, device="cuda")
+        n = G.matmul_resadd(act, w_d, r, so)
+        kc = torch.zeros(nb, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
+        vc = torch.zeros(nb, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
+        q = G.qkv_rope_cache(r0, wqkv, ssq, 4, 1e-5, pos, cos_sin, slots, kc, vc, nq, nkv, d)
+        outs.append((act, r, so[:n], q, kc, vc))
+    for key in ((M, 2 * I, H), (M, H, I), (M, wqkv.shape[0], H)):
+        G._P.tg_plans.pop(key, None)
+        G._P.fused_core.pop(key, None)
+    for a_, b_ in zip(*outs):
+        torch.testing.assert_close(a_.float(), b_.float(), atol=2e-2 * (a_.float().abs().max().item() + 1e-6),
+                                   rtol=2e-2)
