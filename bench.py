@@ -385,12 +385,25 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
+    # this rank's GPU energy over the timed window (amdsmi's cumulative energy counter; no sampling
+    # thread): board energy per generated token next to the reference's J/token
+    meter, smi_idx, e0 = None, None, None
+    if on_gpu:
+        from distributed_llm_amd.bench.power import PowerSampler, smi_index_for_cuda
+        smi_idx = smi_index_for_cuda(local)
+        meter = PowerSampler(gpus=[smi_idx])
+        if not meter.available:
+            meter = None
     records = []
     tokens = 0
     elapsed = 0.0
     st0 = st1 = None
+    e1 = None
     if cluster is not None and rank != 0:
+        if meter:
+            e0 = meter.mark()
         cluster.serve()  # returns when the router stops the pools
+        e1 = meter.mark() if meter else None
         ts = cluster.sync_times
         elapsed = ts[-1] - ts[-2] if len(ts) >= 2 else 0.0
     else:
@@ -418,6 +431,7 @@ def main() -> int:
                 enc0 = encoder_stats()
                 if on_gpu:
                     torch.cuda.synchronize()
+                e0 = meter.mark() if meter else None
                 t0 = time.perf_counter()
                 convs.records = records
             convs.wait_turns((a.warmup + a.steps) * n_convs)
@@ -426,6 +440,7 @@ def main() -> int:
                 if on_gpu:
                     torch.cuda.synchronize()
                 elapsed = time.perf_counter() - t0
+                e1 = meter.mark() if meter else None
                 st1 = [dict(e.stats()) for e in engines]
                 enc1 = encoder_stats()
             convs.stop()
@@ -433,6 +448,7 @@ def main() -> int:
             st0 = [dict(e.stats()) for e in engines]
             enc0 = encoder_stats()
             sync()
+            e0 = meter.mark() if meter else None
             t0 = time.perf_counter()
             dump = [] if a.dump_responses else None
             for _ in range(a.steps):
@@ -442,6 +458,7 @@ def main() -> int:
                     json.dump(dump, f)
             sync()
             elapsed = time.perf_counter() - t0
+            e1 = meter.mark() if meter else None
             st1 = [dict(e.stats()) for e in engines]
             enc1 = encoder_stats()
         if cluster is not None:
@@ -450,11 +467,18 @@ def main() -> int:
             e.stop()
         tokens = sum(r["tok"] for r in records)
     lats = sorted(r["lat"] for r in records)
+    energy_j = -1.0
+    if meter and e0 is not None and e1 is not None:
+        mj, how = meter.energy_between([smi_idx], e0, e1)
+        energy_j = mj / 1000.0 if how == "counter" else -1.0
     if world > 1:
-        t = torch.tensor([float(tokens), elapsed], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([float(tokens), elapsed, energy_j, 1.0 if energy_j < 0 else 0.0], dtype=torch.float64,
+                         device=coll_dev)
         dist.all_reduce(t[:1], op=dist.ReduceOp.SUM)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[2:], op=dist.ReduceOp.SUM)
         tokens_all, elapsed_max = float(t[0]), float(t[1])
+        energy_j = float(t[2]) if float(t[3]) == 0 else -1.0
         gathered = [None] * world
         dist.all_gather_object(gathered, lats)
         lats = sorted(x for g in gathered for x in g)
@@ -511,6 +535,11 @@ def main() -> int:
                                     for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
                                               "t_decode_host_post_s", "t_encode_s", "t_admit_s", "t_output_s")},
         }
+        if energy_j >= 0:
+            # every rank's GPU over the timed window (energy counter deltas summed over ranks)
+            out["gpu_energy_j"] = round(energy_j, 1)
+            out["avg_gpu_power_w"] = round(energy_j / max(elapsed_max, 1e-9) / world, 1)
+            out["j_per_token"] = round(energy_j / max(tokens_all, 1.0), 4)
         if rehearse:
             out["rehearsal_one_gpu"] = True   # N ranks shared ONE GPU: plumbing check, not a number
         # rank-0 wall time not inside any engine timer: routing, prompt formatting, orchestration

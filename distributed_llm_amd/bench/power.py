@@ -133,6 +133,25 @@ class PowerSampler:
         return sum(energy_for_window_trapz(self.samples.get(g, []), start, end) for g in gpus)
 
 
+def smi_index_for_cuda(device: int) -> int:
+    """amdsmi processor index of HIP device ``device`` (matched by PCI bus id: amdsmi lists every
+    GPU the driver sees, HIP only the visible ones), falling back to the HIP index."""
+    try:
+        import amdsmi
+        import torch
+        props = torch.cuda.get_device_properties(device)
+        want = (getattr(props, "pci_domain_id", 0), props.pci_bus_id, props.pci_device_id)
+        amdsmi.amdsmi_init()
+        for i, h in enumerate(amdsmi.amdsmi_get_processor_handles()):
+            bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)          # "dddd:bb:dd.f"
+            dom, bus, rest = bdf.split(":")
+            if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                return i
+    except Exception:
+        pass
+    return device
+
+
 class EnergyMark:
     """Wall time plus each GPU's energy counter (mJ, or None) at one instant."""
     __slots__ = ("time", "counters")
