@@ -638,8 +638,11 @@ def _tg_cands(M: int, N: int, K: int):
                     continue
                 out.append((bm, bn, st, sp, 1, nw, 1, nl))
     # stream-K forms (one workgroup per CU walking equal shares of tiles x k-steps) of the one-split
-    # plans whose tile count leaves CUs idle: M = 320 gives a 64 x 64 grid 160 tiles for N = 2048
-    if torch.cuda.is_available() and os.environ.get("DLLM_TG_SK", "1") == "1":
+    # plans whose tile count leaves CUs idle (M = 320 gives a 64 x 64 grid 160 tiles for N = 2048).
+    # Opt-in (DLLM_TG_SK=1): measured, they never beat the one-unit plans on the TinyLlama shapes at
+    # M = 320-448, because the shared-operand L2 -> LDS traffic, not the idle CUs, sets the time
+    # (profiles/r3_decode_gemm_panel.md section 5)
+    if torch.cuda.is_available() and os.environ.get("DLLM_TG_SK", "0") == "1":
         g = _sk_grid(torch.cuda.current_device())
         for c in list(out):
             bm, bn, st, sp, ks, nw = c[:6]
