@@ -2,7 +2,7 @@
 
 ``bench.py --gpus N --topology pools`` puts the small and large tiers on disjoint ranks (BASELINE
 configs 3-5; parallel/cluster.py): N = 2 is small | large, N = 4 is two small replicas + the large
-tier tensor-parallel over two ranks.  No multi-GPU box is available to these tests, so the ranks
+tier tensor-parallel over two ranks, N = 8 four small replicas + the large tier at TP = 4.  No multi-GPU box is available to these tests, so the ranks
 share cuda:0 (``DLLM_REHEARSE_ONE_GPU=1``: gloo process groups, the one-shot IPC all-reduce for the
 TP pool) and run through ``torch.distributed.run`` exactly as the driver launches it.
 
@@ -25,9 +25,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
-STEPS, WARMUP, CONVS = 4, 0, 12
+STEPS, WARMUP, CONVS = 4, 0, 24
 COMMON = ["--steps", str(STEPS), "--warmup", str(WARMUP), "--kv-gb", "4", "--small-model", "tinyllama-1.1b",
-          "--large-model", "llama-3.2-1b", "--small-new", "16", "--large-new", "24", "--greedy", "--no-graphs"]
+          "--large-model", "llama-3.2-1b", "--small-new", "16", "--large-new", "24", "--greedy", "--no-graphs",
+          "--strategy", "hybrid"]
 
 
 def _port():
@@ -60,7 +61,7 @@ def single(tmp_path_factory):
     return res, json.load(open(dump))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_pools_topology_n_ranks_one_gpu(world, single, tmp_path):
     logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
     os.makedirs(logdir, exist_ok=True)
@@ -70,9 +71,9 @@ def test_pools_topology_n_ranks_one_gpu(world, single, tmp_path):
                 "--topology", "pools", "--convs", str(CONVS // world), "--dump-responses", dump, *COMMON],
                os.path.join(logdir, f"pools_n{world}.log"), timeout=600)
     assert res["n_gpus"] == world and res.get("rehearsal_one_gpu") is True
-    assert res["baseline_config"] == 3 and res["requests"] == CONVS * STEPS
+    assert res["baseline_config"] == (4 if world == 8 else 3) and res["requests"] == CONVS * STEPS
     assert 0.0 < res["small_tier_share"] < 1.0
-    assert ("tp2" in res["config"]["parallelism"]) == (world == 4)
+    assert res["config"]["parallelism"].endswith({2: "tp1", 4: "tp2", 8: "tp4"}[world])
     got = json.load(open(dump))
     ref_res, want = single
     assert len(got) == len(want) == CONVS * STEPS
@@ -86,12 +87,13 @@ def test_pools_topology_n_ranks_one_gpu(world, single, tmp_path):
                 max(1, sum(a[2] == b[2] == t for a, b in zip(got, want))) for t in {r[2] for r in want}}
     print(f"pools n={world}: tier agreement {same_tier:.2f}, text agreement {same_text:.2f}, per tier "
           + ", ".join(f"{t} {v:.2f}" for t, v in sorted(per_tier.items())))
+    assert res["baseline_config"] in (3, 4)
     if world == 2:
         # small | large on two ranks: the same engines see the same batches as the single process,
         # so every routed turn must come back with the same text (measured: 1.00)
         assert same_text >= 0.9, (same_tier, same_text, per_tier)
     else:
-        # two small replicas split the batch differently and the large tier is TP=2 (bf16 partial
+        # the small replicas split the batch differently and the large tier is TP > 1 (bf16 partial
         # sums are rounded before the all-reduce): greedy near-ties of random-init logits flip and
         # the conversations diverge, so only the routing (which depends on the query text and the
         # router's own state) is required to agree
