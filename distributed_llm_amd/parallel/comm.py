@@ -148,8 +148,10 @@ class ParallelContext:
         from .expert_parallel import token_slice
         T = t.shape[0]
         lo, hi = token_slice(T, self.tp_rank, self.tp_size)
-        if not t.is_cuda:  # gloo has no reduce-scatter: all-reduce and slice (CPU tests)
-            dist.all_reduce(t, group=self.tp_group)
+        if not t.is_cuda or dist.get_backend(self.tp_group) != "nccl":
+            # gloo has no reduce-scatter: all-reduce (host-staged for device tensors: the one-GPU
+            # multi-process rehearsal) and slice
+            self._group_all_reduce(t)
             return t[lo:hi].contiguous()
         mx = -(-T // self.tp_size)
         buf = torch.zeros((self.tp_size, mx, *t.shape[1:]), dtype=t.dtype, device=t.device)

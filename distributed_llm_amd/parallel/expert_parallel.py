@@ -39,7 +39,18 @@ def token_slice(T: int, rank: int, size: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _staged(t: torch.Tensor, group) -> bool:
+    """Device tensors on a gloo group (CPU tests' groups, the one-GPU multi-process rehearsal) go
+    through the host: gloo's all-to-all / all-gather take CPU tensors."""
+    return t.is_cuda and dist.get_backend(group) != "nccl"
+
+
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> None:
+    if _staged(out, group):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.contiguous().cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+        return
     dist.all_to_all_single(out, inp.contiguous(), out_splits, in_splits, group=group)
 
 
@@ -64,7 +75,7 @@ def ep_moe_ffn(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13_local:
     tok, eid, wt, dest = tok[order], eid[order], wt[order], dest[order]
     send_counts = torch.bincount(dest, minlength=size).to(torch.int64)
     recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    _a2a(recv_counts, send_counts, None, None, group)
     ss, rs = send_counts.tolist(), recv_counts.tolist()
     n_recv = sum(rs)
     recv_x = torch.empty((n_recv, H), dtype=x.dtype, device=dev)
@@ -91,12 +102,13 @@ def all_gather_rows(x_local: torch.Tensor, T: int, group, size: int) -> torch.Te
     H = x_local.shape[1]
     pad = torch.zeros((mx, H), dtype=x_local.dtype, device=x_local.device)
     pad[:x_local.shape[0]] = x_local
-    if x_local.is_cuda:
+    if x_local.is_cuda and not _staged(x_local, group):
         buf = torch.empty((size, mx, H), dtype=x_local.dtype, device=x_local.device)
         dist.all_gather_into_tensor(buf, pad, group=group)
         parts = [buf[r, :hi - lo] for r, (lo, hi) in enumerate(sizes)]
     else:
-        bufs = [torch.empty_like(pad) for _ in range(size)]
-        dist.all_gather(bufs, pad, group=group)
+        src = pad.cpu()
+        bufs = [torch.empty_like(src) for _ in range(size)]
+        dist.all_gather(bufs, src, group=group)
         parts = [bufs[r][:hi - lo] for r, (lo, hi) in enumerate(sizes)]
-    return torch.cat(parts, 0)
+    return torch.cat(parts, 0).to(x_local.device)

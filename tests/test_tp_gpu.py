@@ -35,14 +35,15 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run_ranks(model, world, tmp_path):
+def _run_ranks(model, world, tmp_path, extra_env=None):
     worker = os.path.join(ROOT, "tests", "workers", "tp_engine_worker.py")
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DLLM_AUTOTUNE="0", OMP_NUM_THREADS="2")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DLLM_AUTOTUNE="0", OMP_NUM_THREADS="2", **(extra_env or {}))
     port = _port()
     # worker logs go to files (DLLM_TEST_LOGDIR, e.g. gpurun_out/, shows progress while they run)
     logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
     os.makedirs(logdir, exist_ok=True)
-    logs = [os.path.join(logdir, f"tp_{model}_w{world}_r{r}.log") for r in range(world)]
+    tag = "_".join(f"{k}{v}" for k, v in sorted((extra_env or {}).items()))
+    logs = [os.path.join(logdir, f"tp_{model}_w{world}{tag}_r{r}.log") for r in range(world)]
     fhs = [open(lp, "w") for lp in logs]
     procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), str(port), ROOT, model,
                                str(tmp_path)], env=env, stdout=fh, stderr=subprocess.STDOUT)
@@ -87,9 +88,17 @@ def _tp1_reference(model, monkeypatch):
     return toks, hid
 
 
-@pytest.mark.parametrize("model,world", [("llama-3-70b", 2), ("llama-3-70b", 4), ("mixtral-8x7b", 4)])
-def test_tensor_parallel_engine_one_gpu(model, world, tmp_path, monkeypatch):
-    res = _run_ranks(model, world, tmp_path)
+# EP: Mixtral's experts split over the group (all-to-all dispatch / combine, parallel/expert_parallel.py);
+# SP: sequence-parallel prefill of the unfused layer (reduce-scatter to a token slice, norms on the
+# slice, all-gather before the column-parallel projections); both host-staged on the gloo group here
+MODES = [("llama-3-70b", 2, None), ("llama-3-70b", 4, None), ("mixtral-8x7b", 4, None),
+         ("mixtral-8x7b", 2, {"DLLM_MOE_PARALLEL": "ep"}),
+         ("llama-3-70b", 2, {"DLLM_FUSED": "0", "DLLM_SEQ_PARALLEL": "1", "DLLM_SP_MIN_TOKENS": "8"})]
+
+
+@pytest.mark.parametrize("model,world,extra_env", MODES, ids=["tp2", "tp4", "moe_tp4", "moe_ep2", "sp2"])
+def test_tensor_parallel_engine_one_gpu(model, world, extra_env, tmp_path, monkeypatch):
+    res = _run_ranks(model, world, tmp_path, extra_env)
     for r in res[1:]:
         for k in ("graph", "eager", "sampled", "after_trip"):
             assert r[k] == res[0][k], (k, r[k], res[0][k])

@@ -43,7 +43,11 @@ def main():
     eng = LLMEngine(cfg, device="cuda:0", par=par, kv_cache_gb=0.25, max_num_seqs=8, max_model_len=1024,
                     prefix_cache=False, seed=0)
     log("engine built")
-    assert eng.model.fused, "the fused tensor-parallel layer must be active"
+    assert eng.model.fused or os.environ.get("DLLM_FUSED") == "0", "the fused tensor-parallel layer must be active"
+    if os.environ.get("DLLM_MOE_PARALLEL") == "ep":
+        assert eng.model.moe_ep, "expert-parallel MoE requested"
+    if os.environ.get("DLLM_SEQ_PARALLEL") == "1":
+        assert par.sequence_parallel and par.use_sp(64), "sequence-parallel prefill requested"
     graphs = eng.use_graphs       # TP decode graphs are opt-in (LLMEngine.TP_GRAPHS)
     assert graphs == (world == 1 or eng.TP_GRAPHS)
     sp = SamplingParams(max_new_tokens=8)
