@@ -266,7 +266,7 @@ def build_pools_from_arg(kind: str, model: str, small_model: Optional[str], larg
                         "top_p": 0.9}}
         return build_pools(spec), {SMALL: [0], LARGE: [1]}, {SMALL: sm, LARGE: lg}
     from ..config import load_config_file
-    spec = load_config_file(kind)
+    spec = {k: v for k, v in load_config_file(kind).items() if not k.startswith("_")}
     tg = {}
     for tier, s in spec.items():
         dev = s.get("device", "cuda:0")

@@ -185,6 +185,8 @@ class HTTPServerManager:
 
     def start_server(self):
         if self.supervisor is not None and not self.is_server_running():
+            if self.pool_name in self.supervisor.procs:
+                self.supervisor.ensure(self.pool_name)   # died: restart, counted
             self.supervisor.start(self.pool_name)
 
     def stop_server(self):

@@ -9,7 +9,11 @@ Topology spec (``config["pools"]``)::
 
 ``share``: pools with the same share key and model use ONE engine (BASELINE config 2: one
 model serving both tiers on one GPU).  ``kind`` may also be ``"http"`` (``url``: a pool
-worker) or ``"echo"``.
+worker), ``"echo"``, or ``"supervised"``: a pool worker process this router starts and owns
+(``port``, ``gpus``, ``tp``: one torchrun rank per GPU for tp > 1, ``worker_kind``), restarted
+lazily by the next request after it died, as the reference's NanoModel restarts its device server
+before a call (src/models/nano.py:19-21, server_manager.py:66-142) — the restartable form of a
+large tensor-parallel pool (``data/topologies/supervised_pools_8gpu.json``).
 """
 from __future__ import annotations
 
@@ -20,16 +24,37 @@ from ..config import LARGE, SMALL, canonical_tier
 from .base import EchoPool, EnginePool, HTTPPool, PoolClient, format_prompt
 
 
-def build_pools(spec: Dict[str, Dict[str, Any]]) -> Dict[str, PoolClient]:
+def build_pools(spec: Dict[str, Dict[str, Any]], supervisor=None) -> Dict[str, PoolClient]:
+    """``supervisor``: the Supervisor that owns ``"supervised"`` workers (created on demand; the
+    caller stops it with ``supervisor.stop_all()``, also reachable as ``pools[t].server_manager``)."""
     engines: Dict[Tuple[str, str], Any] = {}
     pools: Dict[str, PoolClient] = {}
     for name, s in spec.items():
+        if name.startswith("_"):   # "_comment" and other annotations
+            continue
         tier = canonical_tier(name)
         kind = s.get("kind", "engine")
         if kind == "echo":
             pools[tier] = EchoPool(tier, tokens_per_reply=int(s.get("max_new_tokens", 16)))
         elif kind == "http":
             pools[tier] = HTTPPool(tier, s["url"], timeout_s=float(s.get("timeout_s", 180.0)))
+        elif kind == "supervised":
+            from .supervisor import PoolSpec, Supervisor
+            if supervisor is None:
+                supervisor = Supervisor([], log_dir=s.get("log_dir", "gpurun_out/pools"),
+                                        startup_timeout_s=float(s.get("startup_timeout_s", 300.0)))
+            ps = PoolSpec(tier, int(s["port"]), gpus=[int(g) for g in s.get("gpus", [])],
+                          kind=s.get("worker_kind", "engine"), model=s.get("model", "tinyllama-1.1b"),
+                          max_new_tokens=int(s.get("max_new_tokens", 256)),
+                          temperature=float(s.get("temperature", 0.0)), tp=int(s.get("tp", 1)),
+                          extra_args=[str(x) for x in s.get("extra_args", [])])
+            supervisor.specs[tier] = ps
+            supervisor.restarts.setdefault(tier, 0)
+            opts = {k: s[k] for k in ("top_k", "top_p") if k in s}
+            pools[tier] = HTTPPool(tier, ps.url, timeout_s=float(s.get("timeout_s", 180.0)), supervisor=supervisor,
+                                   options=opts)
+            if s.get("start", True):
+                supervisor.start(tier, wait=bool(s.get("wait", True)))
         elif kind == "engine":
             key = (s.get("share", tier), s["model"])
             eng = engines.get(key)

@@ -106,3 +106,41 @@ def test_tensor_parallel_pool_worker_matches_tp1(tmp_path):
     assert "response" in got, got
     assert got["response"] == ref["response"]
     assert all("response" in m for m in many), many
+
+
+def test_supervised_pool_spec_restarts_dead_worker(tmp_path):
+    """Topology kind "supervised" (pools/factory.py): the router owns the worker processes and the
+    next request to a pool whose process died restarts it (reference src/models/nano.py:19-21)."""
+    from distributed_llm_amd.pools.factory import build_pools
+    spec = {SMALL: {"kind": "supervised", "port": _port(), "worker_kind": "echo", "max_new_tokens": 8,
+                    "log_dir": str(tmp_path / "logs"), "startup_timeout_s": 120},
+            LARGE: {"kind": "supervised", "port": _port(), "worker_kind": "echo", "max_new_tokens": 16,
+                    "log_dir": str(tmp_path / "logs"), "startup_timeout_s": 120}}
+    pools = build_pools(spec)
+    sup = pools[SMALL].server_manager.supervisor
+    try:
+        assert sup is pools[LARGE].server_manager.supervisor
+        assert pools[LARGE].process(HIST)["response"]
+        _crash(sup, LARGE)
+        r = pools[LARGE].process(HIST)          # lazy restart before the call
+        assert r["response"] and sup.restarts[LARGE] == 1 and sup.alive(LARGE)
+    finally:
+        sup.stop_all()
+
+
+def test_supervised_topology_file_parses_without_starting():
+    """The shipped config-4 supervised topology builds two supervised pools (TP=4 large tier)."""
+    import json
+    import os
+    from distributed_llm_amd.pools.factory import build_pools
+    path = os.path.join(os.path.dirname(__file__), "..", "distributed_llm_amd", "data", "topologies",
+                        "supervised_pools_8gpu.json")
+    spec = {k: dict(v, start=False) for k, v in json.load(open(path)).items() if not k.startswith("_")}
+    pools = build_pools(spec)
+    sup = pools[SMALL].server_manager.supervisor
+    try:
+        assert set(pools) == {SMALL, LARGE}
+        assert sup.specs[LARGE].tp == 4 and sup.specs[LARGE].gpus == [4, 5, 6, 7]
+        assert not sup.alive(SMALL) and not sup.alive(LARGE)
+    finally:
+        sup.stop_all()
