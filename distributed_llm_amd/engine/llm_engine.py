@@ -1161,13 +1161,13 @@ class LLMEngine:
         self._check_graph_collectives()
         self.collective_trips = getattr(self, "collective_trips", 0) + 1
 
-    # Tensor-parallel decode graphs are opt-in (DLLM_TP_GRAPHS=1): on the one-GPU TP=2 rehearsal a
-    # captured decode graph replayed correctly within its first generation but the first replay
-    # after the next eager prefill faulted on both ranks, while eager TP decode, TP=1 graphs and
-    # graph/eager alternation at TP=1 were all clean (profiles/r3_tp_graph_fault.md).  Until that
-    # replay is proven on hardware, tensor-parallel pools decode eagerly (the one-shot all-reduce
-    # kernels and the in-step health vote run the same way, launch by launch).
-    TP_GRAPHS = os.environ.get("DLLM_TP_GRAPHS", "0") == "1"
+    # Tensor-parallel decode graphs (on by default; DLLM_TP_GRAPHS=0 decodes TP pools eagerly).  A
+    # replay fault seen early in round 3 on the one-GPU TP=2 rehearsal came from torch.topk's
+    # multi-block select inside the captured step; with the vocab-parallel sampler on its own kernels
+    # (ops.tp_candidates / ops.tp_sample) TP=2/4 graphs replay clean across prefills, graph/eager
+    # alternation and an injected collective trip (profiles/r3_tp_graph_fault.md,
+    # profiles/r3_multirank_one_gpu.md), and TP=4 decode runs 23 % faster than eager there.
+    TP_GRAPHS = os.environ.get("DLLM_TP_GRAPHS", "1") == "1"
 
     def _check_graph_collectives(self) -> None:
         """A TP decode graph can only capture device collectives: the one-shot IPC kernels or RCCL.

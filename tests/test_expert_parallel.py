@@ -43,7 +43,8 @@ def _layer_worker(rank, world, port, T, q):
         es = slice(rank * E // world, (rank + 1) * E // world)
         yl = ep_moe_ffn(x[lo:hi], ids, w, w13[es], w2[es], E, None, world)
         y = all_gather_rows(yl, T, None, world)
-        q.put((rank, y.float()))
+        # by value: a shared-memory tensor dies with this process if the parent reads it late
+        q.put((rank, y.float().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -78,6 +79,7 @@ def test_ep_layer_matches_single_rank(world, T):
     ids, w = ops.moe_gate(logits, k)
     want = ops.moe_ffn(x, ids, w, w13, w2).float()
     res = _spawn(_layer_worker, world, T)
+    res = {r: torch.from_numpy(v) for r, v in res.items()}
     for r in range(world):
         torch.testing.assert_close(res[r], want, atol=2e-2, rtol=2e-2)
     assert all(torch.equal(res[0], res[r]) for r in range(world))

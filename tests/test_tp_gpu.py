@@ -8,8 +8,8 @@ peer buffers over IPC exactly as they do across xGMI, only the CPU process group
 Checked for 2-layer truncations of the TRUE shapes (H 8192 / I 28672 / 64 q : 8 kv heads for
 Llama-3-70B; 8 experts top-2, I 14336 for Mixtral):
   * every rank emits the same tokens (greedy and sampled: the vocab-parallel HIP sampler);
-  * decode is eager here (TP decode graphs are opt-in, DLLM_TP_GRAPHS=1: profiles/
-    r3_tp_graph_fault.md); with the opt-in set, hipGraph replay == eager decode, token for token;
+  * TP decode runs as hipGraph replays (DLLM_TP_GRAPHS, default on; never with expert-parallel
+    MoE, whose all-to-all counts vary per step): replay == eager decode, token for token;
   * the final hidden states match the TP=1 engine (bf16 partial sums are rounded before the
     all-reduce, so the tolerance is the bf16 one, not bit equality);
   * an injected all-reduce trip is agreed by every rank, the step is re-run on the fallback
@@ -103,7 +103,8 @@ def test_tensor_parallel_engine_one_gpu(model, world, extra_env, tmp_path, monke
         for k in ("graph", "eager", "sampled", "after_trip"):
             assert r[k] == res[0][k], (k, r[k], res[0][k])
     r0 = res[0]
-    assert r0["graphs_on"] == (os.environ.get("DLLM_TP_GRAPHS") == "1")
+    assert r0["graphs_on"] == (os.environ.get("DLLM_TP_GRAPHS", "1") == "1"
+                               and (extra_env or {}).get("DLLM_MOE_PARALLEL") != "ep")
     assert r0["graph"] == r0["eager"]
     assert all(len(t) == 8 for t in r0["graph"])
     assert r0["trips"] == 1 and not r0["custom_ar_left"]

@@ -48,10 +48,28 @@ def main():
         assert eng.model.moe_ep, "expert-parallel MoE requested"
     if os.environ.get("DLLM_SEQ_PARALLEL") == "1":
         assert par.sequence_parallel and par.use_sp(64), "sequence-parallel prefill requested"
-    graphs = eng.use_graphs       # TP decode graphs are opt-in (LLMEngine.TP_GRAPHS)
-    assert graphs == (world == 1 or eng.TP_GRAPHS)
+    graphs = eng.use_graphs       # TP decode graphs: LLMEngine.TP_GRAPHS; never with expert parallel
+    assert graphs == ((world == 1 or eng.TP_GRAPHS) and not eng.model.moe_ep)
     sp = SamplingParams(max_new_tokens=8)
     mode = os.environ.get("TP_WORKER_MODE", "full")
+    if mode == "time":   # decode ms/step, eager vs graph replay (32 sequences x 48 new tokens)
+        import time
+        prompts = [f"user: question {i} about tensor parallel decode" for i in range(32)]
+        tsp = SamplingParams(max_new_tokens=48, ignore_eos=True)
+        for g in ([False, True] if graphs else [False]):
+            eng.use_graphs = g
+            eng.generate(prompts[:4], SamplingParams(max_new_tokens=4))    # warm / capture
+            dist.barrier()
+            torch.cuda.synchronize()
+            s0, t0 = eng.steps["decode"], time.perf_counter()
+            eng.generate(prompts, tsp)
+            torch.cuda.synchronize()
+            dt, n = time.perf_counter() - t0, eng.steps["decode"] - s0
+            log(f"time graphs={g} decode_steps={n} ms_per_step={1e3 * dt / max(1, n):.3f}")
+        dist.barrier()
+        dist.destroy_process_group()
+        print("OK", flush=True)
+        return
     if mode != "full":   # diagnostics: "graph" / "eager" = 3 gens in that mode, "alt" = graph, eager, graph
         seq = {"graph": [True] * 3, "eager": [False] * 3, "alt": [True, False, True, True]}[mode]
         for k, g in enumerate(seq):
