@@ -231,7 +231,7 @@ class LLMEngine:
         # sampled tokens; slot [bucket] of a TP decode step holds the collectives' health vote
         self.d_out = torch.zeros(mb + 1, dtype=torch.int32, device=self.device)
         self.d_src = torch.zeros(mb, dtype=torch.int64, device=self.device)   # pipelined: id gather rows
-        self._out_bufs = [torch.zeros(mb, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._out_bufs = [torch.zeros(mb + 1, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         # numpy views of the pinned read-back buffers: ndarray.tolist() of a step's tokens costs a few
         # us, torch's Tensor.tolist() ~0.4 ms (it was the largest host item of a pipelined step)
         self._out_np = [b.numpy() for b in self._out_bufs]
@@ -429,9 +429,10 @@ class LLMEngine:
     def _take_inbox(self, final: bool) -> List[_Seq]:
         if self._mirror is not None:
             self._mirror_iter += 1
-            poll = final or self._mirror_iter % self.MIRROR_EVERY == 0
+            poll = final or self._mirror_iter >= self._mirror_due
             if not poll:
                 return []
+            self._mirror_due = self._mirror_iter + self.MIRROR_EVERY
             if not self._mirror[2]:
                 return self._mirror_take()
         with self._inbox_lock:
@@ -456,6 +457,7 @@ class LLMEngine:
         import torch.distributed as dist
         self._mirror = (group, leader, dist.get_rank() == leader)
         self._mirror_iter = 0
+        self._mirror_due = self.MIRROR_EVERY   # next poll (iterations; a pipelined burst counts its steps)
         return self
 
     def _mirror_send(self, msg) -> None:
@@ -998,19 +1000,31 @@ class LLMEngine:
     # max_model_len) are known in advance and never cost a row.
     PIPELINE = os.environ.get("DLLM_DECODE_PIPELINE", "1") == "1"
 
+    # Tensor-parallel pools pipeline too (DLLM_TP_PIPELINE=0: off).  Every rank must take the same
+    # burst decisions, so a TP burst never looks at the leader-only inbox: it ends on the shared
+    # stop rules (tokens, KV blocks and the mirrored waiting list are identical on every rank) or
+    # after MIRROR_EVERY steps, when the next admission exchange is due.  The in-graph health vote
+    # of the one-shot all-reduces is read back with each step's tokens; a trip ends the burst, the
+    # step is re-run on the fallback collectives and the step already in flight is discarded.
+    TP_PIPELINE = os.environ.get("DLLM_TP_PIPELINE", "1") == "1"
+
     def _pipeline_ok(self) -> bool:
-        return (self.PIPELINE and self.on_gpu and self.use_graphs and self.fused_sampler and not self.par.enabled
-                and self._mirror is None)
+        return (self.PIPELINE and self.on_gpu and self.use_graphs and self.fused_sampler
+                and (not self.par.enabled or self.TP_PIPELINE))
 
     def _replay(self, bs: int) -> None:
+        if self.FAULT_TRIP_DECODE >= 0 and self.steps["decode"] == self.FAULT_TRIP_DECODE \
+                and self.par.custom_ar is not None:
+            self.par.custom_ar.err.fill_(1)     # fault injection: as if an all-reduce timed out
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=True):
             g = self._graphs.get(bs)
             if g is None:
                 g = self._capture(bs)
             g.replay()
 
-    def _read_out(self, B: int, p: int) -> "torch.cuda.Event":
-        self._out_bufs[p][:B].copy_(self.d_out[:B], non_blocking=True)
+    def _read_out(self, B: int, p: int, bs: int) -> "torch.cuda.Event":
+        n = bs + 1 if self.par.custom_ar is not None else B    # + the TP health vote at [bs]
+        self._out_bufs[p][:n].copy_(self.d_out[:n], non_blocking=True)
         ev = self._out_evts[p]
         ev.record()
         return ev
@@ -1029,9 +1043,13 @@ class LLMEngine:
         lens = np.fromiter((s.length for s in cur), dtype=np.int64, count=len(cur))
         last = np.fromiter((s.out[-1] for s in cur), dtype=np.int64, count=len(cur))
         pc = 0
-        self._replay(self._prep_decode(cur, lens, last, pc))
-        ev = self._read_out(len(cur), pc)
+        tp = self.par.enabled
+        bsk = self._prep_decode(cur, lens, last, pc)
+        self._replay(bsk)
+        ev = self._read_out(len(cur), pc, bsk)
+        vote = self.par.custom_ar is not None     # this step's tokens carry the health vote
         self.steps["decode"] += 1
+        nsteps = 1
         self.timers["decode_host_pre"] += time.perf_counter() - _t0
         freed = False               # a row finished while requests wait for one: end the burst
         while True:
@@ -1039,7 +1057,8 @@ class LLMEngine:
             alive = [s for s in cur if id(s) not in gone]
             # the next step's rows: sequences that cannot reach a count limit with the token in flight
             nxt = [s for s in alive if len(s.out) + 1 < s.params.max_new_tokens and s.length + 1 < mml]
-            stop = (not nxt or freed or bool(self._inbox) or (bool(waiting) and len(nxt) < len(alive)))
+            stop = (not nxt or freed or (nsteps >= self.MIRROR_EVERY if self._mirror is not None else bool(self._inbox))
+                    or (bool(waiting) and len(nxt) < len(alive)))
             launched = None
             pending_pre: set = set()
             if not stop:
@@ -1078,11 +1097,19 @@ class LLMEngine:
                         self.d_src[:B].copy_(sb[:B], non_blocking=True)
                         self.d_ids[:B] = self.d_out[self.d_src[:B]]
                     self._replay(bs)
-                    launched = (run, pn, self._read_out(B, pn))
+                    launched = (run, pn, self._read_out(B, pn, bs), bs, self.par.custom_ar is not None)
                     self.steps["decode"] += 1
+                    nsteps += 1
             _t1 = time.perf_counter()
             ev.synchronize()
             toks = self._out_np[pc][:len(cur)].tolist()
+            tripped = vote and bool(self._out_np[pc][bsk])
+            if tripped:
+                # a one-shot all-reduce timed out in this step (every rank sees the same vote):
+                # discard the step in flight, re-run this one on the fallback collectives, end the burst
+                if launched is not None:
+                    launched[2].synchronize()
+                toks = self._rerun_tripped(cur, pc)
             _t2 = time.perf_counter()
             fix_ids, fix_toks, done_now = [], [], []
             for s, t in zip(cur, toks):
@@ -1126,7 +1153,9 @@ class LLMEngine:
             self.timers["decode_host_pre"] += _t1 - _t0
             self.timers["decode_gpu_wait"] += _t2 - _t1
             self.timers["decode_host_post"] += time.perf_counter() - _t2
-            if launched is None:
+            if launched is None or tripped:
+                if tp and self._mirror is not None:
+                    self._mirror_iter += nsteps - 1    # admission polls stay ~MIRROR_EVERY steps apart
                 return finished, preempted
             if done_now:
                 # the next step is already on the GPU: detokenise the stopped answers under it and
@@ -1139,7 +1168,19 @@ class LLMEngine:
                     self._complete_early(s)
                 self.timers["output"] += time.perf_counter() - _t3
             freed = bool(waiting) and bool(done_now or preempted)
-            cur, pc, ev = launched
+            cur, pc, ev, bsk, vote = launched
+
+    def _rerun_tripped(self, cur: List[_Seq], p: int) -> List[int]:
+        """Pipelined TP step whose health vote tripped: drop the one-shot all-reduce and re-run the
+        step eagerly on the fallback collectives.  Its inputs are rebuilt from the host state (the
+        previous step's tokens are already appended), its K/V writes are idempotent."""
+        self._collective_trip("decode step")
+        B = len(cur)
+        lens = np.fromiter((s.length for s in cur), dtype=np.int64, count=B)
+        last = np.fromiter((s.out[-1] for s in cur), dtype=np.int64, count=B)
+        bs = self._prep_decode(cur, lens, last, p)
+        self._decode_forward(bs)
+        return self.d_out[:B].tolist()
 
     def _complete_early(self, s: _Seq) -> None:
         """A sequence stopped inside a pipelined burst: record its finish time, form its text and

@@ -297,8 +297,8 @@ class LlamaModel:
 
     def weight_bytes(self) -> int:
         n = self.embed.numel() + (0 if self.lm_head is self.embed else self.lm_head.numel()) + self.final_norm.numel()
-        for L in self.layers:
-            n += sum(t.numel() for t in L.values())
+        for L in self.layers:   # one copy of each matrix: the K-panel copies ("_p") duplicate bytes, not reads
+            n += sum(t.numel() for k, t in L.items() if not k.endswith("_p"))
         return n * self.embed.element_size()
 
     # ------------------------------------------------------------------ forward
