@@ -213,7 +213,8 @@ def test_fused_ops_both_cores(core, M, monkeypatch):
 
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
 @pytest.mark.parametrize("R", [1, 2, 4])
-@pytest.mark.parametrize("N,K", [(256, 512), (2048, 2048), (4096, 5632)])
+@pytest.mark.parametrize("N,K", [(256, 512), (2048, 2048), (4096, 5632), (2048, 5632), (1024, 3000), (1024, 14336)])
+# (2048, 5632) / (1024, 3000) at M <= 2, R = 1: the whole-row 12- / 8-load trips (gemv.hip launch_gemv)
 def test_gemv_resadd(M, R, N, K):
     """Fused-epilogue GEMV, residual form: r += bf16(x . w^T), one partial row sum per workgroup."""
     if M * K * 2 > 64 * 1024:

@@ -14,10 +14,10 @@ TOPO_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(TOPO_DIR, "*.json"))))
 def test_topology_file(path):
-    spec = load_config_file(path)
+    spec = {k: v for k, v in load_config_file(path).items() if not k.startswith("_")}   # "_comment"
     assert {canonical_tier(k) for k in spec} == {SMALL, LARGE}
     for s in spec.values():
-        if s.get("kind", "engine") == "engine":
+        if s.get("kind", "engine") in ("engine", "supervised"):
             assert get_config(s["model"]).name
             assert int(s["max_new_tokens"]) > 0
 
