@@ -338,6 +338,9 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
     // O partials of all splits are in flight together, so the last arriver pays ~2 memory round
     // trips instead of 3 x nsplit dependent ones (the write-through loads go past L2; at batch 1
     // that serial chain was most of a decode attention launch).  sm.o is free scratch here.
+    // (Issuing the O loads before the (m, l) combine as well saves one more round trip, but the
+    // 16 float4 it keeps live raised the kernel past 128 VGPRs: 4 -> 3 waves per SIMD for the
+    // whole kernel and 18 % slower decode attention in the flagship profile, so it is not done.)
     float* s_pm = &sm.o[0][0][0];               // [nsplit][16] maxima, then [nsplit][16] sums
     float* s_pl = s_pm + COMBINE_MAXS * 16;
     if (threadIdx.x < 8 * nsplit) {             // thread (sp, pair): rows 2 pair, 2 pair + 1

@@ -305,9 +305,27 @@ constexpr unsigned gemv_blocks(int N) { return (unsigned)((N + 4 * R - 1) / (4 *
 template <int M, int R, bool SW, bool NORM, int EPI>
 void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
                  const EpiArgs& ea, hipStream_t stream) {
-  constexpr int UNR = M <= 4 ? 4 : 2;
   const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0) +
                      (EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0);
+  // Long rows on a small grid at batch 1-2 (TinyLlama's down projection: K = 5632 is 11
+  // wave-loads per row, N = 2048 is 512 workgroups, 2 per CU): with 4 loads per trip a wave waits
+  // out three dependent HBM latencies; 8 / 12 per trip put a whole row of up to 4096 / 6144
+  // elements in flight at once (64 / 96 VGPRs of W buffers).  Measured (1x MI355X, B = 1 decode
+  // step): TinyLlama 0.890 -> 0.872-0.883 ms; on larger grids (Llama-3-8B, >= 1024 workgroups) the
+  // lower occupancy cost ~1 %, so they keep 4-load trips.  DLLM_GEMV_LONG_TRIP=0 disables it.
+  static const int long_trip = [] { const char* e = getenv("DLLM_GEMV_LONG_TRIP"); return e ? atoi(e) : 1; }();
+  if constexpr (M <= 2 && R == 1) {
+    if (long_trip && K > 2048 && K <= 6144 && gemv_blocks<R>(N) <= 512) {
+      if (K <= 4096)
+        hipLaunchKernelGGL((gemv_kernel<M, R, 8, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
+                           (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
+      else
+        hipLaunchKernelGGL((gemv_kernel<M, R, 12, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
+                           (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
+      return;
+    }
+  }
+  constexpr int UNR = M <= 4 ? 4 : 2;
   hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
                      (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
 }
