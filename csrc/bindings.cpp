@@ -49,6 +49,7 @@ int dllm_car_resadd_slots(int);
 int dllm_car_resadd(const void*, void*, long, float*, long, int, int, int, void* const*, int, int, long, unsigned*, int*,
                     long, hipStream_t);
 int dllm_car_allgather(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
+int dllm_car_vote(int, const int*, void*, int*, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t, int);
 int dllm_moe_max_tiles_bm(int, int, int);
 int dllm_moe_ffn_tg(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int,
@@ -718,6 +719,14 @@ void car_allgather(torch::Tensor x, torch::Tensor out, std::vector<int64_t> base
                         (unsigned*)counters.data_ptr<int>(), err.data_ptr<int>(), spin_limit, stream()),
      "car_allgather");
 }
+// In-graph health vote glue around the 16-byte one-shot all-reduce (mode 0: stage, 1: decide).
+void car_vote(int64_t mode, torch::Tensor err, torch::Tensor v, torch::Tensor out) {
+  check_i32(err, "err");
+  check_i32(out, "out");
+  TORCH_CHECK(v.scalar_type() == torch::kBFloat16 && v.numel() >= 8 && v.is_contiguous(), "car_vote: v bf16 [>= 8]");
+  TORCH_CHECK(err.numel() >= 1 && out.numel() >= 1, "car_vote: err / out");
+  ok(dllm_car_vote((int)mode, err.data_ptr<int>(), v.data_ptr(), out.data_ptr<int>(), stream()), "car_vote");
+}
 
 // ---- fused-epilogue LDS-tiled GEMM (csrc/kernels/tgemm.hip).  epi: 0 plain y = x.w^T (optionally
 // row-scaled by rinv from ssq_in), 1 residual add (y = residual, in place; ssq_out partial row
@@ -968,6 +977,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("car_close", &car_close);
   m.def("car_free", &car_free);
   m.def("car_allreduce", &car_allreduce);
+  m.def("car_vote", &car_vote);
   m.def("car_resadd", &car_resadd);
   m.def("car_resadd_slots", &car_resadd_slots);
   m.def("car_allgather", &car_allgather);

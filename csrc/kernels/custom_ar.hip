@@ -339,3 +339,24 @@ extern "C" int dllm_car_allgather(const void* in, void* out, long n_bytes, void*
   hipLaunchKernelGGL(car_gather_kernel, dim3((int)blocks), dim3(THREADS), 0, stream, a);
   return (int)hipGetLastError();
 }
+
+// In-graph health vote glue (parallel/comm.py graph_error_flag), one launch on each side of the
+// 16-byte one-shot all-reduce instead of a chain of small element-wise launches:
+//   mode 0: v[0..7] = {bf16(err != 0), 0, ..., 0}   (this rank's vote)
+//   mode 1: out[0]  = (sum v[0] > 0) | (err != 0)   (agreed trip, or this rank's own timeout)
+namespace {
+__global__ void car_vote_kernel(int mode, const int* err, u16* v, int* out) {
+  const int t = threadIdx.x;
+  if (mode == 0) {
+    if (t < 8) v[t] = (t == 0 && *err != 0) ? (u16)0x3f80 : (u16)0;
+  } else if (t == 0) {
+    out[0] = (bf2f(v[0]) > 0.f || *err != 0) ? 1 : 0;
+  }
+}
+}  // namespace
+
+extern "C" int dllm_car_vote(int mode, const int* err, void* v, int* out, hipStream_t stream) {
+  if (mode != 0 && mode != 1) return -1;
+  hipLaunchKernelGGL(car_vote_kernel, dim3(1), dim3(64), 0, stream, mode, err, (u16*)v, out);
+  return (int)hipGetLastError();
+}

@@ -104,10 +104,9 @@ class ParallelContext:
             out.zero_()
             return
         v = car.flag_vec
-        v.zero_()
-        v[:1].copy_((car.err != 0).to(v.dtype))
+        car.vote_stage(v)          # v = (err != 0, 0, ...): one launch
         car.all_reduce(v)
-        out.copy_(((v[:1] > 0) | (car.err != 0)).to(out.dtype))
+        car.vote_decide(v, out)    # out = sum > 0 | err != 0: one launch
 
     def drop_custom_ar(self, why: str) -> None:
         """Every rank of the group calls this on the same step (agreed trip): RCCL carries every

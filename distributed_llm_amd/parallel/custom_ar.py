@@ -94,6 +94,14 @@ class CustomAllReduce:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and n % 16 == 0
                 and 0 < n <= self.max_bytes)
 
+    def vote_stage(self, v: torch.Tensor) -> None:
+        """Health vote, before its all-reduce: v[:8] = (this rank's error flag != 0, 0, ...)."""
+        _ext().car_vote(0, self.err, v, self.err)
+
+    def vote_decide(self, v: torch.Tensor, out: torch.Tensor) -> None:
+        """Health vote, after its all-reduce: out[0] = (sum > 0) or this rank's own flag."""
+        _ext().car_vote(1, self.err, v, out)
+
     def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Sum ``t`` over the group into ``out`` (default: in place).  Caller checks eligible()."""
         out = t if out is None else out
