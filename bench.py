@@ -471,6 +471,8 @@ def main() -> int:
     if meter and e0 is not None and e1 is not None:
         mj, how = meter.energy_between([smi_idx], e0, e1)
         energy_j = mj / 1000.0 if how == "counter" else -1.0
+    if rehearse and rank != 0 and energy_j >= 0:
+        energy_j = 0.0   # every rank read the SAME card's counter: count it once (rank 0's)
     if world > 1:
         t = torch.tensor([float(tokens), elapsed, energy_j, 1.0 if energy_j < 0 else 0.0], dtype=torch.float64,
                          device=coll_dev)
@@ -538,7 +540,7 @@ def main() -> int:
         if energy_j >= 0:
             # every rank's GPU over the timed window (energy counter deltas summed over ranks)
             out["gpu_energy_j"] = round(energy_j, 1)
-            out["avg_gpu_power_w"] = round(energy_j / max(elapsed_max, 1e-9) / world, 1)
+            out["avg_gpu_power_w"] = round(energy_j / max(elapsed_max, 1e-9) / (1 if rehearse else world), 1)
             out["j_per_token"] = round(energy_j / max(tokens_all, 1.0), 4)
         if rehearse:
             out["rehearsal_one_gpu"] = True   # N ranks shared ONE GPU: plumbing check, not a number

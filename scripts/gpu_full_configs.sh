@@ -16,7 +16,7 @@ trap "kill $TICK 2>/dev/null" EXIT
 for cfg in ${CFGS:-5 4}; do
   timeout -k 10 ${CFG_TIMEOUT:-600} python -m torch.distributed.run --nnodes=1 --nproc-per-node=8 --master-addr 127.0.0.1 \
     --master-port $((29500 + cfg)) bench.py --gpus 8 --topology pools --baseline-config $cfg --steps 2 --warmup 0 \
-    --convs 2 --kv-gb 2 --small-new 16 --large-new 24 --greedy --no-graphs > $O/cfg$cfg.log 2>&1
+    --convs 2 --kv-gb 2 --small-new 16 --large-new 24 --greedy --no-graphs --strategy hybrid > $O/cfg$cfg.log 2>&1
   rc=$?; echo "config $cfg rc=$rc"; grep '^{"metric"' $O/cfg$cfg.log | cut -c1-400
   [ $rc -ne 0 ] && { tail -30 $O/cfg$cfg.log | cut -c1-300; exit $rc; }
 done
