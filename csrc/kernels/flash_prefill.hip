@@ -80,19 +80,51 @@ __device__ __forceinline__ int kperm(int rho) { return (rho & ~12) | ((rho & 4) 
 // in-block key of S^T accumulator register i of lane half h (C row (i&3) + 8(i>>2) + 4h, permuted)
 __device__ __forceinline__ int keyoff(int i, int h) { return (i & 7) | (h << 3) | ((i & 8) << 1); }
 
-template <int D, int MINW>
+// O^T += V^T . P^T for one staged chunk: k-step s = cache block s of the chunk; lane half h holds
+// keys 16s + 8h + j.  Keys past the context end (never-written cache bytes) get a zeroed V element.
+template <int D, int NB, bool MAYBE_TAIL = true>
+__device__ __forceinline__ void pv_chunk(f32x16 (&acc)[NB], const unsigned char* vbase, const bf16x8 (&pf)[4],
+                                         const int kb, const int kmax, const int rl, const int h) {
+  const bool tail = MAYBE_TAIL && kb + CK > kmax;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int dim = 32 * n + rl;
+      uint4 v = ld16(vbase + s * (32 * D) + dim * 32 + ((h ^ ((dim >> 3) & 1)) << 4));
+      if (tail) {
+        const int k0 = kb + 16 * s + 8 * h;
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (k0 + e >= kmax) w[e >> 1] &= (e & 1) ? 0x0000ffffu : 0xffff0000u;
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v), pf[s], acc[n], 0, 0, 0);
+    }
+  }
+}
+
+// PIPE: the P.V product of chunk t-1 is issued between chunk t's score MFMAs and its softmax, so a
+// wave's MFMA pipe works on P.V(t-1) while its VALU computes exp2 of chunk t (in the plain loop
+// every MFMA of a chunk waits on that chunk's softmax).  The ring grows to 4 stages so chunk t-1's
+// V^T stays resident while chunk t+2 is staged.
+template <int D, int MINW, bool PIPE>
 __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   constexpr int KD = D / 16;            // k-steps of S^T
   constexpr int NB = D / 32;            // 32-dim blocks of O^T
   constexpr int KBYTES = CK * D * 2;    // K chunk: 64 rows x D
   constexpr int VBYTES = CK * D * 2;    // V^T chunk: 4 blocks x D x 16
   constexpr int STAGE = KBYTES + VBYTES;
+  constexpr int NST = PIPE ? STAGES + 1 : STAGES;   // ring stages (chunks in flight ahead: STAGES - 1)
   constexpr int GI = STAGE / 1024 / NWAVES;  // 1-KB global_load_lds pieces per wave per chunk
   static_assert(STAGE % (1024 * NWAVES) == 0, "whole 1-KB pieces per wave");
   static_assert(KBYTES % 1024 == 0, "K and V^T pieces do not share a 1-KB piece");
   // ONE dynamic LDS array: [ring STAGES x STAGE][block-table row, max_blocks entries]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int* s_bt = reinterpret_cast<int*>(smem + STAGES * STAGE);
+  constexpr int ZBYTES = PIPE ? VBYTES : 0;         // PIPE: an all-zero V^T image (first chunk's stand-in)
+  unsigned char* s_zero = smem + NST * STAGE;
+  int* s_bt = reinterpret_cast<int*>(smem + NST * STAGE + ZBYTES);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, rl = lane & 31;
@@ -110,6 +142,10 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   const int* bt = a.block_tables + (long)seq * a.max_blocks;
   const int nbt = min((kmax + 15) / 16, a.max_blocks);
   for (int i = threadIdx.x; i < nbt; i += 64 * NWAVES) s_bt[i] = bt[i];
+  if constexpr (PIPE) {
+    for (int i = threadIdx.x; i < ZBYTES / 16; i += 64 * NWAVES)
+      *reinterpret_cast<uint4*>(s_zero + 16 * i) = make_uint4(0, 0, 0, 0);
+  }
 
   // this lane's query row (both lane halves hold the same row, different keys)
   const int r = 32 * wave + rl;
@@ -132,7 +168,7 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   // staging: piece p (1 KB) of a stage; K pieces first, then V^T pieces
   const long hstride = (long)16 * D;  // elements per (block, head) in either cache
   auto issue = [&](int t) {
-    unsigned char* base = smem + (t % STAGES) * STAGE;
+    unsigned char* base = smem + (t % NST) * STAGE;
     const int bi = (t * CK) >> 4;
 #pragma unroll
     for (int j = 0; j < GI; ++j) {
@@ -166,13 +202,32 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   for (int t = 0; t < STAGES - 1; ++t)
     if (t < nchunks) issue(t);
 
+  // PIPE: the previous chunk's P and V^T stage, not yet multiplied into O.  Before the first chunk
+  // they are zeros (P = 0 against an all-zero V^T image: adds exactly 0), so the in-loop P.V needs no
+  // branch and shares a basic block with the softmax it overlaps.  Only the context's last chunk
+  // has never-written keys to mask, and its P.V always runs in the flush after the loop.
+  bf16x8 pf_prev[4];
+  const unsigned char* vprev = s_zero;
+  int kb_prev = -CK;
+  if constexpr (PIPE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf_prev[i][j] = (__bf16)0.f;
+  }
   for (int t = 0; t < nchunks; ++t) {
     if (t + 1 < nchunks) wait_vm<GI>(); else wait_vm<0>();
     sync_lds();
     if (t + STAGES - 1 < nchunks) issue(t + STAGES - 1);
     const int kb = t * CK;
-    if (kb >= wave_lim) continue;  // wave-uniform: every row of this wave is past its causal limit
-    const unsigned char* kbase = smem + (t % STAGES) * STAGE;
+    if (kb >= wave_lim) {  // wave-uniform: every row of this wave is past its causal limit
+      if constexpr (PIPE) {  // flush before the pending chunk's stage is re-staged
+        if (kb_prev >= 0) pv_chunk<D, NB>(acc, vprev, pf_prev, kb_prev, kmax, rl, h);
+        kb_prev = -CK;
+      }
+      continue;
+    }
+    const unsigned char* kbase = smem + (t % NST) * STAGE;
     const unsigned char* vbase = kbase + KBYTES;
 
     f32x16 sc[2];
@@ -201,6 +256,9 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
     for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sc[1][i]);
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float m_new = fmaxf(m_run, mloc);
+    if constexpr (PIPE) {  // P.V of the previous chunk (never the context's tail), previous max frame
+      pv_chunk<D, NB, false>(acc, vprev, pf_prev, 0, 0, rl, h);
+    }
     if (__ballot(m_new != m_run)) {  // wave-uniform: some row's running max moved -> rescale
       const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * cs);  // exp2(-inf) = 0
       l_run *= alpha;
@@ -224,25 +282,17 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
       }
     l_run += lsum;
 
-    // O^T += V^T . P^T: k-step s = cache block s of the chunk; lane half h holds keys 16s + 8h + j
-    const bool tail = kb + CK > kmax;
+    if constexpr (PIPE) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const int dim = 32 * n + rl;
-        uint4 v = ld16(vbase + s * (32 * D) + dim * 32 + ((h ^ ((dim >> 3) & 1)) << 4));
-        if (tail) {  // zero the elements of keys past the context end (never-written cache bytes)
-          const int k0 = kb + 16 * s + 8 * h;
-          uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (k0 + e >= kmax) w[e >> 1] &= (e & 1) ? 0x0000ffffu : 0xffff0000u;
-          v = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v), pf[s], acc[n], 0, 0, 0);
-      }
+      for (int i = 0; i < 4; ++i) pf_prev[i] = pf[i];
+      vprev = vbase;
+      kb_prev = kb;
+    } else {
+      pv_chunk<D, NB>(acc, vbase, pf, kb, kmax, rl, h);
     }
+  }
+  if constexpr (PIPE) {
+    if (kb_prev >= 0) pv_chunk<D, NB>(acc, vprev, pf_prev, kb_prev, kmax, rl, h);
   }
 
   // acc[n][i] = O^T[dim 32 n + 8 (i >> 2) + 4 h + (i & 3)][row rl]
@@ -275,8 +325,14 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   const dim3 grid((unsigned)num_tiles * (unsigned)nkv);
   // d=64: 4 waves per SIMD (<= 128 VGPRs, 52 KB LDS at a 16K context) = two workgroups per CU;
   // measured 1.14-1.17x over one at 2k-16k tokens (profiles/r2_flash_prefill_microbench.md)
-  auto go = [&](auto kern, int dd) -> int {
-    const size_t lds = (size_t)STAGES * (2 * CK * dd * 2) + ((size_t)max_blocks * 4 + 15) / 16 * 16;
+  // d = 128 runs the software-pipelined P.V variant (4-stage ring + zero V^T image): 4-11 % faster
+  // at 2k-16k tokens; at d = 64 it needs > 128 VGPRs (one workgroup per CU instead of two) and at
+  // d = 96 an earlier form of it gained nothing, so they keep the plain loop
+  // (profiles/r3_flash_prefill.md).  DLLM_FLASH_PIPE=0 turns it off.
+  static const bool pipe = [] { const char* e = getenv("DLLM_FLASH_PIPE"); return !e || atoi(e) != 0; }();
+  auto go = [&](auto kern, int dd, bool piped) -> int {
+    const size_t lds = (size_t)(piped ? STAGES + 1 : STAGES) * (2 * CK * dd * 2) + (piped ? (size_t)CK * dd * 2 : 0) +
+                       ((size_t)max_blocks * 4 + 15) / 16 * 16;
     if (lds > 160 * 1024) return -3;
     if (lds > 64 * 1024) {   // past the default dynamic-LDS cap (d = 64: contexts beyond ~128K keys)
       const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -286,9 +342,9 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
     return (int)hipGetLastError();
   };
   switch (d) {
-    case 64: return go(flash_prefill_kernel<64, 4>, 64);
-    case 96: return go(flash_prefill_kernel<96, 2>, 96);
-    case 128: return go(flash_prefill_kernel<128, 2>, 128);
+    case 64: return go(flash_prefill_kernel<64, 4, false>, 64, false);
+    case 96: return go(flash_prefill_kernel<96, 2, false>, 96, false);
+    case 128: return pipe ? go(flash_prefill_kernel<128, 2, true>, 128, true) : go(flash_prefill_kernel<128, 2, false>, 128, false);
     default: return -4;
   }
 }
