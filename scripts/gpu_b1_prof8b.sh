@@ -12,8 +12,12 @@ if [ -z "$SKIP_TP" ]; then
     -p no:cacheprovider > $O/tp_tests.log 2>&1
   rc=$?; tail -2 $O/tp_tests.log; [ $rc -ne 0 ] && exit $rc
 fi
+# tune and cache the GEMM plans first, so the profiled run replays without autotune trials
+MB_DECODE_B=1 MB_DECODE_C=2048 timeout -k 10 400 python3 scripts/microbench.py --what decode --model ${B1_MODEL:-llama-3-8b} \
+  > $O/tune.log 2>&1 || exit $?
 MB_DECODE_B=1 MB_DECODE_C=2048 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o l8b --output-format csv -- \
   python3 scripts/microbench.py --what decode --model ${B1_MODEL:-llama-3-8b} > $O/prof.log 2>&1 || exit $?
 grep decode_step $O/prof.log | cut -c1-120
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1)
 [ -n "$f" ] && python3 scripts/prof_summary.py "$f" 25 > $O/prof_summary.md && head -22 $O/prof_summary.md
+find $O/prof -name '*kernel_trace.csv' -delete
