@@ -344,7 +344,11 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   switch (d) {
     case 64: return go(flash_prefill_kernel<64, 4, false>, 64, false);
     case 96: return go(flash_prefill_kernel<96, 2, false>, 96, false);
-    case 128: return pipe ? go(flash_prefill_kernel<128, 2, true>, 128, true) : go(flash_prefill_kernel<128, 2, false>, 128, false);
+    case 128: {  // the pipelined ring + zero image need 48 KB more LDS: past ~64K keys of block table, plain loop
+      const bool fits = (size_t)(STAGES + 1) * (2 * CK * 128 * 2) + (size_t)CK * 128 * 2 + ((size_t)max_blocks * 4 + 15) / 16 * 16 <= 160 * 1024;
+      return pipe && fits ? go(flash_prefill_kernel<128, 2, true>, 128, true)
+                          : go(flash_prefill_kernel<128, 2, false>, 128, false);
+    }
     default: return -4;
   }
 }
