@@ -5,26 +5,28 @@ Reference workload (src/tests/routing_chatbot_tester.py:405-486): each query set
 ONE growing conversation; every turn is routed (token / heuristic / semantic / hybrid / perf) to
 the small or large tier and answered there; latency and response tokens are recorded per turn.
 
-Default (``--topology replicated``): BASELINE config 2 on every GPU — TinyLlama-1.1B architecture
+One GPU (the default, ``--topology replicated``): BASELINE config 2 — TinyLlama-1.1B architecture
 (random-init bf16 weights, fixed seed: no checkpoints exist in this environment) serving BOTH tiers
 from one engine, hybrid router with the semantic routing cache on (HBM-resident cache table, GPU
-MiniLM-L6 encoder).  Each GPU serves ``--convs`` concurrent conversations (the three reference
+MiniLM-L6 encoder).  The GPU serves ``--convs`` concurrent conversations (the three reference
 query sets round-robin, each conversation tagged with a unique session so no two share KV prefixes
 or answers).  One *step* = one turn of every conversation: route all, then the engine serves the
 small- and large-tier groups as one continuous batch (paged KV, prefix cache across turns, hipGraph
 decode).  The response cache is OFF (its context-free key would replay other conversations'
 answers = skipped work); small tier greedy (reference Nano), large tier Ollama-default sampling
-(reference Orin).  N ranks = N independent replicas (weak scaling; one process per GPU).
+(reference Orin).
 
-``--topology pools`` (BASELINE configs 3-5): the tiers live on disjoint GPU subsets
-(parallel.cluster.default_topology: 2 GPUs small|large, 4 GPUs 2 small replicas + large TP=2,
-8 GPUs 4 small replicas + large TP=4); rank 0 hosts the router and drives
-``--convs x N`` conversations; requests reach remote pools over the gloo control/data planes,
-RCCL carries only the large pool's tensor-parallel collectives.  Without ``--baseline-config``
-2-4 GPUs run config 3 (Llama-3.2-1B | Llama-3-8B), 8 GPUs config 4 (Llama-3-8B x4 | Llama-3-70B
-TP=4, perf router); ``--baseline-config 5`` puts Mixtral-8x7B on the large half (TP = N/2, not
-co-located with the small pool as in the reference's config).  The JSON line names the config
-it ran in ``baseline_config``.
+N > 1 GPUs default to BASELINE's multi-GPU configurations (``--topology pools``, parallel.cluster):
+2 GPUs config 3 (Llama-3.2-1B small on GPU 0 | Llama-3-8B large on GPU 1), 4 GPUs config 4's models
+at half size (Llama-3-8B x2 | Llama-3-70B TP=2), 8 GPUs config 4 (Llama-3-8B x4 | Llama-3-70B
+TP=4, perf router), and ``--baseline-config 5`` (``--topology colocated``) config 5 as written:
+Mixtral-8x7B TP=N over every GPU with a Llama-3.2-1B small replica co-located on each GPU.  Rank 0
+hosts the router and drives ``--convs x N`` conversations (``--convs`` defaults to 64 per GPU
+there); requests reach remote pools over the gloo control / data planes, RCCL carries the large
+pool's tensor-parallel collectives.  The JSON line names the config (``baseline_config``) and the
+exact GPU layout (``layout``); values at different N are different model configurations, so they
+are not a scaling curve of one workload (``scaling_note``).  ``--topology replicated`` keeps the
+config-2 replicas at any N (N independent engines: weak scaling of one workload).
 
 ``value`` = total generated tokens over all ranks / max rank wall time of the timed steps.
 """
@@ -47,18 +49,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--topology", default="replicated", choices=["replicated", "pools", "tiers"],
-                    help="replicated: both tiers on one engine per GPU (BASELINE config 2); pools: tiers on "
-                         "disjoint GPU subsets (configs 3-5, N>1); tiers: --small-model and --large-model "
-                         "co-located as two engines on every GPU")
+    ap.add_argument("--topology", default=None, choices=["replicated", "pools", "colocated", "tiers"],
+                    help="replicated: both tiers on one engine per GPU (BASELINE config 2; the 1-GPU default); "
+                         "pools: tiers on disjoint GPU subsets (configs 3-4; the N>1 default); colocated: large "
+                         "TP group over every GPU + a small replica on each GPU (config 5); tiers: --small-model "
+                         "and --large-model as two engines on every GPU")
     ap.add_argument("--baseline-config", type=int, default=None, choices=[2, 3, 4, 5],
-                    help="BASELINE.json config to run (default: 2 replicated; --topology pools: 3 at 2-4 GPUs, "
-                         "4 at 8 GPUs); sets topology and models")
+                    help="BASELINE.json config to run (default: 2 on 1 GPU, 3 on 2 GPUs, 4 on 4-8 GPUs); "
+                         "sets topology and models")
     ap.add_argument("--model", default="tinyllama-1.1b")
     ap.add_argument("--small-model", default=None, help="pools/tiers small tier (default per baseline config)")
     ap.add_argument("--large-model", default=None, help="pools/tiers large tier (default per baseline config)")
     ap.add_argument("--large-tp", type=int, default=None)
-    ap.add_argument("--convs", type=int, default=512, help="concurrent conversations per GPU")
+    ap.add_argument("--convs", type=int, default=None,
+                    help="concurrent conversations per GPU (default 512; 64 for the multi-GPU pool configs)")
     ap.add_argument("--strategy", default=None, help="routing strategy (default: perf for config 4, else hybrid)")
     ap.add_argument("--threshold", type=int, default=1000)
     ap.add_argument("--small-new", type=int, default=128)
@@ -88,7 +92,7 @@ BASELINE_CONFIGS = {
     2: ("replicated", None, None, None),
     3: ("pools", "llama-3.2-1b", "llama-3-8b", None),         # 1B | 8B, one GPU each (2 GPUs)
     4: ("pools", "llama-3-8b", "llama-3-70b", 4),             # 8B replicas | 70B TP=4 over xGMI
-    5: ("pools", "llama-3.2-1b", "mixtral-8x7b", None),       # 1B replicas | Mixtral TP=N/2 (MoE)
+    5: ("colocated", "llama-3.2-1b", "mixtral-8x7b", None),   # Mixtral TP=N + a 1B replica on every GPU
 }
 
 
@@ -96,14 +100,20 @@ def resolve_config(a, world: int) -> int:
     """Fill topology / models from ``--baseline-config`` (or infer it) and return the config id
     tagged on the JSON line."""
     cfg = a.baseline_config
+    if a.topology is None and cfg is None:
+        a.topology = "pools" if world > 1 else "replicated"
     if cfg is None:
-        if a.topology == "pools" and world > 1:
-            cfg = 4 if world >= 8 else 3
+        if a.topology == "colocated":
+            cfg = 5
+        elif a.topology == "pools" and world > 1:
+            cfg = 4 if world >= 4 else 3
         else:
             cfg = 2
     topo, sm, lg, tp = BASELINE_CONFIGS[cfg]
-    if a.baseline_config is not None:
+    if a.baseline_config is not None or a.topology is None:
         a.topology = topo
+    if a.convs is None:
+        a.convs = 64 if (world > 1 and a.topology in ("pools", "colocated")) else 512
     a.small_model = a.small_model or sm or "llama-3.2-1b"
     a.large_model = a.large_model or lg or "llama-3-8b"
     if a.large_tp is None and tp is not None and world >= 2 * tp:
@@ -314,6 +324,7 @@ def main() -> int:
     topology = a.topology if (world > 1 or a.topology == "tiers") else "replicated"
     if topology == "replicated":
         baseline_config = 2
+    layout = None
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
 
@@ -341,6 +352,8 @@ def main() -> int:
         engines = [e_small, e_large]
         model_desc = f"{sm} small + {lg} large (two engines co-located per GPU)"
         n_convs, parallelism = a.convs, f"dp{world}-colocated-tiers"
+        layout = {"small": {"model": sm, "replicas": [[r] for r in range(world)], "tp": 1},
+                  "large": {"model": lg, "replicas": [[r] for r in range(world)], "tp": 1}, "colocated": True}
     elif topology == "replicated":
         from distributed_llm_amd.engine.llm_engine import LLMEngine
         from distributed_llm_amd.pools.base import EnginePool
@@ -354,9 +367,12 @@ def main() -> int:
         engines = [engine]
         model_desc = f"{model} (small+large tiers on one engine per GPU)" if on_gpu else model
         n_convs, parallelism = a.convs, f"dp{world}"
+        layout = {"small": {"model": model, "replicas": [[r] for r in range(world)], "tp": 1},
+                  "large": {"model": model, "replicas": [[r] for r in range(world)], "tp": 1,
+                            "shared_engine_with_small": True}}
     else:
         from distributed_llm_amd.parallel.cluster import Cluster, TierSpec, default_topology
-        topo = default_topology(world, a.large_tp)
+        topo = default_topology(world, a.large_tp, colocated=(topology == "colocated"))
         sm = a.small_model if on_gpu else "tiny-llama-test"
         lg = a.large_model if on_gpu else "tiny-moe-test"
         n_small = len(topo.replicas[SMALL])
@@ -373,8 +389,13 @@ def main() -> int:
             for e in engines:
                 e.capture_all(max_bs=e._bucket(min(e.R, max(16, a.convs * world))))
         tp = len(topo.replicas[LARGE][0])
-        model_desc = f"{sm} small x{n_small} + {lg} large TP={tp} (disjoint GPU pools)"
-        n_convs, parallelism = a.convs * world, f"pools:small{n_small}xtp1+large{len(topo.replicas[LARGE])}xtp{tp}"
+        where = "small replicas co-located on the large pool's GPUs" if topology == "colocated" else "disjoint GPU pools"
+        model_desc = f"{sm} small x{n_small} + {lg} large TP={tp} ({where})"
+        n_convs = a.convs * world
+        parallelism = f"{topology}:small{n_small}xtp1+large{len(topo.replicas[LARGE])}xtp{tp}"
+        layout = {"small": {"model": sm, "replicas": topo.replicas[SMALL], "tp": 1},
+                  "large": {"model": lg, "replicas": topo.replicas[LARGE], "tp": tp},
+                  "colocated": topology == "colocated"}
 
     def sync():
         if cluster is not None:
@@ -512,6 +533,10 @@ def main() -> int:
             "per_stream_tok_s_p50": round(per_stream, 1) if per_stream else None,
             "per_stream_vs_baseline": round(per_stream / BASELINE_TOK_S, 2) if per_stream else None,
             "baseline_config": baseline_config,
+            "layout": layout,
+            "scaling_note": ("N = 1 runs BASELINE config 2 and N > 1 the multi-GPU configs 3-5 by default: values "
+                             "at different N are different models and layouts, not one workload's scaling curve "
+                             "(--topology replicated: N config-2 replicas)"),
             "dtype": "bf16",
             "data": "synthetic: reference query sets replayed as growing conversations; random-init weights",
             "config": {"model": model_desc, "global_batch": a.convs * world,

@@ -49,7 +49,7 @@ int dllm_car_resadd_slots(int);
 int dllm_car_resadd(const void*, void*, long, float*, long, int, int, int, void* const*, int, int, long, unsigned*, int*,
                     long, hipStream_t);
 int dllm_car_allgather(const void*, void*, long, void* const*, int, int, long, unsigned*, int*, long, hipStream_t);
-int dllm_car_vote(int, const int*, void*, int*, hipStream_t);
+int dllm_car_vote(int, int*, void*, int*, hipStream_t);
 int dllm_tgemm(const void*, int, int, int, int, int, int, int, hipStream_t, int);
 int dllm_moe_max_tiles_bm(int, int, int);
 int dllm_moe_ffn_tg(const void*, long, long, int, const int*, const float*, int, int, const void*, const void*, int,
@@ -724,7 +724,7 @@ void car_vote(int64_t mode, torch::Tensor err, torch::Tensor v, torch::Tensor ou
   check_i32(err, "err");
   check_i32(out, "out");
   TORCH_CHECK(v.scalar_type() == torch::kBFloat16 && v.numel() >= 8 && v.is_contiguous(), "car_vote: v bf16 [>= 8]");
-  TORCH_CHECK(err.numel() >= 1 && out.numel() >= 1, "car_vote: err / out");
+  TORCH_CHECK(err.numel() >= 2 && out.numel() >= 1, "car_vote: err [flag, staged snapshot] / out");
   ok(dllm_car_vote((int)mode, err.data_ptr<int>(), v.data_ptr(), out.data_ptr<int>(), stream()), "car_vote");
 }
 

@@ -341,21 +341,31 @@ extern "C" int dllm_car_allgather(const void* in, void* out, long n_bytes, void*
 }
 
 // In-graph health vote glue (parallel/comm.py graph_error_flag), one launch on each side of the
-// 16-byte one-shot all-reduce instead of a chain of small element-wise launches:
-//   mode 0: v[0..7] = {bf16(err != 0), 0, ..., 0}   (this rank's vote)
-//   mode 1: out[0]  = (sum v[0] > 0) | (err != 0)   (agreed trip, or this rank's own timeout)
+// 16-byte one-shot all-reduce instead of a chain of small element-wise launches.  err[0] is the
+// communicator's sticky timeout flag, err[1] the snapshot taken when the vote is staged:
+//   mode 0: v[0..7] = {bf16(err[0] != 0), 0, ..., 0} (this rank's vote); err[1] = (err[0] != 0)
+//   mode 1: out[0]  = err[1] ? 1                     (this rank's step data is suspect: it voted 1,
+//                                                     so every rank completing the vote trips too)
+//                   : err[0] ? 0                     (only the vote itself timed out: the step's own
+//                                                     all-reduces were clean, and the sticky flag is
+//                                                     this rank's 1 in the NEXT vote, so all ranks
+//                                                     trip together one step later)
+//                   : (sum v[0] > 0)                 (a peer voted 1)
+// A rank never trips alone on a vote it could not complete (its sum holds stale peer halves).
 namespace {
-__global__ void car_vote_kernel(int mode, const int* err, u16* v, int* out) {
+__global__ void car_vote_kernel(int mode, int* err, u16* v, int* out) {
   const int t = threadIdx.x;
   if (mode == 0) {
-    if (t < 8) v[t] = (t == 0 && *err != 0) ? (u16)0x3f80 : (u16)0;
+    const bool e = *(volatile int*)err != 0;
+    if (t < 8) v[t] = (t == 0 && e) ? (u16)0x3f80 : (u16)0;
+    if (t == 0) err[1] = e ? 1 : 0;
   } else if (t == 0) {
-    out[0] = (bf2f(v[0]) > 0.f || *err != 0) ? 1 : 0;
+    out[0] = err[1] != 0 ? 1 : (err[0] != 0 ? 0 : (bf2f(v[0]) > 0.f ? 1 : 0));
   }
 }
 }  // namespace
 
-extern "C" int dllm_car_vote(int mode, const int* err, void* v, int* out, hipStream_t stream) {
+extern "C" int dllm_car_vote(int mode, int* err, void* v, int* out, hipStream_t stream) {
   if (mode != 0 && mode != 1) return -1;
   hipLaunchKernelGGL(car_vote_kernel, dim3(1), dim3(64), 0, stream, mode, err, (u16*)v, out);
   return (int)hipGetLastError();

@@ -158,6 +158,7 @@ class LLMEngine:
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self.collective_trips = 0
+        self.trip_steps: List[int] = []   # decode-step counter at each collective trip
         self._check_graph_collectives()
         self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
         self.timers = {"prefill": 0.0, "decode_host_pre": 0.0, "decode_gpu_wait": 0.0, "decode_host_post": 0.0,
@@ -682,14 +683,18 @@ class LLMEngine:
         self._bt_hw = max(self._bt_hw, len(t))
         self._bt_dirty = True
 
+    def _note_upd_cols(self) -> None:
+        """Widen the host -> device block-table copy to every column a queued update writes."""
+        if self._bt_upd:
+            cols = np.asarray(self._bt_upd[0::2], dtype=np.int64) % self.max_blocks
+            self._bt_hw = max(self._bt_hw, int(cols.max()) + 1)
+
     def _sync_bt(self) -> None:
         if self._bt_dirty:
             # rare (admission / release): synchronous copy of the columns any row has used (a 128K
             # context table is 8K columns; a 2K-token batch needs 128 of them), which also subsumes
             # the queued per-step updates
-            if self._bt_upd:
-                cols = np.asarray(self._bt_upd[0::2], dtype=np.int64) % self.max_blocks
-                self._bt_hw = max(self._bt_hw, int(cols.max()) + 1)
+            self._note_upd_cols()
             hw = min(self._bt_hw, self.max_blocks)
             if hw == self.max_blocks:
                 self.bt_dev.copy_(self.bt_host_t, non_blocking=False)
@@ -913,6 +918,9 @@ class LLMEngine:
         h[o[8]] = nu
         if nu:
             h[o[8] + 1:o[8] + 1 + 2 * nu] = self._bt_upd
+            # the graph writes these columns on the device: count them in the copy width, or a
+            # released row's stale device columns past it would survive the next admission sync
+            self._note_upd_cols()
             self._bt_upd.clear()
         self.dec_dev[:o[8] + 1 + 2 * nu].copy_(self._dec_bufs[p][0][:o[8] + 1 + 2 * nu], non_blocking=True)
         if n_items:
@@ -929,6 +937,7 @@ class LLMEngine:
         if self.FAULT_TRIP_DECODE >= 0 and self.steps["decode"] == self.FAULT_TRIP_DECODE \
                 and self.par.custom_ar is not None:
             self.par.custom_ar.err.fill_(1)     # fault injection: as if an all-reduce timed out
+        self._arm_vote_fault()
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=self.use_graphs):
             if self.use_graphs:
                 g = self._graphs.get(bs)
@@ -1016,6 +1025,7 @@ class LLMEngine:
         if self.FAULT_TRIP_DECODE >= 0 and self.steps["decode"] == self.FAULT_TRIP_DECODE \
                 and self.par.custom_ar is not None:
             self.par.custom_ar.err.fill_(1)     # fault injection: as if an all-reduce timed out
+        self._arm_vote_fault()
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=True):
             g = self._graphs.get(bs)
             if g is None:
@@ -1193,6 +1203,27 @@ class LLMEngine:
     FAULT_TRIP_DECODE = int(os.environ.get("DLLM_FAULT_CAR_TRIP_DECODE", "-1"))
     FAULT_TRIP_PREFILL = int(os.environ.get("DLLM_FAULT_CAR_TRIP_PREFILL", "-1"))
 
+    # fault injection (tests): on decode step FAULT_VOTE_DECODE, rank FAULT_VOTE_RANK's one-shot
+    # all-reduce flag is raised DURING the in-graph health vote (after its vote was staged)
+    FAULT_VOTE_DECODE = int(os.environ.get("DLLM_FAULT_CAR_VOTE_DECODE", "-1"))
+    FAULT_VOTE_RANK = int(os.environ.get("DLLM_FAULT_CAR_VOTE_RANK", "0"))
+
+    def _arm_vote_fault(self) -> None:
+        car = self.par.custom_ar
+        if car is None or self.FAULT_VOTE_DECODE < 0:
+            return
+        if getattr(car, "fault_vote", None) is None:
+            car.fault_vote = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._graphs.clear()     # re-captured with the injection op
+        # fires once, on the first step replayed at or after FAULT_VOTE_DECODE (a pipelined burst
+        # counts its steps when they are read back, after later steps were already issued)
+        hit = (self.steps["decode"] >= self.FAULT_VOTE_DECODE and not getattr(self, "_vote_fault_fired", False)
+               and self.par.tp_rank == self.FAULT_VOTE_RANK)
+        if hit:
+            self._vote_fault_fired = True
+            self.vote_fault_step = self.steps["decode"]
+        car.fault_vote.fill_(1 if hit else 0)
+
     def _collective_trip(self, where: str) -> None:
         """Every TP rank sees the same trip on the same step: drop the one-shot all-reduce (its
         epochs are out of step), drop the graphs that embed it (re-captured on demand), and let
@@ -1201,6 +1232,7 @@ class LLMEngine:
         self._graphs.clear()
         self._check_graph_collectives()
         self.collective_trips = getattr(self, "collective_trips", 0) + 1
+        self.trip_steps.append(self.steps["decode"])
 
     # Tensor-parallel decode graphs (on by default; DLLM_TP_GRAPHS=0 decodes TP pools eagerly).  A
     # replay fault seen early in round 3 on the one-GPU TP=2 rehearsal came from torch.topk's

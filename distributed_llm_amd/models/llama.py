@@ -2,15 +2,18 @@
 
 One module covers every BASELINE.json family: they differ only in shapes, RoPE parameters,
 tied embeddings and dense-vs-MoE MLP (models.configs).  MI355X-first layout decisions:
-  * fused QKV weight [(nq + 2 nkv) d, H] and fused gate|up weight [2 I, H] — one GEMM each
-    (hipBLASLt via F.linear, K-contiguous "TN" operands);
-  * RoPE + paged-KV write fused in one kernel reading the QKV GEMM output in place;
-  * RMSNorm fused with the residual add (the residual stream is read/written once per norm);
-    ops.norm_linear can also fold it into a batch <= 8 GEMV (opt-in, measured slower);
+  * fused QKV weight [(nq + 2 nkv) d, H] and fused gate|up weight [2 I, H] — one GEMM each, on
+    the LDS-tiled MFMA GEMM with fused epilogues (csrc/kernels/tgemm.hip; the fused-epilogue
+    GEMV at batch <= 8; hipBLASLt core + a standalone epilogue only where the autotuner measured
+    that faster, ops/gemm.py);
+  * RMSNorm folded into the consuming GEMM and RoPE + the paged K / V^T write in the QKV GEMM's
+    epilogue (fused decoder layer below; ``DLLM_FUSED=0`` keeps the unfused reference layer:
+    norm + residual kernel, RoPE + KV-write kernel, SiLU·mul, used for CPU parity);
   * the LM head runs only on the last position of each sequence;
   * tensor parallel (Megatron column/row split): QKV / gate|up column-parallel, o_proj /
-    down_proj row-parallel + ONE all-reduce each, vocab-parallel embedding (masked lookup +
-    all-reduce) and LM head (distributed arg-max / top-k; parallel.comm).
+    down_proj row-parallel + ONE all-reduce each (or reduce-scatter + all-gather under sequence
+    parallelism), vocab-parallel embedding (masked lookup + all-reduce) and LM head (distributed
+    arg-max / top-k; parallel.comm).
 Weights: random init with a fixed seed (no checkpoints in this environment) or HF safetensors.
 
 Fused decoder layer (GPU, any tensor-parallel size; ``DLLM_FUSED=0`` disables): the residual stream
@@ -383,6 +386,11 @@ class LlamaModel:
         ssq_a = torch.empty((slots_n, T), dtype=torch.float32, device=input_ids.device)
         ssq_b = torch.empty((slots_n, T), dtype=torch.float32, device=input_ids.device)
         tp = par.tp_size > 1
+        # sequence parallelism (DLLM_SEQ_PARALLEL=1, prefill-size batches, eager only): every
+        # row-parallel reduction becomes reduce-scatter + residual add on the token slice +
+        # all-gather (ParallelContext.sp_resadd)
+        sp = tp and par.use_sp(T) and not (input_ids.is_cuda and torch.cuda.is_current_stream_capturing())
+        resadd = par.sp_resadd if sp else par.all_reduce_resadd
         if not tp:
             # the gather also leaves each row's sum of squares in slot 0 (first layer's row scale)
             r = ops.embedding(input_ids, self.embed, self.vocab_shard.start, ssq_out=ssq_a[0])
@@ -402,13 +410,13 @@ class LlamaModel:
             if not tp:
                 nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b, wp=L.get("wo_p"))
             else:   # row-parallel o_proj: partial sums -> all-reduce + residual add + row statistics
-                nb = par.all_reduce_resadd(ops.linear(o.view(T, -1), L["wo"], wp=L.get("wo_p")), r, ssq_b)
+                nb = resadd(ops.linear(o.view(T, -1), L["wo"], wp=L.get("wo_p")), r, ssq_b)
             if not cfg.is_moe:
                 act = ops.gemm.swiglu_matmul(r, L["wgu_f"], ssq_b, nb, eps, wp=L.get("wgu_f_p"))
                 if not tp:
                     n = ops.gemm.matmul_resadd(act, L["wd"], r, ssq_a, wp=L.get("wd_p"))
                 else:
-                    n = par.all_reduce_resadd(ops.linear(act, L["wd"], wp=L.get("wd_p")), r, ssq_a)
+                    n = resadd(ops.linear(act, L["wd"], wp=L.get("wd_p")), r, ssq_a)
             else:
                 x = ops.rms_norm(r, L["ln2"], eps)
                 if not tp:
@@ -416,7 +424,7 @@ class LlamaModel:
                 elif self.moe_ep:   # expert parallel: the combined output is already replicated
                     n = ops.gemm.res_add_ssq(self._mlp_out(L, x), r, ssq_a)
                 else:               # TP-within-expert partial sums
-                    n = par.all_reduce_resadd(self._mlp(L, x), r, ssq_a)
+                    n = resadd(self._mlp(L, x), r, ssq_a)
         return ops.rms_norm(r if meta.all_last else r.index_select(0, meta.last_idx), self.final_norm, eps)
 
     def _hidden_states_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,

@@ -1,17 +1,27 @@
-"""Node topology: small / large tier pools on disjoint GPU subsets (one process per GPU).
+"""Node topology: small / large tier pools on GPU subsets (one process per GPU).
 
 BASELINE.json configs 3-5: "Llama-3-1B (small pool, GPU0) + Llama-3-8B (large pool, GPU1)",
 "8B small pool (2 GPUs) + 70B TP=4 large pool", "Mixtral TP=8 large + 1B small co-located".
-The reference's equivalent is two boards behind SSH tunnels (src/models/server_manager.py).
+The reference's equivalent is two models served side by side behind one router, each on its own
+board behind an SSH tunnel (src/devices/nano_api.py:15-16, orin_api.py:17-18; dispatch at
+src/router.py:152-171; lifecycle src/models/server_manager.py).
 
 ``Topology`` lists the replicas of each tier as rank lists (a replica with > 1 rank is one
-tensor-parallel group).  ``Cluster`` (every rank constructs it, in the same order) creates the
-process groups, loads this rank's engine, and then either
-  * rank 0 (router rank): ``router_pools()`` -> {tier: PoolClient} mixing its local engine, remote
-    pools (``pools.remote.RemotePool`` over RCCL P2P) and replica sets (``ReplicatedPool``); or
-  * every other rank: ``serve()`` — the pool loop until the router sends stop.
+tensor-parallel group).  A rank may host more than one replica (``colocated``: BASELINE config 5's
+small pool shares the GPUs of the large pool's TP group; each replica is its own engine, sized by
+its TierSpec's ``kv_cache_gb``: memory partitioning on the shared 288 GB).  ``Cluster`` (every
+rank constructs it, in the same order) creates the process groups, loads this rank's engine(s),
+and then either
+  * rank 0 (router rank): ``router_pools()`` -> {tier: PoolClient} mixing its local engines,
+    remote pools (``pools.remote.RemotePool``: tagged control messages on a gloo pair group, token
+    ids on the data-plane pair group — gloo by default, RCCL with ``DLLM_DATA_PLANE=rccl``) and
+    replica sets (``ReplicatedPool``); or
+  * every other rank: ``serve()`` — one serving loop per replica it hosts (a remote pool leader's
+    request loop, a TP member's scheduler mirror), until the router sends stop.
 Default layouts (``default_topology``): 1 GPU — both tiers on one engine; 2 — small [0], large [1];
-4 — small replicas [0], [1], large TP=2 [2, 3]; 8 — small replicas [0]..[3], large TP=4 [4..7].
+4 — small replicas [0], [1], large TP=2 [2, 3]; 8 — small replicas [0]..[3], large TP=4 [4..7];
+colocated (config 5) — small replicas [0]..[N-1], large TP=N [0..N-1] on the same GPUs.
+RCCL carries the TP groups' collectives only.
 """
 from __future__ import annotations
 
@@ -50,7 +60,15 @@ class Topology:
                 yield tier, ranks
 
 
-def default_topology(world: int, large_tp: Optional[int] = None) -> Topology:
+def default_topology(world: int, large_tp: Optional[int] = None, colocated: bool = False) -> Topology:
+    if colocated:
+        # BASELINE config 5: the large pool's TP group(s) span the node and every GPU also hosts a
+        # small-tier replica (two engines per process)
+        tp = large_tp or world
+        if world % tp:
+            raise ValueError(f"large tp={tp} must divide {world}")
+        return Topology({SMALL: [[r] for r in range(world)],
+                         LARGE: [list(range(i, i + tp)) for i in range(0, world, tp)]})
     if world == 1:
         return Topology({SMALL: [[0]], LARGE: [[0]]})
     if world == 2:
@@ -91,13 +109,20 @@ class Cluster:
             if len(ranks) > 1 and key not in self.tp_groups and init:
                 self.tp_groups[key] = dist.new_group(list(ranks))
                 self.mirror_groups[key] = dist.new_group(list(ranks), backend="gloo")
-        leaders = sorted({ranks[0] for _, ranks in topo.all_groups() if ranks[0] != 0})
+        remote = [ranks for _, ranks in topo.all_groups() if ranks[0] != 0]
+        leaders = sorted({ranks[0] for ranks in remote})
+        if len(leaders) != len({tuple(r) for r in remote}):
+            # one control / data pair group per remote leader: two remote replicas led by one rank
+            # would share (and interleave on) it
+            raise ValueError(f"a rank other than 0 leads two remote replicas: {remote}")
         import os
         data_backend = None if os.environ.get("DLLM_DATA_PLANE", "gloo") == "rccl" else "gloo"
         for ld in leaders:
             self.pair_groups[ld] = dist.new_group([0, ld], backend=data_backend) if init else None
             self.ctrl_groups[ld] = dist.new_group([0, ld], backend="gloo") if init else None
-        # --- this rank's replica(s): a rank serves exactly one replica (both tiers only if shared)
+        # --- this rank's replica(s): one, or several when tiers share GPUs (co-located pools, or
+        # both tiers on one engine at world 1); every rank builds them in all_groups() order, so
+        # the TP groups' collective set-up (custom all-reduce handles) lines up across ranks
         self.my: List[tuple] = [(tier, ranks) for tier, ranks in topo.all_groups() if self.rank in ranks]
         self.engines: Dict[tuple, Any] = {}
         from ..engine.llm_engine import LLMEngine
@@ -183,13 +208,45 @@ class Cluster:
     # ------------------------------------------------------------------ pool side
     def serve(self) -> None:
         """Pool ranks: a remote leader serves the router's requests; TP members follow their
-        leader's scheduler.  Returns when the router stops the pool."""
+        leader's scheduler.  A rank hosting several replicas runs one loop per replica (threads of
+        this process) and joins each node-wide sync ONCE, when all its loops have reached it.
+        Returns when the router has stopped every pool this rank serves."""
         from ..pools.remote import PoolLeader
         assert self.rank != 0
-        tier, ranks = self.my[0]
-        eng = self._engine_for(tier, ranks)
-        if self.rank == ranks[0]:
-            PoolLeader(eng, self.ctrl_groups[self.rank], self.pair_groups[self.rank], 0,
-                       on_sync=self._barrier).serve()
-        else:
-            eng.follow(on_sync=self._barrier)
+        loops = []
+        seen = set()
+        for tier, ranks in self.my:
+            eng = self._engine_for(tier, ranks)
+            if id(eng) in seen:
+                continue
+            seen.add(id(eng))
+            loops.append((eng, ranks))
+        on_sync = self._barrier
+        if len(loops) > 1:
+            gate = threading.Barrier(len(loops), action=self._barrier)
+            on_sync = gate.wait
+
+        def run(eng, ranks):
+            if self.rank == ranks[0]:
+                PoolLeader(eng, self.ctrl_groups[self.rank], self.pair_groups[self.rank], 0,
+                           on_sync=on_sync).serve()
+            else:
+                eng.follow(on_sync=on_sync)
+
+        errors: List[BaseException] = []
+
+        def guarded(eng, ranks):
+            try:
+                run(eng, ranks)
+            except BaseException as e:  # noqa: BLE001 - re-raised on the serving thread
+                errors.append(e)
+
+        threads = [threading.Thread(target=guarded, args=lp, name=f"dllm-serve-{lp[1][0]}", daemon=True)
+                   for lp in loops[1:]]
+        for t in threads:
+            t.start()
+        run(*loops[0])
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]

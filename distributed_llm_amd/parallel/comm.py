@@ -33,6 +33,7 @@ class ParallelContext:
     # and the norms run on a 1/tp token shard (reduce-scatter + all-gather replace each all-reduce)
     sequence_parallel: bool = field(default_factory=lambda: os.environ.get("DLLM_SEQ_PARALLEL", "0") == "1")
     sp_min_tokens: int = field(default_factory=lambda: int(os.environ.get("DLLM_SP_MIN_TOKENS", "256")))
+    sp_calls: int = 0                   # sequence-parallel reductions run (tests: SP really ran)
 
     @property
     def enabled(self) -> bool:
@@ -77,6 +78,26 @@ class ParallelContext:
         r.copy_(y)
         return ops.gemm.res_add_ssq(None, r, ssq)
 
+    def sp_resadd(self, y: torch.Tensor, r: torch.Tensor, ssq: torch.Tensor) -> int:
+        """Sequence-parallel form of :meth:`all_reduce_resadd` for prefill-size batches of the
+        fused layer (Megatron-SP): the row-parallel partial sums are reduce-scattered to this
+        rank's token slice, the residual add runs on the slice only, and the updated slices are
+        all-gathered back into the replicated residual ``r`` that the next column-parallel fused
+        GEMM reads (its RMSNorm row statistics are recomputed from the gathered rows: every rank
+        holds the same r, so the statistics are bitwise equal).  Same bytes on the wire as one
+        all-reduce; the add and the [T, H] reduction output shrink by tp."""
+        from .. import ops
+        from .expert_parallel import token_slice
+        T = y.shape[0]
+        lo, hi = token_slice(T, self.tp_rank, self.tp_size)
+        ys = self.reduce_scatter_rows(y)
+        rs = r[lo:hi]
+        if hi > lo:
+            ops.gemm.res_add_ssq(ys, rs, torch.empty(hi - lo, dtype=torch.float32, device=r.device))
+        r.copy_(self.all_gather_rows(rs, T))
+        self.sp_calls += 1
+        return ops.gemm.res_add_ssq(None, r, ssq)
+
     def enable_custom_all_reduce(self, device, max_bytes: Optional[int] = None) -> bool:
         """Collective over the TP group.  Returns False (RCCL only) when not applicable."""
         if self.tp_size <= 1 or self.tp_size > 8 or torch.device(device).type != "cuda":
@@ -97,16 +118,22 @@ class ParallelContext:
         contributes (its error flag != 0) to one more 16-byte one-shot all-reduce and writes
         ``sum > 0 or own flag`` into ``out`` (an int32 slot read back WITH the step's tokens), so
         live ranks agree on a trip without a per-step host all-reduce: a rank that timed out on a
-        peer still published its own data, so every rank that completes the vote sees its 1, and
-        a rank whose vote itself timed out sees its own flag."""
+        peer during the step votes 1 and trips, and every rank that completes the vote sees that
+        1; a rank whose flag was raised only by the vote's own all-reduce does NOT trip alone (its
+        step data was clean) but carries the sticky flag into the next step's vote, so every rank
+        trips on the same later step (a lone re-run would pair RCCL calls of different
+        steps across ranks)."""
         car = self.custom_ar
         if car is None:
             out.zero_()
             return
         v = car.flag_vec
-        car.vote_stage(v)          # v = (err != 0, 0, ...): one launch
+        car.vote_stage(v)          # v = (err != 0, 0, ...), err[1] = snapshot: one launch
+        fault = getattr(car, "fault_vote", None)
+        if fault is not None:      # fault injection (tests): a timeout raised DURING the vote
+            car.err[:1].bitwise_or_(fault)
         car.all_reduce(v)
-        car.vote_decide(v, out)    # out = sum > 0 | err != 0: one launch
+        car.vote_decide(v, out)    # out = own snapshot | (vote completed and sum > 0): one launch
 
     def drop_custom_ar(self, why: str) -> None:
         """Every rank of the group calls this on the same step (agreed trip): RCCL carries every

@@ -84,7 +84,8 @@ class CustomAllReduce:
             raise CustomAllReduceUnavailable("; ".join(errs))
         self.bases = bases
         self.counters = torch.zeros(2, dtype=torch.int32, device=self.device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # [0]: sticky timeout flag (bit per peer), [1]: its snapshot when the health vote is staged
+        self.err = torch.zeros(2, dtype=torch.int32, device=self.device)
         self.flag_vec = torch.zeros(8, dtype=torch.bfloat16, device=self.device)   # in-graph health vote
         dist.barrier(group=group)  # every region zeroed + mapped before the first flag is written
         self.calls = 0
@@ -95,11 +96,14 @@ class CustomAllReduce:
                 and 0 < n <= self.max_bytes)
 
     def vote_stage(self, v: torch.Tensor) -> None:
-        """Health vote, before its all-reduce: v[:8] = (this rank's error flag != 0, 0, ...)."""
+        """Health vote, before its all-reduce: v[:8] = (this rank's error flag != 0, 0, ...), and
+        the flag's snapshot in err[1]."""
         _ext().car_vote(0, self.err, v, self.err)
 
     def vote_decide(self, v: torch.Tensor, out: torch.Tensor) -> None:
-        """Health vote, after its all-reduce: out[0] = (sum > 0) or this rank's own flag."""
+        """Health vote, after its all-reduce: out[0] = 1 if this rank voted 1 or a peer did; a flag
+        raised only by the vote's own all-reduce defers the trip to the next step's vote (the
+        kernel's comment in custom_ar.hip has the agreement argument)."""
         _ext().car_vote(1, self.err, v, out)
 
     def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -139,7 +143,7 @@ class CustomAllReduce:
 
     def check(self) -> None:
         """Raise if any call timed out waiting for a peer (bitmask of missing peers)."""
-        e = int(self.err.item())
+        e = int(self.err[0].item())
         if e:
             raise RuntimeError(f"custom all-reduce: peer flags never arrived (mask {e:#x}); "
                                "TP ranks are out of step")

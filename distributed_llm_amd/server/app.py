@@ -5,7 +5,9 @@ Reference: POST /chat :27-106, GET /history :109-113, DELETE /history :116-121, 
 (user turn appended before routing and rolled back on error; last 10 messages kept).
 Differences: state is lock-protected (the reference mutates module globals from Flask's threaded
 server), CORS headers are set without flask-cors, and ``GET /metrics`` exposes cache statistics,
-pool health and engine counters; ``GET /`` serves a no-build browser chat client with the same
+pool health, engine counters and the last reply's timing.  A ``/chat`` reply carries exactly the
+reference's seven keys (``src/app.py:83-91`` and ``:98-106``); a client that sends
+``"include_timing": true`` (the bundled UI does) gets an eighth, ``timing``; ``GET /`` serves a no-build browser chat client with the same
 request/metadata contract as the reference React app (server/static/index.html).
 
 Run:  ``python -m distributed_llm_amd.server.app --pools echo|gpu [--port 8000]``
@@ -62,6 +64,7 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
         message = data.get("message", "")
         strategy = STRATEGY_ALIASES.get(data.get("strategy", "hybrid"), data.get("strategy", "hybrid"))
         session = data.get("session_id", "default")
+        want_timing = data.get("include_timing") is True   # opt-in: the reference contract has 7 keys
         if not isinstance(message, str) or not message.strip():
             return jsonify({"error": "No message provided"}), 400
         r = state["router"]
@@ -95,16 +98,22 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
                 hist = state["histories"].setdefault(session, [])
                 hist.append({"role": "assistant", "content": reply})
                 state["histories"][session] = hist[-HISTORY_LIMIT:]
-            return jsonify({"reply": reply, "device": device, "reasoning": reasoning, "method": method,
-                            "confidence": confidence, "cache_hit": cache_hit, "tokens": tokens, "timing": timing})
+                state["last_timing"] = dict(timing, session_id=session)
+            body = {"reply": reply, "device": device, "reasoning": reasoning, "method": method,
+                    "confidence": confidence, "cache_hit": cache_hit, "tokens": tokens}
+            if want_timing:
+                body["timing"] = timing
+            return jsonify(body)
         except Exception as e:
             with lock:
                 hist = state["histories"].get(session, [])
                 if hist and hist[-1]["role"] == "user":
                     hist.pop()
-            return jsonify({"reply": "System Error: The router encountered an issue.", "device": "error",
-                            "reasoning": str(e), "method": strategy, "confidence": 0.0, "cache_hit": False,
-                            "tokens": 0, "timing": {}}), 500
+            body = {"reply": "System Error: The router encountered an issue.", "device": "error",
+                    "reasoning": str(e), "method": strategy, "confidence": 0.0, "cache_hit": False, "tokens": 0}
+            if want_timing:
+                body["timing"] = {}
+            return jsonify(body), 500
 
     @app.route("/", methods=["GET"])
     def ui():
@@ -129,7 +138,7 @@ def create_app(router=None, config: Optional[Dict[str, Any]] = None, pools=None)
         r = state["router"]
         pools = {name: _safe(p.health) for name, p in r.pools.items()}
         return jsonify({"strategy": state["strategy"], "cache": r.query_router.get_cache_stats(), "pools": pools,
-                        "sessions": len(state["histories"])})
+                        "sessions": len(state["histories"]), "last_timing": state.get("last_timing")})
 
     app.config["DLLM_STATE"] = state
     return app

@@ -403,7 +403,10 @@ int main(int argc, char** argv) {
     if (only_n && sh.N != only_n) continue;
     const int N = sh.N, K = sh.K;
     const long wel = (long)N * K;
-    const int copies = std::max(2L, std::min(48L, (640L << 20) / (wel * 2)));
+    // LAB_COPIES=1: one weight copy re-read by every replay (L2 / Infinity-Cache warm) instead of
+    // the rotated cold copies
+    const char* ec = getenv("LAB_COPIES");
+    const int copies = ec ? atoi(ec) : (int)std::max(2L, std::min(48L, (640L << 20) / (wel * 2)));
     std::vector<u16*> ws(copies), wts(copies);
     std::vector<u16> hw(wel);
     u16 *A, *Y, *Wt_scratch, *Ap;

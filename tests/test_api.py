@@ -8,9 +8,34 @@ from distributed_llm_amd.pools.base import EchoPool, FaultInjectingPool
 from distributed_llm_amd.pools.worker import create_worker_app
 from distributed_llm_amd.server.app import BASE_CONFIG, HISTORY_LIMIT, create_app
 
-# the reference client's keys (fyp-chat-frontend/src/App.tsx:115-123) plus our additive `timing`
+# the reference reply's keys (src/app.py:83-91 success, :98-106 error; App.tsx:115-123 reads them)
 REF_KEYS = {"reply", "device", "reasoning", "method", "confidence", "cache_hit", "tokens"}
-CHAT_KEYS = REF_KEYS | {"timing"}
+CHAT_KEYS = REF_KEYS
+REF_APP = "/root/reference/src/app.py"
+
+
+def _reference_reply_keys():
+    """Keys of every jsonify({...}) reply in the reference's /chat with a "reply" key (None when
+    the reference tree is not present, e.g. on a GPU box)."""
+    import ast
+    import os
+    if not os.path.exists(REF_APP):
+        return None
+    out = []
+    for node in ast.walk(ast.parse(open(REF_APP).read())):
+        if isinstance(node, ast.Call) and getattr(node.func, "id", "") == "jsonify" and node.args \
+                and isinstance(node.args[0], ast.Dict):
+            keys = {k.value for k in node.args[0].keys if isinstance(k, ast.Constant)}
+            if "reply" in keys:
+                out.append(keys)
+    return out
+
+
+def test_reply_keys_match_reference_source():
+    got = _reference_reply_keys()
+    if got is None:
+        pytest.skip("reference tree not present")
+    assert got == [REF_KEYS, REF_KEYS]
 
 
 @pytest.fixture()
@@ -27,7 +52,11 @@ def test_chat_contract(client):
     from distributed_llm_amd.router.tokens import TokenCounter
     want = TokenCounter().count_tokens({"role": "assistant", "content": d["reply"]})
     assert set(d) == CHAT_KEYS and d["device"] == SMALL and d["tokens"] == want
-    assert set(d["timing"]) == {"latency_ms", "routing_ms", "ttft_ms", "failover"} and d["timing"]["failover"] is False
+    # the bundled UI opts in to an eighth key with the turn's timing; /metrics keeps the last one
+    d2 = client.post("/chat", json={"message": "Thank you!", "session_id": "s2", "include_timing": True}).get_json()
+    assert set(d2) == CHAT_KEYS | {"timing"}
+    assert set(d2["timing"]) == {"latency_ms", "routing_ms", "ttft_ms", "failover"} and d2["timing"]["failover"] is False
+    assert client.get("/metrics").get_json()["last_timing"]["session_id"] == "s2"
     assert r.headers["Access-Control-Allow-Origin"] == "*"
     h = client.get("/history?session_id=s1").get_json()
     assert [m["role"] for m in h] == ["user", "assistant"] and h[1]["content"] == d["reply"]
@@ -68,7 +97,7 @@ def test_error_rolls_back_history():
     r = c.post("/chat", json={"message": "hi", "strategy": "token", "session_id": "e"})
     assert r.status_code == 500
     d = r.get_json()
-    assert set(d) == CHAT_KEYS and d["device"] == "error" and d["reasoning"] == "kaboom" and d["timing"] == {}
+    assert set(d) == CHAT_KEYS and d["device"] == "error" and d["reasoning"] == "kaboom"
     assert c.get("/history?session_id=e").get_json() == []
 
 

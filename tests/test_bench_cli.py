@@ -19,9 +19,12 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n,extra,par,cfg", [(1, [], "dp1", 2), (2, [], "dp2", 2),
-                                             (4, ["--topology", "pools"], "pools:", 3),
-                                             (4, ["--baseline-config", "4"], "pools:small2xtp1+large1xtp2", 4),
+# N > 1 defaults to BASELINE's multi-GPU configs (3 at 2 ranks, 4 at 4-8); replicas by flag;
+# config 5 = the large TP group over every rank with a small replica co-located on each
+@pytest.mark.parametrize("n,extra,par,cfg", [(1, [], "dp1", 2), (2, [], "pools:small1xtp1+large1xtp1", 3),
+                                             (2, ["--topology", "replicated"], "dp2", 2),
+                                             (4, [], "pools:small2xtp1+large1xtp2", 4),
+                                             (2, ["--baseline-config", "5"], "colocated:small2xtp1+large1xtp2", 5),
                                              (1, ["--topology", "tiers"], "dp1-colocated", 2)])
 def test_bench_json_line(n, extra, par, cfg):
     args = ["bench.py", "--cpu", "--gpus", str(n), "--steps", "1", "--warmup", "1", "--convs", "2",
@@ -43,4 +46,9 @@ def test_bench_json_line(n, extra, par, cfg):
     assert out["config"]["parallelism"].startswith(par)
     assert out["requests"] == 2 * n and out["p50_latency_ms"] > 0
     assert out["baseline_config"] == cfg
+    lay = out["layout"]
+    assert set(lay) >= {"small", "large"} and lay["small"]["replicas"] and lay["large"]["replicas"]
+    if cfg == 5:   # every rank hosts a small replica AND a shard of the large TP group
+        assert lay["colocated"] and lay["large"]["replicas"] == [list(range(n))]
+        assert lay["small"]["replicas"] == [[r] for r in range(n)]
     assert out["per_stream_vs_baseline"] is None or out["per_stream_vs_baseline"] > 0

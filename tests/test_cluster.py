@@ -95,3 +95,54 @@ def test_default_topologies():
     assert default_topology(2).replicas == {SMALL: [[0]], LARGE: [[1]]}
     assert default_topology(8).replicas == {SMALL: [[0], [1], [2], [3]], LARGE: [[4, 5, 6, 7]]}
     assert default_topology(8, large_tp=2).replicas[LARGE] == [[4, 5], [6, 7]]
+
+
+def _coloc_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      DLLM_EMBEDDER="hash")
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from distributed_llm_amd.config import LARGE, SMALL
+        from distributed_llm_amd.orchestrator import Router
+        from distributed_llm_amd.parallel.cluster import Cluster, default_topology
+        topo = default_topology(world, colocated=True)
+        cl = Cluster(topo, _specs(), device="cpu")
+        assert len(cl.engines) == 2      # a small replica and a large TP shard on every rank
+        if rank == 0:
+            pools = cl.router_pools()
+            r = Router("heuristic", config={"cache_enabled": False}, pools=pools)
+            cl.sync()
+            res = r.route_batch(HISTS * 2)
+            cl.sync()
+            cl.shutdown()
+            q.put({"res": [(p["response"], n, d) for p, n, d in res], "syncs": len(cl.sync_times)})
+        else:
+            cl.serve()
+            q.put({"rank": rank, "syncs": len(cl.sync_times)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_colocated_pools_share_ranks():
+    """BASELINE config 5's layout on CPU: the large pool is one TP group over ranks 0-1 and each
+    rank also hosts a small replica (two engines, two serving loops per pool rank).  Both tiers
+    serve, every rank joins each node sync exactly once and exits cleanly."""
+    from distributed_llm_amd.config import LARGE, SMALL
+    from distributed_llm_amd.parallel.cluster import default_topology
+    assert default_topology(8, colocated=True).replicas == {SMALL: [[r] for r in range(8)],
+                                                            LARGE: [list(range(8))]}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_coloc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    main = [o for o in outs if "res" in o][0]
+    assert {d for _, _, d in main["res"]} == {SMALL, LARGE}
+    assert all(n > 0 for _, n, _ in main["res"])
+    assert all(o["syncs"] == 2 for o in outs)

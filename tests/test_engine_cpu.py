@@ -167,3 +167,21 @@ def test_preemption_under_kv_pressure_completes_every_request():
     assert preempts, "expected at least one preemption"
     assert eng.bm.check_invariants() == ""
     assert eng.bm.stats()["active_seqs"] == 0
+
+
+def test_block_table_sync_covers_decode_grown_columns():
+    """A row whose block table grew during decode (updates applied inside the step)
+    must be fully re-synced when it is released and re-used: the device copy of every row equals
+    the host table after the next admission, and the re-used row's output equals a fresh run."""
+    eng = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=1, seed=0)
+    sp_long = SamplingParams(max_new_tokens=70, temperature=0.0, ignore_eos=True)
+    eng.generate(["user: a\nassistant: "], sp_long)         # grows ~5 blocks during decode
+    assert eng._bt_hw >= 5
+    sp = SamplingParams(max_new_tokens=40, temperature=0.0, ignore_eos=True)
+    prompt = "user: the same row again\nassistant: "
+    got = eng.generate([prompt], sp)[0].token_ids
+    eng._bt_dirty = True
+    eng._sync_bt()
+    assert (eng.bt_dev.cpu()[:, :eng._bt_hw] == eng.bt_host_t[:, :eng._bt_hw]).all()
+    fresh = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=1, seed=0)
+    assert got == fresh.generate([prompt], sp)[0].token_ids

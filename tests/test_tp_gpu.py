@@ -93,10 +93,12 @@ def _tp1_reference(model, monkeypatch):
 # slice, all-gather before the column-parallel projections); both host-staged on the gloo group here
 MODES = [("llama-3-70b", 2, None), ("llama-3-70b", 4, None), ("mixtral-8x7b", 4, None),
          ("mixtral-8x7b", 2, {"DLLM_MOE_PARALLEL": "ep"}),
-         ("llama-3-70b", 2, {"DLLM_FUSED": "0", "DLLM_SEQ_PARALLEL": "1", "DLLM_SP_MIN_TOKENS": "8"})]
+         ("llama-3-70b", 2, {"DLLM_FUSED": "0", "DLLM_SEQ_PARALLEL": "1", "DLLM_SP_MIN_TOKENS": "8"}),
+         ("llama-3-70b", 2, {"TP_WORKER_VOTE_FAULT": "1"})]
 
 
-@pytest.mark.parametrize("model,world,extra_env", MODES, ids=["tp2", "tp4", "moe_tp4", "moe_ep2", "sp2"])
+@pytest.mark.parametrize("model,world,extra_env", MODES,
+                         ids=["tp2", "tp4", "moe_tp4", "moe_ep2", "sp2", "tp2_vote_fault"])
 def test_tensor_parallel_engine_one_gpu(model, world, extra_env, tmp_path, monkeypatch):
     res = _run_ranks(model, world, tmp_path, extra_env)
     for r in res[1:]:
@@ -108,6 +110,12 @@ def test_tensor_parallel_engine_one_gpu(model, world, extra_env, tmp_path, monke
     assert r0["graph"] == r0["eager"]
     assert all(len(t) == 8 for t in r0["graph"])
     assert r0["trips"] == 1 and not r0["custom_ar_left"]
+    # every rank tripped on the same decode step
+    assert all(r["trip_steps"] == r0["trip_steps"] for r in res[1:]), [r["trip_steps"] for r in res]
+    if (extra_env or {}).get("TP_WORKER_VOTE_FAULT") == "1":
+        # the rank whose flag rose during the vote did not trip alone on that step
+        fired = res[1]["vote_fault_step"]
+        assert fired >= 0 and r0["trip_steps"][0] > fired, (fired, r0["trip_steps"])
     # after the trip every later all-reduce runs on the fallback collective: the sums are the same
     # values in a possibly different rounding order, so require the first tokens exactly
     for a, b in zip(r0["after_trip"], r0["graph"]):

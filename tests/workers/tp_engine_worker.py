@@ -121,8 +121,16 @@ def main():
             eng.use_graphs = False
     torch.cuda.synchronize()
     log("trip phase")
-    eng.FAULT_TRIP_DECODE = eng.steps["decode"] + 2
+    if os.environ.get("TP_WORKER_VOTE_FAULT") == "1":
+        # the flag of rank 1 only is raised DURING the health vote: no rank may trip alone on
+        # that step; every rank trips together on a later one
+        eng.FAULT_VOTE_RANK = 1
+        eng.FAULT_VOTE_DECODE = eng.steps["decode"] + 2
+    else:
+        eng.FAULT_TRIP_DECODE = eng.steps["decode"] + 2
     res["after_trip"] = [o.token_ids for o in eng.generate(PROMPTS, sp)]
+    res["trip_steps"] = list(eng.trip_steps)
+    res["vote_fault_step"] = getattr(eng, "vote_fault_step", -1)
     log("after-trip decode done", res["after_trip"][0])
     res["trips"] = eng.collective_trips
     res["custom_ar_left"] = par.custom_ar is not None
