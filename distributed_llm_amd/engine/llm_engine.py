@@ -148,7 +148,8 @@ class LLMEngine:
         self.on_gpu = self.device.type == "cuda"
         self._ws_owner = ("engine", id(self))   # split-K workspaces of this engine's kernels/graphs
         # expert-parallel MoE exchanges split sizes on the host (parallel.expert_parallel): eager
-        self.use_graphs = use_graphs and self.on_gpu and not getattr(self.model, "moe_ep", False)
+        # (an expert-parallel MoE model decodes on its TP-within-expert shards: graph-capturable)
+        self.use_graphs = use_graphs and self.on_gpu
         self._gen = torch.Generator(device=self.device if self.on_gpu else "cpu")
         self._gen.manual_seed(seed + 1)
         self._seed_base = (seed * 0x9E3779B1 + 0x5851F42D) & 0x7FFFFFFF

@@ -127,9 +127,14 @@ class LlamaModel:
         self.d = cfg.head_dim
         self.I = cfg.intermediate // tp
         self.vocab_shard = shard_range(cfg.vocab, r, tp)
-        # MoE sharding: TP-within-expert (default; one all-reduce, graph-capturable) or expert
-        # parallel (E/tp whole experts per rank, all-to-all dispatch/combine: parallel.expert_parallel)
+        # MoE sharding: TP-within-expert (default; one all-reduce, graph-capturable) and, with
+        # DLLM_MOE_PARALLEL=ep, ALSO expert parallel for prefill-size batches (E/tp whole experts per
+        # rank, all-to-all dispatch/combine: parallel.expert_parallel).  EP's split sizes are a host
+        # sync, so decode steps (graph-captured) keep the TP-within-expert shards: both layouts are
+        # resident (Mixtral TP=8: +11.6 GB per GPU, cheap on a 288 GB part)
         self.moe_ep = bool(cfg.is_moe and tp > 1 and (par.moe_ep or os.environ.get("DLLM_MOE_PARALLEL") == "ep"))
+        self.ep_min_tokens = int(os.environ.get("DLLM_EP_MIN_TOKENS", "128"))
+        self.ep_calls = 0
         if self.moe_ep and cfg.n_experts % tp:
             raise ValueError(f"{cfg.name}: n_experts {cfg.n_experts} must divide ep={tp}")
         self.expert_shard = shard_range(cfg.n_experts, r, tp) if self.moe_ep else slice(0, cfg.n_experts)
@@ -144,7 +149,7 @@ class LlamaModel:
             self._fuse_weights()
         # MoE experts on the grouped LDS-tiled GEMM (csrc/kernels/moe.hip moe_ffn_tg): gate/up rows
         # of every expert interleaved in place for the SwiGLU epilogue
-        self.moe_tg = bool(cfg.is_moe and not self.moe_ep and self.device.type == "cuda" and ops.native_available()
+        self.moe_tg = bool(cfg.is_moe and self.device.type == "cuda" and ops.native_available()
                            and cfg.hidden % 64 == 0 and self.I % 64 == 0 and os.environ.get("DLLM_MOE_TG", "1") == "1")
         if self.moe_tg:
             idx = gate_up_order(self.I).to(self.device)
@@ -170,14 +175,16 @@ class LlamaModel:
                 L["wgu_f"] = fuse_gate_up_weight(L.pop("wgu"), L["ln2"])
         # K-panel-major copies of the fused decoder GEMM weights (ops.gemm.panel_weight): the tgemm
         # plans stream them; the row-major weights stay for the GEMV / skinny / hipBLASLt paths.  Kept
-        # only while both layouts fit in a quarter of the device's memory (e.g. not Llama-3-70B at
-        # TP=1: 141 GB of weights on a 288 GB part)
-        if not ops.gemm.W_PANEL or self.device.type != "cuda":
+        # only while the copies fit in a quarter of the device memory still FREE (e.g. not
+        # Llama-3-70B at TP=1: 141 GB of weights on a 288 GB part; co-located engines and processes
+        # sharing the GPU each see what the others left), and never in the one-GPU multi-rank
+        # rehearsal (N processes would each add a copy on one card)
+        if not ops.gemm.W_PANEL or self.device.type != "cuda" or os.environ.get("DLLM_REHEARSE_ONE_GPU") == "1":
             return
         names = [n for n in self.PANEL_NAMES if n in self.layers[0] and self.layers[0][n].shape[1] % 64 == 0]
         extra = sum(L[n].numel() * L[n].element_size() for L in self.layers for n in names)
-        total = torch.cuda.get_device_properties(self.device).total_memory
-        if extra > 0.25 * total:
+        free, _ = torch.cuda.mem_get_info(self.device)
+        if extra > 0.25 * free:
             return
         for L in self.layers:
             for n in names:
@@ -231,17 +238,20 @@ class LlamaModel:
             if cfg.is_moe:
                 E = cfg.n_experts
                 L["wgate"] = rnd(E, H)
-                w13 = []
-                w2 = []
+                w13, w2, w13e, w2e = [], [], [], []
                 esl = self.expert_shard
-                fsl = slice(0, cfg.intermediate) if self.moe_ep else isl
                 for e in range(E):  # every rank draws every expert (same stream), keeps its part
                     gate, up, down = rnd(cfg.intermediate, H), rnd(cfg.intermediate, H), rnd(H, cfg.intermediate)
-                    if esl.start <= e < esl.stop:
-                        w13.append(torch.cat([gate[fsl], up[fsl]], 0))
-                        w2.append(down[:, fsl])
-                L["w13"] = torch.stack(w13).contiguous()   # [E, 2I, H]
-                L["w2"] = torch.stack(w2).contiguous()     # [E, H, I]
+                    w13.append(torch.cat([gate[isl], up[isl]], 0))
+                    w2.append(down[:, isl])
+                    if self.moe_ep and esl.start <= e < esl.stop:   # this rank's whole experts (EP prefill)
+                        w13e.append(torch.cat([gate, up], 0))
+                        w2e.append(down)
+                L["w13"] = torch.stack(w13).contiguous()   # [E, 2I/tp, H]
+                L["w2"] = torch.stack(w2).contiguous()     # [E, H, I/tp]
+                if self.moe_ep:
+                    L["w13_ep"] = torch.stack(w13e).contiguous()   # [E/tp, 2I, H]
+                    L["w2_ep"] = torch.stack(w2e).contiguous()     # [E/tp, H, I]
             else:
                 gate, up, down = rnd(cfg.intermediate, H), rnd(cfg.intermediate, H), rnd(H, cfg.intermediate)
                 L["wgu"] = torch.cat([gate[isl], up[isl]], 0).contiguous()
@@ -282,12 +292,15 @@ class LlamaModel:
                 pm = p + "block_sparse_moe."
                 L["wgate"] = put(tensors[pm + "gate.weight"])
                 esl = self.expert_shard
-                fsl = slice(0, cfg.intermediate) if self.moe_ep else isl
-                L["w13"] = put(torch.stack([torch.cat([tensors[pm + f"experts.{e}.w1.weight"][fsl],
-                                                       tensors[pm + f"experts.{e}.w3.weight"][fsl]], 0)
-                                            for e in range(esl.start, esl.stop)]))
-                L["w2"] = put(torch.stack([tensors[pm + f"experts.{e}.w2.weight"][:, fsl]
-                                           for e in range(esl.start, esl.stop)]))
+
+                def experts(fsl, rng):
+                    return (put(torch.stack([torch.cat([tensors[pm + f"experts.{e}.w1.weight"][fsl],
+                                                        tensors[pm + f"experts.{e}.w3.weight"][fsl]], 0)
+                                             for e in rng])),
+                            put(torch.stack([tensors[pm + f"experts.{e}.w2.weight"][:, fsl] for e in rng])))
+                L["w13"], L["w2"] = experts(isl, range(cfg.n_experts))
+                if self.moe_ep:
+                    L["w13_ep"], L["w2_ep"] = experts(slice(0, cfg.intermediate), range(esl.start, esl.stop))
             elif p + "mlp.gate_up_proj.weight" in tensors:
                 w = tensors[p + "mlp.gate_up_proj.weight"]
                 I = cfg.intermediate
@@ -325,17 +338,24 @@ class LlamaModel:
             return ops.moe_ffn_tg(x, ids, w, L["w13"], L["w2"])
         return ops.moe_ffn(x, ids, w, L["w13"], L["w2"])
 
+    def use_ep(self, T: int) -> bool:
+        """Expert-parallel MoE for this batch: EP mode, a prefill-size batch, not inside a graph
+        capture (EP's all-to-all split sizes are a host sync)."""
+        return (self.moe_ep and T >= self.ep_min_tokens
+                and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()))
+
     def _mlp_out(self, L, x: torch.Tensor) -> torch.Tensor:
         """Complete (replicated) MLP output: TP partial sums all-reduced, or the expert-parallel
         path (token slice per rank -> all-to-all dispatch/combine -> all-gather)."""
-        if not self.moe_ep:
+        if not self.use_ep(x.shape[0]):
             return self.par.all_reduce(self._mlp(L, x))
         from ..parallel.expert_parallel import all_gather_rows, ep_moe_ffn, token_slice
         par, T = self.par, x.shape[0]
         lo, hi = token_slice(T, par.tp_rank, par.tp_size)
         xl = x[lo:hi]
         ids, w = ops.moe_gate(F.linear(xl, L["wgate"]).float(), self.cfg.experts_per_token)
-        yl = ep_moe_ffn(xl, ids, w, L["w13"], L["w2"], self.cfg.n_experts, par.tp_group, par.tp_size)
+        yl = ep_moe_ffn(xl, ids, w, L["w13_ep"], L["w2_ep"], self.cfg.n_experts, par.tp_group, par.tp_size)
+        self.ep_calls += 1
         return all_gather_rows(yl, T, par.tp_group, par.tp_size)
 
     def _attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
@@ -421,7 +441,7 @@ class LlamaModel:
                 x = ops.rms_norm(r, L["ln2"], eps)
                 if not tp:
                     n = ops.gemm.res_add_ssq(self._mlp(L, x), r, ssq_a)
-                elif self.moe_ep:   # expert parallel: the combined output is already replicated
+                elif self.use_ep(T):   # expert parallel: the combined output is already replicated
                     n = ops.gemm.res_add_ssq(self._mlp_out(L, x), r, ssq_a)
                 else:               # TP-within-expert partial sums
                     n = resadd(self._mlp(L, x), r, ssq_a)
@@ -451,7 +471,7 @@ class LlamaModel:
             o = self._attention(q, kc, vc, meta)
             h = par.reduce_scatter_rows(ops.linear(o.view(o.shape[0], -1), L["wo"]))
             x = par.all_gather_rows(ops.rms_norm(h, L["ln2"], cfg.rms_eps, residual=residual), T)
-            if self.moe_ep:
+            if self.use_ep(T):
                 h = self._mlp_out(L, x)[lo:hi]
             else:
                 h = par.reduce_scatter_rows(self._mlp(L, x))

@@ -169,10 +169,22 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
 FLASH_ROWS = 256
 
 
+FLASH_CK, FLASH_STAGES = 64, 3   # csrc/kernels/flash_prefill.hip: keys per chunk, K/V ring depth
+
+
+def flash_lds_bytes(d: int, max_blocks: int) -> int:
+    """Dynamic LDS of the flash prefill kernel's plain loop (the launcher's formula): the K/V ring
+    plus the tile's whole block-table row, staged once per workgroup (no re-staging window)."""
+    return FLASH_STAGES * (2 * FLASH_CK * d * 2) + (max_blocks * 4 + 15) // 16 * 16
+
+
 def flash_supported(d: int, group: int, max_blocks: int) -> bool:
-    # any context length: the kernel re-stages its LDS block-table window every 16K keys
+    """The flash kernel stages a tile's ENTIRE block-table row in LDS, sized at launch: it runs any
+    context whose table fits next to the ring in the 160 KB (d = 128: ~1.7M keys; the pipelined
+    d = 128 form needs 48 KB more and falls back to the plain loop on its own); longer tables go to
+    the paged kernel instead of failing at launch (dllm_flash_prefill returns -3)."""
     return d in (64, 96, 128) and FLASH_ROWS % group == 0 and max_blocks >= 1 and \
-        os.environ.get("DLLM_FLASH_PREFILL", "1") == "1"
+        flash_lds_bytes(d, max_blocks) <= 160 * 1024 and os.environ.get("DLLM_FLASH_PREFILL", "1") == "1"
 
 
 def flash_tiles(q_lens, group: int) -> Tuple[list, list]:

@@ -17,8 +17,10 @@ style), and one MoE layer is:
   all-gather: every rank gets the full [T, H] MoE output again (replicated for the next layer)
 
 Split sizes travel first as a tiny all-to-all of counts, so only real rows move (no capacity
-padding, no dropped tokens); that count exchange is a host sync, so EP layers run eagerly
-(the engine disables decode-graph capture for an EP model).  Over xGMI every all-to-all is
+padding, no dropped tokens); that count exchange is a host sync, so EP runs the prefill-size
+batches only (``LlamaModel.use_ep``: >= DLLM_EP_MIN_TOKENS tokens, eager).  Decode steps run the
+TP-within-expert shards that an EP model keeps resident as well, so they stay graph-captured
+(memory for latency: Mixtral TP=8 holds 11.6 GB more per GPU of a 288 GB part).  Over xGMI every all-to-all is
 P-1 point-to-point transfers on distinct links, which is the pattern the fully connected
 MI355X mesh serves best (no ring hops).
 """

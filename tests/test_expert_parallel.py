@@ -90,7 +90,7 @@ PROMPTS = ["user: hello there", "user: explain expert parallelism step by step",
 
 def _engine_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      DLLM_MOE_PARALLEL="ep")
+                      DLLM_MOE_PARALLEL="ep", DLLM_EP_MIN_TOKENS="1")
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -98,8 +98,9 @@ def _engine_worker(rank, world, port, q):
         from distributed_llm_amd.engine.sampling import SamplingParams
         from distributed_llm_amd.parallel.comm import make_tp_groups
         eng = LLMEngine("tiny-moe-test", device="cpu", par=make_tp_groups(world), kv_cache_gb=0.05, max_num_seqs=4)
-        assert eng.model.moe_ep and eng.model.layers[0]["w13"].shape[0] == 4 // world
+        assert eng.model.moe_ep and eng.model.layers[0]["w13_ep"].shape[0] == 4 // world
         outs = eng.generate(PROMPTS, SamplingParams(max_new_tokens=6))
+        assert eng.model.ep_calls > 0
         q.put((rank, [o.token_ids for o in outs]))
     finally:
         dist.destroy_process_group()

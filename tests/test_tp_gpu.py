@@ -89,11 +89,11 @@ def _tp1_reference(model, monkeypatch):
 
 
 # EP: Mixtral's experts split over the group (all-to-all dispatch / combine, parallel/expert_parallel.py);
-# SP: sequence-parallel prefill of the unfused layer (reduce-scatter to a token slice, norms on the
-# slice, all-gather before the column-parallel projections); both host-staged on the gloo group here
+# SP: sequence-parallel prefill of the fused layer (reduce-scatter to a token slice, residual add on
+# the slice, all-gather before the column-parallel projections); both host-staged on the gloo group here
 MODES = [("llama-3-70b", 2, None), ("llama-3-70b", 4, None), ("mixtral-8x7b", 4, None),
-         ("mixtral-8x7b", 2, {"DLLM_MOE_PARALLEL": "ep"}),
-         ("llama-3-70b", 2, {"DLLM_FUSED": "0", "DLLM_SEQ_PARALLEL": "1", "DLLM_SP_MIN_TOKENS": "8"}),
+         ("mixtral-8x7b", 2, {"DLLM_MOE_PARALLEL": "ep", "DLLM_EP_MIN_TOKENS": "8"}),
+         ("llama-3-70b", 2, {"DLLM_SEQ_PARALLEL": "1", "DLLM_SP_MIN_TOKENS": "8"}),
          ("llama-3-70b", 2, {"TP_WORKER_VOTE_FAULT": "1"})]
 
 
@@ -105,11 +105,15 @@ def test_tensor_parallel_engine_one_gpu(model, world, extra_env, tmp_path, monke
         for k in ("graph", "eager", "sampled", "after_trip"):
             assert r[k] == res[0][k], (k, r[k], res[0][k])
     r0 = res[0]
-    assert r0["graphs_on"] == (os.environ.get("DLLM_TP_GRAPHS", "1") == "1"
-                               and (extra_env or {}).get("DLLM_MOE_PARALLEL") != "ep")
+    # expert-parallel models too: EP runs the prefill-size MoE batches, decode graphs use the TP shards
+    assert r0["graphs_on"] == (os.environ.get("DLLM_TP_GRAPHS", "1") == "1")
+    if (extra_env or {}).get("DLLM_MOE_PARALLEL") == "ep":
+        assert r0["ep_calls"] > 0
     assert r0["graph"] == r0["eager"]
     assert all(len(t) == 8 for t in r0["graph"])
     assert r0["trips"] == 1 and not r0["custom_ar_left"]
+    if (extra_env or {}).get("DLLM_SEQ_PARALLEL") == "1":
+        assert r0["sp_calls"] > 0    # sequence parallelism ran inside the fused layer
     # every rank tripped on the same decode step
     assert all(r["trip_steps"] == r0["trip_steps"] for r in res[1:]), [r["trip_steps"] for r in res]
     if (extra_env or {}).get("TP_WORKER_VOTE_FAULT") == "1":

@@ -48,8 +48,8 @@ def main():
         assert eng.model.moe_ep, "expert-parallel MoE requested"
     if os.environ.get("DLLM_SEQ_PARALLEL") == "1":
         assert par.sequence_parallel and par.use_sp(64), "sequence-parallel prefill requested"
-    graphs = eng.use_graphs       # TP decode graphs: LLMEngine.TP_GRAPHS; never with expert parallel
-    assert graphs == ((world == 1 or eng.TP_GRAPHS) and not eng.model.moe_ep)
+    graphs = eng.use_graphs       # TP decode graphs: LLMEngine.TP_GRAPHS (EP models decode on TP shards)
+    assert graphs == (world == 1 or eng.TP_GRAPHS)
     sp = SamplingParams(max_new_tokens=8)
     mode = os.environ.get("TP_WORKER_MODE", "full")
     if mode == "time":   # decode ms/step, eager vs graph replay (32 sequences x 48 new tokens)
@@ -130,6 +130,8 @@ def main():
         eng.FAULT_TRIP_DECODE = eng.steps["decode"] + 2
     res["after_trip"] = [o.token_ids for o in eng.generate(PROMPTS, sp)]
     res["trip_steps"] = list(eng.trip_steps)
+    res["sp_calls"] = par.sp_calls
+    res["ep_calls"] = getattr(eng.model, "ep_calls", 0)
     res["vote_fault_step"] = getattr(eng, "vote_fault_step", -1)
     log("after-trip decode done", res["after_trip"][0])
     res["trips"] = eng.collective_trips
