@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--small-model", default=None, help="pools/tiers small tier (default per baseline config)")
     ap.add_argument("--large-model", default=None, help="pools/tiers large tier (default per baseline config)")
     ap.add_argument("--large-tp", type=int, default=None)
+    ap.add_argument("--layers", type=int, default=None,
+                    help="truncate every model to its first N decoder layers (rehearsals of the big configs on "
+                         "one GPU; the JSON line says so); never for a reported number")
     ap.add_argument("--convs", type=int, default=None,
                     help="concurrent conversations per GPU (default 512; 64 for the multi-GPU pool configs)")
     ap.add_argument("--strategy", default=None, help="routing strategy (default: perf for config 4, else hybrid)")
@@ -73,7 +76,10 @@ def parse():
     ap.add_argument("--groups", type=int, default=1,
                     help="G > 1: G independently pipelined groups of conversations, one thread each")
     ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: turn pipelining (replicated topology): conversations advance independently")
+                    help="turn pipelining (replicated topology): conversations advance independently; "
+                         "1: one thread per conversation, 2: one event-driven driver thread")
+    ap.add_argument("--admit-every", type=int, default=8,
+                    help="turn pipelining: the engine admits new turns every N decode steps of a burst")
     ap.add_argument("--no-encoder-memo", action="store_true",
                     help="encode every routed query with the GPU MiniLM encoder (no per-text memo)")
     ap.add_argument("--greedy", action="store_true",
@@ -129,6 +135,7 @@ class Conversations:
                                                                   "personal_health")]
         self.rank, self._ids = rank, itertools.count(1)   # next() is atomic: safe from worker threads
         self.convs = [self._new(i) for i in range(n)]
+        self.steps_done = 0
 
     def _new(self, i):
         return {"set": self.sets[i % 3], "turn": 0, "hist": [], "tag": f"[session r{self.rank}-{next(self._ids)}] "}
@@ -149,13 +156,15 @@ class Conversations:
             if records is not None:
                 raw = payload.get("raw") or {}
                 records.append({"lat": float(raw.get("latency_ms", 0.0)) if isinstance(raw, dict) else 0.0,
-                                "tok": int(ntok), "dev": device,
+                                "tok": int(ntok), "dev": device, "fo": payload.get("failover_from"),
+                                "ok": bool(payload.get("ok", True)), "step": self.steps_done,
                                 "ovh": float(payload.get("routing_overhead_ms", 0.0)),
                                 "ttft": float(((raw.get("timing") or {}) if isinstance(raw, dict) else {})
                                               .get("ttft_ms", 0.0))})
             c["turn"] += 1
             if c["turn"] >= len(c["set"]):
                 self.convs[i] = self._new(i)
+        self.steps_done += 1
 
 
 class PipelinedConversations(Conversations):
@@ -225,6 +234,75 @@ class PipelinedConversations(Conversations):
         self._stop = True            # workers exit after their in-flight turn
         for t in self._threads:
             t.join()
+
+
+class EventConversations(PipelinedConversations):
+    """Turn pipelining from ONE driver thread (``--pipeline 2``): every conversation whose answer
+    has arrived is routed (one batched decision pass for all of them, ``Router.dispatch_batch``)
+    and its next turn is submitted to the engine without blocking; the driver then collects
+    whatever finished and repeats.  Each conversation stays strictly sequential, the continuous
+    batch stays full (a small-tier answer's conversation re-enters while large-tier answers are
+    still decoding), and there is no per-conversation thread competing for the GIL.  The engine
+    admits new turns every ``--admit-every`` decode steps so its pipelined bursts stay long.
+    Same steady-state window accounting as the parent (a step = ``n_convs`` completed turns)."""
+
+    POLL_S = 0.001
+
+    def start(self, router) -> None:
+        import threading
+        self._cv = threading.Condition()
+        self.completed = 0
+        self.records = None
+        self._stop = False
+        self.errors = []
+
+        def driver():
+            try:
+                ready = list(range(len(self.convs)))
+                inflight = {}
+                while not self._stop:
+                    if ready:
+                        hs = []
+                        for i in ready:
+                            c = self.convs[i]
+                            q = c["set"][c["turn"]].text
+                            if c["turn"] == 0:
+                                q = c["tag"] + q
+                            c["hist"].append({"role": "user", "content": q})
+                            hs.append(c["hist"])
+                        for i, t in zip(ready, router.dispatch_batch(hs)):
+                            inflight[i] = t
+                        ready = []
+                    done = [i for i, t in inflight.items() if router.ticket_done(t)]
+                    if not done:
+                        time.sleep(self.POLL_S)
+                        continue
+                    recs = []
+                    for i in done:
+                        payload, ntok, device = router.finish_ticket(inflight.pop(i))
+                        c = self.convs[i]
+                        c["hist"].append({"role": "assistant", "content": payload["response"]})
+                        raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
+                        recs.append({"lat": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
+                                     "ovh": float(payload.get("routing_overhead_ms", 0.0)),
+                                     "ttft": float((raw.get("timing") or {}).get("ttft_ms", 0.0)),
+                                     "fo": payload.get("failover_from"), "ok": bool(payload.get("ok", True))})
+                        c["turn"] += 1
+                        if c["turn"] >= len(c["set"]):
+                            self.convs[i] = self._new(i)
+                        ready.append(i)
+                    with self._cv:
+                        if self.records is not None:
+                            self.records.extend(recs)
+                        self.completed += len(recs)
+                        self._cv.notify_all()
+            except BaseException as e:  # surfaced by wait_turns
+                with self._cv:
+                    self.errors.append(e)
+                    self._cv.notify_all()
+
+        self._threads = [threading.Thread(target=driver, name="bench-driver", daemon=True)]
+        self._threads[0].start()
 
 
 class GroupedConversations(PipelinedConversations):
@@ -327,11 +405,23 @@ def main() -> int:
     layout = None
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
+    if topology in ("pools", "colocated"):
+        # the multi-GPU configs are failover tests too (config 4: "perf-router failover"): a failed
+        # tier is charged in the perf router, which also tries an unseen tier
+        cfg.update(penalise_failed_primary=True, perf_explore=True)
 
     # reference Orin defaults (Ollama: T 0.8, top-k 40, top-p 0.9); --greedy for exact comparisons
     large_sampling = (dict(temperature=0.0, top_k=0, top_p=1.0) if a.greedy
                       else dict(temperature=0.8, top_k=40, top_p=0.9))
     cluster = None
+
+    def mdl(name):
+        """A model to build: the registry name, or its layer-truncated config under --layers."""
+        if not a.layers:
+            return name
+        from distributed_llm_amd.models.configs import get_model_config
+        return get_model_config(name, n_layers=a.layers)
+
     if topology == "tiers":
         # heterogeneous tiers co-located on each GPU: a small-model engine and a large-model engine
         # (BASELINE config 3's model pair; the reference runs them on two boards)
@@ -340,9 +430,9 @@ def main() -> int:
         sm = a.small_model if on_gpu else "tiny-llama-test"
         lg = a.large_model if on_gpu else "tiny-llama-test"
         kv = (a.kv_gb / 2) if on_gpu else 0.1
-        e_small = LLMEngine(sm, device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
+        e_small = LLMEngine(mdl(sm), device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
                             use_graphs=not a.no_graphs, seed=0)
-        e_large = LLMEngine(lg, device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
+        e_large = LLMEngine(mdl(lg), device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
                             use_graphs=not a.no_graphs, seed=0)   # seed 0 like the pools' engines
         pools = {SMALL: EnginePool(SMALL, e_small, max_new_tokens=a.small_new, temperature=0.0),
                  LARGE: EnginePool(LARGE, e_large, max_new_tokens=a.large_new, **large_sampling)}
@@ -358,7 +448,7 @@ def main() -> int:
         from distributed_llm_amd.engine.llm_engine import LLMEngine
         from distributed_llm_amd.pools.base import EnginePool
         model = a.model if on_gpu else "tiny-llama-test"
-        engine = LLMEngine(model, device=dev, kv_cache_gb=a.kv_gb if on_gpu else 0.2,
+        engine = LLMEngine(mdl(model), device=dev, kv_cache_gb=a.kv_gb if on_gpu else 0.2,
                            max_num_seqs=max(16, a.convs), use_graphs=not a.no_graphs, seed=0)
         pools = {SMALL: EnginePool(SMALL, engine, max_new_tokens=a.small_new, temperature=0.0),
                  LARGE: EnginePool(LARGE, engine, max_new_tokens=a.large_new, **large_sampling)}
@@ -378,9 +468,9 @@ def main() -> int:
         n_small = len(topo.replicas[SMALL])
         # (a one-GPU rehearsal runs the collectives on gloo, which a hipGraph cannot capture)
         graphs = not (a.no_graphs or rehearse)
-        specs = {SMALL: TierSpec(sm, a.small_new, 0.0, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
+        specs = {SMALL: TierSpec(mdl(sm), a.small_new, 0.0, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
                                  max_num_seqs=max(16, a.convs * world), graphs=graphs),
-                 LARGE: TierSpec(lg, a.large_new, large_sampling["temperature"], large_sampling["top_k"],
+                 LARGE: TierSpec(mdl(lg), a.large_new, large_sampling["temperature"], large_sampling["top_k"],
                                  large_sampling["top_p"], kv_cache_gb=a.kv_gb if on_gpu else 0.1,
                                  max_num_seqs=max(16, a.convs * world), graphs=graphs)}
         cluster = Cluster(topo, specs, device=dev)
@@ -434,8 +524,10 @@ def main() -> int:
         pipelined = (bool(a.pipeline) or a.groups > 1) and cluster is None
         if pipelined:
             for e in engines:
+                e.ADMIT_EVERY = max(1, a.admit_every)
                 e.start()              # background step loop: callers only enqueue and wait
             convs = (GroupedConversations(n_convs, rank, a.groups) if a.groups > 1
+                     else EventConversations(n_convs, rank) if a.pipeline == 2
                      else PipelinedConversations(n_convs, rank))
             convs.start(router)
             convs.wait_turns(a.warmup * n_convs)
@@ -494,17 +586,31 @@ def main() -> int:
         energy_j = mj / 1000.0 if how == "counter" else -1.0
     if rehearse and rank != 0 and energy_j >= 0:
         energy_j = 0.0   # every rank read the SAME card's counter: count it once (rank 0's)
+    dead_ranks = []
+    degraded = bool(cluster is not None and cluster.degraded)
     if world > 1:
-        t = torch.tensor([float(tokens), elapsed, energy_j, 1.0 if energy_j < 0 else 0.0], dtype=torch.float64,
-                         device=coll_dev)
-        dist.all_reduce(t[:1], op=dist.ReduceOp.SUM)
-        dist.all_reduce(t[1:2], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[2:], op=dist.ReduceOp.SUM)
-        tokens_all, elapsed_max = float(t[0]), float(t[1])
-        energy_j = float(t[2]) if float(t[3]) == 0 else -1.0
-        gathered = [None] * world
-        dist.all_gather_object(gathered, lats)
-        lats = sorted(x for g in gathered for x in g)
+        # cross-rank reduction through the rendezvous store (hosted by rank 0's process): a pool
+        # rank lost mid-run (fault injection, a dead GPU) leaves a missing key instead of hanging
+        # a collective; rank 0 reduces whatever the survivors reported
+        import datetime
+        store = dist.distributed_c10d._get_default_store()
+        store.set(f"dllm_bench/{rank}", json.dumps({"tokens": float(tokens), "elapsed": elapsed, "energy": energy_j,
+                                                    "lats": lats}))
+        tokens_all, elapsed_max, e_sum, e_bad = 0.0, 0.0, 0.0, False
+        if rank == 0:
+            got = []
+            for r in range(world):
+                try:
+                    store.wait([f"dllm_bench/{r}"], datetime.timedelta(seconds=60 if not degraded else 10))
+                    got.append(json.loads(store.get(f"dllm_bench/{r}")))
+                except Exception:  # noqa: BLE001 - this rank never reported: it died
+                    dead_ranks.append(r)
+            tokens_all = sum(g["tokens"] for g in got)
+            elapsed_max = max(g["elapsed"] for g in got)
+            e_bad = any(g["energy"] < 0 for g in got) or bool(dead_ranks)
+            energy_j = -1.0 if e_bad else sum(g["energy"] for g in got)
+            lats = sorted(x for g in got for x in g["lats"])
+            degraded = degraded or bool(dead_ranks)
     else:
         tokens_all, elapsed_max = float(tokens), elapsed
     if rank == 0:
@@ -542,7 +648,12 @@ def main() -> int:
             "config": {"model": model_desc, "global_batch": a.convs * world,
                        "seq_len": "growing conversation (<=16384)", "parallelism": parallelism,
                        "strategy": a.strategy, "semantic_cache": True, "response_cache": False,
-                       "turn_pipelining": (bool(a.pipeline) or a.groups > 1) and topology == "replicated",
+                       "perf_explore": bool(cfg.get("perf_explore")),
+                       "penalise_failed_primary": bool(cfg.get("penalise_failed_primary")),
+                       "turn_pipelining": ((("event-driver" if a.pipeline == 2 else "thread-per-conversation")
+                                            if a.pipeline else "grouped" if a.groups > 1 else False)
+                                           if topology == "replicated" else False),
+                       "admit_every": a.admit_every if (a.pipeline or a.groups > 1) else None,
                        "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
             "p50_latency_ms": round(statistics.median(lats), 1) if lats else None,
@@ -569,6 +680,20 @@ def main() -> int:
             out["j_per_token"] = round(energy_j / max(tokens_all, 1.0), 4)
         if rehearse:
             out["rehearsal_one_gpu"] = True   # N ranks shared ONE GPU: plumbing check, not a number
+        if a.layers:
+            out["truncated_layers"] = a.layers   # not the named models' full depth: not a number either
+        fo = [r for r in records if r.get("fo")]
+        dead_tiers = sorted({r["fo"] for r in fo})
+        first_fo = min((r["step"] for r in fo), default=None)
+        out["pool_events"] = {
+            "failovers": len(fo), "lost_turns": sum(1 for r in records if not r.get("ok", True)),
+            "dead_ranks": dead_ranks, "degraded": degraded, "failed_tiers": dead_tiers,
+            "first_failover_step": first_fo,
+            # failed-over turns per step from the first failover on (a tier known to be down is
+            # skipped up front: those turns still count here, they are served by the other tier)
+            "failovers_by_step": (
+                [sum(1 for r in fo if r["step"] == st) for st in range(first_fo, a.warmup + a.steps)]
+                if first_fo is not None else [])}
         # rank-0 wall time not inside any engine timer: routing, prompt formatting, orchestration
         out["engine_time_split_s"]["outside_engine_s"] = round(
             elapsed_max - sum(out["engine_time_split_s"].values()), 3) if len(engines) == 1 else None
@@ -582,6 +707,12 @@ def main() -> int:
         from distributed_llm_amd.utils.tracing import tracer
         tracer.dump()
     if world > 1:
+        if degraded:
+            # a peer is gone: no further collectives (they would fail or hang); leave without the
+            # process-group teardown handshake
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -351,6 +351,33 @@ class LLMEngine:
     def generate(self, prompts: Sequence[Union[str, List[int]]],
                  params: Union[SamplingParams, Sequence[SamplingParams], None] = None) -> List[RequestOutput]:
         """Run a batch of requests to completion with continuous batching."""
+        seqs = self._make_seqs(prompts, params)
+        self._submit_and_wait([s for s in seqs if s.error is None])
+        return self.results(seqs)
+
+    def submit(self, prompts: Sequence[Union[str, List[int]]],
+               params: Union[SamplingParams, Sequence[SamplingParams], None] = None) -> List["_Seq"]:
+        """Enqueue requests WITHOUT waiting (the background loop, ``start()``, must be running):
+        returns handles whose ``done`` event is set when each request has finished; ``results``
+        turns them into outputs.  An event-driven client (bench.py turn pipelining) keeps the
+        continuous batch full from one thread this way instead of one blocked thread per request."""
+        if self._bg is None:
+            raise RuntimeError("submit() needs the background loop (start())")
+        seqs = self._make_seqs(prompts, params)
+        live = [s for s in seqs if s.error is None]
+        with self._inbox_lock:
+            self._inbox.extend(live)
+            self._inbox_cv.notify()
+        return seqs
+
+    def results(self, seqs: Sequence["_Seq"]) -> List[RequestOutput]:
+        _t = time.perf_counter()
+        outs = [self._output(s) for s in seqs]
+        self.timers["output"] += time.perf_counter() - _t
+        return outs
+
+    def _make_seqs(self, prompts: Sequence[Union[str, List[int]]],
+                   params: Union[SamplingParams, Sequence[SamplingParams], None]) -> List["_Seq"]:
         if params is None:
             params = SamplingParams()
         plist = list(params) if isinstance(params, (list, tuple)) else [params] * len(prompts)
@@ -368,11 +395,7 @@ class LLMEngine:
                 s.done.set()
             seqs.append(s)
         self.timers["encode"] += time.perf_counter() - _t
-        self._submit_and_wait([s for s in seqs if s.error is None])
-        _t = time.perf_counter()
-        outs = [self._output(s) for s in seqs]
-        self.timers["output"] += time.perf_counter() - _t
-        return outs
+        return seqs
 
     def _submit_and_wait(self, seqs: List[_Seq]) -> None:
         """Continuous batching across callers (leader/follower): requests from concurrent threads
@@ -1009,6 +1032,12 @@ class LLMEngine:
     # and discarded (its KV slot belongs to the finished sequence).  Count limits (max_new_tokens,
     # max_model_len) are known in advance and never cost a row.
     PIPELINE = os.environ.get("DLLM_DECODE_PIPELINE", "1") == "1"
+    # New requests end a pipelined burst (to be admitted and prefilled) only once the burst has run
+    # this many steps: a client that keeps submitting (turn pipelining) would otherwise cut every
+    # burst to one or two steps and lose the host/GPU overlap; the added admission delay is at most
+    # ADMIT_EVERY decode steps.  1 = admit at the next step (turn-synchronous clients submit only
+    # into an idle engine, where it makes no difference).
+    ADMIT_EVERY = max(1, int(os.environ.get("DLLM_ADMIT_EVERY", "1")))
 
     # Tensor-parallel pools pipeline too (DLLM_TP_PIPELINE=0: off).  Every rank must take the same
     # burst decisions, so a TP burst never looks at the leader-only inbox: it ends on the shared
@@ -1068,7 +1097,9 @@ class LLMEngine:
             alive = [s for s in cur if id(s) not in gone]
             # the next step's rows: sequences that cannot reach a count limit with the token in flight
             nxt = [s for s in alive if len(s.out) + 1 < s.params.max_new_tokens and s.length + 1 < mml]
-            stop = (not nxt or freed or (nsteps >= self.MIRROR_EVERY if self._mirror is not None else bool(self._inbox))
+            stop = (not nxt or freed
+                    or (nsteps >= self.MIRROR_EVERY if self._mirror is not None
+                        else (bool(self._inbox) and nsteps >= self.ADMIT_EVERY))
                     or (bool(waiting) and len(nxt) < len(alive)))
             launched = None
             pending_pre: set = set()

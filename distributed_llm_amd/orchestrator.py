@@ -196,6 +196,8 @@ class Router:
                    "routing_method": dec["method"],
                    "routing_confidence": round(dec["confidence"], 4),
                    "routing_reasoning": dec["reasoning"], "ok": ok}
+        if primary_failed:
+            payload["failover_from"] = primary_failed   # the decided tier failed; ``which`` served it
         if isinstance(raw, dict) and "timing" in raw:
             payload["timing"] = dict(raw["timing"], generated_tokens=ntok, counted_tokens=counted)
         return payload, toks, which
@@ -219,6 +221,16 @@ class Router:
             except Exception:  # noqa: BLE001
                 pass
 
+    def _pool_down(self, device: str) -> bool:
+        """A pool known to be out of service (a remote pool whose process died or that failed its
+        health probes: ``alive`` False) while the other tier's pool is up: requests decided for it
+        go straight to the other tier as a failover instead of paying a failed attempt first."""
+        if not self.enable_failover:
+            return False
+        pool, other = self.pools.get(device), self.pools.get(other_tier(device))
+        return (pool is not None and getattr(pool, "alive", True) is False
+                and other is not None and getattr(other, "alive", True) is not False)
+
     def _run(self, device: str, history, failover: bool = False) -> Tuple[Any, str, float]:
         t0 = time.perf_counter()
         try:
@@ -238,6 +250,9 @@ class Router:
         if hit is not None:
             return hit
         dec = self._decide(query, context, ctx_hash, conversation_history)
+        if self._pool_down(dec["device"]):
+            raw, which, lat = self._run(other_tier(dec["device"]), conversation_history, failover=True)
+            return self._finish(query, dec, raw, which, lat, dec["device"])
         raw, which, lat = self._run(dec["device"], conversation_history)
         failed = None
         if self.enable_failover and is_error(raw):
@@ -266,14 +281,20 @@ class Router:
             dec = self._decide(query, context, ctx_hash, h)
             meta[i] = (query, dec)
             groups[dec["device"]].append(i)
+        failed: Dict[int, str] = {}
+        for dev in (SMALL, LARGE):   # a tier that is down: its turns go to the other tier up front
+            if groups[dev] and self._pool_down(dev):
+                for i in groups[dev]:
+                    failed[i] = dev
+                groups[other_tier(dev)].extend(groups[dev])
+                groups[dev] = []
         retry: Dict[str, List[int]] = {SMALL: [], LARGE: []}
         raws: Dict[int, Tuple[Any, str, float]] = {}
         for dev, outs in self._process_groups(groups, histories).items():
             for i, (raw, lat) in zip(groups[dev], outs):
                 raws[i] = (raw, dev, lat)
-                if self.enable_failover and is_error(raw):
+                if self.enable_failover and is_error(raw) and i not in failed:
                     retry[other_tier(dev)].append(i)
-        failed: Dict[int, str] = {}
         if any(retry.values()):
             for dev, outs in self._process_groups(retry, histories).items():
                 for i, (raw, lat) in zip(retry[dev], outs):
@@ -328,6 +349,63 @@ class Router:
         if isinstance(raw, dict) and "latency_ms" in raw:
             lat = float(raw["latency_ms"])
         return self._finish(query, dec, raw, which, lat, failed)
+
+    # ------------------------------------------------------------------ event-driven dispatch
+    def dispatch_batch(self, histories: Sequence[List[Dict[str, Any]]]) -> List[Dict[str, Any]]:
+        """Route a batch of conversations (one batched decision pass) and SUBMIT each request to
+        its tier without waiting: pools with a non-blocking ``submit_batch`` (in-process engines
+        running their background loop) return handles; other pools are served synchronously here.
+        Returns one ticket per history; ``ticket_done`` / ``finish_ticket`` complete them.  A
+        single client thread can keep hundreds of independent conversations in flight this way
+        (each conversation still strictly sequential), instead of one blocked thread each."""
+        tickets: List[Dict[str, Any]] = []
+        groups: Dict[str, List[int]] = {SMALL: [], LARGE: []}
+        for i, (kind, a, dec) in enumerate(self._decide_batch(histories)):
+            t: Dict[str, Any] = {"history": histories[i], "t0": time.perf_counter()}
+            if kind == "hit":
+                t["payload"] = a
+            else:
+                t["query"], t["dec"], t["device"] = a, dec, dec["device"]
+                groups[dec["device"]].append(i)
+            tickets.append(t)
+        for dev, idx in groups.items():
+            if not idx:
+                continue
+            pool = self.pools[dev]
+            hs = [histories[i] for i in idx]
+            sub = getattr(pool, "submit_batch", None)
+            if sub is not None:
+                for i, h in zip(idx, sub(hs)):
+                    tickets[i]["handle"] = h
+            else:
+                for i, raw in zip(idx, self._process_groups({dev: idx}, histories)[dev]):
+                    tickets[i]["raw"] = raw[0]
+        return tickets
+
+    @staticmethod
+    def ticket_done(t: Dict[str, Any]) -> bool:
+        h = t.get("handle")
+        return h is None or h.done.is_set()
+
+    def finish_ticket(self, t: Dict[str, Any]):
+        """(payload, response_tokens, device) of a done ticket: perf feedback, failover to the
+        other tier (synchronously) on an error, response-cache store — as ``route_query``."""
+        if "payload" in t:
+            return t["payload"]
+        which = t["device"]
+        if "handle" in t:
+            raw = self.pools[which].collect([t["handle"]])[0]
+        else:
+            raw = t["raw"]
+        lat = float(raw["latency_ms"]) if isinstance(raw, dict) and "latency_ms" in raw else \
+            (time.perf_counter() - t["t0"]) * 1000.0
+        failed = None
+        if self.enable_failover and is_error(raw):
+            raw2, which2, lat2 = self._run(other_tier(which), t["history"], failover=True)
+            if not is_error(raw2):
+                failed = which
+                raw, which, lat = raw2, which2, lat2
+        return self._finish(t["query"], t["dec"], raw, which, lat, failed)
 
     def _prefetch_embeddings(self, queries: List[str]) -> None:
         """One batched encoder forward for every query of a batch (the GPU encoder keeps it for the

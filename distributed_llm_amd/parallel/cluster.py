@@ -38,9 +38,19 @@ from ..config import LARGE, SMALL
 from .comm import ParallelContext
 
 
+def model_name(model) -> str:
+    """A TierSpec's model: a registry name, or a ``ModelConfig`` (e.g. layer-truncated rehearsals)."""
+    return model if isinstance(model, str) else model.name
+
+
+def model_config(model):
+    from ..models.configs import get_model_config
+    return get_model_config(model) if isinstance(model, str) else model
+
+
 @dataclass
 class TierSpec:
-    model: str = "tinyllama-1.1b"
+    model: Any = "tinyllama-1.1b"     # registry name or models.configs.ModelConfig
     max_new_tokens: int = 256
     temperature: float = 0.0
     top_k: int = 0
@@ -91,6 +101,7 @@ class Cluster:
         self.device = device or ("cuda" if torch.cuda.is_available() else "cpu")
         self.request_timeout_s = request_timeout_s
         self.sync_times: List[float] = []
+        self.degraded = False   # or a reason string: a rank of the node died
         # --- groups (collective: every rank creates every group in the same order)
         #   tp_groups:     RCCL (default backend) per TP replica: model all-reduces
         #   mirror_groups: gloo per TP replica: the leader's scheduler broadcast (engine mirror)
@@ -128,7 +139,7 @@ class Cluster:
         from ..engine.llm_engine import LLMEngine
         for tier, ranks in self.my:
             spec = specs[tier]
-            key = (tuple(ranks), spec.model)
+            key = (tuple(ranks), model_name(spec.model))
             if key in self.engines:
                 continue
             par = ParallelContext(len(ranks), ranks.index(self.rank), self.tp_groups.get(tuple(ranks)),
@@ -143,7 +154,7 @@ class Cluster:
 
     # ------------------------------------------------------------------ router side
     def _engine_for(self, tier: str, ranks: List[int]):
-        return self.engines[(tuple(ranks), self.specs[tier].model)]
+        return self.engines[(tuple(ranks), model_name(self.specs[tier].model))]
 
     def router_pools(self, on_health=None, probe_interval_s: Optional[float] = None):
         """{tier: PoolClient} for the router on rank 0.  ``on_health(name, ok, rtt_us)`` receives
@@ -169,7 +180,7 @@ class Cluster:
                         self.local_engines.append(eng)
                     reps.append(EnginePool(tier, eng, **kw))
                 else:
-                    cfg = get_model_config(spec.model)
+                    cfg = model_config(spec.model)
                     rp = RemotePool(tier, ranks[0], self.ctrl_groups[ranks[0]], self.pair_groups[ranks[0]],
                                     timeout_s=self.request_timeout_s, on_health=on_health,
                                     tokenizer=get_tokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id), **kw)
@@ -192,9 +203,17 @@ class Cluster:
         self._barrier()
 
     def _barrier(self) -> None:
+        """Node-wide barrier.  A rank that died (a pool process lost mid-run) makes the barrier
+        fail on every survivor: the node is then ``degraded`` and later barriers are skipped, so
+        the survivors still finish (the bench reduces its results through the rendezvous store,
+        which outlives any non-zero rank)."""
         if torch.cuda.is_available():
             torch.cuda.synchronize()
-        dist.barrier()
+        if not self.degraded:
+            try:
+                dist.barrier()
+            except Exception as e:  # noqa: BLE001 - a peer died (gloo: connection closed)
+                self.degraded = f"node barrier failed: {e}"
         self.sync_times.append(time.perf_counter())
 
     def shutdown(self) -> None:
@@ -222,16 +241,27 @@ class Cluster:
             seen.add(id(eng))
             loops.append((eng, ranks))
         on_sync = self._barrier
-        if len(loops) > 1:
-            gate = threading.Barrier(len(loops), action=self._barrier)
-            on_sync = gate.wait
+        gate = threading.Barrier(len(loops), action=self._barrier) if len(loops) > 1 else None
+        if gate is not None:
+            def on_sync():
+                try:
+                    gate.wait()
+                except threading.BrokenBarrierError:   # a co-located loop ended (its pool died)
+                    self._barrier()
 
         def run(eng, ranks):
             if self.rank == ranks[0]:
                 PoolLeader(eng, self.ctrl_groups[self.rank], self.pair_groups[self.rank], 0,
                            on_sync=on_sync).serve()
-            else:
+                return
+            try:
                 eng.follow(on_sync=on_sync)
+            except Exception as e:  # noqa: BLE001 - the TP leader's process died: this pool is gone
+                import logging
+                self.degraded = f"TP leader rank {ranks[0]} lost: {e}"
+                logging.getLogger(__name__).error("TP member of %s: %s", ranks, self.degraded)
+                if gate is not None:
+                    gate.abort()   # co-located loops on this rank must not wait for this one
 
         errors: List[BaseException] = []
 

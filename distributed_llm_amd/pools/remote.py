@@ -426,6 +426,12 @@ class PoolLeader:
                     if os.environ.get("DLLM_FAULT_DIE_ON") and any(
                             os.environ["DLLM_FAULT_DIE_ON"] in p for p in msg.get("prompts", [])):
                         os._exit(17)   # fault injection (tests): the pool process dies mid-request
+                    self._gen_seen = getattr(self, "_gen_seen", 0) + 1
+                    die_after = int(os.environ.get("DLLM_FAULT_DIE_AFTER", "0"))
+                    die_rank = os.environ.get("DLLM_FAULT_DIE_RANK")
+                    if die_after and self._gen_seen > die_after and (
+                            die_rank is None or int(die_rank) == int(os.environ.get("RANK", "-1"))):
+                        os._exit(17)   # fault injection (tests): this leader dies after N requests
                     self._ex.submit(self._generate, msg["id"], msg["prompts"], msg.get("params"))
                 elif op == "generate_ids":
                     self._dq.put(msg)

@@ -401,6 +401,9 @@ class PerformanceAwareRouter(BaseRouter):
         super().__init__(config)
         self.window = int(config.get("perf_window", 30))
         self.fail_penalty = float(config.get("perf_fail_penalty", 3000.0))
+        # reference quirk 3: a device without stats scores inf and is never tried
+        # once the other has stats; ``perf_explore`` sends the next request to it instead
+        self.explore = bool(config.get("perf_explore", False))
         self.stats: Dict[str, deque] = {SMALL: deque(), LARGE: deque()}
         self._sums = {SMALL: [0.0, 0, 0], LARGE: [0.0, 0, 0]}
         self._lock = threading.Lock()
@@ -434,6 +437,9 @@ class PerformanceAwareRouter(BaseRouter):
         ns, os_ = self._score(SMALL), self._score(LARGE)
         if ns == float("inf") and os_ == float("inf"):
             return RoutingDecision(SMALL, 0.2, "perf", "no perf stats yet -> default nano")
+        if self.explore and (ns == float("inf") or os_ == float("inf")):
+            dev = SMALL if ns == float("inf") else LARGE
+            return RoutingDecision(dev, 0.2, "perf", f"no perf stats for {dev} yet -> exploring {dev}")
         dev = LARGE if os_ < ns else SMALL
         return RoutingDecision(dev, 0.70, "perf", f"scores nano={ns:.2f} orin={os_:.2f} -> {dev}")
 

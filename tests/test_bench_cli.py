@@ -52,3 +52,27 @@ def test_bench_json_line(n, extra, par, cfg):
         assert lay["colocated"] and lay["large"]["replicas"] == [list(range(n))]
         assert lay["small"]["replicas"] == [[r] for r in range(n)]
     assert out["per_stream_vs_baseline"] is None or out["per_stream_vs_baseline"] > 0
+
+
+def test_bench_survives_pool_leader_death():
+    """Pools topology on 4 CPU ranks (small replicas [0], [1]; large TP=2 on [2, 3]) with the large
+    leader killed by fault injection after its first request batch: plain processes (not torchrun,
+    whose agent would tear every rank down), the survivors exit 0, no turn is lost (failover to the
+    small replicas), and rank 0 reduces the survivors' results through the rendezvous store."""
+    world, port = 4, _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), DLLM_EMBEDDER="hash", OMP_NUM_THREADS="1", DLLM_FAULT_DIE_RANK="2",
+                   DLLM_FAULT_DIE_AFTER="1")
+        procs.append(subprocess.Popen([sys.executable, "bench.py", "--cpu", "--gpus", str(world), "--steps", "3",
+                                       "--warmup", "1", "--convs", "3", "--small-new", "4", "--large-new", "6",
+                                       "--strategy", "hybrid"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.DEVNULL, text=True))
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    assert [p.returncode for p in procs] == [0, 0, 17, 0]
+    line = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
+    out = json.loads(line[0])
+    ev = out["pool_events"]
+    assert ev["dead_ranks"] == [2] and ev["failed_tiers"] == ["orin"] and ev["degraded"]
+    assert ev["failovers"] > 0 and ev["lost_turns"] == 0 and out["requests"] == 3 * world * 3

@@ -130,3 +130,56 @@ def test_penalise_failed_primary_option():
     r.route_query([{"role": "user", "content": "q"}])
     snap = r.query_router.router.snapshot()
     assert snap[SMALL]["n"] == 1 and snap[LARGE]["n"] == 1
+
+
+class _DyingPool(EchoPool):
+    """A remote-pool stand-in: answers until ``die()``, then errors and reports ``alive`` False
+    (as pools.remote.RemotePool does once its process is gone)."""
+
+    def __init__(self, name):
+        super().__init__(name, 20)
+        self.alive = True
+        self.calls = 0
+
+    def die(self):
+        self.alive = False
+
+    def process(self, history):
+        self.calls += 1
+        if not self.alive:
+            return {"error": "pool process died"}
+        return super().process(history)
+
+
+def test_perf_router_with_exploration_stops_choosing_a_dead_pool():
+    """BASELINE config 4's perf-router failover: with ``perf_explore`` the large tier is tried,
+    its death fails turns over to the small tier (none lost), failures are charged to it
+    (``penalise_failed_primary``) and the perf router stops choosing it; a pool reported down
+    is skipped up front (no failed attempt per turn)."""
+    large = _DyingPool(LARGE)
+    r = Router("perf", config={"cache_enabled": False, "perf_explore": True, "penalise_failed_primary": True},
+               pools={SMALL: EchoPool(SMALL, 6), LARGE: large})
+    h = [{"role": "user", "content": "hello"}]
+    devs = [r.route_query(h)[2] for _ in range(2)]
+    assert devs == [SMALL, LARGE]            # no stats -> small; then the unseen large is explored
+    large.die()
+    out = [r.route_query(h) for _ in range(6)]
+    assert all(p["ok"] and d == SMALL for p, _, d in out)   # zero lost turns
+    calls = large.calls
+    decisions = [r.query_router.route_query("hello").device for _ in range(3)]
+    assert decisions == [SMALL] * 3          # the failure penalty keeps the perf router away
+    r.route_batch([h, h])
+    assert large.calls == calls              # a pool that is down is not even attempted
+
+
+def test_dead_pool_skipped_up_front_for_any_strategy():
+    large = _DyingPool(LARGE)
+    r = Router("heuristic", config={"cache_enabled": False}, pools={SMALL: EchoPool(SMALL), LARGE: large})
+    q = [{"role": "user", "content": "Write a Python function for knapsack with dynamic programming"}]
+    assert r.route_query(q)[2] == LARGE
+    large.die()
+    calls = large.calls
+    p, _, d = r.route_query(q)
+    assert d == SMALL and p["ok"] and p["failover_from"] == LARGE and large.calls == calls
+    res = r.route_batch([q, q])
+    assert all(x[2] == SMALL and x[0]["failover_from"] == LARGE for x in res) and large.calls == calls

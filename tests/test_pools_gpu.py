@@ -71,7 +71,7 @@ def test_pools_topology_n_ranks_one_gpu(world, single, tmp_path):
                 "--topology", "pools", "--convs", str(CONVS // world), "--dump-responses", dump, *COMMON],
                os.path.join(logdir, f"pools_n{world}.log"), timeout=600)
     assert res["n_gpus"] == world and res.get("rehearsal_one_gpu") is True
-    assert res["baseline_config"] == (4 if world == 8 else 3) and res["requests"] == CONVS * STEPS
+    assert res["baseline_config"] == (3 if world == 2 else 4) and res["requests"] == CONVS * STEPS
     assert 0.0 < res["small_tier_share"] < 1.0
     assert res["config"]["parallelism"].endswith({2: "tp1", 4: "tp2", 8: "tp4"}[world])
     got = json.load(open(dump))
@@ -98,3 +98,69 @@ def test_pools_topology_n_ranks_one_gpu(world, single, tmp_path):
         # the conversations diverge, so only the routing (which depends on the query text and the
         # router's own state) is required to agree
         assert same_tier >= 0.75, (same_tier, same_text, per_tier)
+
+
+def _launch_ranks(world, args, logdir, tag, extra_env=None, timeout=600):
+    """Start ``world`` bench.py ranks as plain processes (RANK / WORLD_SIZE / MASTER_* set as
+    torch.distributed.run would): a rank that dies does not take the others down with it (torchrun's
+    agent would tear the whole job down), so the survivors' own fault handling is what is tested."""
+    port = _port()
+    procs, logs = [], []
+    for r in range(world):
+        env = dict(_env(), RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_PORT=str(port), **(extra_env or {}))
+        lp = os.path.join(logdir, f"{tag}_rank{r}.log")
+        logs.append(lp)
+        procs.append(subprocess.Popen([sys.executable, "-u", "bench.py", "--gpus", str(world), *args], cwd=ROOT,
+                                      env=env, stdout=open(lp, "w"), stderr=subprocess.STDOUT))
+    try:
+        for p in procs:
+            p.wait(timeout=timeout)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    codes = [p.returncode for p in procs]
+    out = open(logs[0]).read()
+    lines = [ln for ln in out.splitlines() if ln.startswith('{"metric"')]
+    return codes, (json.loads(lines[0]) if lines else None), logs
+
+
+SMALL_RUN = ["--steps", "3", "--warmup", "1", "--kv-gb", "2", "--small-new", "12", "--large-new", "16",
+             "--layers", "2", "--no-graphs", "--strategy", "hybrid", "--convs", "3"]
+
+
+def test_config5_colocated_mixtral_tp8_one_gpu(tmp_path):
+    """BASELINE config 5 as written, rehearsed on one GPU: Mixtral-8x7B (2 layers) tensor-parallel
+    over all 8 ranks AND a Llama-3.2-1B small replica on every rank (two engines, two serving loops
+    per pool process).  Both tiers serve every timed turn and every rank exits cleanly."""
+    logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
+    os.makedirs(logdir, exist_ok=True)
+    codes, res, logs = _launch_ranks(8, ["--baseline-config", "5", *SMALL_RUN], logdir, "cfg5")
+    assert codes == [0] * 8, (codes, open(logs[codes.index(next(c for c in codes if c))]).read()[-3000:]
+                              if any(codes) else "")
+    assert res is not None and res["baseline_config"] == 5 and res["rehearsal_one_gpu"] and res["truncated_layers"] == 2
+    lay = res["layout"]
+    assert lay["colocated"] and lay["large"]["replicas"] == [list(range(8))] and lay["large"]["model"] == "mixtral-8x7b"
+    assert lay["small"]["replicas"] == [[r] for r in range(8)]
+    assert res["requests"] == 3 * 8 * 3 and res["pool_events"]["lost_turns"] == 0
+    assert 0.0 < res["small_tier_share"] < 1.0, "both tiers must serve"
+
+
+def test_config4_large_leader_dies_mid_window_one_gpu(tmp_path):
+    """BASELINE config 4's failover test with GPU engines: 8B replicas on ranks 0-3 and 70B at TP=4
+    on ranks 4-7 (2 layers each); the large pool's leader (rank 4) is killed by fault injection
+    after its 2nd request batch, i.e. inside the timed window.  Every turn is still answered (the
+    router fails them over to the small replicas), the failed tier is charged in the perf router and
+    skipped up front afterwards, and every surviving rank exits cleanly (the results are reduced
+    through the rendezvous store, not a collective that would need the dead rank)."""
+    logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
+    os.makedirs(logdir, exist_ok=True)
+    codes, res, logs = _launch_ranks(8, ["--baseline-config", "4", *SMALL_RUN], logdir, "cfg4fo",
+                                     {"DLLM_FAULT_DIE_RANK": "4", "DLLM_FAULT_DIE_AFTER": "2"})
+    assert codes[4] == 17 and [c for i, c in enumerate(codes) if i != 4] == [0] * 7, codes
+    assert res is not None and res["baseline_config"] == 4
+    ev = res["pool_events"]
+    assert ev["dead_ranks"] == [4] and ev["degraded"] and ev["failed_tiers"] == ["orin"], ev
+    assert ev["failovers"] > 0 and ev["lost_turns"] == 0, ev
+    assert res["requests"] == 3 * 8 * 3 and sum(ev["failovers_by_step"]) == ev["failovers"]
