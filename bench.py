@@ -128,6 +128,22 @@ def resolve_config(a, world: int) -> int:
     return cfg
 
 
+def _router_stream() -> None:
+    """Pipelined drivers route while the engine's loop keeps decode steps queued on its stream:
+    the router's own GPU work (encoder, centroid scores, HBM cache lookups, each read back to the
+    host) goes to a side stream of this thread, so its read-backs wait for the router's kernels
+    only, not for the decode step queued ahead of them on the engine's stream."""
+    import torch
+    global _ROUTER_STREAM
+    if torch.cuda.is_available():
+        if _ROUTER_STREAM is None:
+            _ROUTER_STREAM = torch.cuda.Stream()   # one for every driver thread of the process
+        torch.cuda.set_stream(_ROUTER_STREAM)
+
+
+_ROUTER_STREAM = None
+
+
 class Conversations:
     def __init__(self, n: int, rank: int):
         from distributed_llm_amd.bench.query_sets import normalize_query_set, query_sets
@@ -192,6 +208,7 @@ class PipelinedConversations(Conversations):
 
         def worker(i):
             try:
+                _router_stream()
                 while not self._stop:
                     c = self.convs[i]
                     q = c["set"][c["turn"]].text
@@ -258,6 +275,7 @@ class EventConversations(PipelinedConversations):
 
         def driver():
             try:
+                _router_stream()
                 ready = list(range(len(self.convs)))
                 inflight = {}
                 while not self._stop:
@@ -330,6 +348,7 @@ class GroupedConversations(PipelinedConversations):
 
         def worker(ids):
             try:
+                _router_stream()
                 while not self._stop:
                     hs = []
                     for i in ids:

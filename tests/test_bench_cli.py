@@ -76,3 +76,16 @@ def test_bench_survives_pool_leader_death():
     ev = out["pool_events"]
     assert ev["dead_ranks"] == [2] and ev["failed_tiers"] == ["orin"] and ev["degraded"]
     assert ev["failovers"] > 0 and ev["lost_turns"] == 0 and out["requests"] == 3 * world * 3
+
+
+def test_bench_event_driven_turn_pipelining():
+    """``--pipeline 2``: one driver thread keeps every conversation's next turn in flight through the
+    engine's non-blocking submission; the timed window counts completed turns (about steps x convs)."""
+    args = [sys.executable, "bench.py", "--cpu", "--steps", "2", "--warmup", "1", "--convs", "4",
+            "--small-new", "4", "--large-new", "6", "--pipeline", "2", "--admit-every", "4"]
+    env = dict(os.environ, DLLM_EMBEDDER="hash", OMP_NUM_THREADS="1")
+    r = subprocess.run(args, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["config"]["turn_pipelining"] == "event-driver" and out["config"]["admit_every"] == 4
+    assert out["value"] > 0 and out["requests"] >= 2 * 4 - 4 and out["pool_events"]["lost_turns"] == 0
