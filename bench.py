@@ -14,7 +14,12 @@ or answers).  One *step* = one turn of every conversation: route all, then the e
 small- and large-tier groups as one continuous batch (paged KV, prefix cache across turns, hipGraph
 decode).  The response cache is OFF (its context-free key would replay other conversations'
 answers = skipped work); small tier greedy (reference Nano), large tier Ollama-default sampling
-(reference Orin).
+(reference Orin).  By default the conversations are turn-PIPELINED (``--pipeline 2``): one driver
+thread routes every conversation whose answer has arrived and submits its next turn without
+waiting for the others (each conversation stays strictly sequential, as in the reference harness),
+so the decode batch stays full instead of draining to the large-tier answers at the end of every
+turn; a *step* is then ``--convs`` completed turns, and only turns completed inside the timed
+window are counted.  ``--pipeline 0`` runs the turn-synchronous steps of rounds 1-3.
 
 N > 1 GPUs default to BASELINE's multi-GPU configurations (``--topology pools``, parallel.cluster):
 2 GPUs config 3 (Llama-3.2-1B small on GPU 0 | Llama-3-8B large on GPU 1), 4 GPUs config 4's models
@@ -75,10 +80,12 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (tiny model)")
     ap.add_argument("--groups", type=int, default=1,
                     help="G > 1: G independently pipelined groups of conversations, one thread each")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="turn pipelining (replicated topology): conversations advance independently; "
-                         "1: one thread per conversation, 2: one event-driven driver thread")
-    ap.add_argument("--admit-every", type=int, default=8,
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="turn pipelining (replicated / tiers topologies): conversations advance independently; "
+                         "0: turn-synchronous steps, 1: one thread per conversation, 2: one event-driven driver "
+                         "thread (the default there: +6-7 %% routed tok/s, decode batch 372 -> 495-500 of 512, "
+                         "profiles/r4_turn_pipelining.md)")
+    ap.add_argument("--admit-every", type=int, default=16,
                     help="turn pipelining: the engine admits new turns every N decode steps of a burst")
     ap.add_argument("--no-encoder-memo", action="store_true",
                     help="encode every routed query with the GPU MiniLM encoder (no per-text memo)")
@@ -422,6 +429,8 @@ def main() -> int:
     if topology == "replicated":
         baseline_config = 2
     layout = None
+    if a.pipeline is None:
+        a.pipeline = 2 if topology in ("replicated", "tiers") and a.groups <= 1 else 0
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
     if topology in ("pools", "colocated"):
@@ -671,7 +680,7 @@ def main() -> int:
                        "penalise_failed_primary": bool(cfg.get("penalise_failed_primary")),
                        "turn_pipelining": ((("event-driver" if a.pipeline == 2 else "thread-per-conversation")
                                             if a.pipeline else "grouped" if a.groups > 1 else False)
-                                           if topology == "replicated" else False),
+                                           if cluster is None else False),
                        "admit_every": a.admit_every if (a.pipeline or a.groups > 1) else None,
                        "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},

@@ -44,7 +44,12 @@ def test_bench_json_line(n, extra, par, cfg):
     assert out["n_gpus"] == n and out["steps"] == 1 and out["warmup"] == 1
     assert out["value"] > 0 and out["higher_is_better"] is True and out["scaling"] == "weak"
     assert out["config"]["parallelism"].startswith(par)
-    assert out["requests"] == 2 * n and out["p50_latency_ms"] > 0
+    if out["config"]["turn_pipelining"]:
+        # pipelined (the 1-GPU default): the window counts the turns completed inside it
+        assert out["requests"] >= 2 * n - 2 and out["config"]["turn_pipelining"] == "event-driver"
+    else:
+        assert out["requests"] == 2 * n
+    assert out["p50_latency_ms"] > 0
     assert out["baseline_config"] == cfg
     lay = out["layout"]
     assert set(lay) >= {"small", "large"} and lay["small"]["replicas"] and lay["large"]["replicas"]

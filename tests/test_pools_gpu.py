@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 STEPS, WARMUP, CONVS = 4, 0, 24
 COMMON = ["--steps", str(STEPS), "--warmup", str(WARMUP), "--kv-gb", "4", "--small-model", "tinyllama-1.1b",
           "--large-model", "llama-3.2-1b", "--small-new", "16", "--large-new", "24", "--greedy", "--no-graphs",
-          "--strategy", "hybrid"]
+          "--strategy", "hybrid", "--pipeline", "0"]
 
 
 def _port():
