@@ -85,6 +85,8 @@ def parse():
                          "0: turn-synchronous steps, 1: one thread per conversation, 2: one event-driven driver "
                          "thread (the default there: +6-7 %% routed tok/s, decode batch 372 -> 495-500 of 512, "
                          "profiles/r4_turn_pipelining.md)")
+    ap.add_argument("--gil-switch-ms", type=float, default=5.0,
+                    help="turn pipelining: Python thread switch interval (sys.setswitchinterval) in ms")
     ap.add_argument("--admit-every", type=int, default=16,
                     help="turn pipelining: the engine admits new turns every N decode steps of a burst")
     ap.add_argument("--no-encoder-memo", action="store_true",
@@ -551,6 +553,10 @@ def main() -> int:
                         pools=pools_for_router)
         pipelined = (bool(a.pipeline) or a.groups > 1) and cluster is None
         if pipelined:
+            # the engine's step loop and the routing driver are two Python threads: a short GIL
+            # switch interval (default 5 ms) hands the GIL back to the step loop before the
+            # queued decode step runs dry (profiles/r4_turn_pipelining.md)
+            sys.setswitchinterval(a.gil_switch_ms / 1000.0)
             for e in engines:
                 e.ADMIT_EVERY = max(1, a.admit_every)
                 e.start()              # background step loop: callers only enqueue and wait

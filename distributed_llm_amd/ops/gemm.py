@@ -161,11 +161,30 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
+# Prefill-size buckets (M > MAX_M): the fused ops' core is chosen per (bucket, N, K) between one
+# tgemm launch with the epilogue fused and hipBLASLt + the standalone epilogue kernel
+# (scripts/exp/prefill_gemm_probe.py: tgemm wins some shapes, e.g. TinyLlama gate|up at 8K rows by
+# 13 %, and loses most of the Llama-3-8B ones); a prefill chunk uses the plan of the smallest bucket
+# that holds it.
+PREFILL_MS = tuple(int(x) for x in os.environ.get("DLLM_PREFILL_TUNE_MS", "2048,4096,8192").split(",") if x)
+_PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8), (192, 128, 3, 1, 1, 8),
+             (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4))
+
+
+def prefill_bucket(M: int) -> int:
+    for b in PREFILL_MS:
+        if M <= b:
+            return b
+    return PREFILL_MS[-1] if PREFILL_MS else M
+
+
 def tg_plan(M: int, N: int, K: int) -> Tuple[int, ...]:
     """(bm, bn, stages, splits, ks, waves[, k-groups]) of the fused GEMM for this shape: tuned, else a
     heuristic sized so the grid covers the 256 CUs (bigger tiles first, split-K only for short
     grids)."""
     p = _P.tg_plans.get((M, N, K))
+    if p is None and M > MAX_M and PREFILL_MS:
+        p = _P.tg_plans.get((prefill_bucket(M), N, K))
     if p is not None:
         return tuple(p) + (1, 4)[len(p) - 4:] if len(p) < 6 else tuple(p)
     mt128, nt128 = -(-M // 128), -(-N // 128)
@@ -367,6 +386,8 @@ def use_vendor_core(M: int, N: int, K: int) -> bool:
     if env in ("tg", "blas", "lin"):
         return env != "tg"
     c = _P.fused_core.get((M, N, K))
+    if c is None and M > MAX_M and PREFILL_MS:
+        c = _P.fused_core.get((prefill_bucket(M), N, K))
     if c is not None:
         return c != "tg"
     return M > MAX_M
@@ -569,6 +590,8 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
     # the fused ops' tgemm plans stream the panel weight copies: time them in that layout
     _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set())
     _couple_gemv_choices(fused, list(ms), verbose)
+    if os.environ.get("DLLM_PREFILL_TUNE", "1") == "1":
+        _autotune_prefill(fused, dev, verbose)
     if cache:
         import json
         d = {_plan_key(k): list(v) for k, v in _P.plans.items()}
@@ -578,6 +601,40 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
             os.makedirs(os.path.dirname(cache), exist_ok=True)
         with open(cache, "w") as f:
             json.dump(d, f)
+
+
+def _autotune_prefill(fused, dev, verbose: bool) -> None:
+    """Fused-op core at the prefill buckets: one tgemm launch with the epilogue fused (PLAIN timed,
+    the fused epilogues write the same tile or less) against hipBLASLt + the standalone epilogue
+    kernel; the tgemm plans stream the K-panel weight copy the model keeps (W_PANEL)."""
+    for (N, K) in {tuple(f) for f in fused}:
+        todo = [M for M in PREFILL_MS if (M, N, K) not in _P.fused_core]
+        if not todo or K % 64:
+            continue
+        copies = max(2, min(8, (256 << 20) // (N * K * 2)))
+        ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        wps = [panel_weight(w) for w in ws] if W_PANEL else ws
+        for M in todo:
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            ext = _native(x)
+            lin = _time(lambda i: torch.matmul(x, ws[i % copies].t(), out=y), iters=8) + _post_us(M, N, dev)
+            best, best_t = None, float("inf")
+            for p in _PF_PLANS:
+                try:
+                    t = _time(lambda i: _tgemm(ext, x, wps[i % copies], EPI_PLAIN, p, y=y), iters=8)
+                except Exception:  # noqa: BLE001 - plan refused for this shape
+                    continue
+                if t < best_t:
+                    best, best_t = p, t
+            if best is not None:
+                _P.tg_plans[(M, N, K)] = best
+            _P.fused_core[(M, N, K)] = "tg" if best is not None and best_t < lin else "lin"
+            if verbose:
+                print(f"gemm prefill M={M} N={N} K={K}: blas+post {lin:.1f}us, tgemm {best} {best_t:.1f}us "
+                      f"-> {_P.fused_core[(M, N, K)]}", flush=True)
+            del x, y
+        del ws, wps
 
 
 def _couple_gemv_choices(fused, ms, verbose: bool) -> None:

@@ -30,17 +30,23 @@ def main():
                 res = {"blas": G._time(lambda i: torch.matmul(x, ws[i % copies].t(), out=y), iters=8)}
                 res["post"] = G._post_us(M, N, dev)
                 ext = G._native(x)
+                wps = [G.panel_weight(w) for w in ws]   # the K-panel-major copies the fused decoder weights keep
                 for p in PLANS:
-                    try:
-                        res["tg" + str(p)] = G._time(lambda i: G._tgemm(ext, x, ws[i % copies], G.EPI_PLAIN, p, y=y), iters=8)
-                    except Exception as e:  # noqa: BLE001 - plan refused for this shape
-                        res["tg" + str(p)] = None
+                    for tag, wl in (("tg", ws), ("tgP", wps)):
+                        try:
+                            res[tag + str(p)] = G._time(lambda i: G._tgemm(ext, x, wl[i % copies], G.EPI_PLAIN, p, y=y),
+                                                        iters=8)
+                        except Exception as e:  # noqa: BLE001 - plan refused for this shape
+                            res[tag + str(p)] = None
+                del wps
                 ref = F.linear(x, ws[0]).float()
                 G._tgemm(ext, x, ws[0], G.EPI_PLAIN, PLANS[0], y=y)
                 err = float((y.float() - ref).abs().max() / ref.abs().max())
                 best_tg = min((v, k) for k, v in res.items() if k.startswith("tg") and v)
+                best_row = min((v, k) for k, v in res.items() if k.startswith("tg(") and v)
                 print(json.dumps({"fam": fam, "M": M, "N": N, "K": K, "blas_us": round(res["blas"], 1),
                                   "post_us": round(res["post"], 1), "best_tg": best_tg[1], "tg_us": round(best_tg[0], 1),
+                                  "best_rowmajor_us": round(best_row[0], 1),
                                   "blas_tf": round(flops / res["blas"] / 1e6), "tg_tf": round(flops / best_tg[0] / 1e6),
                                   "err_256": err, "all": {k: (round(v, 1) if v else None) for k, v in res.items()}}),
                       flush=True)

@@ -1,0 +1,70 @@
+"""GPU idle time between kernels from a rocprofv3 kernel-trace CSV.
+
+Usage: python scripts/gap_summary.py <kernel_trace.csv> [skip_fraction]
+
+Busy time is the union of kernel intervals; every gap between consecutive intervals (the GPU ran
+nothing) is charged to the pair (kernel before -> kernel after), so host-side stalls show up by
+where they happen in the step (e.g. before a graph's first kernel, around prefill, after the
+sampler).  ``skip_fraction`` drops the first part of the run (start-up, tuning, capture)."""
+import csv
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0][:70]
+
+
+def main():
+    path = sys.argv[1]
+    skip = float(sys.argv[2]) if len(sys.argv) > 2 else 0.3
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
+            s = r.get("Start_Timestamp") or r.get("BeginNs") or r.get("Start")
+            e = r.get("End_Timestamp") or r.get("EndNs") or r.get("End")
+            if k and s and e:
+                rows.append((int(s), int(e), short(k)))
+    rows.sort()
+    t0, t1 = rows[0][0], max(e for _, e, _ in rows)
+    cut = t0 + skip * (t1 - t0)
+    rows = [r for r in rows if r[0] >= cut]
+    busy, gaps = 0, defaultdict(lambda: [0, 0])
+    cur_s, cur_e, cur_k = rows[0]
+    hist = defaultdict(int)
+    for s, e, k in rows[1:]:
+        if s > cur_e:
+            busy += cur_e - cur_s
+            g = s - cur_e
+            gaps[(cur_k, k)][0] += g
+            gaps[(cur_k, k)][1] += 1
+            b = "<2us" if g < 2000 else "2-5us" if g < 5000 else "5-20us" if g < 20000 else "20-100us" if g < 100000 else ">=100us"
+            hist[b] += g
+            cur_s, cur_e, cur_k = s, e, k
+        else:
+            cur_e, cur_k = max(cur_e, e), k if e >= cur_e else cur_k
+    busy += cur_e - cur_s
+    span = cur_e - rows[0][0]
+    idle = span - busy
+    print(f"window {span / 1e9:.3f} s (first {skip:.0%} of the run skipped): GPU busy {busy / 1e9:.3f} s "
+          f"({100 * busy / span:.1f} %), idle {idle / 1e9:.3f} s\n")
+    print("| gap size | idle s | share of idle |\n|---|---|---|")
+    for b in ("<2us", "2-5us", "5-20us", "20-100us", ">=100us"):
+        print(f"| {b} | {hist[b] / 1e9:.3f} | {100 * hist[b] / max(idle, 1):.1f} % |")
+    print("\n| idle ms | gaps | mean us | kernel before | kernel after |\n|---|---|---|---|---|")
+    for (a, b), (g, n) in sorted(gaps.items(), key=lambda x: -x[1][0])[:25]:
+        print(f"| {g / 1e6:.1f} | {n} | {g / n / 1e3:.1f} | `{a}` | `{b}` |")
+    # a timeline excerpt from the middle of the window: what runs between two idle gaps
+    mid = len(rows) // 2
+    print("\nTimeline excerpt (us from the first row; gap = idle before the row):\n")
+    print("| t | dur | gap | kernel |\n|---|---|---|---|")
+    base, prev_e = rows[mid][0], rows[mid][0]
+    for s_, e_, k in rows[mid:mid + 160]:
+        print(f"| {(s_ - base) / 1e3:.1f} | {(e_ - s_) / 1e3:.1f} | {max(0, s_ - prev_e) / 1e3:.1f} | `{k}` |")
+        prev_e = max(prev_e, e_)
+
+
+if __name__ == "__main__":
+    main()
