@@ -161,11 +161,13 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
-# Prefill-size buckets (M > MAX_M): the fused ops' core is chosen per (bucket, N, K) between one
-# tgemm launch with the epilogue fused and hipBLASLt + the standalone epilogue kernel
-# (scripts/exp/prefill_gemm_probe.py: tgemm wins some shapes, e.g. TinyLlama gate|up at 8K rows by
-# 13 %, and loses most of the Llama-3-8B ones); a prefill chunk uses the plan of the smallest bucket
-# that holds it.
+# Prefill-size buckets (M > MAX_M), opt-in (DLLM_PREFILL_TUNE=1): the fused ops' core is chosen per
+# (bucket, N, K) between one tgemm launch with the epilogue fused and hipBLASLt + the standalone
+# epilogue kernel; a prefill chunk uses the plan of the smallest bucket that holds it.  The probe
+# (scripts/exp/prefill_gemm_probe.py) has tgemm ahead on a few shapes (TinyLlama Wo at 2-4K rows,
+# gate|up at 8K: 9 %), but with those choices the flagship's prefill took 27 % longer (chunks of
+# ~5K rows run the 8K bucket's tile; profiles/r4_prefill_gemm.md), so hipBLASLt stays the default
+# core above MAX_M.
 PREFILL_MS = tuple(int(x) for x in os.environ.get("DLLM_PREFILL_TUNE_MS", "2048,4096,8192").split(",") if x)
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8), (192, 128, 3, 1, 1, 8),
              (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4))
@@ -590,7 +592,7 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
     # the fused ops' tgemm plans stream the panel weight copies: time them in that layout
     _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set())
     _couple_gemv_choices(fused, list(ms), verbose)
-    if os.environ.get("DLLM_PREFILL_TUNE", "1") == "1":
+    if os.environ.get("DLLM_PREFILL_TUNE", "0") == "1":
         _autotune_prefill(fused, dev, verbose)
     if cache:
         import json

@@ -150,7 +150,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) lg_kernel(const u16* __restric
 // consumers (fragments read: lgkmcnt(0) before the barrier) and back.  Split-K over gridDim:
 // S k-chunks per output tile, write-through f32 slabs + relaxed ticket, the last arriver sums
 // the slabs in split order (Guideline 16 R1, as tgemm).
-template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false>
+// AP / WP: the activation / weight operand is stored K-panel-major ([K/64][rows][64]: the 8 rows x
+// 128 B of one ring piece are ONE contiguous 1 KB, like the intake probe's contiguous stream)
+template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false, bool AP = false,
+          bool WP = false>
 __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __restrict__ A, long lda,
                                                                      const u16* __restrict__ W, u16* __restrict__ Y,
                                                                      int M, int N, int K, int S, float* part,
@@ -187,15 +190,20 @@ __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __
   if (loader) {
     const int lw = wave - NC, srow = lane >> 3, spos = lane & 7;
     const u16* src[G];
+    long sstep[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int g = lw + NL * j;
       const int r = 8 * g + srow;
       if (g < BM / 8) {
-        src[j] = A + (long)min(m0 + r, M - 1) * lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+        const long row = min(m0 + r, M - 1);
+        src[j] = (AP ? A + ((long)(kbeg / BK) * M + row) * BK : A + row * lda + kbeg) + 8 * (spos ^ ((r >> 1) & 7));
+        sstep[j] = AP ? (long)M * BK : (long)BK;
       } else {
         const int rb = r - BM;
-        src[j] = W + (long)min(n0 + rb, N - 1) * K + kbeg + 8 * (spos ^ ((rb >> 1) & 7));
+        const long n = min(n0 + rb, N - 1);
+        src[j] = (WP ? W + ((long)(kbeg / BK) * N + n) * BK : W + n * K + kbeg) + 8 * (spos ^ ((rb >> 1) & 7));
+        sstep[j] = WP ? (long)N * BK : (long)BK;
       }
     }
     // ROT: each output tile walks K from its own offset, so the many tiles that stream the SAME
@@ -211,7 +219,8 @@ __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __
         // PROBE 3: loaders move only the W pieces, PROBE 4 only the A pieces (BM == BN: half each)
         const bool isa = (lw + NL * j) < BM / 8;
         if ((PROBE == 3 && isa) || (PROBE == 4 && !isa)) continue;
-        __builtin_amdgcn_global_load_lds((const void*)(src[j] + tt * BK), (lds_void*)(base + (lw + NL * j) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(src[j] + tt * sstep[j]), (lds_void*)(base + (lw + NL * j) * 1024),
+                                         16, 0, 0);
       }
     };
     constexpr int GW = (PROBE == 3 || PROBE == 4) ? G / 2 : G;
@@ -351,6 +360,7 @@ struct Var {
   int bm, bn, S;
   bool wt;
   std::function<void(const u16*, const u16*, u16*, int, int, int, hipStream_t)> launch;
+  bool ap = false, wp = false;
 };
 
 template <int BM, int BN, int WGM, int WGN, int ST, bool WT>
@@ -364,16 +374,21 @@ Var lgv() {
              }};
 }
 
-template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false>
+template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false, bool AP = false,
+          bool WP = false>
 Var rgv(int S) {
-  char nm[96];
-  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s%s", BM, BN, WGM, WGN, NL, ST, S, ROT ? " ROT" : "",
-           PROBE == 1 ? " LOADERS-ONLY" : PROBE == 2 ? " CONSUMERS-ONLY" : PROBE == 3 ? " W-ONLY" : PROBE == 4 ? " A-ONLY" : "");
-  return Var{nm, BM, BN, S, false, [S](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
-               const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
-               hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE, ROT>), dim3(g), dim3(64 * (WGM * WGN + NL)), 0, s,
-                                  A, (long)K, W, Y, M, N, K, S, g_part, g_cnt);
-             }};
+  char nm[128];
+  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s%s%s%s", BM, BN, WGM, WGN, NL, ST, S, ROT ? " ROT" : "",
+           PROBE == 1 ? " LOADERS-ONLY" : PROBE == 2 ? " CONSUMERS-ONLY" : PROBE == 3 ? " W-ONLY" : PROBE == 4 ? " A-ONLY" : "",
+           AP ? " A-PANEL" : "", WP ? " W-PANEL" : "");
+  Var v{nm, BM, BN, S, false, [S](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
+          const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
+          hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE, ROT, AP, WP>), dim3(g),
+                             dim3(64 * (WGM * WGN + NL)), 0, s, A, (long)K, W, Y, M, N, K, S, g_part, g_cnt);
+        }};
+  v.ap = AP;
+  v.wp = WP;
+  return v;
 }
 
 static float hbf(u16 h) { uint32_t u = ((uint32_t)h) << 16; float f; memcpy(&f, &u, 4); return f; }
@@ -392,6 +407,16 @@ int main(int argc, char** argv) {
       rgv<64, 64, 2, 2, 2, 4, 3, true>(1),     rgv<64, 64, 2, 2, 2, 4, 4, true>(1),
       rgv<128, 128, 2, 2, 4, 4, 3, true>(1),   rgv<128, 128, 2, 2, 4, 4, 4, true>(1),
       rgv<64, 64, 2, 2, 4, 8, 3, true>(1),     rgv<64, 64, 2, 2, 4, 8, 4, true>(1),
+      // K-panel-major operands (round 4)
+      rgv<64, 64, 2, 2, 2, 4, 4, true, true>(1),               rgv<64, 64, 2, 2, 4, 8, 4, true, true>(1),
+      rgv<64, 64, 2, 2, 2, 4, 3, true, false, true>(1),        rgv<64, 64, 2, 2, 4, 8, 3, true, false, true>(1),
+      rgv<64, 64, 2, 2, 2, 4, 1, true, true, true>(1),         rgv<64, 64, 2, 2, 4, 8, 1, true, true, true>(1),
+      rgv<64, 64, 2, 2, 2, 4, 0, true, true, true>(1),         rgv<64, 64, 2, 2, 4, 8, 0, true, true, true>(1),
+      rgv<64, 64, 2, 2, 2, 4, 0, true, true, false>(1),        rgv<64, 64, 2, 2, 4, 8, 0, true, false, true>(1),
+      rgv<128, 128, 2, 2, 4, 4, 0, true, true, true>(1),       rgv<128, 128, 2, 2, 4, 4, 4, true, true>(1),
+      rgv<128, 64, 2, 2, 4, 4, 0, true, true, true>(1),        rgv<160, 128, 2, 4, 4, 3, 0, true, true, true>(1),
+      rgv<256, 128, 4, 2, 4, 3, 0, true, true, true>(1),       rgv<64, 64, 2, 2, 4, 4, 0, true, true, true>(2),
+      rgv<128, 64, 2, 2, 4, 4, 0, true, true, true>(2),        rgv<80, 64, 1, 4, 2, 4, 0, true, true, true>(2),
   };
   struct Shape { int N, K; };
   std::vector<Shape> shapes = {{2560, 2048}, {2048, 2048}, {11264, 2048}, {2048, 5632}};
@@ -441,15 +466,21 @@ int main(int argc, char** argv) {
       }
       for (auto& x : hw) { float f = (rand() / (float)RAND_MAX - 0.5f) * 0.05f; uint32_t u; memcpy(&u, &f, 4); x = u >> 16; }
     }
+    std::vector<u16*> wps(copies);
     for (int c = 0; c < copies; ++c) {
       CHECK(hipMalloc(&ws[c], wel * 2));
       CHECK(hipMemcpy(ws[c], hw.data(), wel * 2, hipMemcpyHostToDevice));
+      CHECK(hipMalloc(&wps[c], wel * 2));
+      hipLaunchKernelGGL(lab::panel_kernel, dim3((wel / 8 + 255) / 256), dim3(256), 0, s, ws[c], wps[c], N, K);
     }
+    u16* Apan;
+    CHECK(hipMalloc(&Apan, (long)MAXM * K * 2));
     // tiled copies are re-made per BN (largest tiled footprint: N rounded up to BN)
     const long wt_el = (long)(N + 256) * K;
     for (int c = 0; c < copies; ++c) CHECK(hipMalloc(&wts[c], wt_el * 2));
     (void)Wt_scratch;
     for (int M : ms) {
+      hipLaunchKernelGGL(lab::panel_kernel, dim3(((long)M * K / 8 + 255) / 256), dim3(256), 0, s, A, Apan, M, K);
       hipLaunchKernelGGL(lab::ref_kernel, dim3((N + 255) / 256, M), dim3(256), 0, s, A, ws[0], Yr, M, N, K);
       std::vector<float> yr((long)M * N);
       CHECK(hipMemcpy(yr.data(), Yr, yr.size() * 4, hipMemcpyDeviceToHost));
@@ -540,17 +571,19 @@ int main(int argc, char** argv) {
           CHECK(hipStreamSynchronize(s));
           tiled_bn = v.bn;
         }
-        auto& wsel = v.wt ? wts : ws;
+        auto& wsel = v.wp ? wps : v.wt ? wts : ws;
+        const u16* ain = v.ap ? Apan : A;
         if (K % (64 * v.S)) continue;
         if ((long)((M + v.bm - 1) / v.bm) * ((N + v.bn - 1) / v.bn) * v.S * v.bm * v.bn > (256L << 20)) continue;
-        v.launch(A, wsel[0], Y, M, N, K, s);
+        v.launch(ain, wsel[0], Y, M, N, K, s);
         CHECK(hipStreamSynchronize(s));
         const double err = check(v.name.c_str());
-        const double us = time_graph([&](int i) { v.launch(A, wsel[i], Y, M, N, K, s); });
+        const double us = time_graph([&](int i) { v.launch(ain, wsel[i], Y, M, N, K, s); });
         report(v.name.c_str(), us, err);
       }
     }
-    for (int c = 0; c < copies; ++c) { CHECK(hipFree(ws[c])); CHECK(hipFree(wts[c])); }
+    for (int c = 0; c < copies; ++c) { CHECK(hipFree(ws[c])); CHECK(hipFree(wts[c])); CHECK(hipFree(wps[c])); }
+    CHECK(hipFree(Apan));
     CHECK(hipFree(A)); CHECK(hipFree(Y)); CHECK(hipFree(Yr));
   }
   return 0;
