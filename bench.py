@@ -85,6 +85,8 @@ def parse():
                          "0: turn-synchronous steps, 1: one thread per conversation, 2: one event-driven driver "
                          "thread (the default there: +6-7 %% routed tok/s, decode batch 372 -> 495-500 of 512, "
                          "profiles/r4_turn_pipelining.md)")
+    ap.add_argument("--gc-freeze", type=int, default=1,
+                    help="1: gc.freeze() + higher young-generation thresholds after start-up (0: Python defaults)")
     ap.add_argument("--gil-switch-ms", type=float, default=5.0,
                     help="turn pipelining: Python thread switch interval (sys.setswitchinterval) in ms")
     ap.add_argument("--admit-every", type=int, default=16,
@@ -551,6 +553,15 @@ def main() -> int:
         pools_for_router = cluster.router_pools() if cluster is not None else pools
         router = Router(strategy=a.strategy, config=cfg, threshold_fallback=a.threshold, benchmark_mode=False,
                         pools=pools_for_router)
+        if a.gc_freeze:
+            # serving-process GC hygiene: everything allocated at start-up (weights' Python wrappers,
+            # tokenizer tables, captured graphs) moves to the permanent generation and the young
+            # generations collect less often, so the step loop is not paused by full collections
+            # scanning start-up objects (a paused step loop leaves the GPU idle between steps)
+            import gc
+            gc.collect()
+            gc.freeze()
+            gc.set_threshold(50000, 50, 100)
         pipelined = (bool(a.pipeline) or a.groups > 1) and cluster is None
         if pipelined:
             # the engine's step loop and the routing driver are two Python threads: a short GIL
@@ -688,6 +699,7 @@ def main() -> int:
                                             if a.pipeline else "grouped" if a.groups > 1 else False)
                                            if cluster is None else False),
                        "admit_every": a.admit_every if (a.pipeline or a.groups > 1) else None,
+                       "gc_freeze": bool(a.gc_freeze),
                        "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
             "p50_latency_ms": round(statistics.median(lats), 1) if lats else None,

@@ -10,8 +10,7 @@ from distributed_llm_amd import ops
 from distributed_llm_amd.ops import gemm as G
 
 H, NQ, NKV, D, I = 2048, 32, 4, 64, 5632
-PLANS = [(64, 64, 4, 1, 1, 4), (64, 64, 3, 1, 2, 4), (64, 64, 4, 1, 1, 4, 1, 8), (128, 64, 4, 1, 1, 4, 1, 4),
-         (64, 128, 3, 1, 1, 8), (256, 128, 3, 1, 1, 8, 1, 4), (160, 128, 3, 1, 1, 8, 1, 4)]
+PLANS = [(64, 64, 4, 1, 1, 4), (64, 64, 4, 1, 1, 4, 1, 8), (64, 128, 3, 1, 1, 8)]
 
 
 def main():
@@ -43,6 +42,19 @@ def main():
                 row["qkv_epi"] = G._time(lambda i: G._tgemm(ext, r, wq[i % copies], G.EPI_QKV, p, ssq_in=ssq, ssq_n=8,
                                                             norm_scale=1.0 / H, eps=1e-5, pos=pos, cos_sin=cs, slots=slots,
                                                             q_out=q, kc=kc, vc=vc, nq=NQ, nkv=NKV, d=D), 16)
+                noslot = torch.full_like(slots, -1)      # K / V cache writes skipped: RoPE + q only
+                row["qkv_epi_q_only"] = G._time(lambda i: G._tgemm(ext, r, wq[i % copies], G.EPI_QKV, p, ssq_in=ssq, ssq_n=8,
+                                                                   norm_scale=1.0 / H, eps=1e-5, pos=pos, cos_sin=cs,
+                                                                   slots=noslot, q_out=q, kc=kc, vc=vc, nq=NQ, nkv=NKV,
+                                                                   d=D), 16)
+                seq = torch.arange(M, dtype=torch.int32, device=dev) * 16   # one row per block, offset 0
+                row["qkv_epi_seq_slots"] = G._time(lambda i: G._tgemm(ext, r, wq[i % copies], G.EPI_QKV, p, ssq_in=ssq,
+                                                                      ssq_n=8, norm_scale=1.0 / H, eps=1e-5, pos=pos,
+                                                                      cos_sin=cs, slots=seq, q_out=q, kc=kc, vc=vc, nq=NQ,
+                                                                      nkv=NKV, d=D), 16)
+                row["qkv_plain_rowscale"] = G._time(lambda i: G._tgemm(ext, r, wq[i % copies], G.EPI_PLAIN, p,
+                                                                       y=y[:, :nq_cols], ssq_in=ssq, ssq_n=8,
+                                                                       norm_scale=1.0 / H, eps=1e-5), 16)
                 row["wo_plain"] = G._time(lambda i: G._tgemm(ext, o, wo[i % copies], G.EPI_PLAIN, p, y=y[:, :H]), 16)
                 rr = r.clone()
                 row["wo_resadd"] = G._time(lambda i: G._tgemm(ext, o, wo[i % copies], G.EPI_RESADD, p, y=rr,

@@ -213,12 +213,16 @@ def _router_stuck_data_lock(ctrl, data):
     rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=5, timeout_s=60, data_timeout_s=1.0,
                     tokenizer=get_tokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id))
     rp._data_lock.acquire()             # as if a transfer were stuck forever
+    # a health probe that finds the data plane busy skips (a long hand-off is not a failure)
+    busy = rp.probe_data(timeout=0.3)
+    busy_ok = busy.get("skipped") is not None and rp.data_error is None
     t0 = time.perf_counter()
     r = rp.process_failover([{"role": "user", "content": "hand me over"}])
     dt = time.perf_counter() - t0
     ping = rp.probe_data(timeout=1.0)
     rp.stop()
-    return {"ok": "response" in r, "dt": dt, "retired": rp.data_error is not None, "ping_ok": ping["ok"]}
+    return {"ok": "response" in r, "dt": dt, "retired": rp.data_error is not None, "ping_ok": ping["ok"],
+            "busy_probe_skipped": busy_ok}
 
 
 _ROUTER = {"concurrent": _router_concurrent, "kill": _router_kill, "hang": _router_hang,
@@ -294,3 +298,4 @@ def test_stuck_data_plane_lock_falls_back_to_text():
     out = _run("stuck_lock")
     assert out["ok"] and out["dt"] < 20.0, out
     assert out["retired"] and out["ping_ok"] is False, out
+    assert out["busy_probe_skipped"], out
