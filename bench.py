@@ -85,8 +85,9 @@ def parse():
                          "0: turn-synchronous steps, 1: one thread per conversation, 2: one event-driven driver "
                          "thread (the default there: +6-7 %% routed tok/s, decode batch 372 -> 495-500 of 512, "
                          "profiles/r4_turn_pipelining.md)")
-    ap.add_argument("--gc-freeze", type=int, default=1,
-                    help="1: gc.freeze() + higher young-generation thresholds after start-up (0: Python defaults)")
+    ap.add_argument("--gc-freeze", type=int, default=0,
+                    help="1: gc.freeze() + higher young-generation thresholds after start-up (no measured effect on "
+                         "the flagship: 57.0 / 59.7k off vs 59.3 / 59.0k on, one box)")
     ap.add_argument("--gil-switch-ms", type=float, default=5.0,
                     help="turn pipelining: Python thread switch interval (sys.setswitchinterval) in ms")
     ap.add_argument("--admit-every", type=int, default=16,

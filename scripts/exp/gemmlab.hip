@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) lg_kernel(const u16* __restric
 // AP / WP: the activation / weight operand is stored K-panel-major ([K/64][rows][64]: the 8 rows x
 // 128 B of one ring piece are ONE contiguous 1 KB, like the intake probe's contiguous stream)
 template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false, bool AP = false,
-          bool WP = false>
+          bool WP = false, bool PRIV = false>
 __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __restrict__ A, long lda,
                                                                      const u16* __restrict__ W, u16* __restrict__ Y,
                                                                      int M, int N, int K, int S, float* part,
@@ -197,7 +197,9 @@ __global__ void __launch_bounds__(64 * (WGM * WGN + NL)) rg_kernel(const u16* __
       const int r = 8 * g + srow;
       if (g < BM / 8) {
         const long row = min(m0 + r, M - 1);
-        src[j] = (AP ? A + ((long)(kbeg / BK) * M + row) * BK : A + row * lda + kbeg) + 8 * (spos ^ ((r >> 1) & 7));
+        // PRIV: every n-tile reads its own replica of A (64 copies, 6 MB apart): no CU shares an A line
+        const u16* Ab = PRIV ? A + (long)(n_tile % 64) * (3L << 20) : A;
+        src[j] = (AP ? Ab + ((long)(kbeg / BK) * M + row) * BK : Ab + row * lda + kbeg) + 8 * (spos ^ ((r >> 1) & 7));
         sstep[j] = AP ? (long)M * BK : (long)BK;
       } else {
         const int rb = r - BM;
@@ -375,15 +377,15 @@ Var lgv() {
 }
 
 template <int BM, int BN, int WGM, int WGN, int NL, int ST, int PROBE = 0, bool ROT = false, bool AP = false,
-          bool WP = false>
+          bool WP = false, bool PRIV = false>
 Var rgv(int S) {
   char nm[128];
-  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s%s%s%s", BM, BN, WGM, WGN, NL, ST, S, ROT ? " ROT" : "",
+  snprintf(nm, sizeof nm, "rg<%d,%d,%dx%d+%d,st%d,S%d>%s%s%s%s%s", BM, BN, WGM, WGN, NL, ST, S, ROT ? " ROT" : "",
            PROBE == 1 ? " LOADERS-ONLY" : PROBE == 2 ? " CONSUMERS-ONLY" : PROBE == 3 ? " W-ONLY" : PROBE == 4 ? " A-ONLY" : "",
-           AP ? " A-PANEL" : "", WP ? " W-PANEL" : "");
+           AP ? " A-PANEL" : "", WP ? " W-PANEL" : "", PRIV ? " A-PRIVATE" : "");
   Var v{nm, BM, BN, S, false, [S](const u16* A, const u16* W, u16* Y, int M, int N, int K, hipStream_t s) {
           const int g = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * S;
-          hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE, ROT, AP, WP>), dim3(g),
+          hipLaunchKernelGGL((lab::rg_kernel<BM, BN, WGM, WGN, NL, ST, PROBE, ROT, AP, WP, PRIV>), dim3(g),
                              dim3(64 * (WGM * WGN + NL)), 0, s, A, (long)K, W, Y, M, N, K, S, g_part, g_cnt);
         }};
   v.ap = AP;
@@ -407,6 +409,10 @@ int main(int argc, char** argv) {
       rgv<64, 64, 2, 2, 2, 4, 3, true>(1),     rgv<64, 64, 2, 2, 2, 4, 4, true>(1),
       rgv<128, 128, 2, 2, 4, 4, 3, true>(1),   rgv<128, 128, 2, 2, 4, 4, 4, true>(1),
       rgv<64, 64, 2, 2, 4, 8, 3, true>(1),     rgv<64, 64, 2, 2, 4, 8, 4, true>(1),
+      // private A replicas (round 4): is the SHARED activation tile the slow part?
+      rgv<64, 64, 2, 2, 4, 8, 4, true, false, false, true>(1), rgv<64, 64, 2, 2, 2, 4, 4, true, false, false, true>(1),
+      rgv<64, 64, 2, 2, 4, 8, 1, true, false, false, true>(1), rgv<64, 64, 2, 2, 4, 8, 0, true, false, false, true>(1),
+      rgv<128, 128, 2, 2, 4, 4, 4, true, false, false, true>(1),
       // K-panel-major operands (round 4)
       rgv<64, 64, 2, 2, 2, 4, 4, true, true>(1),               rgv<64, 64, 2, 2, 4, 8, 4, true, true>(1),
       rgv<64, 64, 2, 2, 2, 4, 3, true, false, true>(1),        rgv<64, 64, 2, 2, 4, 8, 3, true, false, true>(1),
@@ -447,14 +453,15 @@ int main(int argc, char** argv) {
     u16 *A, *Y, *Wt_scratch, *Ap;
     int apad = 0;
     float* Yr;
-    CHECK(hipMalloc(&A, (long)MAXM * K * 2));
+    CHECK(hipMalloc(&A, 64L * (3L << 20) * 2));   // 64 replicas of A, 6 MB apart (A-PRIVATE variants)
     CHECK(hipMalloc(&Y, (long)MAXM * N * 2));
     CHECK(hipMalloc(&Yr, (long)MAXM * N * 4));
     {
       std::vector<u16> ha((long)MAXM * K);
       srand(1);
       for (auto& x : ha) { float f = (rand() / (float)RAND_MAX - 0.5f); uint32_t u; memcpy(&u, &f, 4); x = u >> 16; }
-      CHECK(hipMemcpy(A, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+      for (int rep = 0; rep < 64; ++rep)
+        CHECK(hipMemcpy(A + (long)rep * (3L << 20), ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
       // LAB_APAD: a row-padded copy of A (lda = K + pad elements) for the production tgemm runs
       const char* ep = getenv("LAB_APAD");
       apad = ep ? atoi(ep) : 0;
