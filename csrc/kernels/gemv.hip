@@ -62,7 +62,7 @@ struct NormArgs {         // NORM: X is the sub-layer output h; the kernel forms
   float eps;
 };
 
-template <int M, int R, int UNR, bool SWIGLU, bool NORM, int EPI>
+template <int M, int R, int UNR, bool SWIGLU, bool NORM, int EPI, bool XG = false>
 __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, long ldx, const u16* __restrict__ W,
                                                    u16* __restrict__ Y, long ldy, int N, int K, NormArgs na,
                                                    EpiArgs ea) {
@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
   u16* xs = reinterpret_cast<u16*>(xs_raw);
   // epilogue scratch after X (and NORM's reduction slots): rinv [M], accumulators [4][R][M],
   // per-wave row sums [4][M]
-  float* s_ri = reinterpret_cast<float*>(xs + (long)M * K) + (NORM ? 4 * M : 0);
+  float* s_ri = reinterpret_cast<float*>(xs + (XG ? 0L : (long)M * K)) + (NORM ? 4 * M : 0);
   float* s_ep = s_ri + M;
   float* s_red = s_ep + 4 * R * M;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -92,21 +92,48 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
 
   constexpr int STEP = 512;  // K elements per wave-instruction
   constexpr int TRIP = STEP * UNR;
+  // PAIRED: the producer's partial row sums for this wave's first row (up to 1024 slots, 16 loads
+  // per lane) are requested BEFORE the first W trip.  Loads return in order, so a sum requested
+  // after W would wait out the whole W trip and only then let this wave issue its X staging loads:
+  // a second dependent round trip on every workgroup (measured +1.1 us QKV, +2.2 us gate|up at B = 1).
+  float pre[16];
+  if constexpr (PAIRED) {
+    if (wave < M) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = u * 64 + lane;
+        pre[u] = i < ea.ssq_n ? ea.ssq_in[(long)i * ea.ssq_in_ld + wave] : 0.f;
+      }
+    }
+    asm volatile("" ::: "memory");  // keep these requests ahead of the weight stream
+  }
   uint4 w[UNR][R], wn[UNR][R];
-#define DLLM_GEMV_LOAD(DST, KB)                                                                      \
+  // XG (batch 1-2, plain X): X travels with W in every trip (L1/L2 hits, no LDS stage, no barrier)
+  uint4 xg[XG ? UNR : 1][XG ? M : 1], xgn[XG ? UNR : 1][XG ? M : 1];
+#define DLLM_GEMV_LOAD(DST, XDST, KB)                                                                \
   _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                                                 \
     const int k_ = (KB) + u * STEP + 8 * lane;                                                      \
     _Pragma("unroll") for (int r = 0; r < R; ++r) DST[u][r] =                                       \
         (active && k_ < K) ? __builtin_bit_cast(uint4, ldnt_bf16x8(wr[r] + k_)) : make_uint4(0, 0, 0, 0); \
+    if constexpr (XG) {                                                                             \
+      _Pragma("unroll") for (int m = 0; m < M; ++m) XDST[u][m] =                                    \
+          (active && k_ < K) ? ld16(X + (long)m * ldx + k_) : make_uint4(0, 0, 0, 0);               \
+    }                                                                                               \
   }
-  DLLM_GEMV_LOAD(w, 0)  // the first trip of W is in flight while X is staged
+  DLLM_GEMV_LOAD(w, xg, 0)  // the first trip of W is in flight while X is staged
   if constexpr (PAIRED) {
     // folded RMSNorm row scale: lane-parallel sum of the producer's partial sums, wave w -> rows w, w + 4
-    // (a GEMV producer leaves one slot per workgroup, e.g. 512 at N = 2048: 8 independent loads
-    // per lane are issued before the first add, so the sum costs one L2 round trip, not eight)
+    // (a GEMV producer leaves one slot per workgroup, e.g. 512 at N = 2048: the first row's loads
+    // were issued above; further rows / slots beyond 1024 take one more round trip here)
     for (int m = wave; m < M; m += 4) {
       float sacc = 0.f;
-      for (int i0 = 0; i0 < ea.ssq_n; i0 += 512) {
+      int i_first = 0;
+      if (m == wave) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sacc += pre[u];
+        i_first = 1024;
+      }
+      for (int i0 = i_first; i0 < ea.ssq_n; i0 += 512) {
         float part[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -158,7 +185,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
         st16(xs + (long)m * K + c, pack8(a));  // each thread rewrites only the vectors it wrote
       }
     }
-  } else {
+  } else if constexpr (!XG) {
   for (int v = threadIdx.x; v < M * (K >> 3); v += 256) {
     const int m = v / (K >> 3), c = (v - m * (K >> 3)) << 3;
     uint4 xv = ld16(X + (long)m * ldx + c);
@@ -173,7 +200,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
     st16(xs + (long)m * K + c, xv);
   }
   }
-  __syncthreads();
+  if constexpr (!XG) __syncthreads();
 
   float acc[M][R];
 #pragma unroll
@@ -181,7 +208,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[m][r] = 0.f;
   for (int kb = 0; kb < K; kb += TRIP) {
-    if (kb + TRIP < K) { DLLM_GEMV_LOAD(wn, kb + TRIP) }  // next trip in flight during this one
+    if (kb + TRIP < K) { DLLM_GEMV_LOAD(wn, xgn, kb + TRIP) }  // next trip in flight during this one
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int k = kb + u * STEP + 8 * lane;
@@ -192,7 +219,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           float xf[8];
-          unpack8(ld16(xs + (long)m * K + k), xf);
+          if constexpr (XG)
+            unpack8(xg[u][m], xf);
+          else
+            unpack8(ld16(xs + (long)m * K + k), xf);
 #pragma unroll
           for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -201,9 +231,14 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
       }
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u)
+    for (int u = 0; u < UNR; ++u) {
 #pragma unroll
       for (int r = 0; r < R; ++r) w[u][r] = wn[u][r];
+      if constexpr (XG) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) xg[u][m] = xgn[u][m];
+      }
+    }
   }
 #undef DLLM_GEMV_LOAD
 #pragma unroll
@@ -305,6 +340,16 @@ constexpr unsigned gemv_blocks(int N) { return (unsigned)((N + 4 * R - 1) / (4 *
 template <int M, int R, bool SW, bool NORM, int EPI>
 void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
                  const EpiArgs& ea, hipStream_t stream) {
+  // XG (DLLM_GEMV_XG=1, batch 1-2, plain X): X rides along in every W trip instead of an LDS stage
+  static const int xg_on = [] { const char* e = getenv("DLLM_GEMV_XG"); return e ? atoi(e) : 0; }();
+  if constexpr (M <= 2 && !SW && !NORM) {
+    if (xg_on) {
+      const size_t lds_xg = EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0;
+      hipLaunchKernelGGL((gemv_kernel<M, R, 4, SW, NORM, EPI, true>), dim3(gemv_blocks<R>(N)), dim3(256), lds_xg,
+                         stream, (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
+      return;
+    }
+  }
   const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0) +
                      (EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0);
   // Long rows on a small grid at batch 1-2 (TinyLlama's down projection: K = 5632 is 11
