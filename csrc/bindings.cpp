@@ -18,7 +18,7 @@ int dllm_paged_attention(const void*, const void*, const void*, const int*, cons
                          const int*, const int*, void*, float*, float*, int*, const int*, const int*, int, int, int,
                          int, int, int, int, int, int, float, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
-int dllm_embed(const int*, const void*, void*, long, int, long, long, float*, hipStream_t);
+int dllm_embed(const int*, const void*, void*, long, int, long, long, float*, int*, const int*, int, hipStream_t);
 int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, int, const void*, void*, const void*,
               float, hipStream_t);
 int dllm_gelu(const void*, void*, long, hipStream_t);
@@ -258,7 +258,10 @@ void silu_mul(torch::Tensor gu, torch::Tensor out) {
 }
 
 // token-embedding gather; ssq (optional, f32 [>= T]): each row's sum of squares
-void embed(torch::Tensor ids, torch::Tensor table, torch::Tensor out, int64_t lo, c10::optional<torch::Tensor> ssq) {
+// sc_dst / sc_buf (optional, int32): a decode step's block-table updates (scatter_pairs layout),
+// applied by one extra workgroup of the same launch.
+void embed(torch::Tensor ids, torch::Tensor table, torch::Tensor out, int64_t lo, c10::optional<torch::Tensor> ssq,
+           c10::optional<torch::Tensor> sc_dst, c10::optional<torch::Tensor> sc_buf) {
   TORCH_CHECK(ids.scalar_type() == torch::kInt && ids.is_contiguous() && ids.is_cuda(), "ids: contiguous int32");
   check_bf16(table, "table");
   check_bf16(out, "out");
@@ -270,8 +273,19 @@ void embed(torch::Tensor ids, torch::Tensor table, torch::Tensor out, int64_t lo
     TORCH_CHECK(ssq->is_contiguous() && ssq->numel() >= ids.numel(), "ssq [>= T] contiguous");
     sp = ssq->data_ptr<float>();
   }
+  int* dst = nullptr;
+  const int* buf = nullptr;
+  int cap = 0;
+  if (sc_buf.has_value()) {
+    TORCH_CHECK(sc_dst.has_value(), "embed: sc_buf needs sc_dst");
+    for (auto* t : {&*sc_dst, &*sc_buf})
+      TORCH_CHECK(t->scalar_type() == torch::kInt && t->is_contiguous() && t->is_cuda(), "embed: scatter operands int32");
+    dst = sc_dst->data_ptr<int>();
+    buf = sc_buf->data_ptr<int>();
+    cap = (int)((sc_buf->numel() - 1) / 2);
+  }
   ok(dllm_embed(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), table.size(1), lo,
-                table.size(0), sp, stream()),
+                table.size(0), sp, dst, buf, cap, stream()),
      "embed");
 }
 
@@ -988,7 +1002,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("paged_attention", &paged_attention);
   m.def("flash_prefill", &flash_prefill);
   m.def("silu_mul", &silu_mul);
-  m.def("embed", &embed, py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("lo"), py::arg("ssq") = py::none());
+  m.def("embed", &embed, py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("lo"), py::arg("ssq") = py::none(),
+        py::arg("sc_dst") = py::none(), py::arg("sc_buf") = py::none());
   m.def("gelu", &gelu);
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("moe_gate", &moe_gate);

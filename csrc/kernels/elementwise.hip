@@ -30,9 +30,18 @@ __global__ void silu_mul_kernel(const u16* __restrict__ gu, u16* __restrict__ ou
 // registers (a random-row gather reads at ~5.5 TB/s: MI355X_MICROARCH.md)
 // ssq (optional): the row's sum of squares, ssq[t] — the first decoder layer's folded-RMSNorm row
 // scale then needs no separate res_add_ssq pass over the embeddings (one launch less per step)
+// sc_buf != nullptr: the LAST workgroup instead applies a decode step's block-table updates
+// (scatter_pairs_kernel's job: dst[idx_i] = val_i for sc_buf = [n, idx0, val0, ...]), so a decode
+// step starts with one launch instead of two (~4.5 us at batch 1, profiles/r3_single_stream_decode.md)
 __global__ void __launch_bounds__(256) embed_kernel(const int* __restrict__ ids, const u16* __restrict__ table,
                                                     u16* __restrict__ out, long T, int H, long lo, long rows,
-                                                    float* __restrict__ ssq) {
+                                                    float* __restrict__ ssq, int* __restrict__ sc_dst,
+                                                    const int* __restrict__ sc_buf, int sc_cap) {
+  if (sc_buf != nullptr && blockIdx.x == gridDim.x - 1) {
+    const int n = min(sc_buf[0], sc_cap);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_dst[sc_buf[1 + 2 * i]] = sc_buf[2 + 2 * i];
+    return;
+  }
   const long t = blockIdx.x * 4L + (threadIdx.x >> 6);
   if (t >= T) return;
   const long r = ids[t] - lo;
@@ -142,11 +151,12 @@ extern "C" int dllm_silu_mul(const void* gu, void* out, long T, int I, long in_s
 }
 
 extern "C" int dllm_embed(const int* ids, const void* table, void* out, long T, int H, long lo, long rows,
-                          float* ssq, hipStream_t stream) {
+                          float* ssq, int* sc_dst, const int* sc_buf, int sc_cap, hipStream_t stream) {
   if (H % 8 != 0) return -1;
-  if (T == 0) return 0;
-  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, stream, ids, (const u16*)table,
-                     (u16*)out, T, H, lo, rows, ssq);
+  if (T == 0 && sc_buf == nullptr) return 0;
+  const unsigned grid = (unsigned)((T + 3) / 4) + (sc_buf != nullptr ? 1u : 0u);
+  hipLaunchKernelGGL(embed_kernel, dim3(grid), dim3(256), 0, stream, ids, (const u16*)table, (u16*)out, T, H, lo, rows,
+                     ssq, sc_dst, sc_buf, sc_cap);
   return (int)hipGetLastError();
 }
 

@@ -7,7 +7,9 @@
 //     fragment layout of the skinny kernel splits a row into 64-B pieces instead);
 //   * a wave issues UNR x R such loads before its first FMA (16-64 KB in flight per CU at
 //     8 waves/CU), the 'GEMV / M <= 16' row of the staging table: W goes straight to VGPRs;
-//   * X is staged once per workgroup into LDS (M x K bf16 <= 64 KB) while the first W trip is in
+//   * batch 1 (XG): X is loaded with every W trip (16 B per lane beside each 1 KB W piece, L1 / L2
+//     hits) - no LDS stage, no barrier before the first FMA (measured 0.2-1 us faster per GEMV);
+//   * batch 2-8: X is staged once per workgroup into LDS (M x K bf16 <= 64 KB) while the first W trip is in
 //     flight, then read with conflict-free ds_read_b128 (per-iteration L2 reads of X measured
 //     slow: a dependent L2 round trip per k-step); with SWIGLU, X is the fused gate|up output
 //     [M, 2K] and silu(gate) * up is formed in the staging pass (the down projection absorbs the
@@ -92,23 +94,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
 
   constexpr int STEP = 512;  // K elements per wave-instruction
   constexpr int TRIP = STEP * UNR;
-  // PAIRED: the producer's partial row sums for this wave's first row (up to 1024 slots, 16 loads
-  // per lane) are requested BEFORE the first W trip.  Loads return in order, so a sum requested
-  // after W would wait out the whole W trip and only then let this wave issue its X staging loads:
-  // a second dependent round trip on every workgroup (measured +1.1 us QKV, +2.2 us gate|up at B = 1).
-  float pre[16];
-  if constexpr (PAIRED) {
-    if (wave < M) {
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = u * 64 + lane;
-        pre[u] = i < ea.ssq_n ? ea.ssq_in[(long)i * ea.ssq_in_ld + wave] : 0.f;
-      }
-    }
-    asm volatile("" ::: "memory");  // keep these requests ahead of the weight stream
-  }
   uint4 w[UNR][R], wn[UNR][R];
-  // XG (batch 1-2, plain X): X travels with W in every trip (L1/L2 hits, no LDS stage, no barrier)
+  // XG (batch 1, plain X): X travels with W in every trip (L1/L2 hits, no LDS stage, no barrier)
   uint4 xg[XG ? UNR : 1][XG ? M : 1], xgn[XG ? UNR : 1][XG ? M : 1];
 #define DLLM_GEMV_LOAD(DST, XDST, KB)                                                                \
   _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                                                 \
@@ -123,17 +110,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
   DLLM_GEMV_LOAD(w, xg, 0)  // the first trip of W is in flight while X is staged
   if constexpr (PAIRED) {
     // folded RMSNorm row scale: lane-parallel sum of the producer's partial sums, wave w -> rows w, w + 4
-    // (a GEMV producer leaves one slot per workgroup, e.g. 512 at N = 2048: the first row's loads
-    // were issued above; further rows / slots beyond 1024 take one more round trip here)
+    // (a GEMV producer leaves one slot per workgroup, e.g. 512 at N = 2048: 8 independent loads
+    // per lane are issued before the first add, so the sum costs one L2 round trip, not eight;
+    // requesting them ahead of the weight stream instead measured no different, round 4)
     for (int m = wave; m < M; m += 4) {
       float sacc = 0.f;
-      int i_first = 0;
-      if (m == wave) {
-#pragma unroll
-        for (int u = 0; u < 16; ++u) sacc += pre[u];
-        i_first = 1024;
-      }
-      for (int i0 = i_first; i0 < ea.ssq_n; i0 += 512) {
+      for (int i0 = 0; i0 < ea.ssq_n; i0 += 512) {
         float part[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -340,9 +322,13 @@ constexpr unsigned gemv_blocks(int N) { return (unsigned)((N + 4 * R - 1) / (4 *
 template <int M, int R, bool SW, bool NORM, int EPI>
 void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
                  const EpiArgs& ea, hipStream_t stream) {
-  // XG (DLLM_GEMV_XG=1, batch 1-2, plain X): X rides along in every W trip instead of an LDS stage
-  static const int xg_on = [] { const char* e = getenv("DLLM_GEMV_XG"); return e ? atoi(e) : 0; }();
-  if constexpr (M <= 2 && !SW && !NORM) {
+  // XG (batch 1, plain X): X rides along in every W trip (L1 / L2 hits) instead of an LDS stage
+  // and barrier.  Measured at batch 1 (scripts/exp/gemv_probe.py, profiles/r4_single_stream.md):
+  // 0.2-0.6 us off TinyLlama's fused QKV / Wo / gate|up / down GEMVs and up to 1 us off
+  // Llama-3-8B's, never slower; at batch 2 it is slower on the large shapes, so batch 1 only.
+  // DLLM_GEMV_XG=0 disables it.
+  static const int xg_on = [] { const char* e = getenv("DLLM_GEMV_XG"); return e ? atoi(e) : 1; }();
+  if constexpr (M == 1 && !SW && !NORM) {
     if (xg_on) {
       const size_t lds_xg = EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0;
       hipLaunchKernelGGL((gemv_kernel<M, R, 4, SW, NORM, EPI, true>), dim3(gemv_blocks<R>(N)), dim3(256), lds_xg,

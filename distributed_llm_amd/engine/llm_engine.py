@@ -1319,8 +1319,10 @@ class LLMEngine:
             self._decode_forward_inner(bs)
 
     def _decode_forward_inner(self, bs: int) -> None:
-        ops.scatter_pairs(self.bt_dev, self.d_upd)  # this step's block-table updates (inside the graph)
-        hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches)
+        # this step's block-table updates (inside the graph; the fused layer applies them in its
+        # embedding launch)
+        hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches,
+                                       scatter=(self.bt_dev, self.d_upd))
         if self.fused_sampler:
             self.model.sample(hid, self.d_temp[:bs], self.d_topp[:bs], self.d_topk[:bs], self.d_seed,
                               self.d_out[:bs])

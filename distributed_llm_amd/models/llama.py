@@ -368,11 +368,16 @@ class LlamaModel:
                                    xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
 
     def hidden_states(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
-                      kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
-        """Final-normed hidden states of each sequence's last new token: [S, H]."""
+                      kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
+                      scatter: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+        """Final-normed hidden states of each sequence's last new token: [S, H].  ``scatter`` =
+        (block tables, update pairs): a decode step's block-table updates, applied before any
+        attention reads the tables (by the fused path's embedding launch itself)."""
         cfg = self.cfg
         if getattr(self, "fused", False):
-            return self._hidden_states_fused(input_ids, positions, meta, kv_caches)
+            return self._hidden_states_fused(input_ids, positions, meta, kv_caches, scatter=scatter)
+        if scatter is not None:
+            ops.scatter_pairs(*scatter)
         if self.par.use_sp(input_ids.shape[0]) and not (input_ids.is_cuda and torch.cuda.is_current_stream_capturing()):
             return self._hidden_states_sp(input_ids, positions, meta, kv_caches)
         h = self._embed(input_ids)
@@ -397,7 +402,8 @@ class LlamaModel:
         return ops.rms_norm(last_h, self.final_norm, cfg.rms_eps, residual=last_r)
 
     def _hidden_states_fused(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
-                             kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+                             kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
+                             scatter: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
         """Fused layer path (module docstring): residual stream ``r`` updated in place by GEMM
         epilogues; ``ssq``/``n`` = partial row sums of r^2 of the latest residual producer."""
         cfg, par = self.cfg, self.par
@@ -413,14 +419,14 @@ class LlamaModel:
         resadd = par.sp_resadd if sp else par.all_reduce_resadd
         if not tp:
             # the gather also leaves each row's sum of squares in slot 0 (first layer's row scale)
-            r = ops.embedding(input_ids, self.embed, self.vocab_shard.start, ssq_out=ssq_a[0])
+            r = ops.embedding(input_ids, self.embed, self.vocab_shard.start, ssq_out=ssq_a[0], scatter=scatter)
             n = 1
         else:
             # vocab-parallel rows (zero outside this rank's shard) summed by the all-reduce, which
             # also leaves the row statistics of the first RMSNorm
             r = torch.empty((T, H), dtype=self.dtype, device=input_ids.device)
-            n = par.all_reduce_resadd(ops.embedding(input_ids, self.embed, self.vocab_shard.start), r, ssq_a,
-                                      add=False)
+            n = par.all_reduce_resadd(ops.embedding(input_ids, self.embed, self.vocab_shard.start, scatter=scatter),
+                                      r, ssq_a, add=False)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             # column-parallel QKV (this rank's heads) with RMSNorm folded + RoPE + paged K/V write

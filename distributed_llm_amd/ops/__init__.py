@@ -277,19 +277,26 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0,
-              ssq_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              ssq_out: Optional[torch.Tensor] = None,
+              scatter: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Row gather ``table[ids - lo]`` -> [T, H]; ids outside ``[lo, lo + rows)`` give zero rows
     (vocab-parallel shard of a TP rank: the all-reduce then sums the owners' rows).  ``ssq_out``
-    (f32, >= T): also each row's sum of squares, in the same launch."""
+    (f32, >= T): also each row's sum of squares, in the same launch.  ``scatter`` = (dst, buf):
+    also apply ``scatter_pairs(dst, buf)`` (a decode step's block-table updates) in the same launch."""
     ext = _native(table)
     if ext is None:
+        if scatter is not None:
+            scatter_pairs(*scatter)
         out = ref.embedding(ids, table, lo)
         if ssq_out is not None:
             ssq_out[:out.shape[0]] = (out.float() ** 2).sum(1)
         return out
     ids = ids.reshape(-1).to(torch.int32).contiguous()
     out = torch.empty((ids.numel(), table.shape[1]), dtype=table.dtype, device=table.device)
-    ext.embed(ids, table, out, int(lo), ssq_out)
+    if scatter is None:
+        ext.embed(ids, table, out, int(lo), ssq_out)
+    else:
+        ext.embed(ids, table, out, int(lo), ssq_out, scatter[0], scatter[1])
     return out
 
 

@@ -446,6 +446,26 @@ def test_embedding(H, lo, rows):
     assert torch.isnan(ssq[257:]).all()
 
 
+@pytest.mark.parametrize("T,n", [(1, 0), (1, 3), (8, 17), (512, 300)])
+def test_embedding_with_block_table_scatter(T, n):
+    """The decode step's block-table updates ride in the embedding launch (one extra workgroup):
+    same rows as the plain gather, same table as ops.scatter_pairs."""
+    torch.manual_seed(T + n)
+    table = bf(1000, 256)
+    ids = torch.randint(0, 1000, (T,), device=DEV, dtype=torch.int32)
+    bt = torch.randint(0, 9999, (64, 128), device=DEV, dtype=torch.int32)
+    buf = torch.zeros(1 + 2 * 400, dtype=torch.int32, device=DEV)
+    idx = torch.randperm(bt.numel(), device=DEV)[:n].to(torch.int32)
+    buf[0] = n
+    buf[1:1 + 2 * n:2] = idx
+    buf[2:2 + 2 * n:2] = torch.arange(n, device=DEV, dtype=torch.int32) + 50000
+    want_bt = bt.clone()
+    ops.scatter_pairs(want_bt, buf)
+    got = ops.embedding(ids, table, 0, scatter=(bt, buf))
+    assert torch.equal(got, ref.embedding(ids.cpu(), table.cpu(), 0).to(DEV))
+    assert torch.equal(bt, want_bt)
+
+
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
 @pytest.mark.parametrize("N,K,swiglu", [(2560, 2048, False), (2048, 5632, True), (1000, 520, False), (37, 1032, True),
                                          (4096, 3000, True)])

@@ -288,6 +288,30 @@ def test_gemv_swiglu(M, R, H, I):
     torch.testing.assert_close(act.cpu().float(), want.float(), atol=tol, rtol=3e-2)
 
 
+@pytest.mark.parametrize("M", [1, 2, 8])
+@pytest.mark.parametrize("R", [1, 2])
+def test_gemv_swiglu_partials_past_1024_slots(M, R):
+    """The PAIRED GEMV requests its first row's first 1024 partial sums ahead of the weight stream
+    and sums any further slots (and rows past the fourth) afterwards: the same partials spread over
+    1,500 slots, half in the first 1,024 and half after, give the same activation."""
+    H, I = 512, 640
+    torch.manual_seed(M + 31 * R)
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = _rnd(2 * I, H, scale=0.05)
+    wf = fuse_gate_up_weight(wgu, ln)
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
+    n = ops.gemm.res_add_ssq(None, r, ssq)
+    big = torch.zeros(1500, M, device="cuda")
+    big[:n] = ssq[:n] / 2
+    big[1100:1100 + n] = ssq[:n] / 2
+    act_ref = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    act = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    _ext().gemv_swiglu(r, wf, ssq, n, 1.0 / H, 1e-5, act_ref, R)
+    _ext().gemv_swiglu(r, wf, big, 1500, 1.0 / H, 1e-5, act, R)
+    torch.testing.assert_close(act.float(), act_ref.float(), atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("plan", PLANS)
 @pytest.mark.parametrize("M,N,K", [(37, 200, 384), (320, 2048, 2048)])
 def test_panel_weight_matches_row_major(plan, M, N, K):
