@@ -88,7 +88,7 @@ def parse():
     ap.add_argument("--gc-freeze", type=int, default=0,
                     help="1: gc.freeze() + higher young-generation thresholds after start-up (no measured effect on "
                          "the flagship: 57.0 / 59.7k off vs 59.3 / 59.0k on, one box)")
-    ap.add_argument("--gil-switch-ms", type=float, default=5.0,
+    ap.add_argument("--gil-switch-ms", type=float, default=0.5,
                     help="turn pipelining: Python thread switch interval (sys.setswitchinterval) in ms")
     ap.add_argument("--admit-every", type=int, default=16,
                     help="turn pipelining: the engine admits new turns every N decode steps of a burst")
@@ -566,8 +566,8 @@ def main() -> int:
         pipelined = (bool(a.pipeline) or a.groups > 1) and cluster is None
         if pipelined:
             # the engine's step loop and the routing driver are two Python threads: a short GIL
-            # switch interval (default 5 ms) hands the GIL back to the step loop before the
-            # queued decode step runs dry (profiles/r4_turn_pipelining.md)
+            # switch interval (0.5 ms; Python's default is 5) hands the GIL back to the step loop
+            # before the queued decode step runs dry (+1-1.4 % routed tok/s, profiles/r4_driver_window_gaps.md)
             sys.setswitchinterval(a.gil_switch_ms / 1000.0)
             for e in engines:
                 e.ADMIT_EVERY = max(1, a.admit_every)
@@ -701,6 +701,8 @@ def main() -> int:
                                            if cluster is None else False),
                        "admit_every": a.admit_every if (a.pipeline or a.groups > 1) else None,
                        "gc_freeze": bool(a.gc_freeze),
+                       "gil_switch_ms": a.gil_switch_ms if (a.pipeline or a.groups > 1) else None,
+                       "early_prefill": os.environ.get("DLLM_EARLY_PREFILL", "1") == "1",
                        "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
             "p50_latency_ms": round(statistics.median(lats), 1) if lats else None,

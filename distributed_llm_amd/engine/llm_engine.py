@@ -185,6 +185,9 @@ class LLMEngine:
         self.R = R
         self._free_rows = list(range(R - 1, -1, -1))
         self._pf_host = self._pf_dev = self._pf_evt = None   # prefill input staging (_stage_i32)
+        self._h2d_ring = None                                 # small pinned copies (_small_h2d)
+        self._h2d_i = 0
+        self._early_pf = None      # a prefill chunk queued under the last step of a decode burst
         pin = self.on_gpu
         # host mirror of the device block table (pinned); row R is the dummy row of padding tiles.
         self.bt_host_t = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, pin_memory=pin)
@@ -444,6 +447,7 @@ class LLMEngine:
                     s.row = -1
                 s.done.set()
         self._active = []
+        self._early_pf = None
         self._bt_dirty = True
 
     # TP mirror: admissions are exchanged every MIRROR_EVERY scheduler iterations (and whenever the
@@ -606,22 +610,7 @@ class LLMEngine:
             if not (waiting or prefilling or running):
                 break
             # admit
-            _ta = time.perf_counter()
-            while waiting and len(prefilling) + len(running) < self.R:
-                s = waiting[0]
-                s.fill = s.prompt + s.out
-                if not self.bm.can_allocate(len(s.fill) + 1):
-                    break
-                table, cached = self.bm.allocate(s.id, s.fill)
-                if not table:
-                    break
-                waiting.pop(0)
-                s.num_cached = s.num_computed = cached
-                s.admitted = time.perf_counter()
-                s.row = self._free_rows.pop()
-                self._set_row_blocks(s)
-                prefilling.append(s)
-            self.timers["admit"] += time.perf_counter() - _ta
+            self._admit(waiting, prefilling, len(running))
             if not (prefilling or running):
                 if waiting:  # nothing fits even alone -> fail the head request
                     s = waiting.pop(0)
@@ -631,7 +620,11 @@ class LLMEngine:
             if prefilling:
                 _t = time.perf_counter()
                 with tracer.span("engine.prefill", "engine", seqs=len(prefilling)):
-                    done = self._prefill_step(prefilling)
+                    if self._early_pf is not None:   # launched under the last step of a burst
+                        h, self._early_pf = self._early_pf, None
+                        done = self._prefill_finish(h)
+                    else:
+                        done = self._prefill_step(prefilling)
                 self.timers["prefill"] += time.perf_counter() - _t
                 for s in done:
                     prefilling.remove(s)
@@ -648,7 +641,7 @@ class LLMEngine:
                 continue
             with tracer.span("engine.decode", "engine", batch=len(running)):
                 if self._pipeline_ok():
-                    finished, preempted = self._decode_burst(running, waiting)
+                    finished, preempted = self._decode_burst(running, waiting, prefilling)
                 else:
                     finished, preempted = self._decode_step(running)
             if tracer.enabled:
@@ -666,6 +659,25 @@ class LLMEngine:
                     s.error = None
                     waiting.insert(0, s)  # re-admitted with fill = prompt + out (recompute)
                 self.timers["decode_host_post"] += time.perf_counter() - _t
+
+    def _admit(self, waiting: List[_Seq], prefilling: List[_Seq], n_running: int) -> None:
+        """Move waiting requests that fit (a free row, KV blocks for prompt + 1) to ``prefilling``."""
+        _ta = time.perf_counter()
+        while waiting and self._free_rows and len(prefilling) + n_running < self.R:
+            s = waiting[0]
+            s.fill = s.prompt + s.out
+            if not self.bm.can_allocate(len(s.fill) + 1):
+                break
+            table, cached = self.bm.allocate(s.id, s.fill)
+            if not table:
+                break
+            waiting.pop(0)
+            s.num_cached = s.num_computed = cached
+            s.admitted = time.perf_counter()
+            s.row = self._free_rows.pop()
+            self._set_row_blocks(s)
+            prefilling.append(s)
+        self.timers["admit"] += time.perf_counter() - _ta
 
     def _finished(self, s: _Seq) -> bool:
         if s.error is not None and s.error != "__preempt__":
@@ -744,16 +756,20 @@ class LLMEngine:
             hf[base + n:base + pad] = 0.0
         h[base + 3 * stride] = self._next_seed()
 
-    def _sample(self, hidden: torch.Tensor, seqs: List[_Seq], greedy_ids: Optional[torch.Tensor]) -> List[int]:
+    def _sample(self, hidden: torch.Tensor, seqs: List[_Seq], greedy_ids: Optional[torch.Tensor],
+                launch_only: bool = False) -> Union[List[int], torch.Tensor]:
+        """Token per row.  ``launch_only`` (fused sampler): return the device tensor of tokens
+        without waiting for it (the caller reads it back later)."""
         n = len(seqs)
         dev = hidden.device
         if self.fused_sampler:   # one launch: arg-max / top-k / top-p per row
             buf = np.zeros(3 * n + 1, dtype=np.int32)
             self._fill_sampler(buf, buf.view(np.float32), 0, n, seqs, n)
-            t = torch.from_numpy(buf).to(dev, non_blocking=True)
+            t = self._small_h2d(buf) if self.on_gpu else torch.from_numpy(buf).to(dev)
             out = torch.empty(n, dtype=torch.int32, device=dev)
-            return self.model.sample(hidden[:n], t[:n].view(torch.float32), t[n:2 * n].view(torch.float32),
-                                     t[2 * n:3 * n], t[3 * n:], out).tolist()
+            out = self.model.sample(hidden[:n], t[:n].view(torch.float32), t[n:2 * n].view(torch.float32),
+                                    t[2 * n:3 * n], t[3 * n:], out)
+            return out if launch_only else out.tolist()
         ids = greedy_ids[:n] if greedy_ids is not None else self.model.greedy(hidden[:n])
         sampled = [i for i, s in enumerate(seqs) if not s.params.greedy]
         if not sampled:
@@ -778,10 +794,26 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ prefill
     def _prefill_step(self, prefilling: List[_Seq]) -> List[_Seq]:
+        return self._prefill_finish(self._prefill_launch(prefilling))
+
+    def _prefill_launch(self, prefilling: List[_Seq]) -> tuple:
+        """Queue one prefill chunk (and the fused first-token sampler) on the GPU; the host does
+        not wait.  ``_prefill_finish`` reads the first tokens back."""
         with ops.gemm.workspace_owner(self._ws_owner):
             return self._prefill_step_inner(prefilling)
 
-    def _prefill_step_inner(self, prefilling: List[_Seq]) -> List[_Seq]:
+    def _prefill_finish(self, handle: tuple) -> List[_Seq]:
+        done_seqs, toks = handle
+        if torch.is_tensor(toks):
+            toks = toks.tolist()          # the fused sampler's device output: waits for the chunk
+        now = time.perf_counter()
+        for s, tok in zip(done_seqs, toks):
+            if s.first_tok is None:
+                s.first_tok = now
+            self._append(s, tok)
+        return done_seqs
+
+    def _prefill_step_inner(self, prefilling: List[_Seq]) -> tuple:
         budget = self.max_prefill_tokens
         chunk: List[tuple] = []
         for s in prefilling:
@@ -839,17 +871,38 @@ class LLMEngine:
             s.num_computed = b
             self.bm.commit(s.id, b)
         if not done_seqs:
-            return []
+            return [], []
         sel = [i for i, (s, a, b) in enumerate(chunk) if b == len(s.fill)]
-        h = hidden if len(sel) == len(chunk) else hidden.index_select(
-            0, torch.tensor(sel, dtype=torch.int64).to(dev, non_blocking=True))
-        toks = self._sample(h, done_seqs, None)
-        now = time.perf_counter()
-        for s, tok in zip(done_seqs, toks):
-            if s.first_tok is None:
-                s.first_tok = now
-            self._append(s, tok)
-        return done_seqs
+        if len(sel) == len(chunk):
+            h = hidden
+        else:
+            sel_a = np.asarray(sel, dtype=np.int32)
+            sel_d = self._small_h2d(sel_a) if self.on_gpu else torch.from_numpy(sel_a)
+            h = hidden.index_select(0, sel_d.to(torch.int64))
+        return done_seqs, self._sample(h, done_seqs, None, launch_only=True)
+
+    def _small_h2d(self, a: np.ndarray) -> torch.Tensor:
+        """A few KB of int32 to the device without a host stall: through a ring of 4 pinned slots
+        (a slot is rewritten only after the copy that last read it has completed, which is long
+        past by then), never through pageable memory (a pageable async copy may wait for the
+        stream, i.e. for the decode step a prefill is queued behind)."""
+        n = a.size
+        if self._h2d_ring is None or self._h2d_ring[0][0].numel() < n:
+            cap = max(1 << 14, 1 << (int(n) - 1).bit_length())
+            self._h2d_ring = [(torch.empty(cap, dtype=torch.int32, pin_memory=True),
+                               torch.empty(cap, dtype=torch.int32, device=self.device), None) for _ in range(4)]
+            self._h2d_i = 0
+        i = self._h2d_i
+        self._h2d_i = (i + 1) % len(self._h2d_ring)
+        host, dev, ev = self._h2d_ring[i]
+        if ev is not None:
+            ev.synchronize()
+        host.numpy()[:n] = a.reshape(-1)
+        dev[:n].copy_(host[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._h2d_ring[i] = (host, dev, ev)
+        return dev[:n]
 
     def _stage_i32(self, parts) -> List[torch.Tensor]:
         """Pack int sequences / arrays into one pinned int32 buffer and copy it to the device with
@@ -1069,11 +1122,35 @@ class LLMEngine:
         ev.record()
         return ev
 
-    def _decode_burst(self, running: List[_Seq], waiting: List[_Seq]) -> Tuple[List[_Seq], List[_Seq]]:
+    # A burst that ends because new requests arrived admits them and queues their prefill chunk
+    # BEFORE it waits for its last decode step: the chunk runs right behind that step instead of
+    # after the host's admission work (profiles/r4_driver_window_gaps.md: ~2.5 ms of GPU idle per
+    # admission).  New sequences only take free rows and free blocks (nothing is released before
+    # the burst has drained), and a prefix hit only shares full, committed blocks, never the slot
+    # the in-flight step writes.  Single-GPU pools only (TP admissions follow the mirrored schedule).
+    EARLY_PREFILL = os.environ.get("DLLM_EARLY_PREFILL", "1") == "1"
+
+    def _early_admit(self, waiting: List[_Seq], prefilling: Optional[List[_Seq]], n_running: int) -> None:
+        if (prefilling is None or self._early_pf is not None or not self.EARLY_PREFILL or self.par.enabled
+                or not self.fused_sampler):
+            return
+        _t = time.perf_counter()
+        new = self._take_inbox(final=False)
+        self._active.extend(new)          # a failing step must still find them (_abort_all)
+        waiting.extend(new)
+        self._admit(waiting, prefilling, n_running)
+        if prefilling:
+            with tracer.span("engine.prefill_early", "engine", seqs=len(prefilling)):
+                self._early_pf = self._prefill_launch(prefilling)
+        self.timers["prefill"] += time.perf_counter() - _t
+
+    def _decode_burst(self, running: List[_Seq], waiting: List[_Seq],
+                      prefilling: Optional[List[_Seq]] = None) -> Tuple[List[_Seq], List[_Seq]]:
         """Pipelined decode steps until the batch must change (a new request arrived, a waiting
         request could take a freed row, or the batch is empty).  Same contract as ``_decode_step``:
         returns (finished, preempted); the caller releases / re-queues them.  On return every
-        continuing sequence is in the non-pipelined state (its last token appended with a slot)."""
+        continuing sequence is in the non-pipelined state (its last token appended with a slot).
+        ``prefilling`` (the caller's list): see EARLY_PREFILL."""
         eos, mml, mb_ = self.tok.eos_id, self.max_model_len, self.max_blocks
         finished: List[_Seq] = []
         preempted: List[_Seq] = []
@@ -1142,6 +1219,8 @@ class LLMEngine:
                     launched = (run, pn, self._read_out(B, pn, bs), bs, self.par.custom_ar is not None)
                     self.steps["decode"] += 1
                     nsteps += 1
+            if launched is None and stop and self._inbox:
+                self._early_admit(waiting, prefilling, len(cur))
             _t1 = time.perf_counter()
             ev.synchronize()
             toks = self._out_np[pc][:len(cur)].tolist()

@@ -53,6 +53,14 @@ def main():
     print("| gap size | idle s | share of idle |\n|---|---|---|")
     for b in ("<2us", "2-5us", "5-20us", "20-100us", ">=100us"):
         print(f"| {b} | {hist[b] / 1e9:.3f} | {100 * hist[b] / max(idle, 1):.1f} % |")
+    per = defaultdict(lambda: [0, 0])
+    for s_, e_, k in rows:
+        per[k][0] += e_ - s_
+        per[k][1] += 1
+    tot = sum(v[0] for v in per.values())
+    print("\n| kernel | ms in window | calls | avg us | share of kernel time |\n|---|---|---|---|---|")
+    for k, (t, n) in sorted(per.items(), key=lambda x: -x[1][0])[:15]:
+        print(f"| `{k}` | {t / 1e6:.1f} | {n} | {t / n / 1e3:.1f} | {100 * t / max(tot, 1):.1f} % |")
     print("\n| idle ms | gaps | mean us | kernel before | kernel after |\n|---|---|---|---|---|")
     for (a, b), (g, n) in sorted(gaps.items(), key=lambda x: -x[1][0])[:25]:
         print(f"| {g / 1e6:.1f} | {n} | {g / n / 1e3:.1f} | `{a}` | `{b}` |")
