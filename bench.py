@@ -751,6 +751,15 @@ def main() -> int:
                                  "lookups": lk, "memo_hit_rate": round((enc1["hits"] - enc0["hits"]) / lk, 3) if lk else None,
                                  "texts_encoded_in_window": enc1["encoded_texts"] - enc0["encoded_texts"],
                                  "batch_reuse_hits": enc1["batch_hits"] - enc0["batch_hits"]}
+        logs = [e._sync_log for e in engines if getattr(e, "_sync_log", None)]
+        if logs:   # DLLM_SYNC_LOG=1 diagnostics: did the step loop keep a step queued ahead?
+            import numpy as np
+            rec = np.array([r for lg in logs for r in lg], dtype=np.float64)
+            wait = rec[:, 1] * 1e3
+            out["step_loop_sync"] = {"steps": int(len(rec)), "prep_ms_p50": round(float(np.median(rec[:, 0]) * 1e3), 3),
+                                     "wait_ms_p50": round(float(np.median(wait)), 3),
+                                     "wait_under_0.1ms": int((wait < 0.1).sum()),
+                                     "wait_ms_pcts": [round(float(x), 3) for x in np.percentile(wait, [5, 25, 75, 95])]}
         print(json.dumps(out), flush=True)
     if a.trace:
         from distributed_llm_amd.utils.tracing import tracer

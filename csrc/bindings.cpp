@@ -25,6 +25,8 @@ int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
 int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
 int dllm_scatter_pairs(int*, const int*, int, hipStream_t);
+int dllm_step_fetch(const int*, int*, int, int, int, int, const int*, const int*, int*, int, hipStream_t);
+int dllm_step_store(const int*, int*, int, hipStream_t);
 int dllm_argmax(const void*, long, int, int, int, int*, hipStream_t);
 int dllm_sample_topp(const float*, const long*, int, int, const float*, const float*, const float*, int*, hipStream_t);
 int dllm_cosine_scores(const float*, const float*, float*, int, int, int, hipStream_t);
@@ -316,6 +318,46 @@ void moe_gate(torch::Tensor logits, int64_t k, torch::Tensor ids, torch::Tensor 
 }
 
 // dst (int32, any shape, contiguous) flat[idx_i] = val_i for buf = [n, idx0, val0, ...]
+// Device address of a pinned (hipHostMalloc'd) host tensor, for kernels that read / write it.
+static void* mapped_ptr(const torch::Tensor& t, const char* what) {
+  TORCH_CHECK(t.device().is_cpu() && t.is_pinned() && t.is_contiguous() && t.scalar_type() == torch::kInt,
+              what, ": pinned contiguous int32 host tensor");
+  void* dptr = nullptr;
+  ok((int)hipHostGetDevicePointer(&dptr, t.data_ptr(), 0), what);
+  return dptr;
+}
+
+// Decode-step inputs from the pinned staging buffer (device-mapped) into dec_dev, with the
+// pipelined id gather (ids[i] = d_out[src[i]] where src[i] >= 0) and the attention work list.
+void step_fetch(torch::Tensor dec_host, torch::Tensor dec_dev, int64_t ids_off, int64_t src_off, int64_t n_ids,
+                torch::Tensor d_out, c10::optional<torch::Tensor> items_host, c10::optional<torch::Tensor> items_dev) {
+  TORCH_CHECK(dec_dev.is_cuda() && dec_dev.scalar_type() == torch::kInt && dec_dev.is_contiguous() &&
+                  dec_dev.numel() == dec_host.numel(), "step_fetch: dec_dev int32 like dec_host");
+  TORCH_CHECK(d_out.is_cuda() && d_out.scalar_type() == torch::kInt && d_out.numel() > n_ids, "step_fetch: d_out");
+  const int* ih = nullptr;
+  int* idv = nullptr;
+  int cap = 0;
+  if (items_host.has_value()) {
+    TORCH_CHECK(items_dev.has_value() && items_dev->is_cuda() && items_dev->scalar_type() == torch::kInt &&
+                    items_dev->numel() >= items_host->numel(), "step_fetch: items_dev");
+    ih = (const int*)mapped_ptr(*items_host, "step_fetch items_host");
+    idv = items_dev->data_ptr<int>();
+    cap = (int)items_host->numel();
+  }
+  ok(dllm_step_fetch((const int*)mapped_ptr(dec_host, "step_fetch dec_host"), dec_dev.data_ptr<int>(),
+                     (int)dec_host.numel(), (int)ids_off, (int)src_off, (int)n_ids, d_out.data_ptr<int>(), ih, idv, cap,
+                     stream()),
+     "step_fetch");
+}
+
+// out_host[0:n] <- d_out[0:n] by a kernel (last node of a decode-step graph).
+void step_store(torch::Tensor d_out, torch::Tensor out_host, int64_t n) {
+  TORCH_CHECK(d_out.is_cuda() && d_out.scalar_type() == torch::kInt && d_out.numel() >= n && out_host.numel() >= n,
+              "step_store: shapes");
+  ok(dllm_step_store(d_out.data_ptr<int>(), (int*)mapped_ptr(out_host, "step_store out_host"), (int)n, stream()),
+     "step_store");
+}
+
 void scatter_pairs(torch::Tensor dst, torch::Tensor buf) {
   check_i32(dst, "dst");
   check_i32(buf, "buf");
@@ -1009,6 +1051,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("moe_gate", &moe_gate);
   m.def("argmax", &argmax);
   m.def("scatter_pairs", &scatter_pairs);
+  m.def("step_fetch", &step_fetch);
+  m.def("step_store", &step_store);
   m.def("sample_topp", &sample_topp);
   m.def("sample_rows", &sample_rows);
   m.def("tp_cands_k", &tp_cands_k);

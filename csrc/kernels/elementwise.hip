@@ -134,6 +134,46 @@ __global__ void scatter_pairs_kernel(int* __restrict__ dst, const int* __restric
 }
 }  // namespace
 
+// ---- decode-step I/O inside the step's graph (round 4).  The step's inputs are staged by the host
+// in pinned, device-mapped memory and its sampled tokens are read back from pinned memory; moving
+// them with these kernels instead of hipMemcpyAsync keeps every decode step ONE graph launch on
+// one queue: an async H2D copy runs on an SDMA engine and waited ~320 us per step for the
+// read-back blit of the previous step to signal it (profiles/r4_driver_window_gaps.md).
+// step_fetch: dec_dev[0:n_dec] <- dec_host, except the input ids, which the pipelined decode takes
+// from the previous step's sampled tokens still on the device: ids[i] = d_out[src[i]] where
+// src[i] >= 0 (src lives in the host buffer at src_off); and the attention work list
+// items_dev <- items_host, as many words as its header says (decode_work_items layout).
+__global__ void __launch_bounds__(256) step_fetch_kernel(const int* __restrict__ dec_host, int* __restrict__ dec_dev,
+                                                         int n_dec, int ids_off, int src_off, int n_ids,
+                                                         const int* __restrict__ d_out,
+                                                         const int* __restrict__ items_host,
+                                                         int* __restrict__ items_dev, int items_cap) {
+  const int stride = gridDim.x * blockDim.x;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  int n_items = 0;
+  if (items_host != nullptr) {
+    const int h = items_host[0];
+    n_items = min(h < 0 ? 4 + 4 * (-h) : 1 + 2 * h, items_cap);
+  }
+  for (int w = gid; w < n_dec; w += stride) {
+    int v = dec_host[w];
+    const int i = w - ids_off;
+    if (i >= 0 && i < n_ids) {
+      const int s = dec_host[src_off + i];
+      if (s >= 0 && s < n_ids) v = d_out[s];
+    }
+    dec_dev[w] = v;
+  }
+  for (int w = gid; w < n_items; w += stride) items_dev[w] = items_host[w];
+}
+
+// step_store: out_host[0:n] <- d_out (the sampled tokens, + the TP health vote), last node of the graph
+__global__ void __launch_bounds__(256) step_store_kernel(const int* __restrict__ d_out, int* __restrict__ out_host,
+                                                         int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out_host[i] = d_out[i];
+}
+
 static inline int grid_for(long n, int threads) {
   long g = (n + threads - 1) / threads;
   if (g > 65536) g = 65536;
@@ -183,5 +223,21 @@ extern "C" int dllm_moe_gate(const float* logits, int T, int E, int k, int* ids,
   if (E > 64 || k > 8 || k > E) return -1;
   if (T == 0) return 0;
   hipLaunchKernelGGL(moe_gate_kernel, dim3((T + 127) / 128), dim3(128), 0, stream, logits, T, E, k, ids, w);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_step_fetch(const int* dec_host, int* dec_dev, int n_dec, int ids_off, int src_off, int n_ids,
+                               const int* d_out, const int* items_host, int* items_dev, int items_cap,
+                               hipStream_t stream) {
+  if (n_dec <= 0 || ids_off < 0 || src_off < 0 || ids_off + n_ids > n_dec || src_off + n_ids > n_dec) return -1;
+  if ((items_host == nullptr) != (items_dev == nullptr)) return -2;
+  hipLaunchKernelGGL(step_fetch_kernel, dim3(32), dim3(256), 0, stream, dec_host, dec_dev, n_dec, ids_off, src_off,
+                     n_ids, d_out, items_host, items_dev, items_cap);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_step_store(const int* d_out, int* out_host, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(step_store_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_out, out_host, n);
   return (int)hipGetLastError();
 }

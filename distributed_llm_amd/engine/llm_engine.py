@@ -188,6 +188,8 @@ class LLMEngine:
         self._h2d_ring = None                                 # small pinned copies (_small_h2d)
         self._h2d_i = 0
         self._early_pf = None      # a prefill chunk queued under the last step of a decode burst
+        # DLLM_SYNC_LOG=1: per pipelined step (host prep s, wait for the in-flight step s, launched)
+        self._sync_log: Optional[list] = [] if os.environ.get("DLLM_SYNC_LOG", "0") == "1" else None
         pin = self.on_gpu
         # host mirror of the device block table (pinned); row R is the dummy row of padding tiles.
         self.bt_host_t = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, pin_memory=pin)
@@ -201,17 +203,23 @@ class LLMEngine:
         # packed decode buffer: ids | pos | slots | tile_seq  (mb each) | qstart | qlen | ctx (R+1 each)
         #                       | attention split length
         #                       | sampler: temperature, top_p (f32 bits), top_k (mb each) | seed
+        #                       | id sources (mb: row of the previous step's d_out, -1 = ids above)
         #                       | block-table updates [n, (flat idx, block) * R]
         s0 = 4 * mb + 3 * (R + 1) + 1
         o = [0, mb, 2 * mb, 3 * mb, 4 * mb, 4 * mb + R + 1, 4 * mb + 2 * (R + 1), 4 * mb + 3 * (R + 1),
-             s0 + 3 * mb + 1]
+             s0 + 4 * mb + 1, s0 + 3 * mb + 1]
         self._dec_n = o[8] + 1 + 2 * R
+        # Step I/O by kernels inside the step's graph (ops.step_fetch / step_store: the pinned
+        # buffers are device-mapped), not by async copies: an H2D copy runs on an SDMA engine and
+        # waited ~320 us per step for the previous step's read-back to signal it (r4 gap analysis).
+        self._gio = self.on_gpu and ops.native_available() and os.environ.get("DLLM_STEP_IO_KERNEL", "1") == "1"
         self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
         # two pinned staging buffers: the pipelined decode (_decode_burst) fills one while the
         # previous step's async copy may still be reading the other
         self._dec_bufs = []
         for _ in range(2):
             t = torch.zeros(self._dec_n, dtype=torch.int32, pin_memory=pin)
+            t[o[9]:o[9] + mb] = -1
             self._dec_bufs.append((t, t.numpy(), t.numpy().view(np.float32)))
         self.dec_host_t, self.dec_host, self.dec_host_f = self._dec_bufs[0]
         self._off = o
@@ -950,13 +958,15 @@ class LLMEngine:
                 return b
         raise ValueError(f"batch {n} exceeds max_num_seqs")
 
-    def _prep_decode(self, running: List[_Seq], lens: np.ndarray, last: Optional[np.ndarray], p: int) -> int:
-        """Stage one decode step's inputs in pinned buffer ``p`` and copy them to the device (async).
+    def _prep_decode(self, running: List[_Seq], lens: np.ndarray, last: Optional[np.ndarray], p: int,
+                     src: Optional[List[int]] = None) -> int:
+        """Stage one decode step's inputs in pinned buffer ``p`` (the step's graph fetches them, or,
+        without step I/O kernels, an async copy moves them).
 
         ``lens``: context length per row including the input token (position = lens - 1);
         ``last``: the input token per row, or None when it is the previous step's sampled token
-        still on the device (pipelined decode: ``_decode_burst`` gathers it from ``d_out``).
-        Returns the step's bucket."""
+        still on the device (pipelined decode): then ``src[i]`` is the row of ``d_out`` holding
+        row i's input token.  Returns the step's bucket."""
         B = len(running)
         bs = self._bucket(B)
         o = self._off
@@ -999,9 +1009,23 @@ class LLMEngine:
             # released row's stale device columns past it would survive the next admission sync
             self._note_upd_cols()
             self._bt_upd.clear()
+        h[o[9]:o[9] + bs] = -1
+        if src is not None:
+            h[o[9]:o[9] + B] = src
+        if self._gio:
+            return bs               # the step's first kernel (ops.step_fetch) reads buffer p
         self.dec_dev[:o[8] + 1 + 2 * nu].copy_(self._dec_bufs[p][0][:o[8] + 1 + 2 * nu], non_blocking=True)
         if n_items:
             self.items_dev[:n_items].copy_(self._items_bufs[p][0][:n_items], non_blocking=True)
+        if src is not None:
+            # input ids = the in-flight step's sampled tokens, gathered on the device
+            if list(src) == list(range(B)):
+                self.d_ids[:B].copy_(self.d_out[:B])
+            else:
+                sb = self._src_bufs[p]
+                sb[:B] = torch.as_tensor(src, dtype=torch.int64)
+                self.d_src[:B].copy_(sb[:B], non_blocking=True)
+                self.d_ids[:B] = self.d_out[self.d_src[:B]]
         return bs
 
     def _decode_step(self, running: List[_Seq]) -> Tuple[List[_Seq], List[_Seq]]:
@@ -1017,12 +1041,12 @@ class LLMEngine:
         self._arm_vote_fault()
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=self.use_graphs):
             if self.use_graphs:
-                g = self._graphs.get(bs)
+                g = self._graphs.get(self._gkey(bs, 0))
                 if g is None:
-                    g = self._capture(bs)
+                    g = self._capture(bs, 0)
                 g.replay()
             else:
-                self._decode_forward(bs)
+                self._decode_forward(bs, 0)
         self.steps["decode"] += 1
         self.steps["decode_tokens"] += B
         if self.fused_sampler and self.par.custom_ar is not None:
@@ -1030,14 +1054,14 @@ class LLMEngine:
             vals = self.d_out[:bs + 1].tolist()
             if vals[bs]:
                 self._collective_trip("decode step")
-                self._decode_forward(bs)    # re-run on RCCL: same inputs, idempotent K/V writes
+                self._decode_forward(bs, 0)    # re-run on RCCL: same inputs, idempotent K/V writes
                 vals = self.d_out[:bs + 1].tolist()
             toks = vals[:B]
         elif self.fused_sampler:
             toks = self.d_out[:B].tolist()
         else:
             if not self._collectives_ok():
-                self._decode_forward(bs)
+                self._decode_forward(bs, 0)
             toks = self._sample(self.d_hidden[:bs], running, self.d_out[:bs])
         _t2 = time.perf_counter()
         self.timers["decode_host_pre"] += _t1 - _t0
@@ -1104,20 +1128,26 @@ class LLMEngine:
         return (self.PIPELINE and self.on_gpu and self.use_graphs and self.fused_sampler
                 and (not self.par.enabled or self.TP_PIPELINE))
 
-    def _replay(self, bs: int) -> None:
+    def _replay(self, bs: int, p: int) -> None:
         if self.FAULT_TRIP_DECODE >= 0 and self.steps["decode"] == self.FAULT_TRIP_DECODE \
                 and self.par.custom_ar is not None:
             self.par.custom_ar.err.fill_(1)     # fault injection: as if an all-reduce timed out
         self._arm_vote_fault()
         with tracer.gpu_span("engine.decode_forward", bucket=bs, graph=True):
-            g = self._graphs.get(bs)
+            g = self._graphs.get(self._gkey(bs, p))
             if g is None:
-                g = self._capture(bs)
+                g = self._capture(bs, p)
             g.replay()
 
+    def _gkey(self, bs: int, p: int):
+        # with step I/O kernels the staging buffer's address is baked into the graph: one graph
+        # per bucket and buffer parity
+        return (bs, p) if self._gio else bs
+
     def _read_out(self, B: int, p: int, bs: int) -> "torch.cuda.Event":
-        n = bs + 1 if self.par.custom_ar is not None else B    # + the TP health vote at [bs]
-        self._out_bufs[p][:n].copy_(self.d_out[:n], non_blocking=True)
+        if not self._gio:           # else the step's last kernel (ops.step_store) wrote _out_bufs[p]
+            n = bs + 1 if self.par.custom_ar is not None else B    # + the TP health vote at [bs]
+            self._out_bufs[p][:n].copy_(self.d_out[:n], non_blocking=True)
         ev = self._out_evts[p]
         ev.record()
         return ev
@@ -1162,7 +1192,7 @@ class LLMEngine:
         pc = 0
         tp = self.par.enabled
         bsk = self._prep_decode(cur, lens, last, pc)
-        self._replay(bsk)
+        self._replay(bsk, pc)
         ev = self._read_out(len(cur), pc, bsk)
         vote = self.par.custom_ar is not None     # this step's tokens carry the health vote
         self.steps["decode"] += 1
@@ -1206,16 +1236,8 @@ class LLMEngine:
                     pn = pc ^ 1
                     B = len(run)
                     lens = np.fromiter((s.length + 1 for s in run), dtype=np.int64, count=B)
-                    bs = self._prep_decode(run, lens, None, pn)
-                    # input ids = the in-flight step's sampled tokens, gathered on the device
-                    if src == list(range(B)):
-                        self.d_ids[:B].copy_(self.d_out[:B])
-                    else:
-                        sb = self._src_bufs[pn]
-                        sb[:B] = torch.as_tensor(src, dtype=torch.int64)
-                        self.d_src[:B].copy_(sb[:B], non_blocking=True)
-                        self.d_ids[:B] = self.d_out[self.d_src[:B]]
-                    self._replay(bs)
+                    bs = self._prep_decode(run, lens, None, pn, src=src)
+                    self._replay(bs, pn)
                     launched = (run, pn, self._read_out(B, pn, bs), bs, self.par.custom_ar is not None)
                     self.steps["decode"] += 1
                     nsteps += 1
@@ -1223,6 +1245,8 @@ class LLMEngine:
                 self._early_admit(waiting, prefilling, len(cur))
             _t1 = time.perf_counter()
             ev.synchronize()
+            if self._sync_log is not None:   # diagnostics: how long the loop waited for the step
+                self._sync_log.append((_t1 - _t0, time.perf_counter() - _t1, launched is not None))
             toks = self._out_np[pc][:len(cur)].tolist()
             tripped = vote and bool(self._out_np[pc][bsk])
             if tripped:
@@ -1300,7 +1324,7 @@ class LLMEngine:
         lens = np.fromiter((s.length for s in cur), dtype=np.int64, count=B)
         last = np.fromiter((s.out[-1] for s in cur), dtype=np.int64, count=B)
         bs = self._prep_decode(cur, lens, last, p)
-        self._decode_forward(bs)
+        self._decode_forward(bs, p)
         return self.d_out[:B].tolist()
 
     def _complete_early(self, s: _Seq) -> None:
@@ -1393,11 +1417,20 @@ class LLMEngine:
                         last_idx=self.d_last[:bs], all_last=True, splits=self._decode_splits(bs), workspace=self.dec_ws,
                         split_len=self.d_split if self.ATTN_DYNAMIC else None)
 
-    def _decode_forward(self, bs: int) -> None:
+    def _decode_forward(self, bs: int, p: int = 0) -> None:
         with ops.gemm.workspace_owner(self._ws_owner):
-            self._decode_forward_inner(bs)
+            self._decode_forward_inner(bs, p)
 
-    def _decode_forward_inner(self, bs: int) -> None:
+    def _decode_forward_inner(self, bs: int, p: int = 0) -> None:
+        if self._gio:
+            o, mb = self._off, self.buckets[-1]
+            items = (self._items_bufs[p][0], self.items_dev) if self.attn_worklist else (None, None)
+            ops.step_fetch(self._dec_bufs[p][0], self.dec_dev, o[0], o[9], mb, self.d_out, *items)
+        self._decode_body(bs)
+        if self._gio:
+            ops.step_store(self.d_out, self._out_bufs[p], bs + 1)
+
+    def _decode_body(self, bs: int) -> None:
         # this step's block-table updates (inside the graph; the fused layer applies them in its
         # embedding launch)
         hid = self.model.hidden_states(self.d_ids[:bs], self.d_pos[:bs], self._decode_meta(bs), self.kv_caches,
@@ -1411,34 +1444,48 @@ class LLMEngine:
         self.d_hidden[:bs].copy_(hid)
         self.d_out[:bs].copy_(self.model.greedy(hid))
 
-    def _capture(self, bs: int) -> "torch.cuda.CUDAGraph":
-        # warm up (lazy library init must not happen inside capture), then capture
+    def _capture(self, bs: int, p: int = 0) -> "torch.cuda.CUDAGraph":
+        # warm up (lazy library init must not happen inside capture), then capture.  A graph
+        # captured lazily mid-burst warms up on the real step: with the id gather inside the step
+        # (step I/O kernels) the warm-up's sampler would overwrite the previous step's tokens the
+        # replay gathers its input ids from, so d_out is restored after it.
+        saved = self.d_out.clone() if self._gio else None
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            self._decode_forward(bs)
+            self._decode_forward(bs, p)
         torch.cuda.current_stream(self.device).wait_stream(s)
+        if saved is not None:
+            self.d_out.copy_(saved)
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self._graph_pool):
-            self._decode_forward(bs)
-        self._graphs[bs] = g
+            self._decode_forward(bs, p)
+        self._graphs[self._gkey(bs, p)] = g
         return g
 
     def capture_all(self, max_bs: Optional[int] = None) -> None:
         """Pre-capture decode graphs for every bucket up to ``max_bs`` (largest first)."""
         if not self.use_graphs:
             return
-        # a dummy decode state: all padding (qlen 0), so capture writes nothing to the KV cache
-        self.dec_host[:] = 0
-        self.dec_host[self._off[2]:self._off[3]] = -1
-        self.dec_host[self._off[3]:self._off[4]] = self.R
+        # a dummy decode state in both staging buffers: all padding (qlen 0), so the warm-up runs
+        # of the captures write nothing to the KV cache
+        o, mb = self._off, self.buckets[-1]
+        for _, h, _ in self._dec_bufs:
+            h[:] = 0
+            h[o[2]:o[3]] = -1
+            h[o[3]:o[4]] = self.R
+            h[o[9]:o[9] + mb] = -1
+        if self.attn_worklist:
+            for _, it in self._items_bufs:
+                it[:4] = 0
         self.dec_dev.copy_(self.dec_host_t)
         self._sync_bt()
         for b in sorted((b for b in self.buckets if max_bs is None or b <= max_bs), reverse=True):
-            if b not in self._graphs:
-                self._capture(b)
+            for p in ((0, 1) if self._gio else (0,)):
+                if self._gkey(b, p) not in self._graphs:
+                    self._capture(b, p)
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ outputs

@@ -505,6 +505,38 @@ def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tens
 from .gemm import autotune as gemm_autotune, linear, linear_swiglu, norm_linear  # noqa: E402
 
 
+def step_fetch(dec_host: torch.Tensor, dec_dev: torch.Tensor, ids_off: int, src_off: int, n_ids: int,
+               d_out: torch.Tensor, items_host: Optional[torch.Tensor] = None,
+               items_dev: Optional[torch.Tensor] = None) -> None:
+    """Decode-step inputs from a pinned host buffer into ``dec_dev`` by a kernel (graph-capturable,
+    no copy engine): ``dec_dev[:] = dec_host`` except ids ``[ids_off, ids_off + n_ids)``, which take
+    ``d_out[src[i]]`` where ``src[i] = dec_host[src_off + i] >= 0`` (the previous step's tokens);
+    and the work list ``items_dev <- items_host`` (its header's length)."""
+    ext = _native(dec_dev)
+    if ext is None:
+        h = dec_host.to(dec_dev.device)
+        src = h[src_off:src_off + n_ids].long()
+        ids = h[ids_off:ids_off + n_ids].clone()
+        m = (src >= 0) & (src < n_ids)
+        ids[m] = d_out[src[m]].to(ids.dtype)
+        dec_dev.copy_(h)
+        dec_dev[ids_off:ids_off + n_ids] = ids
+        if items_host is not None:
+            n = work_items_len(items_host.numpy())
+            items_dev[:n].copy_(items_host[:n])
+        return
+    ext.step_fetch(dec_host, dec_dev, int(ids_off), int(src_off), int(n_ids), d_out, items_host, items_dev)
+
+
+def step_store(d_out: torch.Tensor, out_host: torch.Tensor, n: int) -> None:
+    """``out_host[:n] = d_out[:n]`` by a kernel writing the pinned host buffer (graph-capturable)."""
+    ext = _native(d_out)
+    if ext is None:
+        out_host[:n].copy_(d_out[:n])
+        return
+    ext.step_store(d_out, out_host, int(n))
+
+
 def scatter_pairs(dst: torch.Tensor, buf: torch.Tensor) -> None:
     """dst.view(-1)[idx_i] = val_i for buf = [n, idx0, val0, idx1, val1, ...] (int32)."""
     ext = _native(dst)

@@ -41,6 +41,8 @@ def prepare(eng, B, C, base):
     pos = np.full(B, C - 1)
     blocks = eng.bt_host[rows, pos // 16]
     h[:] = 0
+    if len(o) > 9:
+        h[o[9]:o[9] + bs] = -1     # input ids from this buffer, not gathered from d_out
     h[o[0]:o[0] + B] = 7
     h[o[1]:o[1] + B] = pos
     h[o[2]:o[2] + bs] = -1
@@ -59,7 +61,7 @@ def prepare(eng, B, C, base):
                               seq=rows, qstart=np.arange(B))
         n = ops.work_items_len(items)
         eng.items_dev[:n].copy_(items_t[:n])
-    return eng._graphs.get(bs) or eng._capture(bs)
+    return eng._graphs.get(eng._gkey(bs, 0)) or eng._capture(bs, 0)
 
 
 def timed(fn, iters=20):

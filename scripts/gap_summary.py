@@ -17,19 +17,26 @@ def short(name: str) -> str:
 
 
 def main():
-    path = sys.argv[1]
+    # argv[1]: kernel-trace CSV, or several joined by commas (e.g. + the memory-copy trace: its
+    # rows are named by their direction, so SDMA copies show up between the kernels)
+    paths = sys.argv[1].split(",")
     skip = float(sys.argv[2]) if len(sys.argv) > 2 else 0.3
     rows = []
-    with open(path) as f:
+    for path in paths:
+      with open(path) as f:
         for r in csv.DictReader(f):
             k = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
+            if not k and (r.get("Direction") or r.get("Kind")):
+                k = "COPY " + (r.get("Direction") or r.get("Kind"))
             s = r.get("Start_Timestamp") or r.get("BeginNs") or r.get("Start")
             e = r.get("End_Timestamp") or r.get("EndNs") or r.get("End")
+            q = r.get("Stream_Id") or r.get("Queue_Id") or ""
             if k and s and e:
-                rows.append((int(s), int(e), short(k)))
+                rows.append((int(s), int(e), short(k) + (f" [q{q}]" if q else "")))
     rows.sort()
     t0, t1 = rows[0][0], max(e for _, e, _ in rows)
-    cut = t0 + skip * (t1 - t0)
+    # skip <= 1: fraction of the run to drop; skip > 1: keep only the last `skip` seconds
+    cut = t0 + skip * (t1 - t0) if skip <= 1 else t1 - int(skip * 1e9)
     rows = [r for r in rows if r[0] >= cut]
     busy, gaps = 0, defaultdict(lambda: [0, 0])
     cur_s, cur_e, cur_k = rows[0]
@@ -48,7 +55,8 @@ def main():
     busy += cur_e - cur_s
     span = cur_e - rows[0][0]
     idle = span - busy
-    print(f"window {span / 1e9:.3f} s (first {skip:.0%} of the run skipped): GPU busy {busy / 1e9:.3f} s "
+    what = f"first {skip:.0%} of the run skipped" if skip <= 1 else f"last {skip:g} s of the run"
+    print(f"window {span / 1e9:.3f} s ({what}): GPU busy {busy / 1e9:.3f} s "
           f"({100 * busy / span:.1f} %), idle {idle / 1e9:.3f} s\n")
     print("| gap size | idle s | share of idle |\n|---|---|---|")
     for b in ("<2us", "2-5us", "5-20us", "20-100us", ">=100us"):
@@ -64,6 +72,16 @@ def main():
     print("\n| idle ms | gaps | mean us | kernel before | kernel after |\n|---|---|---|---|---|")
     for (a, b), (g, n) in sorted(gaps.items(), key=lambda x: -x[1][0])[:25]:
         print(f"| {g / 1e6:.1f} | {n} | {g / n / 1e3:.1f} | `{a}` | `{b}` |")
+    # the neighbourhood of the first mid-size (100-400 us) idle gap in the second half of the window
+    prev_e = rows[0][1]
+    for i in range(len(rows) // 2, len(rows)):
+        g = rows[i][0] - max(e for _, e, _ in rows[max(0, i - 8):i]) if i > 0 else 0
+        if 100_000 <= g <= 400_000:
+            print(f"\nAround a {g / 1e3:.0f} us gap (us relative to the row after it):\n")
+            print("| t | dur | kernel |\n|---|---|---|")
+            for s_, e_, k in rows[max(0, i - 25):i + 12]:
+                print(f"| {(s_ - rows[i][0]) / 1e3:.1f} | {(e_ - s_) / 1e3:.1f} | `{k}` |")
+            break
     # a timeline excerpt from the middle of the window: what runs between two idle gaps
     mid = len(rows) // 2
     print("\nTimeline excerpt (us from the first row; gap = idle before the row):\n")

@@ -146,6 +146,8 @@ def bench_decode(eng, B, C):
     pos = np.full(B, C - 1)
     blocks = eng.bt_host[rows, pos // 16]
     h[:] = 0
+    if len(o) > 9:
+        h[o[9]:o[9] + bs] = -1     # input ids from this buffer, not gathered from d_out
     h[o[0]:o[0] + B] = 7
     h[o[1]:o[1] + B] = pos
     h[o[2]:o[2] + bs] = -1
@@ -166,7 +168,7 @@ def bench_decode(eng, B, C):
                               seq=rows, qstart=np.arange(B))
         n_items = ops.work_items_len(items)
         eng.items_dev[:n_items].copy_(items_t[:n_items])
-    g = eng._graphs.get(bs) or eng._capture(bs)
+    g = eng._graphs.get(eng._gkey(bs, 0)) or eng._capture(bs, 0)
     ms = timeit(g.replay)
     wbytes = eng.model.weight_bytes()
     kv = B * C * eng.cfg.n_layers * eng.model.nkv * eng.model.d * 2 * 2

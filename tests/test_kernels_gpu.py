@@ -446,6 +446,37 @@ def test_embedding(H, lo, rows):
     assert torch.isnan(ssq[257:]).all()
 
 
+@pytest.mark.parametrize("n_ids,ext", [(8, True), (512, True), (64, False)])
+def test_step_fetch_and_store(n_ids, ext):
+    """Decode-step I/O kernels on device-mapped pinned buffers: dec_dev <- dec_host with the ids
+    region taken from d_out where src >= 0; the work list copied as far as its header says; the
+    sampled tokens written back to pinned memory."""
+    torch.manual_seed(n_ids)
+    n_dec, ids_off, src_off = 3 * n_ids + 100, 0, 2 * n_ids + 50
+    dec_host = torch.randint(-5, 1000, (n_dec,), dtype=torch.int32).pin_memory()
+    src = torch.randint(-1, n_ids, (n_ids,), dtype=torch.int32)
+    dec_host[src_off:src_off + n_ids] = src
+    d_out = torch.randint(0, 32000, (n_ids + 1,), dtype=torch.int32, device=DEV)
+    dec_dev = torch.full((n_dec,), -7, dtype=torch.int32, device=DEV)
+    items_host = torch.randint(0, 99, (4 + 4 * 40,), dtype=torch.int32).pin_memory()
+    items_host[0] = -13 if ext else 21           # extended list: 4 + 4 * 13 words; plain: 1 + 2 * 21
+    items_dev = torch.full((items_host.numel(),), -9, dtype=torch.int32, device=DEV)
+    ops.step_fetch(dec_host, dec_dev, ids_off, src_off, n_ids, d_out, items_host, items_dev)
+    want = dec_host.clone()
+    ids = want[ids_off:ids_off + n_ids]
+    m = src >= 0
+    ids[m] = d_out.cpu()[src[m].long()]
+    torch.cuda.synchronize()
+    assert torch.equal(dec_dev.cpu(), want)
+    n_it = 4 + 4 * 13 if ext else 1 + 2 * 21
+    assert torch.equal(items_dev.cpu()[:n_it], items_host[:n_it])
+    assert (items_dev.cpu()[n_it:] == -9).all()
+    out_host = torch.zeros(n_ids + 1, dtype=torch.int32).pin_memory()
+    ops.step_store(d_out, out_host, n_ids + 1)
+    torch.cuda.synchronize()
+    assert torch.equal(out_host, d_out.cpu())
+
+
 @pytest.mark.parametrize("T,n", [(1, 0), (1, 3), (8, 17), (512, 300)])
 def test_embedding_with_block_table_scatter(T, n):
     """The decode step's block-table updates ride in the embedding launch (one extra workgroup):
