@@ -90,6 +90,9 @@ def parse():
                          "the flagship: 57.0 / 59.7k off vs 59.3 / 59.0k on, one box)")
     ap.add_argument("--gil-switch-ms", type=float, default=0.5,
                     help="turn pipelining: Python thread switch interval (sys.setswitchinterval) in ms")
+    ap.add_argument("--yield-to-engine", type=int, default=0,
+                    help="turn pipelining (--pipeline 2): the routing driver holds off while an engine's "
+                         "step loop is at a burst boundary (LLMEngine.host_critical); 0: never")
     ap.add_argument("--admit-every", type=int, default=16,
                     help="turn pipelining: the engine admits new turns every N decode steps of a burst")
     ap.add_argument("--no-encoder-memo", action="store_true",
@@ -265,6 +268,15 @@ class PipelinedConversations(Conversations):
             t.join()
 
 
+def _yield_to_engines(engines, max_s: float = 0.02) -> None:
+    """The routing driver holds off while an engine's step loop is at a burst boundary
+    (``LLMEngine.host_critical``): there the GPU waits for that loop's host work, and both threads
+    would otherwise share the GIL in 0.5 ms slices.  Bounded, so routing never starves."""
+    t0 = time.perf_counter()
+    while any(e.host_critical.is_set() for e in engines) and time.perf_counter() - t0 < max_s:
+        time.sleep(0.0002)
+
+
 class EventConversations(PipelinedConversations):
     """Turn pipelining from ONE driver thread (``--pipeline 2``): every conversation whose answer
     has arrived is routed (one batched decision pass for all of them, ``Router.dispatch_batch``)
@@ -290,8 +302,10 @@ class EventConversations(PipelinedConversations):
                 _router_stream()
                 ready = list(range(len(self.convs)))
                 inflight = {}
+                engines = getattr(self, "engines", None) or []
                 while not self._stop:
                     if ready:
+                        _yield_to_engines(engines)
                         hs = []
                         for i in ready:
                             c = self.convs[i]
@@ -309,6 +323,7 @@ class EventConversations(PipelinedConversations):
                         continue
                     recs = []
                     for i in done:
+                        _yield_to_engines(engines)
                         payload, ntok, device = router.finish_ticket(inflight.pop(i))
                         c = self.convs[i]
                         c["hist"].append({"role": "assistant", "content": payload["response"]})
@@ -575,6 +590,8 @@ def main() -> int:
             convs = (GroupedConversations(n_convs, rank, a.groups) if a.groups > 1
                      else EventConversations(n_convs, rank) if a.pipeline == 2
                      else PipelinedConversations(n_convs, rank))
+            if a.yield_to_engine:
+                convs.engines = engines
             convs.start(router)
             convs.wait_turns(a.warmup * n_convs)
         else:
@@ -702,6 +719,7 @@ def main() -> int:
                        "admit_every": a.admit_every if (a.pipeline or a.groups > 1) else None,
                        "gc_freeze": bool(a.gc_freeze),
                        "gil_switch_ms": a.gil_switch_ms if (a.pipeline or a.groups > 1) else None,
+                       "yield_to_engine": bool(a.yield_to_engine) if a.pipeline == 2 else None,
                        "early_prefill": os.environ.get("DLLM_EARLY_PREFILL", "1") == "1",
                        "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},

@@ -136,6 +136,12 @@ class LLMEngine:
         self._inbox: List[_Seq] = []            # submitted, not yet seen by the driver
         self._inbox_lock = threading.Lock()
         self._inbox_cv = threading.Condition(self._inbox_lock)
+        # Set from the moment a pipelined burst decides to end until the next decode step is on
+        # the GPU: the step loop's host work (drain, release, admission, staging) is then all that
+        # stands between the GPU and its next work, so an in-process client thread (the bench's
+        # routing driver) can hold off its own Python work meanwhile instead of contending for the
+        # GIL (profiles/r4_driver_window_gaps.md).
+        self.host_critical = threading.Event()
         self._driving = False
         self._bg: Optional[threading.Thread] = None   # background step-loop thread (start())
         self._bg_stop = False
@@ -456,6 +462,7 @@ class LLMEngine:
                 s.done.set()
         self._active = []
         self._early_pf = None
+        self.host_critical.clear()
         self._bt_dirty = True
 
     # TP mirror: admissions are exchanged every MIRROR_EVERY scheduler iterations (and whenever the
@@ -616,6 +623,7 @@ class LLMEngine:
             waiting.extend(self._take_inbox(final=not (waiting or prefilling or running)))
             self._active = waiting + prefilling + running
             if not (waiting or prefilling or running):
+                self.host_critical.clear()
                 break
             # admit
             self._admit(waiting, prefilling, len(running))
@@ -1193,6 +1201,7 @@ class LLMEngine:
         tp = self.par.enabled
         bsk = self._prep_decode(cur, lens, last, pc)
         self._replay(bsk, pc)
+        self.host_critical.clear()
         ev = self._read_out(len(cur), pc, bsk)
         vote = self.par.custom_ar is not None     # this step's tokens carry the health vote
         self.steps["decode"] += 1
@@ -1241,8 +1250,10 @@ class LLMEngine:
                     launched = (run, pn, self._read_out(B, pn, bs), bs, self.par.custom_ar is not None)
                     self.steps["decode"] += 1
                     nsteps += 1
-            if launched is None and stop and self._inbox:
-                self._early_admit(waiting, prefilling, len(cur))
+            if launched is None:
+                self.host_critical.set()      # until the next burst's first step is launched
+                if stop and self._inbox:
+                    self._early_admit(waiting, prefilling, len(cur))
             _t1 = time.perf_counter()
             ev.synchronize()
             if self._sync_log is not None:   # diagnostics: how long the loop waited for the step
