@@ -89,6 +89,7 @@ class _Seq:
     error: Optional[str] = None
     done: threading.Event = field(default_factory=threading.Event)
     out_text: Optional[str] = None   # detokenised answer, formed as soon as the sequence stops
+    released: bool = False           # blocks and row returned (_release)
 
     @property
     def length(self) -> int:
@@ -194,6 +195,8 @@ class LLMEngine:
         self._h2d_ring = None                                 # small pinned copies (_small_h2d)
         self._h2d_i = 0
         self._early_pf = None      # a prefill chunk queued under the last step of a decode burst
+        self._pf_tok: Optional[torch.Tensor] = None   # pinned first tokens of a prefill chunk
+        self._in_join_burst = False
         # DLLM_SYNC_LOG=1: per pipelined step (host prep s, wait for the in-flight step s, launched)
         self._sync_log: Optional[list] = [] if os.environ.get("DLLM_SYNC_LOG", "0") == "1" else None
         pin = self.on_gpu
@@ -707,6 +710,9 @@ class LLMEngine:
         return s.length >= self.max_model_len
 
     def _release(self, s: _Seq, keep: bool = True) -> None:
+        if s.released:              # already released inside a decode burst (BURST_JOIN)
+            return
+        s.released = keep
         if keep:
             if s.finished is None:    # _complete_early may have set it when the row stopped
                 s.finished = time.perf_counter()
@@ -741,7 +747,20 @@ class LLMEngine:
             cols = np.asarray(self._bt_upd[0::2], dtype=np.int64) % self.max_blocks
             self._bt_hw = max(self._bt_hw, int(cols.max()) + 1)
 
-    def _sync_bt(self) -> None:
+    def _sync_bt(self, non_blocking: bool = False) -> None:
+        """Host block table -> device (the columns any row has used) when admissions / releases
+        changed it.  ``non_blocking`` (inside a decode burst that admits, BURST_JOIN): an async
+        copy from the pinned mirror, stream-ordered before the next step; the host may rewrite a
+        row before the copy runs only by admitting into it (which queues another copy) or by
+        opening a new block (which the step's in-graph scatter applies as well)."""
+        if self._bt_dirty and non_blocking:
+            self._note_upd_cols()
+            hw = min(self._bt_hw, self.max_blocks)
+            if hw > 0:
+                self.bt_dev[:, :hw].copy_(self.bt_host_t[:, :hw], non_blocking=True)
+            self._bt_dirty = False
+            self._bt_upd.clear()
+            return
         if self._bt_dirty:
             # rare (admission / release): synchronous copy of the columns any row has used (a 128K
             # context table is 8K columns; a 2K-token batch needs 128 of them), which also subsumes
@@ -820,7 +839,11 @@ class LLMEngine:
 
     def _prefill_finish(self, handle: tuple) -> List[_Seq]:
         done_seqs, toks = handle
-        if torch.is_tensor(toks):
+        if isinstance(toks, tuple):       # (pinned tokens, event): wait for the chunk only
+            buf, ev = toks
+            ev.synchronize()
+            toks = buf.numpy()[:len(done_seqs)].tolist()
+        elif torch.is_tensor(toks):
             toks = toks.tolist()          # the fused sampler's device output: waits for the chunk
         now = time.perf_counter()
         for s, tok in zip(done_seqs, toks):
@@ -895,7 +918,18 @@ class LLMEngine:
             sel_a = np.asarray(sel, dtype=np.int32)
             sel_d = self._small_h2d(sel_a) if self.on_gpu else torch.from_numpy(sel_a)
             h = hidden.index_select(0, sel_d.to(torch.int64))
-        return done_seqs, self._sample(h, done_seqs, None, launch_only=True)
+        toks = self._sample(h, done_seqs, None, launch_only=True)
+        if self.on_gpu and torch.is_tensor(toks):
+            # first tokens to pinned memory + an event: the host reads them once the chunk is done
+            # without synchronising the stream (decode steps may be queued behind the chunk)
+            n = len(done_seqs)
+            if self._pf_tok is None or self._pf_tok.numel() < n:
+                self._pf_tok = torch.empty(max(n, self.R), dtype=torch.int32, pin_memory=True)
+            self._pf_tok[:n].copy_(toks[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            return done_seqs, (self._pf_tok, ev)
+        return done_seqs, toks
 
     def _small_h2d(self, a: np.ndarray) -> torch.Tensor:
         """A few KB of int32 to the device without a host stall: through a ring of 4 pinned slots
@@ -1005,7 +1039,7 @@ class LLMEngine:
         h[o[4] + rows] = np.arange(B)
         h[o[5] + rows] = 1
         h[o[6] + rows] = lens
-        self._sync_bt()
+        self._sync_bt(non_blocking=self._in_join_burst)
         h[o[7]] = self._split_len(int(lens.sum()))
         if self.fused_sampler:
             self._fill_sampler(h, hf, self._so, self.buckets[-1], running, bs)
@@ -1182,6 +1216,45 @@ class LLMEngine:
                 self._early_pf = self._prefill_launch(prefilling)
         self.timers["prefill"] += time.perf_counter() - _t
 
+    # BURST_JOIN: a pipelined burst no longer ends for admissions.  New requests are admitted and
+    # prefilled under the running burst (EARLY_PREFILL), their sequences JOIN the next step once
+    # the chunk's first tokens are back, and a finished sequence's blocks and row are released one
+    # step after it stopped (when no in-flight step can still write its reserved slot), so rows
+    # recycle without a drain.  Needs the step I/O kernels (per-row input ids from the host next to
+    # gathered ones); single-GPU pools only.
+    BURST_JOIN = os.environ.get("DLLM_BURST_JOIN", "1") == "1"
+
+    def _take_joiners(self, prefilling: List[_Seq], running: List[_Seq], finished: List[_Seq],
+                      preempted: List[_Seq]) -> List[_Seq]:
+        """Sequences whose early prefill chunk has completed (checked without waiting): their first
+        token is appended; those that continue join the next decode step."""
+        h = self._early_pf
+        if h is None:
+            return []
+        toks = h[1]
+        if isinstance(toks, tuple) and not toks[1].query():
+            return []
+        _t = time.perf_counter()
+        self._early_pf = None
+        done = self._prefill_finish(h)
+        joiners = []
+        for s in done:
+            prefilling.remove(s)
+            if self._finished(s):     # stopped on its first token: no step ever carries its row
+                finished.append(s)
+                self._complete_early(s)
+                self._release(s)
+            elif s.error == "__preempt__":
+                preempted.append(s)
+            else:
+                joiners.append(s)
+                running.append(s)
+        self.steps["burst_joins"] = self.steps.get("burst_joins", 0) + len(joiners)
+        if prefilling and self._early_pf is None:     # chunk budget left some prompts unfinished
+            self._early_pf = self._prefill_launch(prefilling)
+        self.timers["prefill"] += time.perf_counter() - _t
+        return joiners
+
     def _decode_burst(self, running: List[_Seq], waiting: List[_Seq],
                       prefilling: Optional[List[_Seq]] = None) -> Tuple[List[_Seq], List[_Seq]]:
         """Pipelined decode steps until the batch must change (a new request arrived, a waiting
@@ -1193,12 +1266,17 @@ class LLMEngine:
         finished: List[_Seq] = []
         preempted: List[_Seq] = []
         gone: set = set()           # id(s): finished / preempted inside this burst (rows still in flight are ignored)
+        tp = self.par.enabled
+        join = (prefilling is not None and self.BURST_JOIN and self._gio and self.EARLY_PREFILL and not tp
+                and self._mirror is None and self.fused_sampler)
+        self._in_join_burst = join
+        release_next: List[_Seq] = []   # stopped in the step just read back: released after the next one
+        admit_at = 0                    # step count of the last in-burst admission
         _t0 = time.perf_counter()
         cur = list(running)
         lens = np.fromiter((s.length for s in cur), dtype=np.int64, count=len(cur))
         last = np.fromiter((s.out[-1] for s in cur), dtype=np.int64, count=len(cur))
         pc = 0
-        tp = self.par.enabled
         bsk = self._prep_decode(cur, lens, last, pc)
         self._replay(bsk, pc)
         self.host_critical.clear()
@@ -1213,12 +1291,20 @@ class LLMEngine:
             alive = [s for s in cur if id(s) not in gone]
             # the next step's rows: sequences that cannot reach a count limit with the token in flight
             nxt = [s for s in alive if len(s.out) + 1 < s.params.max_new_tokens and s.length + 1 < mml]
-            stop = (not nxt or freed
-                    or (nsteps >= self.MIRROR_EVERY if self._mirror is not None
-                        else (bool(self._inbox) and nsteps >= self.ADMIT_EVERY))
-                    or (bool(waiting) and len(nxt) < len(alive)))
+            joiners = self._take_joiners(prefilling, running, finished, preempted) if join else []
+            if join:
+                stop = (not nxt and not joiners and self._early_pf is None) or bool(preempted)
+            else:
+                stop = (not nxt or freed
+                        or (nsteps >= self.MIRROR_EVERY if self._mirror is not None
+                            else (bool(self._inbox) and nsteps >= self.ADMIT_EVERY))
+                        or (bool(waiting) and len(nxt) < len(alive)))
             launched = None
             pending_pre: set = set()
+            if stop and joiners:
+                # a preemption ends the burst: the joiners' first tokens are appended with slots,
+                # so they are plain running sequences for the caller
+                joiners = []
             if not stop:
                 # commit the in-flight step's input tokens (all alive rows) and reserve the slot of
                 # the token each continuing row is sampling right now (placeholder, fixed in post)
@@ -1241,15 +1327,28 @@ class LLMEngine:
                             self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
                     run.append(s)
                     src.append(idx[id(s)])
+                n_cont = len(run)
+                for s in joiners:           # input token known on the host (the chunk's first token)
+                    run.append(s)
+                    src.append(-1)
                 if run:
                     pn = pc ^ 1
                     B = len(run)
-                    lens = np.fromiter((s.length + 1 for s in run), dtype=np.int64, count=B)
-                    bs = self._prep_decode(run, lens, None, pn, src=src)
+                    lens = np.fromiter((s.length + (1 if i < n_cont else 0) for i, s in enumerate(run)),
+                                       dtype=np.int64, count=B)
+                    last_j = None
+                    if joiners:
+                        last_j = np.zeros(B, dtype=np.int64)
+                        last_j[n_cont:] = [s.out[-1] for s in joiners]
+                    bs = self._prep_decode(run, lens, last_j, pn, src=src)
                     self._replay(bs, pn)
                     launched = (run, pn, self._read_out(B, pn, bs), bs, self.par.custom_ar is not None)
                     self.steps["decode"] += 1
                     nsteps += 1
+                if (join and (self._inbox or waiting) and self._early_pf is None
+                        and nsteps - admit_at >= self.ADMIT_EVERY):
+                    admit_at = nsteps
+                    self._early_admit(waiting, prefilling, len(run))
             if launched is None:
                 self.host_critical.set()      # until the next burst's first step is launched
                 if stop and self._inbox:
@@ -1258,6 +1357,12 @@ class LLMEngine:
             ev.synchronize()
             if self._sync_log is not None:   # diagnostics: how long the loop waited for the step
                 self._sync_log.append((_t1 - _t0, time.perf_counter() - _t1, launched is not None))
+            if release_next:
+                # stopped in the previous read-back: the step that may have carried their row
+                # (launched before they were seen to stop) has now completed
+                for s in release_next:
+                    self._release(s)
+                release_next = []
             toks = self._out_np[pc][:len(cur)].tolist()
             tripped = vote and bool(self._out_np[pc][bsk])
             if tripped:
@@ -1312,6 +1417,7 @@ class LLMEngine:
             if launched is None or tripped:
                 if tp and self._mirror is not None:
                     self._mirror_iter += nsteps - 1    # admission polls stay ~MIRROR_EVERY steps apart
+                self._in_join_burst = False
                 return finished, preempted
             if done_now:
                 # the next step is already on the GPU: detokenise the stopped answers under it and
@@ -1323,6 +1429,8 @@ class LLMEngine:
                 for s in done_now:
                     self._complete_early(s)
                 self.timers["output"] += time.perf_counter() - _t3
+                if join:
+                    release_next.extend(done_now)
             freed = bool(waiting) and bool(done_now or preempted)
             cur, pc, ev, bsk, vote = launched
 

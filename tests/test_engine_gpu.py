@@ -92,6 +92,7 @@ def test_pipelined_decode_matches_stepwise(monkeypatch):
     """Pipelined decode (one step of host lookahead, tokens gathered on the device) gives the
     same tokens as the step-by-step loop: mixed max_new_tokens (count limits are predicted),
     more requests than rows (admissions between bursts), greedy and seeded sampling."""
+    monkeypatch.setattr(LLMEngine, "BURST_JOIN", False)   # the drained-burst schedule is what matches stepwise
     sps = [SamplingParams(max_new_tokens=3 + 5 * (i % 4), ignore_eos=True, temperature=0.0 if i % 3 else 0.8,
                           top_k=40, top_p=0.9) for i in range(12)]
     a = [o.token_ids for o in _engine(max_num_seqs=4).generate(PROMPTS12, sps)]
@@ -104,6 +105,7 @@ def test_pipelined_decode_matches_stepwise(monkeypatch):
 def test_pipelined_decode_preemption_matches_stepwise(monkeypatch):
     """Out of KV blocks mid-decode: the pipelined loop preempts the same sequences (slot
     reservation fails at the look-ahead commit) and the outputs match the step-by-step loop."""
+    monkeypatch.setattr(LLMEngine, "BURST_JOIN", False)   # the drained-burst schedule is what matches stepwise
     sp = SamplingParams(max_new_tokens=40, ignore_eos=True)
     prompts = ["user: " + "word " * 30 + str(i) for i in range(6)]
 
@@ -122,6 +124,7 @@ def test_pipelined_decode_eos_zombie_rows(monkeypatch):
     """A sequence that samples EOS is already in the next launched step: that row is discarded.
     Outputs equal the step-by-step loop up to the first EOS step of the batch, end at EOS, and the
     engine's block accounting is clean afterwards."""
+    monkeypatch.setattr(LLMEngine, "BURST_JOIN", False)   # the drained-burst schedule is what matches stepwise
     sp = SamplingParams(max_new_tokens=24, ignore_eos=True)
     probe = [o.token_ids for o in _engine().generate(PROMPTS, sp)]
     # an EOS id that some sequences emit early and others late or never
@@ -151,6 +154,7 @@ def test_pipelined_decode_eos_zombie_rows(monkeypatch):
 def test_pipelined_text_and_turn_memo_match_stepwise(monkeypatch):
     """Answers detokenised inside the pipelined burst (under the next GPU step) give the same text
     as the step-by-step loop, and the memoised prompt+answer ids make turn 2 a prefix-cache hit."""
+    monkeypatch.setattr(LLMEngine, "BURST_JOIN", False)   # the drained-burst schedule is what matches stepwise
     sps = [SamplingParams(max_new_tokens=6 + 4 * (i % 3), ignore_eos=True) for i in range(len(PROMPTS))]
 
     def two_turns():
@@ -194,3 +198,48 @@ def test_pipelined_short_request_completes_before_long_one():
     finally:
         e.stop()
     assert e.bm.check_invariants() == "" and e.bm.stats()["active_seqs"] == 0
+
+
+def test_burst_join_matches_drained_bursts(monkeypatch):
+    """BURST_JOIN: requests admitted and prefilled under a running burst join it without a drain,
+    and finished rows are released one step later.  Greedy outputs equal the drained-burst
+    schedule's (a row's decode numerics do not depend on the rest of the batch), every request gets
+    its token count, joins happened, and the block accounting is clean."""
+    sps = [SamplingParams(max_new_tokens=3 + 5 * (i % 4), ignore_eos=True) for i in range(12)]
+    monkeypatch.setattr(LLMEngine, "ADMIT_EVERY", 2)
+    e = _engine(max_num_seqs=4)
+    a = [o.token_ids for o in e.generate(PROMPTS12, sps)]
+    assert e.steps.get("burst_joins", 0) > 0
+    assert e.bm.check_invariants() == "" and e.bm.stats()["active_seqs"] == 0
+    assert [len(x) for x in a] == [sp.max_new_tokens for sp in sps]
+    monkeypatch.setattr(LLMEngine, "BURST_JOIN", False)
+    b = [o.token_ids for o in _engine(max_num_seqs=4).generate(PROMPTS12, sps)]
+    assert a == b
+
+
+def test_burst_join_background_loop_under_load():
+    """Background step loop with requests arriving while bursts run (turn pipelining): every
+    request completes with its count, none errors, rows and blocks all come back."""
+    import threading
+    e = _engine(max_num_seqs=6).start()
+    outs = []
+    lock = threading.Lock()
+    try:
+        def client(k):
+            for t in range(3):
+                o = e.generate([PROMPTS12[(k + t) % 12]], SamplingParams(max_new_tokens=4 + (k + t) % 7,
+                                                                        ignore_eos=True))[0]
+                with lock:
+                    outs.append((4 + (k + t) % 7, o))
+
+        ts = [threading.Thread(target=client, args=(k,)) for k in range(10)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+    finally:
+        e.stop()
+    assert len(outs) == 30
+    assert all(o.error is None and o.num_generated == n for n, o in outs)
+    assert e.bm.check_invariants() == "" and e.bm.stats()["active_seqs"] == 0
+    assert sorted(e._free_rows) == list(range(e.R))
