@@ -1207,6 +1207,8 @@ class LLMEngine:
                 or not self.fused_sampler):
             return
         _t = time.perf_counter()
+        crit = self.host_critical.is_set()
+        self.host_critical.set()          # admission host work: in-process clients hold off (bench)
         new = self._take_inbox(final=False)
         self._active.extend(new)          # a failing step must still find them (_abort_all)
         waiting.extend(new)
@@ -1214,6 +1216,8 @@ class LLMEngine:
         if prefilling:
             with tracer.span("engine.prefill_early", "engine", seqs=len(prefilling)):
                 self._early_pf = self._prefill_launch(prefilling)
+        if not crit:
+            self.host_critical.clear()
         self.timers["prefill"] += time.perf_counter() - _t
 
     # BURST_JOIN: a pipelined burst no longer ends for admissions.  New requests are admitted and
@@ -1235,6 +1239,8 @@ class LLMEngine:
         if isinstance(toks, tuple) and not toks[1].query():
             return []
         _t = time.perf_counter()
+        crit = self.host_critical.is_set()
+        self.host_critical.set()
         self._early_pf = None
         done = self._prefill_finish(h)
         joiners = []
@@ -1252,6 +1258,8 @@ class LLMEngine:
         self.steps["burst_joins"] = self.steps.get("burst_joins", 0) + len(joiners)
         if prefilling and self._early_pf is None:     # chunk budget left some prompts unfinished
             self._early_pf = self._prefill_launch(prefilling)
+        if not crit:
+            self.host_critical.clear()
         self.timers["prefill"] += time.perf_counter() - _t
         return joiners
 
