@@ -68,7 +68,7 @@ int dllm_qkv_post(const void*, long, const float*, int, long, float, float, cons
                   void*, void*, int, int, int, int, hipStream_t);
 int dllm_swiglu_post(const void*, long, const float*, int, long, float, float, void*, long, int, int, hipStream_t);
 int dllm_flash_prefill(const void*, const void*, const void*, const int*, const int*, const int*, const int*, const int*,
-                       const int*, void*, int, int, int, int, int, int, float, hipStream_t);
+                       const int*, void*, int, int, int, int, int, int, float, int, float*, float*, int*, hipStream_t);
 int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
                               unsigned long long*, hipStream_t);
 }
@@ -224,7 +224,9 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
 // staged once per workgroup in LDS.  tile_seq/tile_tok0 hold 256 / G tokens per tile.
 void flash_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor block_tables,
                    torch::Tensor qstart, torch::Tensor qlen, torch::Tensor ctx, torch::Tensor tile_seq,
-                   torch::Tensor tile_tok0, torch::Tensor out, bool causal, double scale) {
+                   torch::Tensor tile_tok0, torch::Tensor out, bool causal, double scale, int64_t splits,
+                   c10::optional<torch::Tensor> part_o, c10::optional<torch::Tensor> part_ml,
+                   c10::optional<torch::Tensor> counters) {
   check_bf16(q, "q");
   check_bf16(kc, "k_cache");
   check_bf16(vc, "v_cache");
@@ -242,10 +244,27 @@ void flash_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::T
   const int S = block_tables.size(0);
   TORCH_CHECK(qstart.numel() == S && qlen.numel() == S && ctx.numel() == S, "seq metadata len");
   TORCH_CHECK(tile_tok0.numel() == tile_seq.numel(), "tile metadata len");
+  float* po = nullptr;
+  float* pml = nullptr;
+  int* cnt = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(splits <= 16 && part_o.has_value() && part_ml.has_value() && counters.has_value(),
+                "flash_prefill: split-KV needs part_o / part_ml / counters, splits <= 16");
+    const long units = (long)tile_seq.numel() * nkv * splits;
+    check_f32(*part_o, "part_o");
+    check_f32(*part_ml, "part_ml");
+    check_i32(*counters, "counters");
+    TORCH_CHECK(part_o->numel() >= units * 256 * d && part_ml->numel() >= units * 256 * 4 &&
+                    counters->numel() >= (long)tile_seq.numel() * nkv,
+                "flash_prefill: split-KV workspace too small");
+    po = part_o->data_ptr<float>();
+    pml = part_ml->data_ptr<float>();
+    cnt = counters->data_ptr<int>();
+  }
   ok(dllm_flash_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(), qstart.data_ptr<int>(),
                         qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(), tile_tok0.data_ptr<int>(),
                         out.data_ptr(), tile_seq.numel(), nq, nkv, d, block_tables.size(1), causal ? 1 : 0,
-                        (float)scale, stream()),
+                        (float)scale, (int)std::max<int64_t>(1, splits), po, pml, cnt, stream()),
      "flash_prefill");
 }
 
@@ -1042,7 +1061,10 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("rope_kv", &rope_kv);
   m.def("kv_write", &kv_write);
   m.def("paged_attention", &paged_attention);
-  m.def("flash_prefill", &flash_prefill);
+  m.def("flash_prefill", &flash_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
+        py::arg("qstart"), py::arg("qlen"), py::arg("ctx"), py::arg("tile_seq"), py::arg("tile_tok0"), py::arg("out"),
+        py::arg("causal"), py::arg("scale"), py::arg("splits") = 1, py::arg("part_o") = py::none(),
+        py::arg("part_ml") = py::none(), py::arg("counters") = py::none());
   m.def("silu_mul", &silu_mul);
   m.def("embed", &embed, py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("lo"), py::arg("ssq") = py::none(),
         py::arg("sc_dst") = py::none(), py::arg("sc_buf") = py::none());

@@ -53,6 +53,13 @@ struct FlashArgs {
   u16* out;
   int nq, nkv, G, max_blocks, causal, num_tiles;
   float scale_log2;
+  // split-KV (splits > 1, for grids that would leave CUs idle: short prompts): the chunks of a
+  // tile's key range are dealt to `splits` workgroups; each writes its unnormalised O and (m, l)
+  // per row write-through, takes a ticket, and the LAST one combines (common.h R1 hand-off)
+  int splits;
+  float* part_o;    // [num_tiles * nkv * splits, ROWS, D]
+  float* part_ml;   // [num_tiles * nkv * splits, ROWS, 4]: m (raw score units), l, -, -
+  int* counters;    // [num_tiles * nkv], zero at launch (memset by the launcher), re-armed by the last
 };
 
 template <int N>
@@ -109,7 +116,7 @@ __device__ __forceinline__ void pv_chunk(f32x16 (&acc)[NB], const unsigned char*
 // wave's MFMA pipe works on P.V(t-1) while its VALU computes exp2 of chunk t (in the plain loop
 // every MFMA of a chunk waits on that chunk's softmax).  The ring grows to 4 stages so chunk t-1's
 // V^T stays resident while chunk t+2 is staged.
-template <int D, int MINW, bool PIPE>
+template <int D, int MINW, bool PIPE, bool SPLIT = false>
 __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   constexpr int KD = D / 16;            // k-steps of S^T
   constexpr int NB = D / 32;            // 32-dim blocks of O^T
@@ -129,7 +136,10 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, rl = lane & 31;
   const int kvh = blockIdx.x % a.nkv;
-  const int tile = a.num_tiles - 1 - (int)(blockIdx.x / a.nkv);
+  const int rest = (int)(blockIdx.x / a.nkv);
+  const int nsp = SPLIT ? a.splits : 1;
+  const int split = SPLIT ? rest % nsp : 0;
+  const int tile = a.num_tiles - 1 - rest / nsp;
   const int seq = a.tile_seq[tile];
   if (seq < 0) return;  // uniform
   const int G = a.G, tpt = ROWS / G;
@@ -138,7 +148,13 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   const int last_tok = min(tok0 + tpt, qlen) - 1;
   if (last_tok < tok0) return;
   const int kmax = a.causal ? ctx - qlen + last_tok + 1 : ctx;
-  const int nchunks = (kmax + CK - 1) / CK;
+  const int nchunks_all = (kmax + CK - 1) / CK;
+  // this workgroup's chunks [c0, c1): per = ceil(chunks / splits), n_split non-empty splits
+  const int per = (nchunks_all + nsp - 1) / nsp;
+  const int n_split = per > 0 ? (nchunks_all + per - 1) / per : 1;
+  if (split >= n_split) return;  // uniform: a short tile needs fewer splits
+  const int c0 = split * per, c1 = min(nchunks_all, c0 + per);
+  const int nchunks = c1;
   const int* bt = a.block_tables + (long)seq * a.max_blocks;
   const int nbt = min((kmax + 15) / 16, a.max_blocks);
   for (int i = threadIdx.x; i < nbt; i += 64 * NWAVES) s_bt[i] = bt[i];
@@ -200,7 +216,7 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
 
 #pragma unroll
   for (int t = 0; t < STAGES - 1; ++t)
-    if (t < nchunks) issue(t);
+    if (c0 + t < nchunks) issue(c0 + t);
 
   // PIPE: the previous chunk's P and V^T stage, not yet multiplied into O.  Before the first chunk
   // they are zeros (P = 0 against an all-zero V^T image: adds exactly 0), so the in-loop P.V needs no
@@ -215,7 +231,7 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) pf_prev[i][j] = (__bf16)0.f;
   }
-  for (int t = 0; t < nchunks; ++t) {
+  for (int t = c0; t < nchunks; ++t) {
     if (t + 1 < nchunks) wait_vm<GI>(); else wait_vm<0>();
     sync_lds();
     if (t + STAGES - 1 < nchunks) issue(t + STAGES - 1);
@@ -260,7 +276,9 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
       pv_chunk<D, NB, false>(acc, vprev, pf_prev, 0, 0, rl, h);
     }
     if (__ballot(m_new != m_run)) {  // wave-uniform: some row's running max moved -> rescale
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * cs);  // exp2(-inf) = 0
+      // exp2(-inf) = 0; a split whose first chunks are all masked for a row (SPLIT) still has
+      // m_run = m_new = -inf there when another row's max moves: (-inf) - (-inf) would be NaN
+      const float alpha = (SPLIT && m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_new) * cs);
       l_run *= alpha;
 #pragma unroll
       for (int n = 0; n < NB; ++n) acc[n] *= alpha;
@@ -296,7 +314,53 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
   }
 
   // acc[n][i] = O^T[dim 32 n + 8 (i >> 2) + 4 h + (i & 3)][row rl]
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (SPLIT && n_split > 1) {
+    // split-KV: publish this split's unnormalised O and (m, l) write-through, take the ticket
+    const long unit = (long)(tile * a.nkv + kvh);
+    const long pbase = (unit * a.splits + split) * ROWS;     // first row of this partial
+    const unsigned obytes = (unsigned)min((long)a.num_tiles * a.nkv * a.splits * ROWS * D * 4, 0x7fffffffL);
+    const unsigned mlbytes = (unsigned)min((long)a.num_tiles * a.nkv * a.splits * ROWS * 4 * 4, 0x7fffffffL);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.part_o, obytes), rml = make_rsrc(a.part_ml, mlbytes);
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        st_wt16(ro, (unsigned)(((pbase + r) * D + 32 * n + 8 * g + 4 * h) * 4),
+                make_float4(acc[n][4 * g], acc[n][4 * g + 1], acc[n][4 * g + 2], acc[n][4 * g + 3]));
+    if (h == 0) st_wt16(rml, (unsigned)((pbase + r) * 16), make_float4(m_run, l_tot, 0.f, 0.f));
+    __shared__ int s_last;
+    if (!ticket_last(a.counters + unit, n_split, &s_last)) return;
+    // the last arriver: every split's partial of this lane's row (sc1 loads, R1) in one frame;
+    // two passes over the (m, l) pairs instead of per-split arrays (dynamic indexing would spill)
+    float M = -INFINITY;
+    for (int q = 0; q < n_split; ++q)
+      M = fmaxf(M, ld_wt16(rml, (unsigned)(((unit * a.splits + q) * ROWS + r) * 16)).x);
+    const float Ms = (M == -INFINITY) ? 0.f : M * cs;
+    float L = 0.f;
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[n][i] = 0.f;
+    for (int q = 0; q < n_split; ++q) {
+      const long qb = (unit * a.splits + q) * ROWS + r;
+      const float4 ml = ld_wt16(rml, (unsigned)(qb * 16));
+      const float f = ml.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ml.x * cs - Ms);
+      if (f == 0.f) continue;      // a split with no key for this row contributes nothing
+      L += ml.y * f;
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 v = ld_wt16(ro, (unsigned)((qb * D + 32 * n + 8 * g + 4 * h) * 4));
+          acc[n][4 * g] += v.x * f;
+          acc[n][4 * g + 1] += v.y * f;
+          acc[n][4 * g + 2] += v.z * f;
+          acc[n][4 * g + 3] += v.w * f;
+        }
+    }
+    l_tot = L;
+  }
   if (!row_ok) return;
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   u16* o = a.out + ((long)(qstart + my_tok) * a.nq + my_head) * D + 4 * h;
@@ -312,17 +376,26 @@ __global__ void __launch_bounds__(512, MINW) flash_prefill_kernel(FlashArgs a) {
 }  // namespace
 
 // Tiles: 256 / G query tokens per tile (host-built, ops.flash_tiles); 1-D grid of tiles x nkv.
+// splits > 1: split-KV (part_o [num_tiles * nkv * splits, 256, d] f32, part_ml [.., 256, 4] f32,
+// counters [num_tiles * nkv] int, zeroed here); splits <= 16.
 extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc, const int* block_tables,
                                   const int* seq_qstart, const int* seq_qlen, const int* seq_ctx, const int* tile_seq,
                                   const int* tile_tok0, void* out, int num_tiles, int nq, int nkv, int d,
-                                  int max_blocks, int causal, float scale, hipStream_t stream) {
+                                  int max_blocks, int causal, float scale, int splits, float* part_o, float* part_ml,
+                                  int* counters, hipStream_t stream) {
   if (nq % nkv) return -1;
   const int G = nq / nkv;
   if (ROWS % G || G > 32) return -2;
   if (num_tiles <= 0) return 0;
+  if (splits < 1 || splits > 16 || (splits > 1 && (!part_o || !part_ml || !counters))) return -5;
+  if (splits > 1) {
+    const hipError_t e = hipMemsetAsync(counters, 0, (size_t)num_tiles * nkv * sizeof(int), stream);
+    if (e != hipSuccess) return (int)e;
+  }
   FlashArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
-              tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, num_tiles, scale * LOG2E_F};
-  const dim3 grid((unsigned)num_tiles * (unsigned)nkv);
+              tile_seq, tile_tok0, (u16*)out, nq, nkv, G, max_blocks, causal, num_tiles, scale * LOG2E_F,
+              splits, part_o, part_ml, counters};
+  const dim3 grid((unsigned)num_tiles * (unsigned)nkv * (unsigned)splits);
   // d=64: 4 waves per SIMD (<= 128 VGPRs, 52 KB LDS at a 16K context) = two workgroups per CU;
   // measured 1.14-1.17x over one at 2k-16k tokens (profiles/r2_flash_prefill_microbench.md)
   // d = 128 runs the software-pipelined P.V variant (4-stage ring + zero V^T image): 4-11 % faster
@@ -341,6 +414,14 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
     hipLaunchKernelGGL(kern, grid, dim3(64 * NWAVES), lds, stream, a);
     return (int)hipGetLastError();
   };
+  if (splits > 1) {   // split-KV instantiations (small grids only): 2 waves per SIMD, plain loop
+    switch (d) {
+      case 64: return go(flash_prefill_kernel<64, 2, false, true>, 64, false);
+      case 96: return go(flash_prefill_kernel<96, 2, false, true>, 96, false);
+      case 128: return go(flash_prefill_kernel<128, 2, false, true>, 128, false);
+      default: return -4;
+    }
+  }
   switch (d) {
     case 64: return go(flash_prefill_kernel<64, 4, false>, 64, false);
     case 96: return go(flash_prefill_kernel<96, 2, false>, 96, false);

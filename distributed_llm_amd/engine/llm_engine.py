@@ -897,7 +897,7 @@ class LLMEngine:
             last_d, ids_d, pos_d, bt_d = T(last, torch.int64), T(ids), T(pos), torch.from_numpy(np.ascontiguousarray(bt))
         meta = AttnMeta(slots=slots_d, block_tables=bt_d, qstart=qstart_d, qlen=qlen_d,
                         ctx=ctx_d, tile_seq=tseq_d, tile_tok0=ttok_d, last_idx=last_d,
-                        splits=splits, xcd_remap=True, flash=flash)
+                        splits=splits, xcd_remap=True, flash=flash, max_ctx=max(ctx))
         hidden = self.model.hidden_states(ids_d, pos_d, meta, self.kv_caches)
         if not self._collectives_ok():
             # a one-shot all-reduce timed out on some rank: every rank re-runs the chunk on RCCL

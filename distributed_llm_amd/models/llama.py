@@ -61,6 +61,7 @@ class AttnMeta:
     items: Optional[torch.Tensor] = None       # decode: persistent attention work list (ops.decode_work_items)
     grid_items: int = 0                        # workgroups walking ``items``
     flash: bool = False                        # prefill: tile_seq/tile_tok0 are 128-row flash tiles
+    max_ctx: int = 0                           # prefill: longest context (host-known; flash split-KV choice)
     all_last: bool = False                     # decode: every row is its sequence's last token (no gather)
 
 
@@ -361,7 +362,8 @@ class LlamaModel:
     def _attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         if meta.flash:   # prefill: 128-row tiles, K/V staged once per workgroup (flash_prefill.hip)
             return ops.flash_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
-                                       meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True)
+                                       meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
+                                       max_ctx=meta.max_ctx)
         return ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,

@@ -201,18 +201,60 @@ def flash_tiles(q_lens, group: int) -> Tuple[list, list]:
 def flash_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                     seq_qstart: torch.Tensor, seq_qlen: torch.Tensor, seq_ctx: torch.Tensor, tile_seq: torch.Tensor,
                     tile_tok0: torch.Tensor, scale: Optional[float] = None, causal: bool = True,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    out: Optional[torch.Tensor] = None, max_ctx: int = 0) -> torch.Tensor:
     """Flash-style prefill over the paged cache (csrc/kernels/flash_prefill.hip); tiles from
-    :func:`flash_tiles`.  Same contract as :func:`paged_attention` (CPU: the same reference)."""
+    :func:`flash_tiles`.  Same contract as :func:`paged_attention` (CPU: the same reference).
+    ``max_ctx`` (host-known longest context, 0 = unknown) enables split-KV for small grids."""
     d = q.shape[-1]
     scale = (1.0 / math.sqrt(d)) if scale is None else scale
     ext = _native(q)
     if ext is None:
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, scale, causal)
     o = out if out is not None else torch.empty_like(q)
-    ext.flash_prefill(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
-                      causal, scale)
+    units = int(tile_seq.numel()) * int(k_cache.shape[1])
+    sp = flash_splits(units, max_ctx)
+    if sp > 1:
+        po, pml, cnt = _flash_workspace(q.device, units * sp * FLASH_ROWS * d, units * sp * FLASH_ROWS * 4, units)
+        ext.flash_prefill(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
+                          causal, scale, sp, po, pml, cnt)
+    else:
+        ext.flash_prefill(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
+                          causal, scale)
     return o
+
+
+# Split-KV for flash grids that leave CUs idle: each (tile, kv head) unit's key chunks are dealt to
+# `splits` workgroups and the last one combines their partials.  Measured (profiles/r4_flash_split.md):
+# the partial write + ticket + combine costs more than it saves on a cold 1K prompt (short key chains:
+# 50 vs 35 us), so it is only chosen for a small grid over LONG contexts (a few new tokens behind a
+# long cached history: one unit walks thousands of keys).  DLLM_FLASH_SPLITS=N forces N (1 = off).
+FLASH_SPLIT_TARGET = 512
+FLASH_SPLIT_MIN_CTX = 4096
+
+
+def flash_splits(units: int, max_ctx: int = 0) -> int:
+    e = os.environ.get("DLLM_FLASH_SPLITS")
+    if e is not None:
+        return max(1, min(16, int(e)))
+    if units <= 0 or units >= FLASH_SPLIT_TARGET // 2 or max_ctx < FLASH_SPLIT_MIN_CTX:
+        return 1
+    return max(1, min(8, -(-FLASH_SPLIT_TARGET // units), max_ctx // 2048))
+
+
+_FLASH_WS: dict = {}
+
+
+def _flash_workspace(dev, n_o: int, n_ml: int, n_cnt: int):
+    """Grow-only per-device split-KV workspace (partials and tickets; the launcher zeroes the
+    tickets of every call)."""
+    key = str(dev)
+    ws = _FLASH_WS.get(key)
+    if ws is None or ws[0].numel() < n_o or ws[1].numel() < n_ml or ws[2].numel() < n_cnt:
+        ws = (torch.empty(max(n_o, ws[0].numel() if ws else 0), dtype=torch.float32, device=dev),
+              torch.empty(max(n_ml, ws[1].numel() if ws else 0), dtype=torch.float32, device=dev),
+              torch.zeros(max(n_cnt, ws[2].numel() if ws else 0), dtype=torch.int32, device=dev))
+        _FLASH_WS[key] = ws
+    return ws
 
 
 def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,

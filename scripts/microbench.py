@@ -270,6 +270,30 @@ def bench_flash(L, nq, nkv, d, B=1):
             "speedup": round(ms_p / ms_f, 2), "max_abs_diff": round(float((a.float() - b.float()).abs().max()), 4)}
 
 
+def bench_flash_cached(Q, C, nq, nkv, d):
+    """One prompt's new tokens behind a cached history (a conversation turn with a prefix hit):
+    Q query tokens at the end of a C-key context, causal; split-KV auto (max_ctx given) vs off."""
+    g = torch.Generator(device="cuda").manual_seed(Q + C + d)
+    nb = (C + 15) // 16
+    kc = (torch.randn(nb + 4, nkv, 16, d, device="cuda", generator=g)).to(torch.bfloat16)
+    vc = (torch.randn(nb + 4, nkv, d, 16, device="cuda", generator=g)).to(torch.bfloat16)
+    bt = (torch.randperm(nb, device="cuda", generator=g) + 1).view(1, nb).to(torch.int32)
+    q = torch.randn(Q, nq, d, device="cuda", generator=g).to(torch.bfloat16)
+    I = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    qs, ql, cx = I([0]), I([Q]), I([C])
+    fts, ftt = ops.flash_tiles([Q], nq // nkv)
+    fts, ftt = I(fts), I(ftt)
+    run = lambda mc: ops.flash_attention(q, kc, vc, bt, qs, ql, cx, fts, ftt, max_ctx=mc)
+    ms_s = timeit(lambda: run(C), iters=10, warm=2)
+    ms_1 = timeit(lambda: run(0), iters=10, warm=2)
+    diff = float((run(C).float() - run(0).float()).abs().max())
+    flops = 4.0 * nq * d * Q * C
+    return {"bench": "flash_cached", "Q": Q, "C": C, "nq": nq, "nkv": nkv, "d": d,
+            "splits": ops.flash_splits(len(fts) * nkv, C), "split_us": round(ms_s * 1000, 1),
+            "nosplit_us": round(ms_1 * 1000, 1), "split_TFLOPs": round(flops / ms_s / 1e9, 1),
+            "nosplit_TFLOPs": round(flops / ms_1 / 1e9, 1), "max_abs_diff": round(diff, 4)}
+
+
 def bench_gemm(M, N, K):
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
@@ -292,6 +316,10 @@ if __name__ == "__main__":
         if os.environ.get("MB_TUNE_SHAPES"):
             shapes = [tuple(int(v) for v in t.split("x")) + (False,) for t in os.environ["MB_TUNE_SHAPES"].split(",")]
         G.autotune(shapes, ms, "cuda", verbose=True)
+    if "flash_cached" in what:
+        for (nq, nkv, d) in ((32, 4, 64), (32, 8, 128)):
+            for (Q, C) in ((130, 2048), (130, 4096), (130, 16384), (512, 16384), (1024, 32768)):
+                print(json.dumps(bench_flash_cached(Q, C, nq, nkv, d)), flush=True)
     if "flash" in what:
         for (nq, nkv, d) in ((32, 4, 64), (32, 8, 128), (32, 32, 96)):
             for L in (1024, 4096, 16384):

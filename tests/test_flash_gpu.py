@@ -109,3 +109,33 @@ def test_flash_prefill_past_one_block_table_window(causal):
     want = ref.paged_attention(q, kc.nan_to_num(0.0), vc.nan_to_num(0.0), bt, qs, ql, cx, 1.0 / math.sqrt(d), causal)
     assert torch.isfinite(got.float()).all()
     torch.testing.assert_close(got.cpu().float(), want.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("splits", ["1", "2", "3", "16"])
+@pytest.mark.parametrize("d,nq,nkv", [(64, 32, 4), (128, 32, 8), (96, 32, 32)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_prefill_split_kv_matches_reference(splits, d, nq, nkv, causal, monkeypatch):
+    """Split-KV (short prompts leave the grid small): each (tile, kv head)'s key chunks dealt to
+    1-16 workgroups, the last arriver combining their (m, l, O) partials; more splits than a short
+    tile has chunks leaves the surplus workgroups empty.  Same fp32 reference, NaN-poisoned tails,
+    rising maxima; the default (auto) split is covered by the tests above."""
+    monkeypatch.setenv("DLLM_FLASH_SPLITS", splits)
+    seqs = [(1024, 1024), (130, 1830), (1, 50), (40, 40)]
+    q, kc, vc, bt, qs, ql, cx = _case(d, nq, nkv, seqs, seed=d + int(splits), rising=True)
+    ts, tt = ops.flash_tiles(ql.tolist(), nq // nkv)
+    C = lambda t: t.cuda()
+    got = ops.flash_attention(C(q), C(kc), C(vc), C(bt), C(qs), C(ql), C(cx), C(torch.tensor(ts, dtype=torch.int32)),
+                              C(torch.tensor(tt, dtype=torch.int32)), causal=causal)
+    again = ops.flash_attention(C(q), C(kc), C(vc), C(bt), C(qs), C(ql), C(cx), C(torch.tensor(ts, dtype=torch.int32)),
+                                C(torch.tensor(tt, dtype=torch.int32)), causal=causal)
+    want = ref.paged_attention(q, kc.nan_to_num(0.0), vc.nan_to_num(0.0), bt, qs, ql, cx, 1.0 / math.sqrt(d), causal)
+    assert torch.isfinite(got.float()).all()
+    torch.testing.assert_close(got.cpu().float(), want.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(got, again)     # the tickets re-arm: a second launch combines the same way
+
+
+def test_flash_split_choice():
+    """Auto split-KV only for small grids over long contexts (measured slower on short ones)."""
+    assert ops.flash_splits(1000, 16384) == 1 and ops.flash_splits(256, 16384) == 1
+    assert ops.flash_splits(128, 1024) == 1 and ops.flash_splits(20, 0) == 1
+    assert ops.flash_splits(128, 16384) == 4 and ops.flash_splits(20, 16384) == 8 and ops.flash_splits(20, 4096) == 2
