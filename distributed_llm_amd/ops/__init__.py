@@ -241,20 +241,12 @@ def flash_splits(units: int, max_ctx: int = 0) -> int:
     return max(1, min(8, -(-FLASH_SPLIT_TARGET // units), max_ctx // 2048))
 
 
-_FLASH_WS: dict = {}
-
-
 def _flash_workspace(dev, n_o: int, n_ml: int, n_cnt: int):
-    """Grow-only per-device split-KV workspace (partials and tickets; the launcher zeroes the
-    tickets of every call)."""
-    key = str(dev)
-    ws = _FLASH_WS.get(key)
-    if ws is None or ws[0].numel() < n_o or ws[1].numel() < n_ml or ws[2].numel() < n_cnt:
-        ws = (torch.empty(max(n_o, ws[0].numel() if ws else 0), dtype=torch.float32, device=dev),
-              torch.empty(max(n_ml, ws[1].numel() if ws else 0), dtype=torch.float32, device=dev),
-              torch.zeros(max(n_cnt, ws[2].numel() if ws else 0), dtype=torch.int32, device=dev))
-        _FLASH_WS[key] = ws
-    return ws
+    """Split-KV workspace of ONE launch (partials and tickets; the launcher zeroes the tickets),
+    from the caching allocator on the current stream: two engines prefilling on one device
+    (co-located tiers, separate step loops and streams) never share partials or tickets."""
+    return (torch.empty(n_o, dtype=torch.float32, device=dev), torch.empty(n_ml, dtype=torch.float32, device=dev),
+            torch.empty(n_cnt, dtype=torch.int32, device=dev))
 
 
 def decode_work_items(ctx, nkv: int, max_splits: int, target_items: int, min_chunk: int = 256,
