@@ -11,3 +11,18 @@ def test_flash_supported_applies_the_launchers_lds_bound():
         assert ops.flash_supported(d, 4, fit) and not ops.flash_supported(d, 4, fit + 64)
     assert ops.flash_lds_bytes(128, 8192) == 3 * 2 * 64 * 128 * 2 + 8192 * 4
     assert not ops.flash_supported(80, 4, 16) and not ops.flash_supported(128, 3, 16)
+
+
+def test_flash_split_heuristic(monkeypatch):
+    """Flash split-KV is chosen only for a small grid over a long context (measured slower on cold
+    short prompts, 1.5-5x faster on a turn's new tokens over a long cached history:
+    profiles/r4_flash_split.md); DLLM_FLASH_SPLITS forces a factor (1 = off, capped at 16)."""
+    monkeypatch.delenv("DLLM_FLASH_SPLITS", raising=False)
+    assert ops.flash_splits(20, 2048) == 1          # short context: never
+    assert ops.flash_splits(300, 32768) == 1        # the grid already fills the chip
+    assert ops.flash_splits(20, 4096) == 2 and ops.flash_splits(20, 16384) == 8
+    assert ops.flash_splits(128, 16384) == 4        # capped by the 512-workgroup target
+    monkeypatch.setenv("DLLM_FLASH_SPLITS", "3")
+    assert ops.flash_splits(1000, 0) == 3
+    monkeypatch.setenv("DLLM_FLASH_SPLITS", "99")
+    assert ops.flash_splits(1, 0) == 16
