@@ -7,7 +7,7 @@ O=gpurun_out/ab19
 mkdir -p $O
 export DLLM_GEMM_PLANS=$O/gemm_plans.json
 i=0
-for ae in 4 8 16 2; do
+for ae in ${AES:-4 8 16 2}; do
   i=$((i+1))
   timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 --admit-every $ae > $O/run$i.log 2>&1 \
     || { echo "run $i failed"; tail -30 $O/run$i.log; exit 1; }
