@@ -41,6 +41,7 @@ import argparse
 import itertools
 import json
 import os
+import queue
 import statistics
 import sys
 import time
@@ -268,6 +269,19 @@ class PipelinedConversations(Conversations):
             t.join()
 
 
+def _thread_cpu() -> dict:
+    """CPU seconds per named Python thread of this process (``DLLM_THREAD_CPU=1`` diagnostics:
+    how much of the window the routing driver and each engine's step loop hold a core / the GIL)."""
+    import threading
+    import psutil
+    names = {t.native_id: t.name for t in threading.enumerate()}
+    out = {}
+    for th in psutil.Process().threads():
+        k = names.get(th.id, "other")
+        out[k] = out.get(k, 0.0) + th.user_time + th.system_time
+    return out
+
+
 def _yield_to_engines(engines, max_s: float = 0.02) -> None:
     """The routing driver holds off while an engine's step loop is at a burst boundary
     (``LLMEngine.host_critical``): there the GPU waits for that loop's host work, and both threads
@@ -280,14 +294,16 @@ def _yield_to_engines(engines, max_s: float = 0.02) -> None:
 class EventConversations(PipelinedConversations):
     """Turn pipelining from ONE driver thread (``--pipeline 2``): every conversation whose answer
     has arrived is routed (one batched decision pass for all of them, ``Router.dispatch_batch``)
-    and its next turn is submitted to the engine without blocking; the driver then collects
-    whatever finished and repeats.  Each conversation stays strictly sequential, the continuous
+    and its next turn is submitted to the engine without blocking; the driver then blocks on a
+    completion queue the engines feed (``notify``) and collects whatever finished -- no polling
+    of in-flight handles (at 512 conversations that scan cost the driver ~0.1 of a core in GIL
+    holds, profiles/r4_host_cpu_budget.md).  Each conversation stays strictly sequential, the continuous
     batch stays full (a small-tier answer's conversation re-enters while large-tier answers are
     still decoding), and there is no per-conversation thread competing for the GIL.  The engine
     admits new turns every ``--admit-every`` decode steps so its pipelined bursts stay long.
     Same steady-state window accounting as the parent (a step = ``n_convs`` completed turns)."""
 
-    POLL_S = 0.001
+    WAIT_S = 0.05     # longest block on the completion queue (re-checks the stop flag)
 
     def start(self, router) -> None:
         import threading
@@ -298,12 +314,20 @@ class EventConversations(PipelinedConversations):
         self.errors = []
 
         def driver():
+            prof = None
+            if os.environ.get("DLLM_DRIVER_PROFILE"):   # cProfile of this thread, dumped at stop()
+                import cProfile
+                prof = cProfile.Profile()
+                prof.enable()
             try:
                 _router_stream()
                 ready = list(range(len(self.convs)))
-                inflight = {}
+                inflight = {}          # id(handle) -> (conversation, ticket); handle-less: own key
+                keys = {}              # conversation -> its in-flight ticket's key
+                finished = queue.SimpleQueue()   # handles the engines finished (notify)
                 engines = getattr(self, "engines", None) or []
                 while not self._stop:
+                    done = []
                     if ready:
                         _yield_to_engines(engines)
                         hs = []
@@ -314,17 +338,37 @@ class EventConversations(PipelinedConversations):
                                 q = c["tag"] + q
                             c["hist"].append({"role": "user", "content": q})
                             hs.append(c["hist"])
-                        for i, t in zip(ready, router.dispatch_batch(hs)):
-                            inflight[i] = t
+                        for i, t in zip(ready, router.dispatch_batch(hs, notify=finished.put)):
+                            h = t.get("handle")
+                            keys[i] = id(h) if h is not None else ("t", i)
+                            inflight[keys[i]] = (i, t)
+                            if router.ticket_done(t):        # cache hit, served inline, rejected,
+                                done.append(i)               # or already finished
                         ready = []
-                    done = [i for i, t in inflight.items() if router.ticket_done(t)]
+                    # block on the engines' completion queue instead of scanning every ticket
+                    items = []
+                    try:
+                        if not done:
+                            items.append(finished.get(timeout=self.WAIT_S))
+                        while True:
+                            items.append(finished.get_nowait())
+                    except queue.Empty:
+                        pass
+                    for h in items:
+                        e = inflight.get(id(h))
+                        if e is not None and e[1].get("handle") is h:
+                            done.append(e[0])
                     if not done:
-                        time.sleep(self.POLL_S)
                         continue
+                    tickets = {}       # a ticket can be both notified and seen done on dispatch
+                    for i in done:
+                        if i not in tickets:
+                            tickets[i] = inflight.pop(keys.pop(i))[1]
+                    done = list(tickets)
                     recs = []
                     for i in done:
                         _yield_to_engines(engines)
-                        payload, ntok, device = router.finish_ticket(inflight.pop(i))
+                        payload, ntok, device = router.finish_ticket(tickets[i])
                         c = self.convs[i]
                         c["hist"].append({"role": "assistant", "content": payload["response"]})
                         raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
@@ -345,6 +389,10 @@ class EventConversations(PipelinedConversations):
                 with self._cv:
                     self.errors.append(e)
                     self._cv.notify_all()
+            finally:
+                if prof is not None:
+                    prof.disable()
+                    prof.dump_stats(os.environ["DLLM_DRIVER_PROFILE"])
 
         self._threads = [threading.Thread(target=driver, name="bench-driver", daemon=True)]
         self._threads[0].start()
@@ -608,6 +656,7 @@ def main() -> int:
                 if on_gpu:
                     torch.cuda.synchronize()
                 e0 = meter.mark() if meter else None
+                cpu0 = _thread_cpu() if os.environ.get("DLLM_THREAD_CPU") == "1" else None
                 t0 = time.perf_counter()
                 convs.records = records
             convs.wait_turns((a.warmup + a.steps) * n_convs)
@@ -616,6 +665,7 @@ def main() -> int:
                 if on_gpu:
                     torch.cuda.synchronize()
                 elapsed = time.perf_counter() - t0
+                cpu1 = _thread_cpu() if cpu0 is not None else None
                 e1 = meter.mark() if meter else None
                 st1 = [dict(e.stats()) for e in engines]
                 enc1 = encoder_stats()
@@ -769,6 +819,9 @@ def main() -> int:
                                  "lookups": lk, "memo_hit_rate": round((enc1["hits"] - enc0["hits"]) / lk, 3) if lk else None,
                                  "texts_encoded_in_window": enc1["encoded_texts"] - enc0["encoded_texts"],
                                  "batch_reuse_hits": enc1["batch_hits"] - enc0["batch_hits"]}
+        if pipelined and cpu1 is not None:   # share of the window each thread spent on a core
+            out["thread_cpu_share"] = {k: round((v - cpu0.get(k, 0.0)) / elapsed, 3) for k, v in cpu1.items()
+                                       if v - cpu0.get(k, 0.0) > 0.01 * elapsed}
         logs = [e._sync_log for e in engines if getattr(e, "_sync_log", None)]
         if logs:   # DLLM_SYNC_LOG=1 diagnostics: did the step loop keep a step queued ahead?
             import numpy as np

@@ -24,7 +24,7 @@ import threading
 import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple, Union
+from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -90,6 +90,14 @@ class _Seq:
     done: threading.Event = field(default_factory=threading.Event)
     out_text: Optional[str] = None   # detokenised answer, formed as soon as the sequence stops
     released: bool = False           # blocks and row returned (_release)
+    notify: Optional[Callable[["_Seq"], None]] = None   # called with the sequence once it is done
+
+    def finish(self) -> None:
+        """Mark done: wakes ``done`` waiters, then hands the sequence to ``notify`` (an event-driven
+        client's completion queue), so one client thread never has to poll hundreds of handles."""
+        self.done.set()
+        if self.notify is not None:
+            self.notify(self)
 
     @property
     def length(self) -> int:
@@ -376,15 +384,20 @@ class LLMEngine:
         return self.results(seqs)
 
     def submit(self, prompts: Sequence[Union[str, List[int]]],
-               params: Union[SamplingParams, Sequence[SamplingParams], None] = None) -> List["_Seq"]:
+               params: Union[SamplingParams, Sequence[SamplingParams], None] = None,
+               notify: Optional[Callable[["_Seq"], None]] = None) -> List["_Seq"]:
         """Enqueue requests WITHOUT waiting (the background loop, ``start()``, must be running):
         returns handles whose ``done`` event is set when each request has finished; ``results``
         turns them into outputs.  An event-driven client (bench.py turn pipelining) keeps the
-        continuous batch full from one thread this way instead of one blocked thread per request."""
+        continuous batch full from one thread this way instead of one blocked thread per request.
+        ``notify(seq)`` is called (from the engine's loop thread) when a submitted request finishes;
+        requests rejected here (``error`` already set) are returned done and are not notified."""
         if self._bg is None:
             raise RuntimeError("submit() needs the background loop (start())")
         seqs = self._make_seqs(prompts, params)
         live = [s for s in seqs if s.error is None]
+        for s in live:
+            s.notify = notify
         with self._inbox_lock:
             self._inbox.extend(live)
             self._inbox_cv.notify()
@@ -412,7 +425,7 @@ class LLMEngine:
                 s.prompt = ids[:1] + ids[len(ids) - limit + 1:]
             if len(s.prompt) == 0 or limit <= 1:
                 s.error = "prompt too long for max_model_len"
-                s.done.set()
+                s.finish()
             seqs.append(s)
         self.timers["encode"] += time.perf_counter() - _t
         return seqs
@@ -462,7 +475,7 @@ class LLMEngine:
                     self.bt_host[s.row].fill(0)
                     self._free_rows.append(s.row)
                     s.row = -1
-                s.done.set()
+                s.finish()
         self._active = []
         self._early_pf = None
         self.host_critical.clear()
@@ -634,7 +647,7 @@ class LLMEngine:
                 if waiting:  # nothing fits even alone -> fail the head request
                     s = waiting.pop(0)
                     s.error = "insufficient KV cache for request"
-                    s.done.set()
+                    s.finish()
                 continue
             if prefilling:
                 _t = time.perf_counter()
@@ -720,7 +733,7 @@ class LLMEngine:
                 self._trace_request(s)
         self.bm.free(s.id)
         if keep:
-            s.done.set()
+            s.finish()
         if s.row >= 0:
             self.bt_host[s.row].fill(0)
             self._free_rows.append(s.row)
@@ -1459,7 +1472,7 @@ class LLMEngine:
         wake its caller; ``_release`` (after the burst) frees its blocks and row."""
         s.finished = time.perf_counter()
         self._finalize_text(s)
-        s.done.set()
+        s.finish()
 
     # fault injection (tests): force a collective trip on the Nth decode / prefill step of every rank
     FAULT_TRIP_DECODE = int(os.environ.get("DLLM_FAULT_CAR_TRIP_DECODE", "-1"))

@@ -24,7 +24,7 @@ import hashlib
 import logging
 import threading
 import time
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 from .config import LARGE, PRODUCTION_CFG, BENCHMARK_CFG, SMALL, other_tier
 from .router.query_router import QueryRouter
@@ -351,13 +351,18 @@ class Router:
         return self._finish(query, dec, raw, which, lat, failed)
 
     # ------------------------------------------------------------------ event-driven dispatch
-    def dispatch_batch(self, histories: Sequence[List[Dict[str, Any]]]) -> List[Dict[str, Any]]:
+    def dispatch_batch(self, histories: Sequence[List[Dict[str, Any]]],
+                       notify: Optional[Callable[[Any], None]] = None) -> List[Dict[str, Any]]:
         """Route a batch of conversations (one batched decision pass) and SUBMIT each request to
         its tier without waiting: pools with a non-blocking ``submit_batch`` (in-process engines
         running their background loop) return handles; other pools are served synchronously here.
         Returns one ticket per history; ``ticket_done`` / ``finish_ticket`` complete them.  A
         single client thread can keep hundreds of independent conversations in flight this way
-        (each conversation still strictly sequential), instead of one blocked thread each."""
+        (each conversation still strictly sequential), instead of one blocked thread each.
+        ``notify(handle)`` is called when a submitted ticket's handle (``ticket["handle"]``)
+        finishes, so the client can block on a completion queue instead of polling every ticket.
+        Tickets without a handle, and requests a pool rejected up front, come back done and are
+        never notified; a handle can finish (and be notified) before this returns."""
         tickets: List[Dict[str, Any]] = []
         groups: Dict[str, List[int]] = {SMALL: [], LARGE: []}
         for i, (kind, a, dec) in enumerate(self._decide_batch(histories)):
@@ -375,7 +380,7 @@ class Router:
             hs = [histories[i] for i in idx]
             sub = getattr(pool, "submit_batch", None)
             if sub is not None:
-                for i, h in zip(idx, sub(hs)):
+                for i, h in zip(idx, sub(hs) if notify is None else sub(hs, notify=notify)):
                     tickets[i]["handle"] = h
             else:
                 for i, raw in zip(idx, self._process_groups({dev: idx}, histories)[dev]):

@@ -279,10 +279,11 @@ class EnginePool(PoolClient):
         prompts = [self.prompt_for(h) for h in histories]
         return self.to_payloads(self.engine.generate(prompts, self._params(overrides)))
 
-    def submit_batch(self, histories, overrides: Optional[Dict[str, Any]] = None):
+    def submit_batch(self, histories, overrides: Optional[Dict[str, Any]] = None, notify=None):
         """Non-blocking ``process_batch`` (the engine's background loop must run): request handles
-        whose ``done`` event fires on completion; ``collect`` turns finished handles into payloads."""
-        return self.engine.submit([self.prompt_for(h) for h in histories], self._params(overrides))
+        whose ``done`` event fires on completion (and which are passed to ``notify``, if given);
+        ``collect`` turns finished handles into payloads."""
+        return self.engine.submit([self.prompt_for(h) for h in histories], self._params(overrides), notify=notify)
 
     def collect(self, handles) -> List[Dict[str, Any]]:
         return self.to_payloads(self.engine.results(handles))

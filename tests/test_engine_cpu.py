@@ -122,6 +122,26 @@ def test_background_loop_serves_staggered_callers():
     assert eng.generate([p_short], short)[0].token_ids == ref_short   # leader mode again
 
 
+def test_submit_notifies_each_finished_request_once():
+    """``submit(..., notify=)``: every request reaches the completion queue exactly once, already
+    done, with the same tokens as a blocking ``generate`` (the event driver's no-polling path)."""
+    import queue
+    eng = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=16, seed=0)
+    sps = [SamplingParams(max_new_tokens=n, temperature=0.0, ignore_eos=True) for n in (3, 9, 5, 1)]
+    prompts = [f"user: request {i}\nassistant: " for i in range(len(sps))]
+    ref = [eng.generate([p], sp)[0].token_ids for p, sp in zip(prompts, sps)]
+    eng.start()
+    try:
+        q = queue.SimpleQueue()
+        hs = eng.submit(prompts, sps, notify=q.put)
+        got = [q.get(timeout=120) for _ in hs]
+        assert sorted(map(id, got)) == sorted(map(id, hs)) and q.empty()
+        assert all(h.done.is_set() for h in got)
+        assert [o.token_ids for o in eng.results(hs)] == ref
+    finally:
+        eng.stop()
+
+
 def test_route_concurrent_matches_route_query():
     from distributed_llm_amd.config import BENCHMARK_CFG, LARGE, SMALL
     from distributed_llm_amd.orchestrator import Router
