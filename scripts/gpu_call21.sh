@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B on one box: event driver blocking on the engines' completion queue (bench.py) vs the
-# previous 1 ms poll over every in-flight ticket (scripts/exp/bench_poll_old.py), alternated.
+# previous 1 ms poll over every in-flight ticket (scripts/exp/bench_poll_old.py = `git show
+# a33ccc8:bench.py`, not kept in the tree), alternated.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
