@@ -35,6 +35,10 @@ int dllm_sample_rows(const void*, long, int, int, const float*, const float*, co
 int dllm_tp_cands_k();
 int dllm_tp_cands(const void*, long, int, int, int, void*, hipStream_t);
 int dllm_tp_sample(const void*, int, int, const float*, const float*, const int*, const unsigned*, int*, hipStream_t);
+int dllm_sample_split(const void*, long, int, int, int, const float*, const float*, const int*, const unsigned*, void*,
+                      long, int*, int*, hipStream_t);
+int dllm_sample_split_maxp();
+int dllm_sample_split_kmax();
 int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                      hipStream_t);
 int dllm_moe_max_tiles(int, int);
@@ -436,6 +440,33 @@ void sample_rows(torch::Tensor logits, torch::Tensor temp, torch::Tensor top_p, 
                       top_p.data_ptr<float>(), top_k.data_ptr<int>(), (const unsigned*)seed.data_ptr<int>(),
                       out.data_ptr<int>(), stream()),
      "sample_rows");
+}
+
+// Split-vocab sampler for small batches: grid (P shards, B rows), same tokens as sample_rows.
+// part: f32/int32 workspace >= B * P * KMAX * 2 elements; counters: int32 >= B, zero (re-armed).
+int64_t sample_split_maxp() { return dllm_sample_split_maxp(); }
+int64_t sample_split_kmax() { return dllm_sample_split_kmax(); }
+void sample_split(torch::Tensor logits, torch::Tensor temp, torch::Tensor top_p, torch::Tensor top_k,
+                  torch::Tensor seed, torch::Tensor part, torch::Tensor counters, torch::Tensor out, int64_t P) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0,
+              "logits [B, V] row-major, 16-B aligned rows");
+  check_f32(temp, "temperature");
+  check_f32(top_p, "top_p");
+  check_i32(top_k, "top_k");
+  check_i32(seed, "seed");
+  check_i32(out, "out");
+  check_i32(counters, "counters");
+  const int B = logits.size(0);
+  TORCH_CHECK(temp.numel() >= B && top_p.numel() >= B && top_k.numel() >= B && out.numel() >= B &&
+                  seed.numel() >= 1 && counters.numel() >= B,
+              "per-row parameter lengths");
+  TORCH_CHECK(part.is_cuda() && part.is_contiguous() && part.element_size() == 4, "part: 4-byte workspace");
+  TORCH_CHECK(P >= 1 && P <= dllm_sample_split_maxp(), "shards P");
+  ok(dllm_sample_split(logits.data_ptr(), logits.stride(0), B, logits.size(1), (int)P, temp.data_ptr<float>(),
+                       top_p.data_ptr<float>(), top_k.data_ptr<int>(), (const unsigned*)seed.data_ptr<int>(),
+                       part.data_ptr(), (long)part.numel() * 4, counters.data_ptr<int>(), out.data_ptr<int>(), stream()),
+     "sample_split");
 }
 
 // vocab-parallel sampler (csrc/kernels/sampling.hip): a shard's ranked top-KC candidates as int32
@@ -1077,6 +1108,9 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("step_store", &step_store);
   m.def("sample_topp", &sample_topp);
   m.def("sample_rows", &sample_rows);
+  m.def("sample_split", &sample_split);
+  m.def("sample_split_maxp", &sample_split_maxp);
+  m.def("sample_split_kmax", &sample_split_kmax);
   m.def("tp_cands_k", &tp_cands_k);
   m.def("tp_cands", &tp_cands);
   m.def("tp_sample", &tp_sample);

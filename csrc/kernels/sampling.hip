@@ -144,8 +144,8 @@ static __device__ __forceinline__ float row_uniform(unsigned seed, unsigned row)
 
 // Shared state of one row's selection (one workgroup per row).
 struct SrShared {
-  unsigned hist[4096];
-  float2 cand[SR_CAP];          // (value, index bits)
+  alignas(16) unsigned hist[4096];
+  alignas(16) float2 cand[SR_CAP];   // (value, index bits)
   float w_r[SR_KMAX];           // value by rank
   int i_r[SR_KMAX];             // token id by rank
   unsigned wsum[SR_THREADS / 64];
@@ -177,10 +177,22 @@ static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V,
     sh.hist[tid] = tmax;
     if (tid == 0) { sh.s_n = 0; sh.s_lo = 0; }
     __syncthreads();
-    int r = 0;  // rank among the thread maxima (ties -> lower thread first)
-    for (int j = 0; j < SR_THREADS; ++j) {
-      const unsigned o = sh.hist[j];
-      r += (o > tmax || (o == tmax && j < tid)) ? 1 : 0;
+    // rank among the thread maxima (ties -> lower thread first).  16-B broadcast reads, 8 in
+    // flight: one LDS round trip per maximum made this loop ~13 us of a ~30 us batch-1 launch.
+    int r = 0;
+    const uint4* h4 = reinterpret_cast<const uint4*>(sh.hist);
+    for (int j8 = 0; j8 < SR_THREADS / 4; j8 += 8) {
+      uint4 o[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) o[u] = h4[j8 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = 4 * (j8 + u);
+        r += (o[u].x > tmax || (o[u].x == tmax && j < tid)) ? 1 : 0;
+        r += (o[u].y > tmax || (o[u].y == tmax && j + 1 < tid)) ? 1 : 0;
+        r += (o[u].z > tmax || (o[u].z == tmax && j + 2 < tid)) ? 1 : 0;
+        r += (o[u].w > tmax || (o[u].w == tmax && j + 3 < tid)) ? 1 : 0;
+      }
     }
     if (r == k - 1) sh.s_lo = (int)tmax;
     __syncthreads();
@@ -321,17 +333,44 @@ static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V,
   nt = min(sh.s_nt, SR_CAP - amax);
   }
   const int n = min(na, SR_CAP) + nt;
-  // candidate j of the union [0, na) u [SR_CAP - nt, SR_CAP)
-  auto cidx = [&](int j) { return j < na ? j : SR_CAP - nt + (j - na); };
+  // the ties (slots [SR_CAP - nt, SR_CAP)) move down behind the [0, na) block: one contiguous list
+  if (nt > 0 && na < SR_CAP - nt) {
+    float2 t[SR_CAP / SR_THREADS];
+#pragma unroll
+    for (int u = 0; u < SR_CAP / SR_THREADS; ++u) {
+      const int j = tid + u * SR_THREADS;
+      if (j < nt) t[u] = sh.cand[SR_CAP - nt + j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SR_CAP / SR_THREADS; ++u) {
+      const int j = tid + u * SR_THREADS;
+      if (j < nt) sh.cand[na + j] = t[u];
+    }
+    __syncthreads();
+  }
 
-  // ---- 3. rank = #strictly better candidates; ranks < k are the top-k
+  // ---- 3. rank = #strictly better candidates; ranks < k are the top-k.  Candidates are read 16 B
+  // (two) at a time, 8 reads in flight (a dependent LDS round trip per candidate was ~8 us at
+  // n ~ 150 and most of the k = 256 launch).
+  const float4* c4 = reinterpret_cast<const float4*>(sh.cand);
+  const int n2 = (n + 1) >> 1;
   for (int j = tid; j < n; j += SR_THREADS) {
-    const float2 cj = sh.cand[cidx(j)];
+    const float2 cj = sh.cand[j];
     const int ij = __float_as_int(cj.y);
     int r = 0;
-    for (int i = 0; i < n; ++i) {
-      const float2 ci = sh.cand[cidx(i)];
-      r += (ci.x > cj.x || (ci.x == cj.x && __float_as_int(ci.y) < ij)) ? 1 : 0;
+    for (int i0 = 0; i0 < n2; i0 += 8) {
+      float4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = c4[min(i0 + u, n2 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = 2 * (i0 + u);
+        if (i0 + u < n2) {
+          r += (q[u].x > cj.x || (q[u].x == cj.x && __float_as_int(q[u].y) < ij)) ? 1 : 0;
+          if (i + 1 < n) r += (q[u].z > cj.x || (q[u].z == cj.x && __float_as_int(q[u].w) < ij)) ? 1 : 0;
+        }
+      }
     }
     if (r < k) { sh.i_r[r] = ij; sh.w_r[r] = cj.x; }
     if (r == 0) sh.s_m = cj.x;
@@ -507,7 +546,141 @@ __global__ void __launch_bounds__(SR_THREADS) tp_sample_kernel(const int2* __res
     if (lane == 0) out[row] = pick >= 0 ? sh.i_r[pick] : 0;
   }
 }
+// ---------------------------------------------------------------------------- split-vocab sampler
+// Small batches: one workgroup per row leaves ~250 CUs idle and puts a whole 32K-128K logit row
+// behind one CU's load queue (batch-1 sampler: 10 us TinyLlama, 28 us Llama-3-8B,
+// profiles/r3_single_stream_decode.md).  sample_split_kernel runs grid (P, B): workgroup (p, row)
+// reduces vocab shard p of the row to its ranked top-k (k = the row's top_k; a greedy row: its
+// arg-max), stores the list write-through and takes the row's ticket (recipe R1, common.h); the
+// last arriver merges the P ranked lists (rank = position in its own list + a binary search in
+// every other list, the tp_sample_kernel rule) and draws exactly as sample_rows_kernel does.  The
+// global top-k lies inside the union of the shards' top-k, so the token is the one
+// sample_rows_kernel picks from the whole row.
+constexpr int SS_MAXP = 8;
+
+// part: [B][P][SR_KMAX] int2 (value f32 bits, id) -- part_bytes covers it; counters [B], zero
+// (re-armed by every last arriver)
+__global__ void __launch_bounds__(SR_THREADS) sample_split_kernel(const u16* __restrict__ logits, long stride, int V,
+                                                                  int P, int vs, const float* __restrict__ temp,
+                                                                  const float* __restrict__ top_p,
+                                                                  const int* __restrict__ top_k,
+                                                                  const unsigned* __restrict__ seed, void* part,
+                                                                  unsigned part_bytes, int* __restrict__ counters,
+                                                                  int* __restrict__ out) {
+  __shared__ SrShared sh;
+  __shared__ int2 lists[SS_MAXP * SR_KMAX];
+  __shared__ int s_last;
+  const int p = blockIdx.x, row = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int start = p * vs, len = min(vs, V - start);
+  const u16* l = logits + (long)row * stride + start;
+  const float t = temp[row];
+  const bool greedy = !(t > 0.f);
+  int k = greedy ? 1 : top_k[row];
+  if (k <= 0 || k > SR_KMAX) k = SR_KMAX;
+  if (k > V) k = V;
+  const int kp = (k + 1) & ~1;                    // list length: whole 16-B pairs
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(part, part_bytes);
+  const unsigned base = (unsigned)(((long)row * P + p) * SR_KMAX * 8);
+  if (greedy) {                                   // shard arg-max, ties -> lowest index
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    const int nv = len >> 3;
+    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) better(bv, bi, f[j], start + c * 8 + j);
+    });
+    for (int i = (nv << 3) + tid; i < len; i += SR_THREADS) better(bv, bi, bf2f(l[i]), start + i);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      better(bv, bi, ov, oi);
+    }
+    if (lane == 0) { sh.sv[wid] = bv; sh.si[wid] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < SR_THREADS / 64; ++w) better(bv, bi, sh.sv[w], sh.si[w]);
+      st_wt16(rs, base, make_float4(bv, __int_as_float(bi), -INFINITY, __int_as_float(0x7fffffff)));
+    }
+  } else {
+    const int n = min(row_topk(l, len, min(k, len), sh), k);
+    for (int r2 = tid; 2 * r2 < kp; r2 += SR_THREADS) {
+      const int r = 2 * r2;
+      const float v0 = r < n ? sh.w_r[r] : -INFINITY, v1 = r + 1 < n ? sh.w_r[r + 1] : -INFINITY;
+      const int i0 = r < n ? sh.i_r[r] + start : 0x7fffffff, i1 = r + 1 < n ? sh.i_r[r + 1] + start : 0x7fffffff;
+      st_wt16(rs, base + r * 8, make_float4(v0, __int_as_float(i0), v1, __int_as_float(i1)));
+    }
+  }
+  if (!ticket_last(counters + row, P, &s_last)) return;
+
+  // ---- last arriver of the row: gather the P lists, merge, draw
+  const unsigned rbase = (unsigned)((long)row * P * SR_KMAX * 8);
+  for (int j = tid; 2 * j < P * kp; j += SR_THREADS) {
+    const int q = (2 * j) / kp, r = (2 * j) % kp;
+    const float4 v = ld_wt16(rs, rbase + (unsigned)((q * SR_KMAX + r) * 8));
+    lists[q * kp + r] = make_int2(__float_as_int(v.x), __float_as_int(v.y));
+    lists[q * kp + r + 1] = make_int2(__float_as_int(v.z), __float_as_int(v.w));
+  }
+  if (tid == 0) sh.s_n = 0;
+  __syncthreads();
+  if (greedy) {
+    if (tid == 0) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int q = 0; q < P; ++q) better(bv, bi, __int_as_float(lists[q * kp].x), lists[q * kp].y);
+      out[row] = (bi == 0x7fffffff) ? 0 : bi;
+    }
+    return;
+  }
+  int valid = 0;
+  for (int j = tid; j < P * kp; j += SR_THREADS) {
+    const int q = j / kp, i = j % kp;
+    const int2 c = lists[j];
+    if (c.y == 0x7fffffff) continue;                 // padding
+    ++valid;
+    int r = i;                                       // better ones in its own (sorted) list
+    for (int o = 0; o < P; ++o) {
+      if (o == q) continue;
+      int lo = 0, hi = kp;                           // # of list o strictly better than c
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cand_better(lists[o * kp + mid], c)) lo = mid + 1; else hi = mid;
+      }
+      r += lo;
+    }
+    if (r < k) { sh.i_r[r] = c.y; sh.w_r[r] = __int_as_float(c.x); }
+    if (r == 0) sh.s_m = __int_as_float(c.x);
+  }
+  atomicAdd(&sh.s_n, valid);
+  __syncthreads();
+  const int kk = min(k, sh.s_n);
+  if (wid == 0) {
+    const int pick = draw_rank(sh, kk, t, top_p[row], *seed, (unsigned)row);
+    if (lane == 0) out[row] = pick >= 0 ? sh.i_r[pick] : 0;
+  }
+}
 }  // namespace
+
+extern "C" int dllm_sample_split_maxp() { return SS_MAXP; }
+extern "C" int dllm_sample_split_kmax() { return SR_KMAX; }
+
+// logits [B, V] bf16 (row stride % 8 == 0) -> out [B]; P vocab shards of vs (% 8 == 0) logits each;
+// part >= B * P * SR_KMAX int2, counters >= B ints, zero.  Same tokens as dllm_sample_rows.
+extern "C" int dllm_sample_split(const void* logits, long stride, int B, int V, int P, const float* temp,
+                                 const float* top_p, const int* top_k, const unsigned* seed, void* part,
+                                 long part_bytes, int* counters, int* out, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (V <= 0 || stride % 8 != 0 || P < 1 || P > SS_MAXP) return -1;
+  const int vs = ((V + P - 1) / P + 7) / 8 * 8;
+  if ((long)(P - 1) * vs >= V) return -2;              // an empty shard: use fewer
+  const long need = (long)B * P * SR_KMAX * 8;
+  if (part_bytes < need || need > 0x7fffffffL) return -3;
+  hipLaunchKernelGGL(sample_split_kernel, dim3(P, B), dim3(SR_THREADS), 0, stream, (const u16*)logits, stride, V, P,
+                     vs, temp, top_p, top_k, seed, part, (unsigned)need, counters, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int dllm_sample_rows(const void* logits, long stride, int B, int V, const float* temp, const float* top_p,
                                 const int* top_k, const unsigned* seed, int* out, hipStream_t stream) {

@@ -461,7 +461,9 @@ def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Te
     """One-launch sampler over bf16 logits [B, V] (csrc/kernels/sampling.hip sample_rows_kernel):
     per row, temperature <= 0 -> arg-max, else exact top-k (top_k <= 0 -> 256 candidates),
     temperature, top-p and an inverse-CDF draw with u = hash(seed, row).  All parameters are
-    device tensors (f32 / int32, ``seed`` an int32 scalar), so the call is graph-capturable."""
+    device tensors (f32 / int32, ``seed`` an int32 scalar), so the call is graph-capturable.
+    Batches of <= ``DLLM_SAMPLE_SPLIT_MAX_B`` rows run sample_split_kernel instead (the row's vocab
+    on up to 8 workgroups, same tokens)."""
     ext = _native(logits)
     if ext is None:
         r = ref.sample_rows(logits, temperature.cpu(), top_p.cpu(), top_k.cpu(), int(seed.reshape(-1)[0]))
@@ -470,8 +472,30 @@ def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Te
             return out
         return r
     o = out if out is not None else torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
-    ext.sample_rows(logits, temperature, top_p, top_k, seed, o)
+    B, V = logits.shape
+    P = sample_split_shards(B, V)
+    if P > 1:
+        # small batch: P vocab shards per row on P workgroups, merged by the row's last arriver
+        # (sample_split_kernel); the ranked lists go through the owner's split-K workspace
+        from . import gemm as _gemm
+        part, counters = _gemm._P.workspace(logits.device, B * P * SAMPLE_SPLIT_KMAX * 2, B)
+        ext.sample_split(logits, temperature, top_p, top_k, seed, part, counters, o, P)
+    else:
+        ext.sample_rows(logits, temperature, top_p, top_k, seed, o)
     return o
+
+
+SAMPLE_SPLIT_KMAX = 256      # csrc/kernels/sampling.hip SR_KMAX (per-shard list capacity)
+SAMPLE_SPLIT_MAX_B = int(os.environ.get("DLLM_SAMPLE_SPLIT_MAX_B", "8"))
+SAMPLE_SPLIT_SHARD = 4096    # logits per shard at least (smaller shards: merge cost > load time)
+
+
+def sample_split_shards(B: int, V: int) -> int:
+    """Vocab shards per row for ``sample_rows``: 1 (one workgroup per row) unless the batch is
+    small (<= ``DLLM_SAMPLE_SPLIT_MAX_B``, 0 disables), then up to 8 shards of >= 4096 logits."""
+    if B > SAMPLE_SPLIT_MAX_B:
+        return 1
+    return max(1, min(8, V // SAMPLE_SPLIT_SHARD))
 
 
 TP_KC = 256   # candidates per vocab shard (csrc/kernels/sampling.hip TP_KC)

@@ -157,6 +157,12 @@ def bench_decode(eng, B, C):
     h[o[4] + rows] = np.arange(B)
     h[o[5] + rows] = 1
     h[o[6] + rows] = C
+    t = float(os.environ.get("MB_TEMP", "0"))   # > 0: sampled rows (top-k 40, top-p 0.9), else greedy
+    if t > 0:
+        s0, mb, hf = eng._so, eng.buckets[-1], eng.dec_host_f
+        hf[s0:s0 + bs] = t
+        hf[s0 + mb:s0 + mb + bs] = 0.9
+        h[s0 + 2 * mb:s0 + 2 * mb + bs] = 40
     eng._sync_bt()
     eng.dec_dev.copy_(eng.dec_host_t)
     if eng._use_worklist(bs):

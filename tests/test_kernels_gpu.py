@@ -284,6 +284,68 @@ def test_sample_rows_tie_flood_keeps_strictly_better_candidates():
     assert bool((a >= V - 10).all()), a
 
 
+@pytest.mark.parametrize("B,V", [(1, 32000), (3, 32000), (8, 128256), (2, 32005), (5, 8200)])
+def test_sample_split_matches_one_workgroup_per_row(B, V):
+    """Small batches run the split-vocab sampler (P shards per row, last arriver merges): the token
+    of every row equals the one-workgroup-per-row kernel's, greedy and sampled, any top_k."""
+    P = ops.sample_split_shards(B, V)
+    assert P > 1
+    torch.manual_seed(B * 7 + V)
+    Vp = (V + 7) // 8 * 8
+    ext = ops._native(torch.empty(1, device=DEV))
+    for trial in range(4):
+        lg = (torch.randn(B, Vp, device=DEV) * 3.0).to(torch.bfloat16)[:, :V]
+        temp = torch.where(torch.arange(B, device=DEV) % 3 == trial % 3, torch.zeros(B, device=DEV),
+                           torch.rand(B, device=DEV) + 0.3)
+        top_p = torch.rand(B, device=DEV) * 0.9 + 0.1
+        top_k = torch.tensor([[0, 1, 5, 40, 256, 300][(i + trial) % 6] for i in range(B)], dtype=torch.int32,
+                             device=DEV)
+        seed = torch.tensor([1000 + trial], dtype=torch.int32, device=DEV)
+        a = ops.sample_rows(lg, temp, top_p, top_k, seed)
+        b = torch.empty(B, dtype=torch.int32, device=DEV)
+        ext.sample_rows(lg, temp, top_p, top_k, seed, b)
+        assert torch.equal(a.cpu(), b.cpu()), (trial, a, b)
+    # the tie flood of the test above on the split path: strictly better logits are never dropped
+    lg = torch.full((B, V), -4.0, device=DEV)
+    lg[:, 1000:4000] = 1.0
+    lg[:, V - 10:] = 5.0
+    lg = torch.cat([lg, torch.zeros(B, Vp - V, device=DEV)], 1).to(torch.bfloat16)[:, :V]
+    p = lambda x: torch.full((B,), x, device=DEV)
+    a = ops.sample_rows(lg, p(1.0), p(0.5), torch.full((B,), 50, dtype=torch.int32, device=DEV),
+                        torch.tensor([17], dtype=torch.int32, device=DEV)).cpu()
+    assert bool((a >= V - 10).all()), a
+    # a NaN row yields a real token, as the unsplit kernel does
+    lg[0] = float("nan")     # in place: keeps the padded (16-B aligned) row stride
+    a = ops.sample_rows(lg, p(0.0), p(1.0), torch.zeros(B, dtype=torch.int32, device=DEV),
+                        torch.tensor([1], dtype=torch.int32, device=DEV))
+    b = torch.empty(B, dtype=torch.int32, device=DEV)
+    ext.sample_rows(lg, p(0.0), p(1.0), torch.zeros(B, dtype=torch.int32, device=DEV),
+                    torch.tensor([1], dtype=torch.int32, device=DEV), b)
+    assert torch.equal(a.cpu(), b.cpu())
+
+
+def test_sample_split_in_a_graph():
+    """The split sampler replays in a captured graph (its ticket counters re-arm themselves)."""
+    B, V = 2, 32000
+    lg = (torch.randn(B, V, device=DEV) * 3.0).to(torch.bfloat16)
+    temp, top_p = torch.full((B,), 0.8, device=DEV), torch.full((B,), 0.9, device=DEV)
+    top_k = torch.full((B,), 40, dtype=torch.int32, device=DEV)
+    seed = torch.tensor([5], dtype=torch.int32, device=DEV)
+    out = torch.empty(B, dtype=torch.int32, device=DEV)
+    ops.sample_rows(lg, temp, top_p, top_k, seed, out=out)     # workspace created outside capture
+    want = out.clone()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ops.sample_rows(lg, temp, top_p, top_k, seed, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want)
+
+
 def test_cosine_kernels():
     torch.manual_seed(9)
     q, c = torch.randn(5, 384, device=DEV), torch.randn(7, 384, device=DEV)
