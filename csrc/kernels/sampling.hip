@@ -161,8 +161,8 @@ struct SrShared {
 static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V, int k, SrShared& sh) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nv = V >> 3;
-  // ---- 0. fast bound (no histogram): T0 = the k-th largest of the 256 per-thread maximum keys.
-  // At least k logits are >= T0 (one per thread whose maximum is), so every top-k logit is too;
+  // ---- 0. fast bound (no histogram): T0 from the 256 per-thread maximum keys (below) such that
+  // at least k logits are >= T0, so every top-k logit is too;
   // when few logits reach T0 (typical: ~k-3k of 32 K) they are the whole candidate list and the
   // 4096-bin LDS-atomic histogram (hot bins serialise its atomics: ~40 us for one row) is skipped.
   // A flat row (> SR_MAXN logits at or above T0) falls through to the histogram path.
@@ -174,38 +174,43 @@ static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V,
       for (int j = 0; j < 8; ++j) tmax = max(tmax, bf_key(e[j]));
     });
     for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) tmax = max(tmax, bf_key(l[i]));
-    sh.hist[tid] = tmax;
-    if (tid == 0) { sh.s_n = 0; sh.s_lo = 0; }
-    __syncthreads();
-    // rank among the thread maxima (ties -> lower thread first).  16-B broadcast reads, 8 in
-    // flight: one LDS round trip per maximum made this loop ~13 us of a ~30 us batch-1 launch.
+    if (tid == 0) sh.s_n = 0;
+    // T0 = the smallest of the 4 waves' ceil(k/4)-th largest thread maximum: every wave has at
+    // least ceil(k/4) threads whose maximum is >= T0, so at least k logits are.  Per wave: each
+    // lane counts the wave's maxima above its own (uniform lane reads, no LDS); the lane of rank
+    // ceil(k/4) - 1 (ties -> lower lane) publishes.  (An exact k-th of all 256 maxima through LDS
+    // was ~5 us of a ~27 us batch-1 launch, profiles/r4_sampler.md.)
+    const int kw = (k + 3) >> 2;
     int r = 0;
-    const uint4* h4 = reinterpret_cast<const uint4*>(sh.hist);
-    for (int j8 = 0; j8 < SR_THREADS / 4; j8 += 8) {
-      uint4 o[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) o[u] = h4[j8 + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = 4 * (j8 + u);
-        r += (o[u].x > tmax || (o[u].x == tmax && j < tid)) ? 1 : 0;
-        r += (o[u].y > tmax || (o[u].y == tmax && j + 1 < tid)) ? 1 : 0;
-        r += (o[u].z > tmax || (o[u].z == tmax && j + 2 < tid)) ? 1 : 0;
-        r += (o[u].w > tmax || (o[u].w == tmax && j + 3 < tid)) ? 1 : 0;
-      }
+    for (int j = 0; j < 64; ++j) {
+      const unsigned o = (unsigned)__builtin_amdgcn_readlane((int)tmax, j);
+      r += (o > tmax || (o == tmax && j < lane)) ? 1 : 0;
     }
-    if (r == k - 1) sh.s_lo = (int)tmax;
+    if (r == kw - 1) sh.wsum[wid] = tmax;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned t = sh.wsum[0];
+      for (int w = 1; w < SR_THREADS / 64; ++w) t = min(t, sh.wsum[w]);
+      sh.s_lo = (int)t;
+    }
     __syncthreads();
     const unsigned t0 = (unsigned)sh.s_lo;
+    // candidates are rare (~k-3k of 32K): a branch-free 8-bit mask per vector, and the appends
+    // (LDS atomics) only for set bits -- one branch per vector instead of one per logit (the
+    // per-logit form was ~12 us of the batch-1 launch)
     for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
       const u16* e = reinterpret_cast<const u16*>(&v);
+      unsigned m = 0u;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const unsigned key = bf_key(e[j]);
-        if (key >= t0 && key != 0u) {
-          const int p = atomicAdd(&sh.s_n, 1);
-          if (p < SR_CAP) sh.cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
-        }
+        m |= (key >= t0 && key != 0u) ? (1u << j) : 0u;
+      }
+      while (m) {
+        const int j = __builtin_ctz(m);
+        m &= m - 1u;
+        const int p = atomicAdd(&sh.s_n, 1);
+        if (p < SR_CAP) sh.cand[p] = make_float2(key_f(bf_key(e[j])), __int_as_float(c * 8 + j));
       }
     });
     for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {

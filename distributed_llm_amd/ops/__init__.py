@@ -457,13 +457,13 @@ def sample_top_p(cand_vals: torch.Tensor, cand_idx: torch.Tensor, temperature: t
 
 
 def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
-                seed: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                seed: torch.Tensor, out: Optional[torch.Tensor] = None, shards: Optional[int] = None) -> torch.Tensor:
     """One-launch sampler over bf16 logits [B, V] (csrc/kernels/sampling.hip sample_rows_kernel):
     per row, temperature <= 0 -> arg-max, else exact top-k (top_k <= 0 -> 256 candidates),
     temperature, top-p and an inverse-CDF draw with u = hash(seed, row).  All parameters are
     device tensors (f32 / int32, ``seed`` an int32 scalar), so the call is graph-capturable.
-    Batches of <= ``DLLM_SAMPLE_SPLIT_MAX_B`` rows run sample_split_kernel instead (the row's vocab
-    on up to 8 workgroups, same tokens)."""
+    Small batches of large-vocab rows run sample_split_kernel instead (the row's vocab on up to 8
+    workgroups, same tokens; ``sample_split_shards``); ``shards`` forces a shard count (1: never)."""
     ext = _native(logits)
     if ext is None:
         r = ref.sample_rows(logits, temperature.cpu(), top_p.cpu(), top_k.cpu(), int(seed.reshape(-1)[0]))
@@ -473,7 +473,7 @@ def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Te
         return r
     o = out if out is not None else torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
     B, V = logits.shape
-    P = sample_split_shards(B, V)
+    P = sample_split_shards(B, V) if shards is None else max(1, min(8, int(shards)))
     if P > 1:
         # small batch: P vocab shards per row on P workgroups, merged by the row's last arriver
         # (sample_split_kernel); the ranked lists go through the owner's split-K workspace
@@ -488,12 +488,16 @@ def sample_rows(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Te
 SAMPLE_SPLIT_KMAX = 256      # csrc/kernels/sampling.hip SR_KMAX (per-shard list capacity)
 SAMPLE_SPLIT_MAX_B = int(os.environ.get("DLLM_SAMPLE_SPLIT_MAX_B", "8"))
 SAMPLE_SPLIT_SHARD = 4096    # logits per shard at least (smaller shards: merge cost > load time)
+SAMPLE_SPLIT_MIN_V = 65536   # below, one workgroup per row is as fast for sampled rows
 
 
 def sample_split_shards(B: int, V: int) -> int:
     """Vocab shards per row for ``sample_rows``: 1 (one workgroup per row) unless the batch is
-    small (<= ``DLLM_SAMPLE_SPLIT_MAX_B``, 0 disables), then up to 8 shards of >= 4096 logits."""
-    if B > SAMPLE_SPLIT_MAX_B:
+    small (<= ``DLLM_SAMPLE_SPLIT_MAX_B``, 0 disables) and the vocab large (>= 64K), then up to 8
+    shards of >= 4096 logits.  Batch 1, top-k 40 (profiles/r4_sampler.md): 128K vocab 52 -> 38 us,
+    greedy 26 -> 9 us; at 32K the split only helps greedy rows (9.5 -> 5.9 us) and costs sampled
+    ones 3 us, so 32K rows stay on one workgroup."""
+    if B > SAMPLE_SPLIT_MAX_B or V < SAMPLE_SPLIT_MIN_V:
         return 1
     return max(1, min(8, V // SAMPLE_SPLIT_SHARD))
 

@@ -9,4 +9,5 @@ timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_tp_sa
   -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && exit $rc
 DLLM_AUTOTUNE=0 timeout -k 10 400 python3 -u scripts/exp/sampler_probe.py > $O/out.log 2>&1
-rc=$?; grep "{" $O/out.log; exit $rc
+rc=$?; grep "{" $O/out.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 ./expbin/sampler_phases > $O/phases.jsonl 2>&1; rc=$?; cat $O/phases.jsonl; exit $rc

@@ -288,8 +288,8 @@ def test_sample_rows_tie_flood_keeps_strictly_better_candidates():
 def test_sample_split_matches_one_workgroup_per_row(B, V):
     """Small batches run the split-vocab sampler (P shards per row, last arriver merges): the token
     of every row equals the one-workgroup-per-row kernel's, greedy and sampled, any top_k."""
-    P = ops.sample_split_shards(B, V)
-    assert P > 1
+    P = max(2, min(8, V // ops.SAMPLE_SPLIT_SHARD))
+    split = lambda *a, **kw: ops.sample_rows(*a, shards=P, **kw)
     torch.manual_seed(B * 7 + V)
     Vp = (V + 7) // 8 * 8
     ext = ops._native(torch.empty(1, device=DEV))
@@ -301,7 +301,7 @@ def test_sample_split_matches_one_workgroup_per_row(B, V):
         top_k = torch.tensor([[0, 1, 5, 40, 256, 300][(i + trial) % 6] for i in range(B)], dtype=torch.int32,
                              device=DEV)
         seed = torch.tensor([1000 + trial], dtype=torch.int32, device=DEV)
-        a = ops.sample_rows(lg, temp, top_p, top_k, seed)
+        a = split(lg, temp, top_p, top_k, seed)
         b = torch.empty(B, dtype=torch.int32, device=DEV)
         ext.sample_rows(lg, temp, top_p, top_k, seed, b)
         assert torch.equal(a.cpu(), b.cpu()), (trial, a, b)
@@ -311,12 +311,12 @@ def test_sample_split_matches_one_workgroup_per_row(B, V):
     lg[:, V - 10:] = 5.0
     lg = torch.cat([lg, torch.zeros(B, Vp - V, device=DEV)], 1).to(torch.bfloat16)[:, :V]
     p = lambda x: torch.full((B,), x, device=DEV)
-    a = ops.sample_rows(lg, p(1.0), p(0.5), torch.full((B,), 50, dtype=torch.int32, device=DEV),
+    a = split(lg, p(1.0), p(0.5), torch.full((B,), 50, dtype=torch.int32, device=DEV),
                         torch.tensor([17], dtype=torch.int32, device=DEV)).cpu()
     assert bool((a >= V - 10).all()), a
     # a NaN row yields a real token, as the unsplit kernel does
     lg[0] = float("nan")     # in place: keeps the padded (16-B aligned) row stride
-    a = ops.sample_rows(lg, p(0.0), p(1.0), torch.zeros(B, dtype=torch.int32, device=DEV),
+    a = split(lg, p(0.0), p(1.0), torch.zeros(B, dtype=torch.int32, device=DEV),
                         torch.tensor([1], dtype=torch.int32, device=DEV))
     b = torch.empty(B, dtype=torch.int32, device=DEV)
     ext.sample_rows(lg, p(0.0), p(1.0), torch.zeros(B, dtype=torch.int32, device=DEV),
@@ -326,7 +326,8 @@ def test_sample_split_matches_one_workgroup_per_row(B, V):
 
 def test_sample_split_in_a_graph():
     """The split sampler replays in a captured graph (its ticket counters re-arm themselves)."""
-    B, V = 2, 32000
+    B, V = 2, 128256
+    assert ops.sample_split_shards(B, V) > 1 and ops.sample_split_shards(B, 32000) == 1
     lg = (torch.randn(B, V, device=DEV) * 3.0).to(torch.bfloat16)
     temp, top_p = torch.full((B,), 0.8, device=DEV), torch.full((B,), 0.9, device=DEV)
     top_k = torch.full((B,), 40, dtype=torch.int32, device=DEV)

@@ -26,3 +26,12 @@ def test_flash_split_heuristic(monkeypatch):
     assert ops.flash_splits(1000, 0) == 3
     monkeypatch.setenv("DLLM_FLASH_SPLITS", "99")
     assert ops.flash_splits(1, 0) == 16
+
+
+def test_sample_split_policy():
+    """Split-vocab sampler only for small batches of large-vocab rows (profiles/r4_sampler.md)."""
+    from distributed_llm_amd import ops
+    assert ops.sample_split_shards(1, 32000) == 1          # TinyLlama: one workgroup per row
+    assert ops.sample_split_shards(1, 128256) == 8         # Llama-3: 8 shards of ~16K
+    assert ops.sample_split_shards(ops.SAMPLE_SPLIT_MAX_B + 1, 128256) == 1
+    assert ops.sample_split_shards(4, 65536) == 8 and ops.sample_split_shards(4, 65535) == 1
