@@ -167,8 +167,31 @@ static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V,
   // 4096-bin LDS-atomic histogram (hot bins serialise its atomics: ~40 us for one row) is skipped.
   // A flat row (> SR_MAXN logits at or above T0) falls through to the histogram path.
   {
+    // rows of <= 32K logits (16 vectors per thread) are loaded ONCE, all 16 loads in flight, and
+    // both scans below read the registers; longer rows stream twice (for_each_vec)
+    constexpr int RC = 16;
+    uint4 cv[RC];
+    const bool cached = nv <= RC * SR_THREADS;
+    if (cached) {
+#pragma unroll
+      for (int u = 0; u < RC; ++u) {
+        const int c = tid + u * SR_THREADS;
+        cv[u] = c < nv ? ld16(l + (long)c * 8) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    auto visit = [&](auto f) {
+      if (cached) {
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+          const int c = tid + u * SR_THREADS;
+          if (c < nv) f(cv[u], c);
+        }
+      } else {
+        for_each_vec<SR_THREADS>(l, nv, tid, f);
+      }
+    };
     unsigned tmax = 0u;
-    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int) {
+    visit([&](const uint4 v, int) {
       const u16* e = reinterpret_cast<const u16*>(&v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) tmax = max(tmax, bf_key(e[j]));
@@ -198,7 +221,7 @@ static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V,
     // candidates are rare (~k-3k of 32K): a branch-free 8-bit mask per vector, and the appends
     // (LDS atomics) only for set bits -- one branch per vector instead of one per logit (the
     // per-logit form was ~12 us of the batch-1 launch)
-    for_each_vec<SR_THREADS>(l, nv, tid, [&](const uint4 v, int c) {
+    visit([&](const uint4 v, int c) {
       const u16* e = reinterpret_cast<const u16*>(&v);
       unsigned m = 0u;
 #pragma unroll
@@ -209,8 +232,11 @@ static __device__ __forceinline__ int row_topk(const u16* __restrict__ l, int V,
       while (m) {
         const int j = __builtin_ctz(m);
         m &= m - 1u;
+        // element j without indexing the vector (a dynamic index would put it in scratch)
+        const unsigned w = (j < 4) ? ((j < 2) ? v.x : v.y) : ((j < 6) ? v.z : v.w);
+        const unsigned key = bf_key((u16)((j & 1) ? (w >> 16) : (w & 0xffffu)));
         const int p = atomicAdd(&sh.s_n, 1);
-        if (p < SR_CAP) sh.cand[p] = make_float2(key_f(bf_key(e[j])), __int_as_float(c * 8 + j));
+        if (p < SR_CAP) sh.cand[p] = make_float2(key_f(key), __int_as_float(c * 8 + j));
       }
     });
     for (int i = (nv << 3) + tid; i < V; i += SR_THREADS) {
