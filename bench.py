@@ -79,21 +79,13 @@ def parse():
     ap.add_argument("--kv-gb", type=float, default=64.0)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (tiny model)")
-    ap.add_argument("--groups", type=int, default=1,
-                    help="G > 1: G independently pipelined groups of conversations, one thread each")
-    ap.add_argument("--pipeline", type=int, default=None,
-                    help="turn pipelining (replicated / tiers topologies): conversations advance independently; "
-                         "0: turn-synchronous steps, 1: one thread per conversation, 2: one event-driven driver "
-                         "thread (the default there: +6-7 %% routed tok/s, decode batch 372 -> 495-500 of 512, "
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="turn pipelining: conversations advance independently; 0: turn-synchronous steps, "
+                         "1: one thread per conversation, 2: one event-driven driver thread (the default, every "
+                         "topology: +6-7 %% routed tok/s on one GPU, decode batch 372 -> 495-500 of 512, "
                          "profiles/r4_turn_pipelining.md)")
-    ap.add_argument("--gc-freeze", type=int, default=0,
-                    help="1: gc.freeze() + higher young-generation thresholds after start-up (no measured effect on "
-                         "the flagship: 57.0 / 59.7k off vs 59.3 / 59.0k on, one box)")
     ap.add_argument("--gil-switch-ms", type=float, default=0.5,
                     help="turn pipelining: Python thread switch interval (sys.setswitchinterval) in ms")
-    ap.add_argument("--yield-to-engine", type=int, default=0,
-                    help="turn pipelining (--pipeline 2): the routing driver holds off while an engine's "
-                         "step loop is at a burst boundary (LLMEngine.host_critical); 0: never")
     ap.add_argument("--admit-every", type=int, default=16,
                     help="turn pipelining: the engine admits new turns every N decode steps of a burst")
     ap.add_argument("--no-encoder-memo", action="store_true",
@@ -180,14 +172,17 @@ class Conversations:
                 q = c["tag"] + q
             c["hist"].append({"role": "user", "content": q})
             hs.append(c["hist"])
+        t0 = time.perf_counter()
         res = router.route_batch(hs)
+        lat = (time.perf_counter() - t0) * 1000.0   # client side: every turn of the step waits for the batch
         for i, (c, (payload, ntok, device)) in enumerate(zip(self.convs, res)):
             c["hist"].append({"role": "assistant", "content": payload["response"]})
             if dump is not None:
                 dump.append([i, c["turn"], device, payload["response"]])
             if records is not None:
                 raw = payload.get("raw") or {}
-                records.append({"lat": float(raw.get("latency_ms", 0.0)) if isinstance(raw, dict) else 0.0,
+                records.append({"lat": lat,
+                                "lat_engine": float(raw.get("latency_ms", 0.0)) if isinstance(raw, dict) else 0.0,
                                 "tok": int(ntok), "dev": device, "fo": payload.get("failover_from"),
                                 "ok": bool(payload.get("ok", True)), "step": self.steps_done,
                                 "ovh": float(payload.get("routing_overhead_ms", 0.0)),
@@ -231,10 +226,12 @@ class PipelinedConversations(Conversations):
                     if c["turn"] == 0:
                         q = c["tag"] + q
                     c["hist"].append({"role": "user", "content": q})
+                    t0 = time.perf_counter()
                     payload, ntok, device = router.route_concurrent(c["hist"])
+                    lat = (time.perf_counter() - t0) * 1000.0
                     c["hist"].append({"role": "assistant", "content": payload["response"]})
                     raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
-                    rec = {"lat": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
+                    rec = {"lat": lat, "lat_engine": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
                            "ovh": float(payload.get("routing_overhead_ms", 0.0)),
                            "ttft": float((raw.get("timing") or {}).get("ttft_ms", 0.0))}
                     c["turn"] += 1
@@ -282,15 +279,6 @@ def _thread_cpu() -> dict:
     return out
 
 
-def _yield_to_engines(engines, max_s: float = 0.02) -> None:
-    """The routing driver holds off while an engine's step loop is at a burst boundary
-    (``LLMEngine.host_critical``): there the GPU waits for that loop's host work, and both threads
-    would otherwise share the GIL in 0.5 ms slices.  Bounded, so routing never starves."""
-    t0 = time.perf_counter()
-    while any(e.host_critical.is_set() for e in engines) and time.perf_counter() - t0 < max_s:
-        time.sleep(0.0002)
-
-
 class EventConversations(PipelinedConversations):
     """Turn pipelining from ONE driver thread (``--pipeline 2``): every conversation whose answer
     has arrived is routed (one batched decision pass for all of them, ``Router.dispatch_batch``)
@@ -324,12 +312,18 @@ class EventConversations(PipelinedConversations):
                 ready = list(range(len(self.convs)))
                 inflight = {}          # id(handle) -> (conversation, ticket); handle-less: own key
                 keys = {}              # conversation -> its in-flight ticket's key
-                finished = queue.SimpleQueue()   # handles the engines finished (notify)
-                engines = getattr(self, "engines", None) or []
+                finished = queue.SimpleQueue()   # handles the pools finished (notify)
+
+                def track(i, t):
+                    h = t.get("handle")
+                    keys[i] = id(h) if h is not None else ("t", i)
+                    inflight[keys[i]] = (i, t)
+                    return router.ticket_done(t)   # cache hit, served inline, rejected, or already finished
+
+                again = []             # failed-over tickets already done when re-submitted
                 while not self._stop:
-                    done = []
+                    done, again = again, []
                     if ready:
-                        _yield_to_engines(engines)
                         hs = []
                         for i in ready:
                             c = self.convs[i]
@@ -339,13 +333,10 @@ class EventConversations(PipelinedConversations):
                             c["hist"].append({"role": "user", "content": q})
                             hs.append(c["hist"])
                         for i, t in zip(ready, router.dispatch_batch(hs, notify=finished.put)):
-                            h = t.get("handle")
-                            keys[i] = id(h) if h is not None else ("t", i)
-                            inflight[keys[i]] = (i, t)
-                            if router.ticket_done(t):        # cache hit, served inline, rejected,
-                                done.append(i)               # or already finished
+                            if track(i, t):
+                                done.append(i)
                         ready = []
-                    # block on the engines' completion queue instead of scanning every ticket
+                    # block on the pools' completion queue instead of scanning every ticket
                     items = []
                     try:
                         if not done:
@@ -362,20 +353,25 @@ class EventConversations(PipelinedConversations):
                         continue
                     tickets = {}       # a ticket can be both notified and seen done on dispatch
                     for i in done:
-                        if i not in tickets:
+                        if i not in tickets and i in keys:
                             tickets[i] = inflight.pop(keys.pop(i))[1]
-                    done = list(tickets)
                     recs = []
-                    for i in done:
-                        _yield_to_engines(engines)
-                        payload, ntok, device = router.finish_ticket(tickets[i])
+                    for i, t in tickets.items():
+                        res = router.finish_ticket(t, notify=finished.put)
+                        if res is None:              # failed over: in flight on the other tier
+                            if track(i, t):
+                                again.append(i)
+                            continue
+                        payload, ntok, device = res
                         c = self.convs[i]
                         c["hist"].append({"role": "assistant", "content": payload["response"]})
                         raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
-                        recs.append({"lat": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
-                                     "ovh": float(payload.get("routing_overhead_ms", 0.0)),
+                        recs.append({"lat": float(t.get("latency_ms", 0.0)),
+                                     "lat_engine": float(raw.get("latency_ms", 0.0)), "tok": int(ntok),
+                                     "dev": device, "ovh": float(payload.get("routing_overhead_ms", 0.0)),
                                      "ttft": float((raw.get("timing") or {}).get("ttft_ms", 0.0)),
-                                     "fo": payload.get("failover_from"), "ok": bool(payload.get("ok", True))})
+                                     "fo": payload.get("failover_from"), "ok": bool(payload.get("ok", True)),
+                                     "step": self.completed // max(1, len(self.convs))})
                         c["turn"] += 1
                         if c["turn"] >= len(c["set"]):
                             self.convs[i] = self._new(i)
@@ -398,66 +394,23 @@ class EventConversations(PipelinedConversations):
         self._threads[0].start()
 
 
-class GroupedConversations(PipelinedConversations):
-    """Turn pipelining with few threads: G groups of conversations, each driven by ONE thread in
-    lock-step (route the group's turn as a batch -> serve -> next turn), groups independent.
+STEP_LOOP_TIMERS = ("t_prefill_s", "t_admit_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
+                    "t_decode_host_post_s", "t_complete_s")
+CLIENT_TIMERS = ("t_encode_s", "t_output_s")
 
-    A group still waits for its slowest answer, but while it routes and formats its next turn or
-    drains its long large-tier answers, the other groups' requests keep the engine's continuous
-    batch full; unlike one thread per conversation (``PipelinedConversations``) this adds only
-    G Python threads, so routing does not fight 512 threads for the GIL.  Same steady-state
-    window accounting as the parent (a step = ``n_convs`` completed turns)."""
 
-    def __init__(self, n: int, rank: int, groups: int):
-        super().__init__(n, rank)
-        self.groups = max(1, min(groups, n))
-
-    def start(self, router) -> None:
-        import threading
-        self._cv = threading.Condition()
-        self.completed = 0
-        self.records = None
-        self._stop = False
-        self.errors = []
-        idx = [list(range(g, len(self.convs), self.groups)) for g in range(self.groups)]
-
-        def worker(ids):
-            try:
-                _router_stream()
-                while not self._stop:
-                    hs = []
-                    for i in ids:
-                        c = self.convs[i]
-                        q = c["set"][c["turn"]].text
-                        if c["turn"] == 0:
-                            q = c["tag"] + q
-                        c["hist"].append({"role": "user", "content": q})
-                        hs.append(c["hist"])
-                    res = router.route_batch(hs)
-                    recs = []
-                    for i, (payload, ntok, device) in zip(ids, res):
-                        c = self.convs[i]
-                        c["hist"].append({"role": "assistant", "content": payload["response"]})
-                        raw = payload.get("raw") if isinstance(payload.get("raw"), dict) else {}
-                        recs.append({"lat": float(raw.get("latency_ms", 0.0)), "tok": int(ntok), "dev": device,
-                                     "ovh": float(payload.get("routing_overhead_ms", 0.0)),
-                                     "ttft": float((raw.get("timing") or {}).get("ttft_ms", 0.0))})
-                        c["turn"] += 1
-                        if c["turn"] >= len(c["set"]):
-                            self.convs[i] = self._new(i)
-                    with self._cv:
-                        if self.records is not None:
-                            self.records.extend(recs)
-                        self.completed += len(recs)
-                        self._cv.notify_all()
-            except BaseException as e:  # surfaced by wait_turns
-                with self._cv:
-                    self.errors.append(e)
-                    self._cv.notify_all()
-
-        self._threads = [threading.Thread(target=worker, args=(ids,), daemon=True) for ids in idx]
-        for t in self._threads:
-            t.start()
+def engine_time_split(st0, st1, window_s: float) -> dict:
+    """Where the timed window went, per THREAD.  The step-loop timers are disjoint, so with one engine
+    they partition its thread's window (``step_loop_other_s``: waiting for work, scheduling glue);
+    the caller-side timers (prompt encode at submit, results) run on the routing threads at the same
+    time and are reported apart, never subtracted from the window (which made the round-4 field
+    negative).  Several engines (co-located tiers, replicas) each have their own step loop: their
+    sums are reported without the remainder."""
+    d = lambda k: round(sum(b.get(k, 0.0) - a.get(k, 0.0) for a, b in zip(st0, st1)), 3)
+    loop = {k: d(k) for k in STEP_LOOP_TIMERS}
+    if len(st0) == 1:
+        loop["step_loop_other_s"] = round(max(0.0, window_s - sum(loop.values())), 3)
+    return {"step_loop": loop, "caller_threads": {k: d(k) for k in CLIENT_TIMERS}, "engines": len(st0)}
 
 
 def main() -> int:
@@ -497,8 +450,6 @@ def main() -> int:
     if topology == "replicated":
         baseline_config = 2
     layout = None
-    if a.pipeline is None:
-        a.pipeline = 2 if topology in ("replicated", "tiers") and a.groups <= 1 else 0
     cfg = dict(PRODUCTION_CFG, token_threshold=a.threshold, enable_response_cache=False, tokens_from_engine=True,
                cache_index_device=dev if on_gpu else None, cache_max_size=1 << 20)
     if topology in ("pools", "colocated"):
@@ -617,16 +568,7 @@ def main() -> int:
         pools_for_router = cluster.router_pools() if cluster is not None else pools
         router = Router(strategy=a.strategy, config=cfg, threshold_fallback=a.threshold, benchmark_mode=False,
                         pools=pools_for_router)
-        if a.gc_freeze:
-            # serving-process GC hygiene: everything allocated at start-up (weights' Python wrappers,
-            # tokenizer tables, captured graphs) moves to the permanent generation and the young
-            # generations collect less often, so the step loop is not paused by full collections
-            # scanning start-up objects (a paused step loop leaves the GPU idle between steps)
-            import gc
-            gc.collect()
-            gc.freeze()
-            gc.set_threshold(50000, 50, 100)
-        pipelined = (bool(a.pipeline) or a.groups > 1) and cluster is None
+        pipelined = bool(a.pipeline)
         if pipelined:
             # the engine's step loop and the routing driver are two Python threads: a short GIL
             # switch interval (0.5 ms; Python's default is 5) hands the GIL back to the step loop
@@ -635,11 +577,7 @@ def main() -> int:
             for e in engines:
                 e.ADMIT_EVERY = max(1, a.admit_every)
                 e.start()              # background step loop: callers only enqueue and wait
-            convs = (GroupedConversations(n_convs, rank, a.groups) if a.groups > 1
-                     else EventConversations(n_convs, rank) if a.pipeline == 2
-                     else PipelinedConversations(n_convs, rank))
-            if a.yield_to_engine:
-                convs.engines = engines
+            convs = EventConversations(n_convs, rank) if a.pipeline == 2 else PipelinedConversations(n_convs, rank)
             convs.start(router)
             convs.wait_turns(a.warmup * n_convs)
         else:
@@ -647,8 +585,11 @@ def main() -> int:
             for _ in range(a.warmup):
                 convs.step(router)
         if pipelined:
-            # steady-state window: the turns completing from here on are the timed ones
-            if world > 1:
+            # steady-state window: the turns completing from here on are the timed ones; the node
+            # barrier (cluster: every pool rank records it as its window start) opens it everywhere
+            if cluster is not None:
+                cluster.sync()
+            elif world > 1:
                 dist.barrier()         # replicas open their windows together
             with convs._cv:
                 st0 = [dict(e.stats()) for e in engines]
@@ -659,7 +600,8 @@ def main() -> int:
                 cpu0 = _thread_cpu() if os.environ.get("DLLM_THREAD_CPU") == "1" else None
                 t0 = time.perf_counter()
                 convs.records = records
-            convs.wait_turns((a.warmup + a.steps) * n_convs)
+                start_count = convs.completed   # (turns completed during the opening barrier are warmup)
+            convs.wait_turns(start_count + a.steps * n_convs)
             with convs._cv:
                 convs.records = None
                 if on_gpu:
@@ -669,6 +611,8 @@ def main() -> int:
                 e1 = meter.mark() if meter else None
                 st1 = [dict(e.stats()) for e in engines]
                 enc1 = encoder_stats()
+            if cluster is not None:
+                cluster.sync()         # closes the pool ranks' windows
             convs.stop()
         else:
             st0 = [dict(e.stats()) for e in engines]
@@ -763,17 +707,18 @@ def main() -> int:
                        "strategy": a.strategy, "semantic_cache": True, "response_cache": False,
                        "perf_explore": bool(cfg.get("perf_explore")),
                        "penalise_failed_primary": bool(cfg.get("penalise_failed_primary")),
-                       "turn_pipelining": ((("event-driver" if a.pipeline == 2 else "thread-per-conversation")
-                                            if a.pipeline else "grouped" if a.groups > 1 else False)
-                                           if cluster is None else False),
-                       "admit_every": a.admit_every if (a.pipeline or a.groups > 1) else None,
-                       "gc_freeze": bool(a.gc_freeze),
-                       "gil_switch_ms": a.gil_switch_ms if (a.pipeline or a.groups > 1) else None,
-                       "yield_to_engine": bool(a.yield_to_engine) if a.pipeline == 2 else None,
+                       "turn_pipelining": (("event-driver" if a.pipeline == 2 else "thread-per-conversation")
+                                           if a.pipeline else False),
+                       "admit_every": a.admit_every if a.pipeline else None,
+                       "gil_switch_ms": a.gil_switch_ms if a.pipeline else None,
                        "early_prefill": os.environ.get("DLLM_EARLY_PREFILL", "1") == "1",
-                       "conversation_groups": a.groups,
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
+            # client side, as the reference harness times a turn (routing_chatbot_tester.py:408-442):
+            # dispatch (routing included) to the answer being back in the driver, failover included
             "p50_latency_ms": round(statistics.median(lats), 1) if lats else None,
+            "latency_basis": "client: turn dispatched -> answer collected (routing, queueing, failover included)",
+            "p50_engine_latency_ms": (round(statistics.median(r["lat_engine"] for r in records), 1)
+                                      if records and all("lat_engine" in r for r in records) else None),
             "p90_latency_ms": round(pct(0.9), 1),
             "p50_speedup_vs_baseline_mean_latency": (round(BASELINE_S_PER_QUERY * 1000.0 / statistics.median(lats), 1)
                                                      if lats else None),
@@ -786,9 +731,7 @@ def main() -> int:
                                          / max(elapsed_max, 1e-9), 1),
             "avg_decode_batch": round(sum(b["decode_tokens"] - a_["decode_tokens"] for a_, b in zip(st0, st1))
                                       / max(1, sum(b["decode"] - a_["decode"] for a_, b in zip(st0, st1))), 1),
-            "engine_time_split_s": {k: round(sum(b_.get(k, 0.0) - a_.get(k, 0.0) for a_, b_ in zip(st0, st1)), 3)
-                                    for k in ("t_prefill_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
-                                              "t_decode_host_post_s", "t_encode_s", "t_admit_s", "t_output_s")},
+            "engine_time_split_s": engine_time_split(st0, st1, elapsed_max),
         }
         if energy_j >= 0:
             # every rank's GPU over the timed window (energy counter deltas summed over ranks)
@@ -811,9 +754,6 @@ def main() -> int:
             "failovers_by_step": (
                 [sum(1 for r in fo if r["step"] == st) for st in range(first_fo, a.warmup + a.steps)]
                 if first_fo is not None else [])}
-        # rank-0 wall time not inside any engine timer: routing, prompt formatting, orchestration
-        out["engine_time_split_s"]["outside_engine_s"] = round(
-            elapsed_max - sum(out["engine_time_split_s"].values()), 3) if len(engines) == 1 else None
         lk = enc1["lookups"] - enc0["lookups"]
         out["router_encoder"] = {"kinds": enc1["kinds"], "memo": bool(enc1.get("memo_enabled", False)),
                                  "lookups": lk, "memo_hit_rate": round((enc1["hits"] - enc0["hits"]) / lk, 3) if lk else None,

@@ -32,6 +32,7 @@ import torch
 from .. import ops
 from ..models.configs import ModelConfig, get_model_config
 from ..models.llama import AttnMeta, LlamaModel
+from ..utils.faults import fault
 from ..parallel.comm import SINGLE, ParallelContext
 from ..utils.tracing import tracer
 from .sampling import SamplingParams
@@ -94,7 +95,11 @@ class _Seq:
 
     def finish(self) -> None:
         """Mark done: wakes ``done`` waiters, then hands the sequence to ``notify`` (an event-driven
-        client's completion queue), so one client thread never has to poll hundreds of handles."""
+        client's completion queue), so one client thread never has to poll hundreds of handles.
+        Idempotent: a row that stops inside a pipelined burst is finished early (``_complete_early``)
+        and again when its blocks are released; ``notify`` fires only on the first call."""
+        if self.done.is_set():
+            return
         self.done.set()
         if self.notify is not None:
             self.notify(self)
@@ -178,7 +183,9 @@ class LLMEngine:
         self._check_graph_collectives()
         self.steps = {"prefill": 0, "decode": 0, "prefill_tokens": 0, "decode_tokens": 0}
         self.timers = {"prefill": 0.0, "decode_host_pre": 0.0, "decode_gpu_wait": 0.0, "decode_host_post": 0.0,
-                       "encode": 0.0, "admit": 0.0, "output": 0.0}
+                       "encode": 0.0, "admit": 0.0, "output": 0.0, "complete": 0.0}
+        # step-loop timers (disjoint): prefill, admit, decode_host_pre / gpu_wait / host_post, complete
+        # (answers detokenised under the next step); caller-side: encode (submit), output (results)
 
     # ------------------------------------------------------------------ setup
     def _alloc_kv(self, kv_cache_gb: Optional[float]) -> None:
@@ -214,6 +221,7 @@ class LLMEngine:
         self.bt_dev = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, device=self.device)
         self._bt_dirty = True          # whole-table copy needed (admissions / releases)
         self._bt_hw = 0                # block-table columns ever used (the host -> device copy width)
+        self._bt_rows = [R + 1, -1]    # [lo, hi] rows rewritten since the last sync (async copy range)
         self._bt_upd: List[int] = []   # (flat index, block) pairs applied inside the decode graph
         self.buckets = decode_buckets(R)
         mb = self.buckets[-1]
@@ -692,13 +700,16 @@ class LLMEngine:
                     waiting.insert(0, s)  # re-admitted with fill = prompt + out (recompute)
                 self.timers["decode_host_post"] += time.perf_counter() - _t
 
-    def _admit(self, waiting: List[_Seq], prefilling: List[_Seq], n_running: int) -> None:
-        """Move waiting requests that fit (a free row, KV blocks for prompt + 1) to ``prefilling``."""
+    def _admit(self, waiting: List[_Seq], prefilling: List[_Seq], n_running: int, reserve_blocks: int = 0) -> None:
+        """Move waiting requests that fit (a free row, KV blocks for prompt + 1) to ``prefilling``.
+        ``reserve_blocks``: free blocks held back for running rows that are about to open a new block
+        (an admission under a running burst must not take the block a continuing row reserves next)."""
         _ta = time.perf_counter()
+        margin = reserve_blocks * BS
         while waiting and self._free_rows and len(prefilling) + n_running < self.R:
             s = waiting[0]
             s.fill = s.prompt + s.out
-            if not self.bm.can_allocate(len(s.fill) + 1):
+            if not self.bm.can_allocate(len(s.fill) + 1 + margin):
                 break
             table, cached = self.bm.allocate(s.id, s.fill)
             if not table:
@@ -736,6 +747,7 @@ class LLMEngine:
             s.finish()
         if s.row >= 0:
             self.bt_host[s.row].fill(0)
+            self._mark_bt_row(s.row)
             self._free_rows.append(s.row)
             s.row = -1
 
@@ -753,6 +765,11 @@ class LLMEngine:
         self.bt_host[s.row, :len(t)] = t
         self._bt_hw = max(self._bt_hw, len(t))
         self._bt_dirty = True
+        self._mark_bt_row(s.row)
+
+    def _mark_bt_row(self, row: int) -> None:
+        lo, hi = self._bt_rows
+        self._bt_rows = [min(lo, row), max(hi, row)]
 
     def _note_upd_cols(self) -> None:
         """Widen the host -> device block-table copy to every column a queued update writes."""
@@ -767,12 +784,15 @@ class LLMEngine:
         row before the copy runs only by admitting into it (which queues another copy) or by
         opening a new block (which the step's in-graph scatter applies as well)."""
         if self._bt_dirty and non_blocking:
-            self._note_upd_cols()
-            hw = min(self._bt_hw, self.max_blocks)
-            if hw > 0:
-                self.bt_dev[:, :hw].copy_(self.bt_host_t[:, :hw], non_blocking=True)
-            self._bt_dirty = False
-            self._bt_upd.clear()
+            # whole rows of the pinned mirror are contiguous, so this copy really is asynchronous
+            # (a column slice would be staged through pageable memory, which waits for the stream:
+            # ADVICE r4); the range spans every row rewritten since the last sync, and queued
+            # per-step updates of other rows are applied by the step's own in-graph scatter
+            lo, hi = self._bt_rows
+            if hi >= lo:
+                self.bt_dev[lo:hi + 1].copy_(self.bt_host_t[lo:hi + 1], non_blocking=True)
+            self._bt_rows = [self.bt_host_t.shape[0], -1]
+            self._bt_dirty = False   # (_bt_upd stays queued for the next step's scatter)
             return
         if self._bt_dirty:
             # rare (admission / release): synchronous copy of the columns any row has used (a 128K
@@ -784,6 +804,7 @@ class LLMEngine:
                 self.bt_dev.copy_(self.bt_host_t, non_blocking=False)
             elif hw > 0:
                 self.bt_dev[:, :hw].copy_(self.bt_host_t[:, :hw], non_blocking=False)
+            self._bt_rows = [self.bt_host_t.shape[0], -1]
             self._bt_dirty = False
             self._bt_upd.clear()
 
@@ -1215,23 +1236,28 @@ class LLMEngine:
     # the in-flight step writes.  Single-GPU pools only (TP admissions follow the mirrored schedule).
     EARLY_PREFILL = os.environ.get("DLLM_EARLY_PREFILL", "1") == "1"
 
-    def _early_admit(self, waiting: List[_Seq], prefilling: Optional[List[_Seq]], n_running: int) -> None:
+    def _early_admit(self, waiting: List[_Seq], prefilling: Optional[List[_Seq]], running: List[_Seq]) -> None:
         if (prefilling is None or self._early_pf is not None or not self.EARLY_PREFILL or self.par.enabled
                 or not self.fused_sampler):
             return
         _t = time.perf_counter()
+        adm0 = self.timers["admit"]
         crit = self.host_critical.is_set()
         self.host_critical.set()          # admission host work: in-process clients hold off (bench)
         new = self._take_inbox(final=False)
         self._active.extend(new)          # a failing step must still find them (_abort_all)
         waiting.extend(new)
-        self._admit(waiting, prefilling, n_running)
+        # the drain's commit_append runs after this admission: hold back one block for every running
+        # row whose next two tokens cross a block boundary (otherwise a just-admitted
+        # request can take the block and preempt a running row into a full recompute)
+        reserve = sum(1 for s in running if (s.length + 2) // BS != s.length // BS)
+        self._admit(waiting, prefilling, len(running), reserve_blocks=reserve)
         if prefilling:
             with tracer.span("engine.prefill_early", "engine", seqs=len(prefilling)):
                 self._early_pf = self._prefill_launch(prefilling)
         if not crit:
             self.host_critical.clear()
-        self.timers["prefill"] += time.perf_counter() - _t
+        self.timers["prefill"] += time.perf_counter() - _t - (self.timers["admit"] - adm0)
 
     # BURST_JOIN: a pipelined burst no longer ends for admissions.  New requests are admitted and
     # prefilled under the running burst (EARLY_PREFILL), their sequences JOIN the next step once
@@ -1309,6 +1335,7 @@ class LLMEngine:
         freed = False               # a row finished while requests wait for one: end the burst
         while True:
             _t0 = time.perf_counter()
+            nested0 = self.timers["prefill"] + self.timers["admit"]   # in-burst admission work (own timers)
             alive = [s for s in cur if id(s) not in gone]
             # the next step's rows: sequences that cannot reach a count limit with the token in flight
             nxt = [s for s in alive if len(s.out) + 1 < s.params.max_new_tokens and s.length + 1 < mml]
@@ -1369,11 +1396,11 @@ class LLMEngine:
                 if (join and (self._inbox or waiting) and self._early_pf is None
                         and nsteps - admit_at >= self.ADMIT_EVERY):
                     admit_at = nsteps
-                    self._early_admit(waiting, prefilling, len(run))
+                    self._early_admit(waiting, prefilling, run)
             if launched is None:
                 self.host_critical.set()      # until the next burst's first step is launched
                 if stop and self._inbox:
-                    self._early_admit(waiting, prefilling, len(cur))
+                    self._early_admit(waiting, prefilling, [c for c in cur if id(c) not in gone])
             _t1 = time.perf_counter()
             ev.synchronize()
             if self._sync_log is not None:   # diagnostics: how long the loop waited for the step
@@ -1432,7 +1459,7 @@ class LLMEngine:
                     if self.bt_host[s.row, nblk - 1] != blk:
                         self.bt_host[s.row, nblk - 1] = blk
                         self._bt_upd.extend((s.row * mb_ + nblk - 1, blk))
-            self.timers["decode_host_pre"] += _t1 - _t0
+            self.timers["decode_host_pre"] += _t1 - _t0 - (self.timers["prefill"] + self.timers["admit"] - nested0)
             self.timers["decode_gpu_wait"] += _t2 - _t1
             self.timers["decode_host_post"] += time.perf_counter() - _t2
             if launched is None or tripped:
@@ -1449,7 +1476,7 @@ class LLMEngine:
                 _t3 = time.perf_counter()
                 for s in done_now:
                     self._complete_early(s)
-                self.timers["output"] += time.perf_counter() - _t3
+                self.timers["complete"] += time.perf_counter() - _t3
                 if join:
                     release_next.extend(done_now)
             freed = bool(waiting) and bool(done_now or preempted)
@@ -1475,13 +1502,13 @@ class LLMEngine:
         s.finish()
 
     # fault injection (tests): force a collective trip on the Nth decode / prefill step of every rank
-    FAULT_TRIP_DECODE = int(os.environ.get("DLLM_FAULT_CAR_TRIP_DECODE", "-1"))
-    FAULT_TRIP_PREFILL = int(os.environ.get("DLLM_FAULT_CAR_TRIP_PREFILL", "-1"))
+    FAULT_TRIP_DECODE = fault("car_trip_decode", -1, int)
+    FAULT_TRIP_PREFILL = fault("car_trip_prefill", -1, int)
 
     # fault injection (tests): on decode step FAULT_VOTE_DECODE, rank FAULT_VOTE_RANK's one-shot
     # all-reduce flag is raised DURING the in-graph health vote (after its vote was staged)
-    FAULT_VOTE_DECODE = int(os.environ.get("DLLM_FAULT_CAR_VOTE_DECODE", "-1"))
-    FAULT_VOTE_RANK = int(os.environ.get("DLLM_FAULT_CAR_VOTE_RANK", "0"))
+    FAULT_VOTE_DECODE = fault("car_vote_decode", -1, int)
+    FAULT_VOTE_RANK = fault("car_vote_rank", 0, int)
 
     def _arm_vote_fault(self) -> None:
         car = self.par.custom_ar

@@ -365,36 +365,66 @@ class Router:
         never notified; a handle can finish (and be notified) before this returns."""
         tickets: List[Dict[str, Any]] = []
         groups: Dict[str, List[int]] = {SMALL: [], LARGE: []}
+        t0 = time.perf_counter()
         for i, (kind, a, dec) in enumerate(self._decide_batch(histories)):
-            t: Dict[str, Any] = {"history": histories[i], "t0": time.perf_counter()}
+            t: Dict[str, Any] = {"history": histories[i], "t0": t0}
             if kind == "hit":
                 t["payload"] = a
+                t["latency_ms"] = (time.perf_counter() - t0) * 1000.0
             else:
                 t["query"], t["dec"], t["device"] = a, dec, dec["device"]
-                groups[dec["device"]].append(i)
+                if self._pool_down(dec["device"]):   # a tier known to be down: fail over up front
+                    t["failover_from"], t["device"] = dec["device"], other_tier(dec["device"])
+                groups[t["device"]].append(i)
             tickets.append(t)
         for dev, idx in groups.items():
             if not idx:
                 continue
-            pool = self.pools[dev]
-            hs = [histories[i] for i in idx]
-            sub = getattr(pool, "submit_batch", None)
-            if sub is not None:
-                for i, h in zip(idx, sub(hs) if notify is None else sub(hs, notify=notify)):
-                    tickets[i]["handle"] = h
-            else:
-                for i, raw in zip(idx, self._process_groups({dev: idx}, histories)[dev]):
-                    tickets[i]["raw"] = raw[0]
+            self._submit_tickets(dev, [tickets[i] for i in idx], notify)
         return tickets
+
+    def _submit_tickets(self, dev: str, tickets: List[Dict[str, Any]], notify) -> None:
+        """Hand tickets to pool ``dev`` without waiting where it can (``submit_batch``; a failover
+        ticket goes by ``submit_failover`` - token ids over the data plane to a remote pool - when
+        the pool has it); a pool with only the blocking API is served here."""
+        pool = self.pools[dev]
+        hs = [t["history"] for t in tickets]
+        fo = all("failover_from" in t for t in tickets)
+        sub = (getattr(pool, "submit_failover", None) if fo else None) or getattr(pool, "submit_batch", None)
+        if sub is not None:
+            try:
+                handles = sub(hs) if notify is None else sub(hs, notify=notify)
+            except Exception as exc:  # noqa: BLE001 - a pool that raises: error payloads, done now
+                for t in tickets:
+                    t.pop("handle", None)
+                    t["raw"] = {"error": f"pool {dev} failed: {exc}"}
+                return
+            for t, h in zip(tickets, handles):
+                t["handle"] = h
+                t.pop("raw", None)
+        else:
+            for t in tickets:
+                raw, _, _ = self._run(dev, t["history"], failover="failover_from" in t)
+                t.pop("handle", None)
+                t["raw"] = raw
 
     @staticmethod
     def ticket_done(t: Dict[str, Any]) -> bool:
         h = t.get("handle")
         return h is None or h.done.is_set()
 
-    def finish_ticket(self, t: Dict[str, Any]):
+    def finish_ticket(self, t: Dict[str, Any], notify: Optional[Callable[[Any], None]] = None):
         """(payload, response_tokens, device) of a done ticket: perf feedback, failover to the
-        other tier (synchronously) on an error, response-cache store — as ``route_query``."""
+        other tier on an error, response-cache store — as ``route_query``.
+
+        Failover is non-blocking when the client passes its completion sink (``notify``) and the
+        other tier's pool can submit: the request is re-submitted there and this returns ``None``
+        (the ticket is in flight again, under its new ``handle``; finish it once more when that is
+        done), so one failed turn never stalls the client's other conversations (the reference
+        fails over on the request's own thread, src/router.py:277-282).  Otherwise (no sink, a
+        blocking pool) the failover generation runs here, as before.  ``t["latency_ms"]`` is set to
+        the client-side turn latency: dispatch to completion, failover included (the reference
+        harness times the whole ``route_query``, routing_chatbot_tester.py:408-442)."""
         if "payload" in t:
             return t["payload"]
         which = t["device"]
@@ -404,12 +434,25 @@ class Router:
             raw = t["raw"]
         lat = float(raw["latency_ms"]) if isinstance(raw, dict) and "latency_ms" in raw else \
             (time.perf_counter() - t["t0"]) * 1000.0
-        failed = None
-        if self.enable_failover and is_error(raw):
-            raw2, which2, lat2 = self._run(other_tier(which), t["history"], failover=True)
+        failed = t.get("failover_from")
+        if self.enable_failover and is_error(raw) and failed is None:
+            other = other_tier(which)
+            pool = self.pools[other]
+            if notify is not None and (getattr(pool, "submit_failover", None) or getattr(pool, "submit_batch", None)):
+                t["failover_from"], t["device"] = which, other
+                t["primary_error"] = raw
+                self._submit_tickets(other, [t], notify)
+                if "handle" in t:
+                    return None   # in flight on the other tier
+                return self.finish_ticket(t, notify)   # the pool refused it at once: finish now
+            raw2, which2, lat2 = self._run(other, t["history"], failover=True)
             if not is_error(raw2):
                 failed = which
                 raw, which, lat = raw2, which2, lat2
+        elif failed is not None and is_error(raw) and "primary_error" in t:
+            # the failover failed too: report the primary's error, no failover (as route_query)
+            raw, which, failed = t["primary_error"], failed, None
+        t["latency_ms"] = (time.perf_counter() - t["t0"]) * 1000.0
         return self._finish(t["query"], t["dec"], raw, which, lat, failed)
 
     def _prefetch_embeddings(self, queries: List[str]) -> None:

@@ -23,7 +23,7 @@ import threading
 import time
 import urllib.error
 import urllib.request
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 from ..config import LARGE, SMALL
 
@@ -88,6 +88,73 @@ class Coalescer:
         return job["out"]
 
 
+class PoolHandle:
+    """One request submitted without waiting (``submit_batch``): ``done`` fires when ``reply`` (a
+    pool payload: ``{"response": ...}`` or ``{"error": ...}``) is set, and ``notify(handle)`` (an
+    event-driven client's completion queue) is called exactly once, from whichever thread
+    completed it.  Remote pools complete handles from their receiver thread; a deadline reaper
+    fails handles a hung pool never answers (the reference's per-request ``timeout=(5, 180)``)."""
+
+    __slots__ = ("done", "reply", "notify", "deadline", "owner", "_lock")
+
+    def __init__(self, notify: Optional[Callable[["PoolHandle"], None]] = None, deadline: Optional[float] = None):
+        self.done = threading.Event()
+        self.reply: Optional[Dict[str, Any]] = None
+        self.notify = notify
+        self.deadline = deadline
+        self.owner = None            # ReplicatedPool: the replica that serves it
+        self._lock = threading.Lock()
+
+    def complete(self, reply: Dict[str, Any]) -> bool:
+        """Set the reply once (later completions - a late reply after a timeout - are dropped)."""
+        with self._lock:
+            if self.done.is_set():
+                return False
+            self.reply = reply
+            self.done.set()
+        if self.notify is not None:
+            try:
+                self.notify(self)
+            except Exception:  # noqa: BLE001 - a client sink must never kill a pool thread
+                pass
+        return True
+
+    def payload(self) -> Dict[str, Any]:
+        return self.reply if self.reply is not None else {"error": "request not finished"}
+
+
+class ThreadSubmit:
+    """``submit_batch`` / ``collect`` for a pool whose only entry is the blocking
+    ``process_batch`` (echo / fault-injecting / HTTP pools): the batch is served on a small
+    executor and its handles complete when it returns, so an event-driven client is never blocked
+    by a synchronous pool."""
+
+    _submit_workers = 8
+
+    def submit_batch(self, histories, overrides: Optional[Dict[str, Any]] = None, notify=None) -> List[PoolHandle]:
+        ex = getattr(self, "_submit_ex", None)
+        if ex is None:
+            from concurrent.futures import ThreadPoolExecutor
+            ex = self._submit_ex = ThreadPoolExecutor(self._submit_workers, thread_name_prefix=f"dllm-sub-{self.name}")
+        hs = [PoolHandle(notify) for _ in histories]
+
+        def run():
+            try:
+                res = list(self.process_batch(list(histories)))
+                if len(res) != len(hs):
+                    raise RuntimeError(f"pool returned {len(res)} results for {len(hs)} requests")
+            except Exception as e:  # noqa: BLE001 - every handle sees the failure
+                res = [{"error": f"pool {self.name} failed: {e}"}] * len(hs)
+            for h, r in zip(hs, res):
+                h.complete(r)
+        ex.submit(run)
+        return hs
+
+    @staticmethod
+    def collect(handles) -> List[Dict[str, Any]]:
+        return [h.payload() for h in handles]
+
+
 class NullServerManager:
     """In-process pools are always 'running'; kept for harness API compatibility."""
 
@@ -120,7 +187,7 @@ class PoolClient:
         return {"ok": True}
 
 
-class EchoPool(PoolClient):
+class EchoPool(ThreadSubmit, PoolClient):
     """Deterministic CPU backend: echoes the last user turn, ``tokens_per_reply`` words long."""
 
     def __init__(self, name: str = SMALL, tokens_per_reply: int = 16, delay_s: float = 0.0):
@@ -145,7 +212,7 @@ class EchoPool(PoolClient):
         return {"response": reply, "num_tokens": self.tokens_per_reply}
 
 
-class FaultInjectingPool(PoolClient):
+class FaultInjectingPool(ThreadSubmit, PoolClient):
     """Wraps a pool; ``mode`` in {"ok", "error", "timeout", "flaky"}."""
 
     def __init__(self, inner: PoolClient, mode: str = "error", p: float = 0.5, seed: int = 0,

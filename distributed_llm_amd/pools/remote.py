@@ -46,7 +46,8 @@ from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 from ..parallel import p2p
-from .base import EnginePool, NullServerManager, PoolClient, format_prompt
+from ..utils.faults import fault
+from .base import EnginePool, NullServerManager, PoolClient, PoolHandle, format_prompt
 
 TAG_REQ, TAG_REP = 1, 2
 
@@ -125,7 +126,9 @@ class RemotePool(PoolClient):
                 return
             with self._plock:
                 ent = self._pending.pop(msg.get("id"), None)
-            if ent is not None:
+            if isinstance(ent, PoolHandle):       # a submitted request: its own payload
+                ent.complete(msg.get("result") or {"error": msg.get("error", "empty reply")})
+            elif ent is not None:
                 ent.reply = msg
                 ent.event.set()
 
@@ -134,8 +137,11 @@ class RemotePool(PoolClient):
         with self._plock:
             pend, self._pending = self._pending, {}
         for ent in pend.values():
-            ent.reply = {"error": why}
-            ent.event.set()
+            if isinstance(ent, PoolHandle):
+                ent.complete({"error": why})
+            else:
+                ent.reply = {"error": why}
+                ent.event.set()
 
     def _send(self, msg: Dict[str, Any]) -> None:
         with self._send_lock:
@@ -216,6 +222,99 @@ class RemotePool(PoolClient):
             if not (isinstance(r, dict) and "data plane" in str(r.get("error", ""))):
                 return r
         return self.process(history)
+
+    # ------------------------------------------------------------------ non-blocking requests
+    def submit_batch(self, histories: Sequence[Any], overrides: Optional[Dict[str, Any]] = None,
+                     notify=None) -> List[PoolHandle]:
+        """Send the requests WITHOUT waiting: one tagged id per request, so the leader's engine
+        admits each into its running continuous batch and answers each on its own as soon as it
+        is done (``notify(handle)`` from the receiver thread).  Same deadline as ``process``: a
+        request the pool never answers is failed by the reaper; a dead pool fails every handle.
+        A pool already out of service returns handles that are done (error) and not notified."""
+        params = dict(self.params, **(overrides or {}))
+        return self._submit({"op": "submit", "prompts": [self.prompt_for(h) for h in histories], "params": params},
+                            len(histories), notify)
+
+    def submit_failover(self, histories: Sequence[Any], notify=None) -> List[PoolHandle]:
+        """Non-blocking failover hand-off: the prompts go over the data plane as token ids (as
+        ``process_failover``) when this router holds the pool's tokenizer and a live data plane,
+        else as text on the control plane."""
+        if self.tokenizer is not None and self.data_ok():
+            ids = [list(map(int, self.tokenizer.encode(self.prompt_for(h)))) for h in histories]
+
+            def ship():
+                for p in ids:
+                    p2p.send_tokens(p, self.leader, self.data, timeout_s=self.data_timeout_s)
+            hs = self._submit({"op": "submit_ids", "n": len(ids), "params": dict(self.params)}, len(ids), notify,
+                              data_fn=ship)
+            if not any(h.done.is_set() and "data plane" in str(h.payload().get("error", "")) for h in hs):
+                return hs
+        return self.submit_batch(histories, notify=notify)
+
+    def _submit(self, msg: Dict[str, Any], n: int, notify, data_fn=None) -> List[PoolHandle]:
+        deadline = time.monotonic() + self.timeout_s
+        hs = [PoolHandle(notify, deadline) for _ in range(n)]
+        if not self.alive:
+            for h in hs:
+                h.reply = {"error": f"pool {self.name} unavailable"}
+                h.done.set()
+            return hs
+        ids = [next(self._ids) for _ in range(n)]
+        msg["ids"] = ids
+        msg["id"] = 0
+        with self._plock:
+            for rid, h in zip(ids, hs):
+                self._pending[rid] = h
+        err = None
+        try:
+            if data_fn is None:
+                self._send(msg)
+            else:
+                if not self._data_lock.acquire(timeout=self.data_timeout_s):
+                    raise p2p.DataPlaneTimeout("data plane busy (a transfer is stuck)")
+                try:
+                    self._send(msg)
+                    data_fn()
+                finally:
+                    self._data_lock.release()
+        except p2p.DataPlaneTimeout as e:
+            self._retire_data(str(e))
+            err = {"error": f"pool {self.name} data plane: {e}", "data_plane_failed": True}
+        except Exception as e:  # noqa: BLE001 - transport gone: this pool is out of service
+            self._fail_all(f"pool {self.name} send failed: {e}")
+            return hs
+        if err is not None:
+            with self._plock:
+                for rid in ids:
+                    self._pending.pop(rid, None)
+            for h in hs:   # not sent / not shipped: done, not notified (the caller sees it at once)
+                h.reply = err
+                h.done.set()
+            return hs
+        self._start_reaper()
+        return hs
+
+    def _start_reaper(self) -> None:
+        if getattr(self, "_reaper", None) is not None:
+            return
+        self._reaper = threading.Thread(target=self._reap_loop, name=f"dllm-reap-{self.name}", daemon=True)
+        self._reaper.start()
+
+    def _reap_loop(self, period_s: float = 0.5) -> None:
+        """Fail submitted requests past their deadline (a hung pool): the caller fails over."""
+        while not self._probe_stop.wait(period_s):
+            now = time.monotonic()
+            with self._plock:
+                late = [rid for rid, e in self._pending.items()
+                        if isinstance(e, PoolHandle) and e.deadline is not None and e.deadline < now]
+                ents = [self._pending.pop(rid) for rid in late]
+            for e in ents:
+                self.timeouts += 1
+                e.complete({"error": f"Request timed out on {self.name} after {self.timeout_s:.1f}s"})
+
+    @staticmethod
+    def collect(handles: Sequence[PoolHandle]) -> List[Dict[str, Any]]:
+        return [h.payload() for h in handles]
 
     @staticmethod
     def _results(rep: Dict[str, Any], n: int) -> List[Dict[str, Any]]:
@@ -338,6 +437,14 @@ class PoolLeader:
         self._dq: "queue.Queue" = queue.Queue()
         self._dthread = threading.Thread(target=self._data_loop, name="dllm-pool-data", daemon=True)
         self._dthread.start()
+        # submitted requests (op "submit" / "submit_ids"): the engine's completion callback only
+        # queues the finished sequence; this thread forms its payload and replies, so the engine's
+        # step loop never blocks on the control-plane socket
+        self._rq: "queue.Queue" = queue.Queue()
+        self._rid: Dict[int, int] = {}          # id(sequence) -> request id
+        self._rid_cv = threading.Condition()
+        self._rthread = threading.Thread(target=self._reply_loop, name="dllm-pool-reply", daemon=True)
+        self._rthread.start()
 
     def _data_loop(self) -> None:
         while True:
@@ -348,21 +455,30 @@ class PoolLeader:
             if self.data_error is not None:   # retired: answer what needs an answer, move nothing
                 if op == "generate_ids":
                     self._safe_reply({"id": msg["id"], "error": f"data plane retired: {self.data_error}"})
+                elif op == "submit_ids":
+                    for rid in msg["ids"]:
+                        self._safe_reply({"id": rid, "error": f"data plane retired: {self.data_error}"})
                 continue
             try:
-                if op == "ping_data" and os.environ.get("DLLM_FAULT_DIE_ON_DATA_PING") == "1":
+                if op == "ping_data" and fault("die_on_data_ping") == "1":
                     os._exit(17)   # fault injection (tests): the leader dies during a data-plane ping
                 if op == "ping_data":
                     p2p.ping(self.router, self.data, initiator=False,
                              timeout_s=float(msg.get("timeout_s") or self.data_timeout_s))
-                elif op == "generate_ids":
+                elif op in ("generate_ids", "submit_ids"):
                     prompts = [p2p.recv_tokens(self.router, self.data, timeout_s=self.data_timeout_s).tolist()
                                for _ in range(int(msg["n"]))]
-                    self._ex.submit(self._generate, msg["id"], prompts, msg.get("params"))
+                    if op == "submit_ids":
+                        self._submit(msg["ids"], prompts, msg.get("params"))
+                    else:
+                        self._ex.submit(self._generate, msg["id"], prompts, msg.get("params"))
             except Exception as e:  # noqa: BLE001 - DataPlaneTimeout / transport: retire, report
                 self.data_error = str(e)
                 if op == "generate_ids":
                     self._safe_reply({"id": msg["id"], "error": f"data plane: {e}"})
+                elif op == "submit_ids":
+                    for rid in msg["ids"]:
+                        self._safe_reply({"id": rid, "error": f"data plane: {e}"})
 
     def _safe_reply(self, msg: Dict[str, Any]) -> None:
         try:
@@ -377,9 +493,9 @@ class PoolLeader:
     def _generate(self, rid: int, prompts, params) -> None:
         import os
         from ..engine.sampling import SamplingParams
-        hang = os.environ.get("DLLM_FAULT_HANG_ON")
+        hang = fault("hang_on")
         if hang and any(isinstance(p, str) and hang in p for p in prompts):
-            time.sleep(float(os.environ.get("DLLM_FAULT_HANG_S", "5")))   # fault injection (tests)
+            time.sleep(fault("hang_s", 5.0, float))   # fault injection (tests)
         try:
             sp = SamplingParams.from_dict(params or {})
             outs = self.engine.generate(prompts, sp)
@@ -390,6 +506,41 @@ class PoolLeader:
             self._reply(rep)
         except Exception:  # noqa: BLE001 - router gone; nothing to report to
             pass
+
+    def _submit(self, rids, prompts, params) -> None:
+        """Admit requests into the engine's running batch without a worker thread each; every
+        request is answered on its own when it finishes (``_reply_loop``)."""
+        from ..engine.sampling import SamplingParams
+        try:
+            seqs = self.engine.submit(prompts, SamplingParams.from_dict(params or {}), notify=self._rq.put)
+        except Exception as e:  # noqa: BLE001 - report, never kill the receiver loop
+            for rid in rids:
+                self._safe_reply({"id": rid, "error": f"engine failed: {e}"})
+            return
+        with self._rid_cv:
+            for s_, rid in zip(seqs, rids):
+                self._rid[id(s_)] = rid
+            self._rid_cv.notify_all()
+        for s_ in seqs:
+            if s_.error is not None and s_.done.is_set() and s_.notify is None:   # rejected up front
+                self._rq.put(s_)
+
+    def _reply_loop(self) -> None:
+        while True:
+            s_ = self._rq.get()
+            if s_ is None:
+                return
+            with self._rid_cv:   # the engine may finish a request before _submit has mapped it
+                rid = self._rid.pop(id(s_), None)
+                while rid is None and self._rid_cv.wait(timeout=5.0):
+                    rid = self._rid.pop(id(s_), None)
+            if rid is None:
+                continue
+            try:
+                res = EnginePool.to_payloads(self.engine.results([s_]))[0]
+            except Exception as e:  # noqa: BLE001
+                res = {"error": f"engine failed: {e}"}
+            self._safe_reply({"id": rid, "result": res})
 
     def serve(self) -> None:
         """Receive until the router sends stop (or disappears)."""
@@ -405,14 +556,16 @@ class PoolLeader:
                 if op == "stop":
                     self._dq.put(None)
                     self._ex.shutdown(wait=True)
+                    self._rq.put(None)
+                    self._rthread.join(timeout=30)
                     self._reply({"op": "bye"})
                     return
                 if op == "ping":
-                    nd = int(os.environ.get("DLLM_FAULT_PING_DELAY_N", "0"))
+                    nd = fault("ping_delay_n", 0, int)
                     if nd > 0:   # fault injection (tests): the first pings stall the receiver loop
                         self._pings_seen = getattr(self, "_pings_seen", 0) + 1
                         if self._pings_seen <= nd:
-                            time.sleep(float(os.environ.get("DLLM_FAULT_PING_DELAY_S", "1")))
+                            time.sleep(fault("ping_delay_s", 1.0, float))
                     self._reply({"id": msg["id"], "op": "pong",
                                  "stats": {k: v for k, v in self.engine.stats().items()
                                            if isinstance(v, (int, float, str))}})
@@ -423,20 +576,26 @@ class PoolLeader:
                     if self.on_sync is not None:
                         self.on_sync()
                 elif op == "generate":
-                    if os.environ.get("DLLM_FAULT_DIE_ON") and any(
-                            os.environ["DLLM_FAULT_DIE_ON"] in p for p in msg.get("prompts", [])):
+                    if fault("die_on") and any(fault("die_on") in p for p in msg.get("prompts", [])):
                         os._exit(17)   # fault injection (tests): the pool process dies mid-request
                     self._gen_seen = getattr(self, "_gen_seen", 0) + 1
-                    die_after = int(os.environ.get("DLLM_FAULT_DIE_AFTER", "0"))
-                    die_rank = os.environ.get("DLLM_FAULT_DIE_RANK")
+                    die_after, die_rank = fault("die_after", 0, int), fault("die_rank")
                     if die_after and self._gen_seen > die_after and (
                             die_rank is None or int(die_rank) == int(os.environ.get("RANK", "-1"))):
                         os._exit(17)   # fault injection (tests): this leader dies after N requests
                     self._ex.submit(self._generate, msg["id"], msg["prompts"], msg.get("params"))
-                elif op == "generate_ids":
+                elif op == "submit":
+                    self._gen_seen = getattr(self, "_gen_seen", 0) + 1
+                    die_after, die_rank = fault("die_after", 0, int), fault("die_rank")
+                    if die_after and self._gen_seen > die_after and (
+                            die_rank is None or int(die_rank) == int(os.environ.get("RANK", "-1"))):
+                        os._exit(17)   # fault injection (tests): this leader dies after N requests
+                    self._submit(msg["ids"], msg["prompts"], msg.get("params"))
+                elif op in ("generate_ids", "submit_ids"):
                     self._dq.put(msg)
         finally:
             self._dq.put(None)
+            self._rq.put(None)
             self.engine.stop()
 
 
@@ -452,6 +611,8 @@ class ReplicatedPool(PoolClient):
         self.inflight = [0] * len(replicas)
         self._lock = threading.Lock()
         self._ex = ThreadPoolExecutor(max_workers=len(replicas))
+        self._owner: Dict[int, int] = {}   # id(submitted handle) -> replica index (collect)
+        self._released: set = set()         # id(handle) already counted off its replica's load
 
     def _pick(self) -> int:
         with self._lock:
@@ -490,6 +651,76 @@ class ReplicatedPool(PoolClient):
                 with self._lock:
                     self.inflight[k] -= len(shards[k])
             for j, r in zip(shards[k], res):
+                out[j] = r
+        return out
+
+    # ------------------------------------------------------------------ non-blocking requests
+    def submit_batch(self, histories: Sequence[Any], overrides: Optional[Dict[str, Any]] = None,
+                     notify=None, failover: bool = False) -> List[Any]:
+        """Shard the requests over the live replicas (least-loaded first, round robin) and submit
+        each shard WITHOUT waiting; a replica's load drops as each of its requests completes.
+        Replicas without ``submit_batch`` are served on a thread (``ThreadSubmit``)."""
+        n = len(self.replicas)
+        with self._lock:
+            live = [k for k in range(n) if getattr(self.replicas[k], "alive", True)] or list(range(n))
+            order = sorted(live, key=lambda k: self.inflight[k])
+            shards: Dict[int, List[int]] = {k: [] for k in order}
+            for j in range(len(histories)):
+                shards[order[j % len(order)]].append(j)
+            for k, idx in shards.items():
+                self.inflight[k] += len(idx)
+        out: List[Any] = [None] * len(histories)
+        for k, idx in shards.items():
+            if not idx:
+                continue
+            rep = self.replicas[k]
+
+            def done_cb(h, k=k):
+                self._release(h, k)
+                if notify is not None:
+                    notify(h)
+            hs_ = [histories[j] for j in idx]
+            sub = getattr(rep, "submit_failover", None) if failover else None
+            if sub is not None:
+                hs = sub(hs_, notify=done_cb)
+            elif getattr(rep, "submit_batch", None) is not None:
+                hs = rep.submit_batch(hs_, overrides, notify=done_cb) if overrides else rep.submit_batch(hs_, notify=done_cb)
+            else:
+                from .base import ThreadSubmit
+                hs = ThreadSubmit.submit_batch(rep, hs_, overrides, notify=done_cb)
+            for j, h in zip(idx, hs):
+                self._owner[id(h)] = k
+                out[j] = h
+            for h in hs:   # finished already, or rejected up front (never notified): counted down now
+                if h.done.is_set():
+                    self._release(h, k)
+        return out
+
+    def _release(self, h, k: int) -> None:
+        """A submitted request stopped loading replica k (exactly once per handle)."""
+        with self._lock:
+            if id(h) in self._released:
+                return
+            self._released.add(id(h))
+            self.inflight[k] -= 1
+
+    def submit_failover(self, histories: Sequence[Any], notify=None) -> List[Any]:
+        return self.submit_batch(histories, notify=notify, failover=True)
+
+    def collect(self, handles: Sequence[Any]) -> List[Dict[str, Any]]:
+        out: List[Any] = [None] * len(handles)
+        by: Dict[int, List[int]] = {}
+        for j, h in enumerate(handles):
+            k = self._owner.pop(id(h), 0)
+            self._release(h, k)
+            with self._lock:
+                self._released.discard(id(h))
+            by.setdefault(k, []).append(j)
+        for k, idx in by.items():
+            rep = self.replicas[k]
+            col = getattr(rep, "collect", None)
+            res = col([handles[j] for j in idx]) if col is not None else [handles[j].payload() for j in idx]
+            for j, r in zip(idx, res):
                 out[j] = r
         return out
 

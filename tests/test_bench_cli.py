@@ -68,8 +68,7 @@ def test_bench_survives_pool_leader_death():
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), DLLM_EMBEDDER="hash", OMP_NUM_THREADS="1", DLLM_FAULT_DIE_RANK="2",
-                   DLLM_FAULT_DIE_AFTER="1")
+                   MASTER_PORT=str(port), DLLM_EMBEDDER="hash", OMP_NUM_THREADS="1", DLLM_FAULT="die_rank=2,die_after=1")
         procs.append(subprocess.Popen([sys.executable, "bench.py", "--cpu", "--gpus", str(world), "--steps", "3",
                                        "--warmup", "1", "--convs", "3", "--small-new", "4", "--large-new", "6",
                                        "--strategy", "hybrid"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
@@ -80,7 +79,8 @@ def test_bench_survives_pool_leader_death():
     out = json.loads(line[0])
     ev = out["pool_events"]
     assert ev["dead_ranks"] == [2] and ev["failed_tiers"] == ["orin"] and ev["degraded"]
-    assert ev["failovers"] > 0 and ev["lost_turns"] == 0 and out["requests"] == 3 * world * 3
+    # pipelined (the default): the window closes once steps x convs turns have completed in it
+    assert ev["failovers"] > 0 and ev["lost_turns"] == 0 and out["requests"] >= 3 * world * 3
 
 
 def test_bench_event_driven_turn_pipelining():

@@ -142,6 +142,30 @@ def test_submit_notifies_each_finished_request_once():
         eng.stop()
 
 
+def test_seq_finish_notifies_once():
+    """a row that stops inside a pipelined burst is finished by ``_complete_early`` and
+    again by ``_release``; the completion callback must still fire exactly once."""
+    from distributed_llm_amd.engine.llm_engine import _Seq
+    calls = []
+    s = _Seq(id=7, prompt=[1, 2], params=SamplingParams(), arrival=0.0, notify=calls.append)
+    s.finish()
+    s.finish()
+    assert calls == [s] and s.done.is_set()
+    eng = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=4, seed=0)
+    calls.clear()
+    sp = SamplingParams(max_new_tokens=4, temperature=0.0, ignore_eos=True)
+    eng.start()
+    try:
+        hs = eng.submit(["user: x\nassistant: "], [sp], notify=calls.append)
+        for h in hs:
+            assert h.done.wait(60)
+    finally:
+        eng.stop()
+    for h in hs:
+        eng._complete_early(h)   # a second completion path on an already-finished sequence
+    assert calls == hs
+
+
 def test_route_concurrent_matches_route_query():
     from distributed_llm_amd.config import BENCHMARK_CFG, LARGE, SMALL
     from distributed_llm_amd.orchestrator import Router

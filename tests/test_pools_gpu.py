@@ -157,7 +157,7 @@ def test_config4_large_leader_dies_mid_window_one_gpu(tmp_path):
     logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
     os.makedirs(logdir, exist_ok=True)
     codes, res, logs = _launch_ranks(8, ["--baseline-config", "4", *SMALL_RUN], logdir, "cfg4fo",
-                                     {"DLLM_FAULT_DIE_RANK": "4", "DLLM_FAULT_DIE_AFTER": "2"})
+                                     {"DLLM_FAULT": "die_rank=4,die_after=2"})
     assert codes[4] == 17 and [c for i, c in enumerate(codes) if i != 4] == [0] * 7, codes
     assert res is not None and res["baseline_config"] == 4
     ev = res["pool_events"]

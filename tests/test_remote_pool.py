@@ -58,7 +58,7 @@ def _worker(rank, world, port, scenario, q, env):
         import traceback
         q.put({"rank": rank, "error": f"{e!r}\n{traceback.format_exc()}"})
     finally:
-        if scenario in ("concurrent", "handoff", "revive", "stuck_lock"):
+        if scenario in ("concurrent", "handoff", "revive", "stuck_lock", "submit"):
             dist.destroy_process_group()
         else:
             q.close()
@@ -225,9 +225,38 @@ def _router_stuck_data_lock(ctrl, data):
             "busy_probe_skipped": busy_ok}
 
 
+def _router_submit(ctrl, data):
+    """Non-blocking submission (the event driver's path): one long and three short requests are
+    submitted from ONE thread without waiting; each completes on its own (the shorts first) and
+    reaches the completion queue exactly once; a failover hand-off is submitted the same way
+    (token ids over the data plane)."""
+    import queue
+    from distributed_llm_amd.pools.remote import RemotePool
+    from distributed_llm_amd.engine.tokenizer import get_tokenizer
+    from distributed_llm_amd.models.configs import get_model_config
+    cfg = get_model_config("tiny-llama-test")
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=4, timeout_s=120,
+                    tokenizer=get_tokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id))
+    q = queue.SimpleQueue()
+    t0 = time.perf_counter()
+    long_h = rp.submit_batch([[{"role": "user", "content": "request long"}]], {"max_new_tokens": 200}, notify=q.put)
+    time.sleep(0.3)
+    shorts = rp.submit_batch([[{"role": "user", "content": f"request s{i}"}] for i in range(3)],
+                             {"max_new_tokens": 3}, notify=q.put)
+    fo = rp.submit_failover([[{"role": "user", "content": "request fo"}]], notify=q.put)
+    submit_s = time.perf_counter() - t0
+    names = {id(long_h[0]): "long", id(fo[0]): "fo", **{id(h): f"s{i}" for i, h in enumerate(shorts)}}
+    order = [names[id(q.get(timeout=120))] for _ in range(5)]
+    extra = q.empty()
+    res = rp.collect(long_h + shorts + fo)
+    rp.stop()
+    return {"order": order, "once": extra, "errors": [r.get("error") for r in res],
+            "tokens": [r.get("num_tokens") for r in res], "submit_s": submit_s}
+
+
 _ROUTER = {"concurrent": _router_concurrent, "kill": _router_kill, "hang": _router_hang,
            "handoff": _router_handoff, "data_die": _router_die_in_data_ping, "revive": _router_revive,
-           "stuck_lock": _router_stuck_data_lock}
+           "stuck_lock": _router_stuck_data_lock, "submit": _router_submit}
 
 
 def _run(scenario, env=None, timeout=240):
@@ -239,7 +268,7 @@ def _run(scenario, env=None, timeout=240):
         p.start()
     outs = []
     try:
-        for _ in range(2 if scenario in ("concurrent", "handoff", "revive", "stuck_lock") else 1):
+        for _ in range(2 if scenario in ("concurrent", "handoff", "revive", "stuck_lock", "submit") else 1):
             outs.append(q.get(timeout=timeout))
     finally:
         for p in procs:
@@ -260,7 +289,7 @@ def test_concurrent_requests_complete_out_of_order():
 
 
 def test_dead_pool_fails_over_within_deadline():
-    out = _run("kill", env={"DLLM_FAULT_DIE_ON": "__die__"})
+    out = _run("kill", env={"DLLM_FAULT": "die_on=__die__"})
     assert out["ok"] and out["dev"] == "nano", out
     assert out["dt"] < 30.0, out                              # transport error, not the 60 s deadline
     assert out["alive"] is False
@@ -268,7 +297,7 @@ def test_dead_pool_fails_over_within_deadline():
 
 
 def test_hung_request_times_out_and_pool_stays_usable():
-    out = _run("hang", env={"DLLM_FAULT_HANG_ON": "__hang__", "DLLM_FAULT_HANG_S": "4"})
+    out = _run("hang", env={"DLLM_FAULT": "hang_on=__hang__,hang_s=4"})
     assert "timed out" in out["err"] and 1.5 < out["dt"] < 10.0, out
     assert out["probe"] and out["after"] and out["timeouts"] == 1
 
@@ -280,7 +309,7 @@ def test_failover_token_id_handoff_matches_text():
 
 
 def test_leader_dies_during_data_ping_while_request_fails_over():
-    out = _run("data_die", env={"DLLM_FAULT_DIE_ON_DATA_PING": "1"})
+    out = _run("data_die", env={"DLLM_FAULT": "die_on_data_ping=1"})
     assert out["ok"] and out["dev"] == "nano", out
     assert out["dt"] < 30.0, out
     assert out["ping_ok"] is False and out["ping_dt"] < 8.0, out
@@ -288,7 +317,7 @@ def test_leader_dies_during_data_ping_while_request_fails_over():
 
 
 def test_pool_dead_by_probes_is_revived_when_probes_recover():
-    out = _run("revive", env={"DLLM_FAULT_PING_DELAY_N": "3", "DLLM_FAULT_PING_DELAY_S": "1.5"})
+    out = _run("revive", env={"DLLM_FAULT": "ping_delay_n=3,ping_delay_s=1.5"})
     assert out["dead_seen"] and out["alive"] and out["revivals"] == 1, out
     assert out["after"], out
     assert False in out["health"] and out["health"][-1] is True
@@ -299,3 +328,11 @@ def test_stuck_data_plane_lock_falls_back_to_text():
     assert out["ok"] and out["dt"] < 20.0, out
     assert out["retired"] and out["ping_ok"] is False, out
     assert out["busy_probe_skipped"], out
+
+
+def test_submit_batch_completes_each_request_on_its_own():
+    out = _run("submit")
+    assert out["errors"] == [None] * 5 and out["once"]
+    assert out["order"][-1] == "long", out["order"]          # submitted earlier, finished last
+    assert out["tokens"][0] == 200 and out["tokens"][1:4] == [3, 3, 3] and out["tokens"][4] == 4
+    assert out["submit_s"] < 5.0                              # submission never waits for generation
