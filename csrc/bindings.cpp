@@ -16,7 +16,7 @@ int dllm_rope_kv(const void*, long, const int*, const float*, const int*, void*,
 int dllm_kv_write(const void*, const void*, long, const int*, void*, void*, int, int, int, int, hipStream_t);
 int dllm_paged_attention(const void*, const void*, const void*, const int*, const int*, const int*, const int*,
                          const int*, const int*, void*, float*, float*, int*, const int*, const int*, int, int, int,
-                         int, int, int, int, int, int, float, hipStream_t);
+                         int, int, int, int, int, int, float, const void*, hipStream_t);
 int dllm_silu_mul(const void*, void*, long, int, long, hipStream_t);
 int dllm_embed(const int*, const void*, void*, long, int, long, long, float*, int*, const int*, int, hipStream_t);
 int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, int, const void*, void*, const void*,
@@ -164,7 +164,7 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
                      torch::Tensor tile_tok0, torch::Tensor out, c10::optional<torch::Tensor> part_o,
                      c10::optional<torch::Tensor> part_ml, c10::optional<torch::Tensor> counters, int64_t splits,
                      bool causal, double scale, c10::optional<torch::Tensor> split_len, bool xcd_remap,
-                     c10::optional<torch::Tensor> items, int64_t grid_items) {
+                     c10::optional<torch::Tensor> items, int64_t grid_items, c10::optional<torch::Tensor> v_new) {
   check_bf16(q, "q");
   check_bf16(kc, "k_cache");
   check_bf16(vc, "v_cache");
@@ -216,11 +216,17 @@ void paged_attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch:
     TORCH_CHECK(grid_items >= 1 && !xcd_remap, "work-list attention: grid >= 1, no XCD remap");
     it = items->data_ptr<int>();
   }
+  const void* vn = nullptr;
+  if (v_new.has_value()) {   // decode: the newest token's V row-major [T, nkv * d] (tgemm v_rows)
+    check_bf16(*v_new, "v_new");
+    TORCH_CHECK(v_new->is_contiguous() && v_new->numel() >= (int64_t)q.size(0) * nkv * d, "v_new [T, nkv * d]");
+    vn = v_new->data_ptr();
+  }
   ok(dllm_paged_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                           qstart.data_ptr<int>(), qlen.data_ptr<int>(), ctx.data_ptr<int>(), tile_seq.data_ptr<int>(),
                           tile_tok0.data_ptr<int>(), out.data_ptr(), po, pml, cnt, sl, it, (int)grid_items,
                           xcd_remap ? 1 : 0, num_tiles, nq, nkv, d, block_tables.size(1), splits, causal ? 1 : 0,
-                          (float)scale, stream()),
+                          (float)scale, vn, stream()),
      "paged_attention");
 }
 
@@ -845,7 +851,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
            int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk, int64_t nl,
-           c10::optional<torch::Tensor> sk_table, int64_t sk_cmax) {
+           c10::optional<torch::Tensor> sk_table, int64_t sk_cmax, c10::optional<torch::Tensor> v_rows) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   if (nl > 0) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
@@ -968,6 +974,14 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
     a.kc = (uint16_t*)kc->data_ptr();
     a.vc = (uint16_t*)vc->data_ptr();
     a.nq = nq; a.nkv = nkv; a.d = d;
+    if (v_rows.has_value()) {   // V row-major [M, nkv * d] instead of the V^T cache (decode attention writes it)
+      check_bf16(*v_rows, "v_rows");
+      TORCH_CHECK(v_rows->dim() == 2 && v_rows->stride(1) == 1 && v_rows->size(0) >= M && v_rows->size(1) == nkv * d &&
+                      v_rows->stride(0) % 8 == 0,
+                  "v_rows [>= M, nkv * d], 16-B aligned rows");
+      a.v_rows = (uint16_t*)v_rows->data_ptr();
+      a.v_ld = v_rows->stride(0);
+    }
   }
   ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)wk, (int)epi, stream(), (int)nl), "tgemm");
 }

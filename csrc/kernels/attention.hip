@@ -49,8 +49,13 @@ struct AttnArgs {
   int xcd_remap;         // 1: XCD-contiguous block order (prefill K/V reuse in L2)
   int nq, nkv, G, max_blocks, causal;
   int num_tiles, split_stride;  // partial-workspace geometry: [num_tiles, nkv, split_stride, 16, d]
-  int wl_dynamic;        // work list: 1 = units fetched with an atomic cursor (counters[num_tiles * nkv])
   float scale_log2;
+  // decode (qlen 1): the newest token's V, row-major [T, nkv, d] (the fused QKV GEMM's V output,
+  // tgemm GemmArgs.v_rows).  The unit that owns a sequence's newest key writes it into the V^T
+  // cache and patches it into its last chunk's registers, so the GEMM's V-column workgroups no
+  // longer scatter 2-byte V^T stores (they were that launch's stragglers).  Null: V^T is in the
+  // cache already.
+  const u16* v_new;
 };
 // NOTE (measured, MI355X): surplus blocks are not free — a grid whose z-splits are mostly empty
 // for short contexts ran 1.5-4.7x slower than the same work with z = 1, so the engine uses static
@@ -79,9 +84,10 @@ __device__ __forceinline__ TileMeta load_tile_meta(const AttnArgs& a, int tile) 
   return t;
 }
 
-template <int D, int W, int CH, bool PF>
+template <int D, int W>
 __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, const int tile, const int kvh,
                                           const int split, int nsplit, const TileMeta tm) {
+  constexpr int CH = 1;   // 32-key chunks per wave trip (2, and a block-table prefetch one trip ahead, measured no gain)
   constexpr int KSTEPS = D / 32;
   constexpr int NT = D / 16;
   auto& s_o = sm.o;
@@ -136,29 +142,25 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   // +30 VGPRs cost a wave per SIMD, and occupancy hides the K/V latency better than ILP here).
   // (Plain local arrays in the loop body: an earlier lambda + struct form made hipcc keep part
   // of the K/V registers in scratch for some instantiations — 48-80 B/lane of scratch traffic.)
-  // CH 32-key chunks per wave trip: all CH chunks' K/V loads are issued before the first chunk's
-  // MFMAs, so a wave keeps CH x 8 KB (d = 64) in flight (CH = 2 for decode: more bytes in flight
-  // per CU at the cost of VGPRs).
-  // Block-table entries are prefetched one trip ahead (PF): the K/V addresses of a trip then do
-  // not wait on a dependent block-table load, so each trip has one memory latency, not two.
-  // (a macro, not a lambda: a by-reference lambda over these arrays put them in scratch)
-#define DLLM_BT_LOOKUP(KB, B0, B1)                                   \
-  _Pragma("unroll") for (int c = 0; c < CH; ++c) {                   \
-    const int kc_ = (KB) + 32 * c;                                   \
-    B0[c] = kc_ < k_end ? bt[kc_ >> 4] : bt[(KB) >> 4];              \
-    B1[c] = (kc_ + 16 < k_end) ? bt[(kc_ >> 4) + 1] : B0[c];         \
+
+  // the newest key's V handed over row-major (AttnArgs.v_new): only the unit whose key range ends
+  // at the sequence's context owns it (chunks are 32-key aligned, so no other unit reads its block)
+  const int vkey = (a.v_new != nullptr && seq >= 0 && qlen == 1 && k_end == kmax && k_end > k_begin) ? kmax - 1 : -1;
+  u16 vnv[NT];
+  if (vkey >= 0) {
+    const u16* vp = a.v_new + ((long)qstart * a.nkv + kvh) * D + rl;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) vnv[n] = vp[16 * n];
   }
-  int nb0[CH], nb1[CH];
-  if (PF && k_begin + 32 * CH * wave < k_end) { DLLM_BT_LOOKUP(k_begin + 32 * CH * wave, nb0, nb1) }
   for (int kb = k_begin + 32 * CH * wave; kb < k_end; kb += 32 * CH * W) {
     uint4 kr[CH][2][KSTEPS];
     uint2 vr[CH][2][NT];
     int cb0[CH], cb1[CH];
-    if (PF) {
 #pragma unroll
-      for (int c = 0; c < CH; ++c) { cb0[c] = nb0[c]; cb1[c] = nb1[c]; }
-    } else {
-      DLLM_BT_LOOKUP(kb, cb0, cb1)
+    for (int c = 0; c < CH; ++c) {
+      const int kc_ = kb + 32 * c;
+      cb0[c] = kc_ < k_end ? bt[kc_ >> 4] : bt[kb >> 4];
+      cb1[c] = (kc_ + 16 < k_end) ? bt[(kc_ >> 4) + 1] : cb0[c];
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -178,7 +180,6 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
         vr[c][1][n] = *reinterpret_cast<const uint2*>(v1 + 16 * n * BS);
       }
     }
-    if (PF && kb + 32 * CH * W < k_end) { DLLM_BT_LOOKUP(kb + 32 * CH * W, nb0, nb1) }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int kc = kb + 32 * c;
@@ -213,6 +214,19 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
       l_run = l_run * alpha + lsum;
       m_run = m_new;
       const bf16x8 pf = __builtin_bit_cast(bf16x8, pack8(p));
+      if (vkey >= kc && vkey < kc + 32) {   // wave-uniform: this chunk holds the newest key
+        const int h = (vkey - kc) >> 4, q = vkey & 3;
+        if (g == ((vkey & 15) >> 2)) {       // lanes whose 8-byte V^T load covers that key
+          u16* vcp = const_cast<u16*>(a.vc) + ((long)(h ? cb1[c] : cb0[c]) * a.nkv + kvh) * head_stride + rl * BS +
+                     (vkey & 15);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            uint32_t& w = (q < 2) ? vr[c][h][n].x : vr[c][h][n].y;
+            w = (q & 1) ? ((w & 0x0000ffffu) | ((uint32_t)vnv[n] << 16)) : ((w & 0xffff0000u) | vnv[n]);
+            vcp[16 * n * BS] = vnv[n];   // dim 16 n + rl of the newest key, into the V^T cache
+          }
+        }
+      }
       // Keys past k_end sit in the tail of the last KV block: never written for this sequence
       // (uninitialised or stale memory, possibly NaN/Inf bit patterns).  Their P is 0, but
       // 0 * NaN = NaN inside the PV MFMA, so zero those V^T columns (wave-uniform tail test).
@@ -237,8 +251,6 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
       }
     }
   }
-
-#undef DLLM_BT_LOOKUP
 
   // ---- combine the waves through LDS.  acc[n][r] = O^T[dim 16n + 4g + r][row rl]
   if constexpr (W == 8) {  // waves 4..7 fold into waves 0..3 first (keeps LDS at 4 slots)
@@ -422,7 +434,7 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   }
 }
 
-template <int D, int W, int CH, bool PF>
+template <int D, int W>
 __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   __shared__ AttnSmem<D> sm;
   if (a.items != nullptr) {
@@ -436,18 +448,9 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     const int n0 = a.items[0];
     const bool ext = n0 < 0;
     const int n = ext ? -n0 : n0;
-    // static: units blockIdx.x, + gridDim.x, ...; dynamic: workgroups take the next unit from an
-    // atomic cursor (greedy longest-first scheduling of unequal units) and the last workgroup to
-    // leave re-arms cursor and exit count.  (One attn_unit call site: a lambda wrapper here made
-    // hipcc spill 176 B/lane to scratch.)
-    int* cur = a.counters + (long)a.num_tiles * a.nkv;
+    // units blockIdx.x, + gridDim.x, ... (an atomic-cursor fetch measured no gain: removed).
+    // (One attn_unit call site: a lambda wrapper here made hipcc spill 176 B/lane to scratch.)
     int it = blockIdx.x;
-    if (a.wl_dynamic) {
-      if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      it = sm.last;
-      __syncthreads();
-    }
     while (it < n) {
       int w0, w1;
       TileMeta tm;
@@ -464,23 +467,9 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
       if (!ext) tm = load_tile_meta(a, tile < a.num_tiles ? tile : 0);
       // a malformed unit is skipped rather than trusted (it would index past the workspaces)
       if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.split_stride && split < nsplit && tm.ctx >= 0)
-        attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, nsplit, tm);
+        attn_unit<D, W>(a, sm, tile, kvh, split, nsplit, tm);
       __syncthreads();
-      if (a.wl_dynamic) {
-        if (threadIdx.x == 0) sm.last = __hip_atomic_fetch_add(cur, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        it = sm.last;
-        __syncthreads();
-      } else {
-        it += gridDim.x;
-      }
-    }
-    if (a.wl_dynamic && threadIdx.x == 0) {
-      const int done = __hip_atomic_fetch_add(cur + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (done == (int)gridDim.x - 1) {
-        __hip_atomic_store(cur, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cur + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      it += gridDim.x;
     }
     return;
   }
@@ -502,21 +491,12 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     kvh = (int)(rest % ny);
     split = (int)(rest / ny);
   }
-  attn_unit<D, W, CH, PF>(a, sm, tile, kvh, split, splits, load_tile_meta(a, tile));
+  attn_unit<D, W>(a, sm, tile, kvh, split, splits, load_tile_meta(a, tile));
 }
 
 template <int D, int W>
 void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
-  static const int ch = [] { const char* e = getenv("DLLM_ATTN_CH"); return e ? atoi(e) : 1; }();
-  static const int pf = [] { const char* e = getenv("DLLM_ATTN_BT_PREFETCH"); return e ? atoi(e) : 0; }();
-  if (ch == 2 && pf)
-    hipLaunchKernelGGL((paged_attn_kernel<D, W, 2, true>), grid, dim3(64 * W), 0, stream, a);
-  else if (ch == 2)
-    hipLaunchKernelGGL((paged_attn_kernel<D, W, 2, false>), grid, dim3(64 * W), 0, stream, a);
-  else if (pf)
-    hipLaunchKernelGGL((paged_attn_kernel<D, W, 1, true>), grid, dim3(64 * W), 0, stream, a);
-  else
-    hipLaunchKernelGGL((paged_attn_kernel<D, W, 1, false>), grid, dim3(64 * W), 0, stream, a);
+  hipLaunchKernelGGL((paged_attn_kernel<D, W>), grid, dim3(64 * W), 0, stream, a);
 }
 }  // namespace
 
@@ -525,7 +505,8 @@ extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* v
                                     const int* tile_seq, const int* tile_tok0, void* out, float* part_o,
                                     float* part_ml, int* counters, const int* split_len, const int* items,
                                     int grid_items, int xcd_remap, int num_tiles, int nq, int nkv, int d,
-                                    int max_blocks, int splits, int causal, float scale, hipStream_t stream) {
+                                    int max_blocks, int splits, int causal, float scale, const void* v_new,
+                                    hipStream_t stream) {
   if (nq % nkv != 0) return -1;
   const int G = nq / nkv;
   if (16 % G != 0) return -2;
@@ -534,16 +515,12 @@ extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* v
   if (num_tiles <= 0) return 0;
   AttnArgs a{(const u16*)q, (const u16*)kc, (const u16*)vc, block_tables, seq_qstart, seq_qlen, seq_ctx,
              tile_seq, tile_tok0, (u16*)out, part_o, part_ml, counters, split_len, items, xcd_remap, nq, nkv, G,
-             max_blocks, causal, num_tiles, splits, 0, scale * LOG2E};
-  static const int env_dyn = [] { const char* e = getenv("DLLM_ATTN_WL_DYNAMIC"); return e ? atoi(e) : 0; }();
-  a.wl_dynamic = items != nullptr && env_dyn ? 1 : 0;
+             max_blocks, causal, num_tiles, splits, scale * LOG2E, (const u16*)v_new};
   // 8 waves per workgroup when the grid alone cannot fill the CUs with memory requests
-  // (decode at moderate batch: tiles x kv-heads x splits workgroups are all resident at once).
-  static const int env_w = [] { const char* e = getenv("DLLM_ATTN_WAVES"); return e ? atoi(e) : 0; }();
+  // (decode at moderate batch: tiles x kv-heads x splits workgroups are all resident at once;
+  // dynamic splitting bounds every block's key range, where 8 waves measured best)
   const long wgs = (long)num_tiles * nkv * splits;
-  // (dynamic splitting bounds every block's key range, where 8 waves measured best)
-  const int W = env_w == 4 || env_w == 8 ? env_w
-                : ((items != nullptr || split_len != nullptr || wgs <= 2048) ? 8 : 4);
+  const int W = (items != nullptr || split_len != nullptr || wgs <= 2048) ? 8 : 4;
   const dim3 grid = items != nullptr ? dim3(grid_items, 1, 1) : dim3(num_tiles, nkv, splits);
 switch (d) {
     case 64: W == 8 ? launch_attn<64, 8>(grid, a, stream) : launch_attn<64, 4>(grid, a, stream); break;

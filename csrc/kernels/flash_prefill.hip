@@ -388,6 +388,9 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   if (ROWS % G || G > 32) return -2;
   if (num_tiles <= 0) return 0;
   if (splits < 1 || splits > 16 || (splits > 1 && (!part_o || !part_ml || !counters))) return -5;
+  // split partials are addressed through 32-bit buffer descriptors (stores past 2 GiB would be
+  // dropped silently): refuse a workspace that large instead of returning wrong attention
+  if (splits > 1 && (long)num_tiles * nkv * splits * ROWS * d * 4 >= (1L << 31)) return -6;
   if (splits > 1) {
     const hipError_t e = hipMemsetAsync(counters, 0, (size_t)num_tiles * nkv * sizeof(int), stream);
     if (e != hipSuccess) return (int)e;

@@ -149,6 +149,26 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     }
   }
 
+  // ---- QKV row metadata: the positions and cache slots of this lane's output rows are loaded
+  // with the row-scale partials, before the ring (they retire at its first wait), so the epilogue
+  // starts with them in registers: its RoPE table reads are then ONE round trip, not two dependent
+  // ones (pos -> cos/sin), and the K copy-out reads its slots from LDS
+  constexpr int QR = (EPI == EPI_QKV) ? FM * 4 : 1;
+  int q_pos[QR], q_slot[QR];
+  if constexpr (EPI == EPI_QKV) {
+    if (!loader) {
+      const int rlq = wm * WM + 4 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int mm = min(m0 + rlq + 16 * i + e, M - 1);
+          q_pos[4 * i + e] = a.pos[mm];
+          q_slot[4 * i + e] = a.slots[mm];
+        }
+    }
+  }
+
   // ---- staging: wave w owns ring rows [8 (w*GA + j), +8) of A and [8 (w*GB + j), +8) of B;
   // lane -> row + lane/8, LDS chunk lane%8 <- source chunk (lane%8) ^ ((row >> 1) & 7)
   const int srow = lane >> 3, spos = lane & 7;
@@ -384,15 +404,16 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     // registers (transposed cache layout: no row vectors to form), q/k staged.
     const int d = a.d, hd = d / 2, nq = a.nq, nkv = a.nkv;
     const int qcols = nq * d, kcols = nkv * d;
+    int* s_slot = reinterpret_cast<int*>(s_red);   // [BM] cache slot per tile row (copy-out)
     if (fw) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rl = rl0 + 16 * i + e, m = m0 + rl;
-        const int mm = min(m, M - 1);
-        const int slot = a.slots[mm];
-        const float* cs = a.cos_sin + (long)a.pos[mm] * d;
+        const int slot = q_slot[4 * i + e];
+        if (wn == 0 && cl == 0) s_slot[rl] = slot;
+        const float* cs = a.cos_sin + (long)q_pos[4 * i + e] * d;
         const long blk = slot >> 4, off = slot & 15;
 #pragma unroll
         for (int jp = 0; jp < FN / 2; ++jp) {
@@ -406,7 +427,13 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
             const float co = cs[d1], si = cs[hd + d1];
             so[rl * OLD + cb + cl] = f2bf(x1 * co - x2 * si);
             so[rl * OLD + cb + 16 + cl] = f2bf(x2 * co + x1 * si);
+          } else if (a.v_rows != nullptr) {
+            // V staged like q/k and copied out as 16-B row vectors (natural dim order)
+            so[rl * OLD + cb + cl] = f2bf(x1);
+            so[rl * OLD + cb + 16 + cl] = f2bf(x2);
           } else if (m < M && slot >= 0) {
+            // V^T cache directly: 2-byte stores 32 B apart (the slow form: a workgroup holding
+            // V columns takes several us longer than its q/k neighbours at decode batch sizes)
             const int cc = nb - qcols - kcols;
             const int head = cc / d, dim = cc % d + cl;
             u16* vo = a.vc + ((blk * nkv + head) * d) * 16 + off;
@@ -421,7 +448,11 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     for (int e = threadIdx.x; e < BM * (BN / 8); e += NT) {
       const int rl = e / (BN / 8), c0 = (e % (BN / 8)) * 8;
       const int m = m0 + rl, n = n0 + c0;
-      if (m >= M || n >= qcols + kcols || n >= N) continue;
+      if (m >= M || n >= N) continue;
+      if (n >= qcols + kcols) {
+        if (a.v_rows != nullptr) st16(a.v_rows + (long)m * a.v_ld + (n - qcols - kcols), *reinterpret_cast<const uint4*>(so + rl * OLD + c0));
+        continue;
+      }
       const bool isq = n < qcols;
       const int cc = isq ? n : n - qcols;
       const int head = cc / d, o = cc % d;
@@ -430,7 +461,7 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
       if (isq) {
         st16(a.q_out + ((long)m * nq + head) * d + dim, v);
       } else {
-        const int slot = a.slots[m];
+        const int slot = s_slot[rl];
         if (slot >= 0) st16(a.kc + (((long)(slot >> 4) * nkv + head) * 16 + (slot & 15)) * d + dim, v);
       }
     }

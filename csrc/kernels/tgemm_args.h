@@ -29,6 +29,10 @@ struct GemmArgs {
   uint16_t* q_out;            // [M, nq, d]
   uint16_t* kc;               // [blocks, nkv, 16, d]
   uint16_t* vc;               // [blocks, nkv, d, 16]
+  // non-null (decode): V rows go here row-major [M][v_ld] (16-B stores) instead of the V^T cache;
+  // the decode attention kernel writes the newest token's V^T itself (attention.hip AttnArgs.v_new)
+  uint16_t* v_rows;
+  long v_ld;
   int nq, nkv, d;
   // PLAIN / RESADD / GELU: bias[n] added to the product before the epilogue op (null: none)
   const uint16_t* bias;

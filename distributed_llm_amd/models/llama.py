@@ -359,7 +359,8 @@ class LlamaModel:
         self.ep_calls += 1
         return all_gather_rows(yl, T, par.tp_group, par.tp_size)
 
-    def _attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+    def _attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta,
+                   v_new: Optional[torch.Tensor] = None) -> torch.Tensor:
         if meta.flash:   # prefill: 128-row tiles, K/V staged once per workgroup (flash_prefill.hip)
             return ops.flash_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                        meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
@@ -367,7 +368,8 @@ class LlamaModel:
         return ops.paged_attention(q, kc, vc, meta.block_tables, meta.qstart, meta.qlen, meta.ctx,
                                    meta.tile_seq, meta.tile_tok0, scale=self.scale, causal=True,
                                    splits=meta.splits, workspace=meta.workspace, split_len=meta.split_len,
-                                   xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items)
+                                   xcd_remap=meta.xcd_remap, items=meta.items, grid_items=meta.grid_items,
+                                   v_new=v_new)
 
     def hidden_states(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMeta,
                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
@@ -429,12 +431,19 @@ class LlamaModel:
             r = torch.empty((T, H), dtype=self.dtype, device=input_ids.device)
             n = par.all_reduce_resadd(ops.embedding(input_ids, self.embed, self.vocab_shard.start, scatter=scatter),
                                       r, ssq_a, add=False)
+        # decode (one new token per sequence, TP 1): the QKV GEMM hands V over row-major and the
+        # attention kernel writes each sequence's newest V^T itself (ops.gemm.qkv_rope_cache)
+        vn = (torch.empty((T, self.nkv * self.d), dtype=self.dtype, device=input_ids.device)
+              if (not tp and meta.all_last and meta.items is not None and input_ids.is_cuda) else None)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             # column-parallel QKV (this rank's heads) with RMSNorm folded + RoPE + paged K/V write
             q = ops.gemm.qkv_rope_cache(r, L["wqkv_f"], ssq_a, n, eps, positions, self.cos_sin, meta.slots, kc, vc,
-                                        self.nq, self.nkv, self.d, wp=L.get("wqkv_f_p"))
-            o = self._attention(q, kc, vc, meta)
+                                        self.nq, self.nkv, self.d, wp=L.get("wqkv_f_p"), v_new=vn)
+            v_new = None
+            if vn is not None:
+                q, v_new = q
+            o = self._attention(q, kc, vc, meta, v_new=v_new)
             if not tp:
                 nb = ops.gemm.matmul_resadd(o.view(T, -1), L["wo"], r, ssq_b, wp=L.get("wo_p"))
             else:   # row-parallel o_proj: partial sums -> all-reduce + residual add + row statistics

@@ -136,8 +136,13 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                     causal: bool = True, splits: int = 1, out: Optional[torch.Tensor] = None,
                     workspace: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
                     split_len: Optional[torch.Tensor] = None, xcd_remap: bool = False,
-                    items: Optional[torch.Tensor] = None, grid_items: int = 0) -> torch.Tensor:
+                    items: Optional[torch.Tensor] = None, grid_items: int = 0,
+                    v_new: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Paged attention over new query tokens ``q [T, nq, d]`` (see csrc/kernels/attention.hip).
+
+    ``v_new`` (decode, one query token per sequence): the new tokens' V row-major [T, nkv * d],
+    NOT yet in the V^T cache (``gemm.qkv_rope_cache(v_new=...)``); the kernel writes each
+    sequence's newest V into the cache and uses it (CPU: the reference writes it first).
 
     ``splits`` is the split-K grid depth; with ``split_len`` (int32 device scalar, keys per split)
     each tile uses only ceil(its keys / split_len) of them (dynamic, balanced split-K).
@@ -149,6 +154,8 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     scale = (1.0 / math.sqrt(d)) if scale is None else scale
     ext = _native(q)
     if ext is None:
+        if v_new is not None:   # the newest token of each sequence: V into the V^T cache first
+            ref.write_newest_v(v_new, v_cache, block_tables, seq_qstart, seq_ctx)
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, scale, causal)
     o = out if out is not None else torch.empty_like(q)
     po = pml = cnt = None
@@ -162,7 +169,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
             po, pml, cnt = workspace
     ext.paged_attention(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,
                         po, pml, cnt, splits, causal, scale, split_len if splits > 1 and items is None else None,
-                        xcd_remap, items, int(grid_items))
+                        xcd_remap, items, int(grid_items), v_new)
     return o
 
 
@@ -180,9 +187,10 @@ def flash_lds_bytes(d: int, max_blocks: int) -> int:
 
 def flash_supported(d: int, group: int, max_blocks: int) -> bool:
     """The flash kernel stages a tile's ENTIRE block-table row in LDS, sized at launch: it runs any
-    context whose table fits next to the ring in the 160 KB (d = 128: ~1.7M keys; the pipelined
-    d = 128 form needs 48 KB more and falls back to the plain loop on its own); longer tables go to
-    the paged kernel instead of failing at launch (dllm_flash_prefill returns -3)."""
+    context whose table fits next to the 3-stage K/V ring in the 160 KB: 16,384 blocks = 262K keys at
+    d = 128, 360K at d = 96, 458K at d = 64 (the pipelined d = 128 form needs 48 KB more and falls
+    back to the plain loop on its own).  Longer contexts are served by the slower paged kernel
+    (``paged_attention``) instead of failing at launch (dllm_flash_prefill returns -3)."""
     return d in (64, 96, 128) and FLASH_ROWS % group == 0 and max_blocks >= 1 and \
         flash_lds_bytes(d, max_blocks) <= 160 * 1024 and os.environ.get("DLLM_FLASH_PREFILL", "1") == "1"
 
@@ -213,6 +221,10 @@ def flash_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     o = out if out is not None else torch.empty_like(q)
     units = int(tile_seq.numel()) * int(k_cache.shape[1])
     sp = flash_splits(units, max_ctx)
+    # the kernel addresses its split partials through 32-bit buffer descriptors: keep the O
+    # partials under 2 GiB (a forced DLLM_FLASH_SPLITS on a long prompt could exceed it: ADVICE r4)
+    while sp > 1 and units * sp * FLASH_ROWS * d * 4 >= (1 << 31):
+        sp -= 1
     if sp > 1:
         po, pml, cnt = _flash_workspace(q.device, units * sp * FLASH_ROWS * d, units * sp * FLASH_ROWS * 4, units)
         ext.flash_prefill(q, k_cache, v_cache, block_tables, seq_qstart, seq_qlen, seq_ctx, tile_seq, tile_tok0, o,

@@ -286,7 +286,8 @@ def _sk_tensor(dev, M, N, K, bm, bn, ks):
 
 
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
-           pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None):
+           pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None,
+           v_rows=None):
     """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves[, stream-K]]]])"""
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
@@ -308,7 +309,8 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
         floats, tiles = _need_tg(M, N, K, bm, bn, sp, ks)
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
-              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl), tab, int(cmax))
+              pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl), tab, int(cmax),
+              v_rows)
 
 
 def ref_silu_mul(gu):
@@ -417,28 +419,36 @@ def _core(x: torch.Tensor, w: torch.Tensor, wp: Optional[torch.Tensor] = None) -
 
 def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: int, eps: float,
                    positions: torch.Tensor, cos_sin: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
-                   v_cache: torch.Tensor, nq: int, nkv: int, d: int, wp: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   v_cache: torch.Tensor, nq: int, nkv: int, d: int, wp: Optional[torch.Tensor] = None,
+                   v_new: Optional[torch.Tensor] = None):
     """q [T, nq, d] of ``rope(rmsnorm(r) . Wqkv^T)``, K/V written to the paged caches, one launch.
 
     ``w`` is the folded/permuted weight of models.llama.fuse_qkv_weight; ``ssq[:ssq_n]`` holds
-    the partial row sums of r^2 written by the producer of ``r``."""
+    the partial row sums of r^2 written by the producer of ``r``.
+
+    ``v_new`` ([T, nkv * d], decode steps only): where the one-launch GEMM runs, V is written there
+    row-major instead of into the V^T cache, and the decode attention kernel moves each sequence's
+    newest V into the cache itself (``paged_attention(v_new=...)``: the GEMM's V-column workgroups
+    were its stragglers, profiles/r5_qkv_epilogue.md).  Returns ``(q, v_new or None)`` then — None
+    where another implementation ran and the cache already holds V."""
     T, H = r.shape
     q = torch.empty((T, nq, d), dtype=r.dtype, device=r.device)
     if T == 0:
-        return q
+        return q if v_new is None else (q, None)
+    out = (lambda used: q if v_new is None else (q, v_new if used else None))
     R = fused_gemv_r(r, w.shape[0])
     if R:
         _native(r).gemv_qkv(r, w, ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q, k_cache,
                             v_cache, nq, nkv, d, R)
-        return q
+        return out(False)
     if use_vendor_core(T, w.shape[0], H):
         _native(r).qkv_post(_core(r, w, wp), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
                             k_cache, v_cache, nq, nkv, d)
-        return q
+        return out(False)
     _tgemm(_native(r), r, wp if wp is not None else w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
            eps=eps, pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv,
-           d=d)
-    return q
+           d=d, v_rows=v_new)
+    return out(True)
 
 
 def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_out: torch.Tensor,

@@ -79,6 +79,19 @@ def kv_write(k, v, slots, k_cache, v_cache):
     v_cache[blk, :, :, off] = v.to(v_cache.dtype)
 
 
+def write_newest_v(v_new, v_cache, block_tables, seq_qstart, seq_ctx):
+    """Decode hand-over (attention.hip AttnArgs.v_new): each sequence's newest key ctx - 1 takes V
+    row ``v_new[qstart]`` ([T, nkv * d] row-major) in the V^T cache."""
+    nkv, d = v_cache.shape[1], v_cache.shape[2]
+    for s in range(block_tables.shape[0]):
+        ctx, qs = int(seq_ctx[s]), int(seq_qstart[s])
+        if ctx <= 0:
+            continue
+        key = ctx - 1
+        blk = int(block_tables[s, key // BS])
+        v_cache[blk, :, :, key % BS] = v_new[qs].view(nkv, d).to(v_cache.dtype)
+
+
 def gather_kv(k_cache, v_cache, block_table, n):
     """Dense K, V [n, nkv, d] of one sequence from the paged caches."""
     nb = (n + BS - 1) // BS

@@ -21,7 +21,7 @@ extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* v
                                     const int* tile_seq, const int* tile_tok0, void* out, float* part_o,
                                     float* part_ml, int* counters, const int* split_len, const int* items,
                                     int grid_items, int xcd_remap, int num_tiles, int nq, int nkv, int d,
-                                    int max_blocks, int splits, int causal, float scale, hipStream_t stream);
+                                    int max_blocks, int splits, int causal, float scale, const void* v_new, hipStream_t stream);
 extern "C" int dllm_decode_attention(const void* q, const void* kc, const void* vc, const int* block_tables,
                                      const int* seq_qstart, const int* seq_ctx, const int* tile_seq, void* out,
                                      float* part_o, float* part_ml, int* counters, const int* split_len,
@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
   for (int sp : {1, 2, 4}) {
     float ms = timeit([&] {
       int r = dllm_paged_attention(q, kc, vc, bt, dqs, dql, dcx, dts, dtt, o1, po, pml, cnt, nullptr, nullptr, 0, 0, B,
-                                   nq, nkv, d, maxb, sp, 1, scale, 0);
+                                   nq, nkv, d, maxb, sp, 1, scale, nullptr, 0);
       if (r) { printf("paged rc %d\n", r); exit(1); }
     });
     rep("paged", sp, ms);
@@ -155,7 +155,7 @@ int main(int argc, char** argv) {
     {  // the engine's current path: attention.hip walking the same list with 512 workgroups
       float ms = timeit([&] {
         int r = dllm_paged_attention(q, kc, vc, bt, dqs, dql, dcx, dts, dtt, o1, po, pml, cnt, nullptr, ditems, 512, 0,
-                                     B, nq, nkv, d, maxb, NSMAX, 1, scale, 0);
+                                     B, nq, nkv, d, maxb, NSMAX, 1, scale, nullptr, 0);
         if (r) { printf("paged wl rc %d\n", r); exit(1); }
       });
       printf("{\"exp\": \"attnbench\", \"kernel\": \"paged_wl\", \"B\": %d, \"C\": %d, \"var\": %d, \"d\": %d, "

@@ -168,6 +168,44 @@ def test_paged_attention_worklist(nq, nkv, d, grid, target, min_chunk, ext):
     assert int(ws[2].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("nq,nkv,d", [(32, 4, 64), (32, 8, 128), (32, 32, 96)])
+@pytest.mark.parametrize("ext,grid", [(True, 7), (True, 512), (False, 64)])
+def test_paged_attention_decode_writes_newest_v(nq, nkv, d, ext, grid):
+    """Decode hand-over (AttnArgs.v_new): each sequence's newest V arrives row-major and its V^T
+    cache slot holds garbage (NaN); the unit that owns the newest key must write it into the cache
+    and attend with it.  Output equals the reference with V written first, the cache slot holds the
+    new V afterwards, and a repeated launch (now reading the written cache) agrees."""
+    ctxs = [1000, 1, 17, 300, 64, 2047, 33, 512, 129, 5, 16, 32]
+    seqs = [(1, c) for c in ctxs]
+    q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(nq, nkv, d, seqs, NB=320)
+    T = q.shape[0]
+    vnew = (torch.randn(T, nkv * d, device=DEV) * 2).to(torch.bfloat16)
+    vc_ref = vc.clone()
+    ref.write_newest_v(vnew, vc_ref, bt, qs, cx)
+    for s_, c in enumerate(ctxs):          # poison the newest slot in the cache the kernel reads
+        key = c - 1
+        vc[int(bt[s_, key // 16]), :, :, key % 16] = float("nan")
+    order = np.argsort(-np.array(ctxs), kind="stable")
+    ts = torch.tensor(order.astype(np.int32), device=DEV)
+    tt = torch.zeros_like(ts)
+    z, nt = 16, ts.numel()
+    ws = (torch.empty(nt * nkv * z * 16 * d, device=DEV), torch.empty(nt * nkv * z * 16 * 2, device=DEV),
+          torch.zeros(nt * nkv + 2, dtype=torch.int32, device=DEV))
+    if ext:
+        items = ops.decode_work_items(np.array(ctxs)[order], nkv, z, 256, min_chunk=32, seq=order,
+                                      qstart=qs.cpu().numpy()[order])
+    else:
+        items = ops.decode_work_items(np.array(ctxs)[order], nkv, z, 256, min_chunk=32)
+    it = torch.tensor(items, device=DEV)
+    o2 = ref.paged_attention(q, kc.clone(), vc_ref, bt, qs, ql, cx, 1 / math.sqrt(d))
+    o = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, workspace=ws, items=it, grid_items=grid,
+                            v_new=vnew)
+    torch.testing.assert_close(o.float(), o2.float(), atol=3e-2, rtol=3e-2)
+    assert torch.equal(vc, vc_ref)          # every newest slot written, nothing else touched
+    o3 = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, workspace=ws, items=it, grid_items=grid)
+    torch.testing.assert_close(o3.float(), o2.float(), atol=3e-2, rtol=3e-2)
+
+
 def test_paged_attention_bidirectional():
     seqs = [(20, 20), (7, 7)]
     q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(16, 16, 64, seqs)

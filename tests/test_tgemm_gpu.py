@@ -79,9 +79,10 @@ def test_residual_add_and_row_sums(plan, M):
     torch.testing.assert_close(tot, (r.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("v_rows", [False, True])
 @pytest.mark.parametrize("plan", PLANS)
 @pytest.mark.parametrize("d,nq,nkv", [(64, 8, 2), (128, 4, 4), (96, 3, 1)])
-def test_qkv_rope_cache(plan, d, nq, nkv):
+def test_qkv_rope_cache(plan, d, nq, nkv, v_rows):
     torch.manual_seed(d)
     M, H = 45, 256
     G.reserve("cuda")
@@ -99,8 +100,9 @@ def test_qkv_rope_cache(plan, d, nq, nkv):
     kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
     vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
     q = torch.empty(M, nq, d, dtype=torch.bfloat16, device="cuda")
+    vrow = torch.full((M, nkv * d), float("nan"), dtype=torch.bfloat16, device="cuda") if v_rows else None
     G._tgemm(_ext(), r, wf, G.EPI_QKV, plan, ssq_in=ssq, ssq_n=1, norm_scale=1.0 / H, eps=1e-5, pos=pos,
-             cos_sin=cos_sin, slots=slots, q_out=q, kc=kc, vc=vc, nq=nq, nkv=nkv, d=d)
+             cos_sin=cos_sin, slots=slots, q_out=q, kc=kc, vc=vc, nq=nq, nkv=nkv, d=d, v_rows=vrow)
     # reference: rmsnorm -> plain GEMM -> rope + cache write (ops.reference, f32 math)
     x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
     qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
@@ -109,7 +111,13 @@ def test_qkv_rope_cache(plan, d, nq, nkv):
     qr = ref.rope_and_cache(qkv, pos.cpu(), cos_sin.cpu(), slots.cpu(), kr, vr, nq, nkv, d)
     torch.testing.assert_close(q.cpu().float(), qr.float(), atol=4e-2, rtol=3e-2)
     torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=4e-2, rtol=3e-2)
-    torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=4e-2, rtol=3e-2)
+    if v_rows:
+        # V handed over row-major (every row, slot or not); the V^T cache is left to the attention kernel
+        v_ref = qkv[:, (nq + nkv) * d:].float()
+        torch.testing.assert_close(vrow.cpu().float(), v_ref, atol=4e-2, rtol=3e-2)
+        assert (vc == 0).all()
+    else:
+        torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=4e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("plan", PLANS)
