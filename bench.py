@@ -46,6 +46,8 @@ import statistics
 import sys
 import time
 
+from distributed_llm_amd.utils.faults import diag
+
 BASELINE_TOK_S = 10.57        # best published routed throughput (Jetson Nano+Orin)
 BASELINE_S_PER_QUERY = 39.6   # best published mean routed e2e latency per query
 
@@ -267,7 +269,7 @@ class PipelinedConversations(Conversations):
 
 
 def _thread_cpu() -> dict:
-    """CPU seconds per named Python thread of this process (``DLLM_THREAD_CPU=1`` diagnostics:
+    """CPU seconds per named Python thread of this process (``DLLM_DIAG=cpu`` diagnostics:
     how much of the window the routing driver and each engine's step loop hold a core / the GIL)."""
     import threading
     import psutil
@@ -303,7 +305,7 @@ class EventConversations(PipelinedConversations):
 
         def driver():
             prof = None
-            if os.environ.get("DLLM_DRIVER_PROFILE"):   # cProfile of this thread, dumped at stop()
+            if diag("profile"):   # cProfile of this thread, dumped at stop() (DLLM_DIAG=profile=PATH)
                 import cProfile
                 prof = cProfile.Profile()
                 prof.enable()
@@ -388,7 +390,7 @@ class EventConversations(PipelinedConversations):
             finally:
                 if prof is not None:
                     prof.disable()
-                    prof.dump_stats(os.environ["DLLM_DRIVER_PROFILE"])
+                    prof.dump_stats(diag("profile"))
 
         self._threads = [threading.Thread(target=driver, name="bench-driver", daemon=True)]
         self._threads[0].start()
@@ -597,7 +599,7 @@ def main() -> int:
                 if on_gpu:
                     torch.cuda.synchronize()
                 e0 = meter.mark() if meter else None
-                cpu0 = _thread_cpu() if os.environ.get("DLLM_THREAD_CPU") == "1" else None
+                cpu0 = _thread_cpu() if diag("cpu") else None
                 t0 = time.perf_counter()
                 convs.records = records
                 start_count = convs.completed   # (turns completed during the opening barrier are warmup)
@@ -711,7 +713,6 @@ def main() -> int:
                                            if a.pipeline else False),
                        "admit_every": a.admit_every if a.pipeline else None,
                        "gil_switch_ms": a.gil_switch_ms if a.pipeline else None,
-                       "early_prefill": os.environ.get("DLLM_EARLY_PREFILL", "1") == "1",
                        "small_max_new": a.small_new, "large_max_new": a.large_new},
             # client side, as the reference harness times a turn (routing_chatbot_tester.py:408-442):
             # dispatch (routing included) to the answer being back in the driver, failover included
@@ -752,7 +753,7 @@ def main() -> int:
             # failed-over turns per step from the first failover on (a tier known to be down is
             # skipped up front: those turns still count here, they are served by the other tier)
             "failovers_by_step": (
-                [sum(1 for r in fo if r["step"] == st) for st in range(first_fo, a.warmup + a.steps)]
+                [sum(1 for r in fo if r["step"] == st) for st in range(first_fo, max(r["step"] for r in fo) + 1)]
                 if first_fo is not None else [])}
         lk = enc1["lookups"] - enc0["lookups"]
         out["router_encoder"] = {"kinds": enc1["kinds"], "memo": bool(enc1.get("memo_enabled", False)),
@@ -763,7 +764,7 @@ def main() -> int:
             out["thread_cpu_share"] = {k: round((v - cpu0.get(k, 0.0)) / elapsed, 3) for k, v in cpu1.items()
                                        if v - cpu0.get(k, 0.0) > 0.01 * elapsed}
         logs = [e._sync_log for e in engines if getattr(e, "_sync_log", None)]
-        if logs:   # DLLM_SYNC_LOG=1 diagnostics: did the step loop keep a step queued ahead?
+        if logs:   # DLLM_DIAG=sync diagnostics: did the step loop keep a step queued ahead?
             import numpy as np
             rec = np.array([r for lg in logs for r in lg], dtype=np.float64)
             wait = rec[:, 1] * 1e3

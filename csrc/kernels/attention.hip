@@ -84,7 +84,7 @@ __device__ __forceinline__ TileMeta load_tile_meta(const AttnArgs& a, int tile) 
   return t;
 }
 
-template <int D, int W>
+template <int D, int W, bool VN>
 __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, const int tile, const int kvh,
                                           const int split, int nsplit, const TileMeta tm) {
   constexpr int CH = 1;   // 32-key chunks per wave trip (2, and a block-table prefetch one trip ahead, measured no gain)
@@ -145,13 +145,8 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
 
   // the newest key's V handed over row-major (AttnArgs.v_new): only the unit whose key range ends
   // at the sequence's context owns it (chunks are 32-key aligned, so no other unit reads its block)
-  const int vkey = (a.v_new != nullptr && seq >= 0 && qlen == 1 && k_end == kmax && k_end > k_begin) ? kmax - 1 : -1;
-  u16 vnv[NT];
-  if (vkey >= 0) {
-    const u16* vp = a.v_new + ((long)qstart * a.nkv + kvh) * D + rl;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) vnv[n] = vp[16 * n];
-  }
+  // (VN: a separate instantiation, so the other paths keep their register budget)
+  const int vkey = (VN && seq >= 0 && qlen == 1 && k_end == kmax && k_end > k_begin) ? kmax - 1 : -1;
   for (int kb = k_begin + 32 * CH * wave; kb < k_end; kb += 32 * CH * W) {
     uint4 kr[CH][2][KSTEPS];
     uint2 vr[CH][2][NT];
@@ -179,6 +174,15 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
         vr[c][0][n] = *reinterpret_cast<const uint2*>(v0 + 16 * n * BS);
         vr[c][1][n] = *reinterpret_cast<const uint2*>(v1 + 16 * n * BS);
       }
+    }
+    // the newest key's V (row-major hand-over) rides along with the trip that reads its chunk, so
+    // it costs no extra round trip and holds no registers outside that trip
+    uint32_t vnv[NT];
+    const bool vtrip = VN && vkey >= kb && vkey < kb + 32 * CH;   // wave-uniform
+    if (vtrip) {
+      const u16* vp = a.v_new + ((long)qstart * a.nkv + kvh) * D + rl;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) vnv[n] = vp[16 * n];
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -214,16 +218,29 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
       l_run = l_run * alpha + lsum;
       m_run = m_new;
       const bf16x8 pf = __builtin_bit_cast(bf16x8, pack8(p));
-      if (vkey >= kc && vkey < kc + 32) {   // wave-uniform: this chunk holds the newest key
-        const int h = (vkey - kc) >> 4, q = vkey & 3;
+      if (VN && vkey >= kc && vkey < kc + 32) {   // wave-uniform: this chunk holds the newest key
+        // (every index below is a compile-time constant or a uniform branch: a runtime-indexed
+        // vr[..][h][..] would put the whole K/V register stage in scratch, cdna_hip_programming.md
+        // §5.4 rule 20)
+        const int hv = (vkey - kc) >> 4, q = vkey & 3;
         if (g == ((vkey & 15) >> 2)) {       // lanes whose 8-byte V^T load covers that key
-          u16* vcp = const_cast<u16*>(a.vc) + ((long)(h ? cb1[c] : cb0[c]) * a.nkv + kvh) * head_stride + rl * BS +
+          u16* vcp = const_cast<u16*>(a.vc) + ((long)(hv ? cb1[c] : cb0[c]) * a.nkv + kvh) * head_stride + rl * BS +
                      (vkey & 15);
 #pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            uint32_t& w = (q < 2) ? vr[c][h][n].x : vr[c][h][n].y;
-            w = (q & 1) ? ((w & 0x0000ffffu) | ((uint32_t)vnv[n] << 16)) : ((w & 0xffff0000u) | vnv[n]);
-            vcp[16 * n * BS] = vnv[n];   // dim 16 n + rl of the newest key, into the V^T cache
+          for (int h = 0; h < 2; ++h) {
+            if (h != hv) continue;
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+              const uint32_t nv = vnv[n];
+              uint32_t wx = vr[c][h][n].x, wy = vr[c][h][n].y;
+              if (q == 0) wx = (wx & 0xffff0000u) | nv;
+              else if (q == 1) wx = (wx & 0x0000ffffu) | (nv << 16);
+              else if (q == 2) wy = (wy & 0xffff0000u) | nv;
+              else wy = (wy & 0x0000ffffu) | (nv << 16);
+              vr[c][h][n].x = wx;
+              vr[c][h][n].y = wy;
+              vcp[16 * n * BS] = (u16)nv;   // dim 16 n + rl of the newest key, into the V^T cache
+            }
           }
         }
       }
@@ -434,7 +451,7 @@ __device__ __forceinline__ void attn_unit(const AttnArgs& a, AttnSmem<D>& sm, co
   }
 }
 
-template <int D, int W>
+template <int D, int W, bool VN>
 __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
   __shared__ AttnSmem<D> sm;
   if (a.items != nullptr) {
@@ -467,7 +484,7 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
       if (!ext) tm = load_tile_meta(a, tile < a.num_tiles ? tile : 0);
       // a malformed unit is skipped rather than trusted (it would index past the workspaces)
       if (tile < a.num_tiles && kvh < a.nkv && nsplit <= a.split_stride && split < nsplit && tm.ctx >= 0)
-        attn_unit<D, W>(a, sm, tile, kvh, split, nsplit, tm);
+        attn_unit<D, W, VN>(a, sm, tile, kvh, split, nsplit, tm);
       __syncthreads();
       it += gridDim.x;
     }
@@ -491,12 +508,21 @@ __global__ void __launch_bounds__(64 * W) paged_attn_kernel(AttnArgs a) {
     kvh = (int)(rest % ny);
     split = (int)(rest / ny);
   }
-  attn_unit<D, W>(a, sm, tile, kvh, split, splits, load_tile_meta(a, tile));
+  attn_unit<D, W, VN>(a, sm, tile, kvh, split, splits, load_tile_meta(a, tile));
 }
 
 template <int D, int W>
 void launch_attn(dim3 grid, const AttnArgs& a, hipStream_t stream) {
-  hipLaunchKernelGGL((paged_attn_kernel<D, W>), grid, dim3(64 * W), 0, stream, a);
+  // the newest-V patch costs ~10 VGPRs: only d = 64 with 8 waves keeps its occupancy (123 <= 128
+  // VGPRs, 4 waves/SIMD); d = 96 / 128 would drop a wave per SIMD, so those callers keep the QKV
+  // GEMM's V^T scatter (dllm_paged_attention refuses v_new for them)
+  if constexpr (D == 64 && W == 8) {
+    if (a.v_new != nullptr) {
+      hipLaunchKernelGGL((paged_attn_kernel<D, W, true>), grid, dim3(64 * W), 0, stream, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((paged_attn_kernel<D, W, false>), grid, dim3(64 * W), 0, stream, a);
 }
 }  // namespace
 
@@ -521,6 +547,7 @@ extern "C" int dllm_paged_attention(const void* q, const void* kc, const void* v
   // dynamic splitting bounds every block's key range, where 8 waves measured best)
   const long wgs = (long)num_tiles * nkv * splits;
   const int W = (items != nullptr || split_len != nullptr || wgs <= 2048) ? 8 : 4;
+  if (v_new != nullptr && (d != 64 || W != 8)) return -7;
   const dim3 grid = items != nullptr ? dim3(grid_items, 1, 1) : dim3(num_tiles, nkv, splits);
 switch (d) {
     case 64: W == 8 ? launch_attn<64, 8>(grid, a, stream) : launch_attn<64, 4>(grid, a, stream); break;

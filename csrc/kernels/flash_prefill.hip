@@ -404,8 +404,8 @@ extern "C" int dllm_flash_prefill(const void* q, const void* kc, const void* vc,
   // d = 128 runs the software-pipelined P.V variant (4-stage ring + zero V^T image): 4-11 % faster
   // at 2k-16k tokens; at d = 64 it needs > 128 VGPRs (one workgroup per CU instead of two) and at
   // d = 96 an earlier form of it gained nothing, so they keep the plain loop
-  // (profiles/r3_flash_prefill.md).  DLLM_FLASH_PIPE=0 turns it off.
-  static const bool pipe = [] { const char* e = getenv("DLLM_FLASH_PIPE"); return !e || atoi(e) != 0; }();
+  // (profiles/r3_flash_prefill.md).
+  constexpr bool pipe = true;
   auto go = [&](auto kern, int dd, bool piped) -> int {
     const size_t lds = (size_t)(piped ? STAGES + 1 : STAGES) * (2 * CK * dd * 2) + (piped ? (size_t)CK * dd * 2 : 0) +
                        ((size_t)max_blocks * 4 + 15) / 16 * 16;

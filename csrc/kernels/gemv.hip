@@ -326,15 +326,11 @@ void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int 
   // and barrier.  Measured at batch 1 (scripts/exp/gemv_probe.py, profiles/r4_single_stream.md):
   // 0.2-0.6 us off TinyLlama's fused QKV / Wo / gate|up / down GEMVs and up to 1 us off
   // Llama-3-8B's, never slower; at batch 2 it is slower on the large shapes, so batch 1 only.
-  // DLLM_GEMV_XG=0 disables it.
-  static const int xg_on = [] { const char* e = getenv("DLLM_GEMV_XG"); return e ? atoi(e) : 1; }();
   if constexpr (M == 1 && !SW && !NORM) {
-    if (xg_on) {
-      const size_t lds_xg = EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0;
-      hipLaunchKernelGGL((gemv_kernel<M, R, 4, SW, NORM, EPI, true>), dim3(gemv_blocks<R>(N)), dim3(256), lds_xg,
-                         stream, (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
-      return;
-    }
+    const size_t lds_xg = EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0;
+    hipLaunchKernelGGL((gemv_kernel<M, R, 4, SW, NORM, EPI, true>), dim3(gemv_blocks<R>(N)), dim3(256), lds_xg,
+                       stream, (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
+    return;
   }
   const size_t lds = (size_t)M * K * 2 + (NORM ? 4 * M * sizeof(float) : 0) +
                      (EPI != GV_PLAIN ? (size_t)(M + 4 * R * M + 4 * M) * sizeof(float) : 0);
@@ -343,10 +339,9 @@ void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int 
   // out three dependent HBM latencies; 8 / 12 per trip put a whole row of up to 4096 / 6144
   // elements in flight at once (64 / 96 VGPRs of W buffers).  Measured (1x MI355X, B = 1 decode
   // step): TinyLlama 0.890 -> 0.872-0.883 ms; on larger grids (Llama-3-8B, >= 1024 workgroups) the
-  // lower occupancy cost ~1 %, so they keep 4-load trips.  DLLM_GEMV_LONG_TRIP=0 disables it.
-  static const int long_trip = [] { const char* e = getenv("DLLM_GEMV_LONG_TRIP"); return e ? atoi(e) : 1; }();
+  // lower occupancy cost ~1 %, so they keep 4-load trips.
   if constexpr (M <= 2 && R == 1) {
-    if (long_trip && K > 2048 && K <= 6144 && gemv_blocks<R>(N) <= 512) {
+    if (K > 2048 && K <= 6144 && gemv_blocks<R>(N) <= 512) {
       if (K <= 4096)
         hipLaunchKernelGGL((gemv_kernel<M, R, 8, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
                            (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);

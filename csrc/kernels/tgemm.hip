@@ -152,10 +152,12 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   // ---- QKV row metadata: the positions and cache slots of this lane's output rows are loaded
   // with the row-scale partials, before the ring (they retire at its first wait), so the epilogue
   // starts with them in registers: its RoPE table reads are then ONE round trip, not two dependent
-  // ones (pos -> cos/sin), and the K copy-out reads its slots from LDS
-  constexpr int QR = (EPI == EPI_QKV) ? FM * 4 : 1;
+  // ones (pos -> cos/sin), and the K copy-out reads its slots from LDS.  Decode-sized tiles only
+  // (FM <= 2): 2 FM*4 live registers across the ring spill the large prefill tiles
+  constexpr bool QPF = EPI == EPI_QKV && FM <= 2;
+  constexpr int QR = QPF ? FM * 4 : 1;
   int q_pos[QR], q_slot[QR];
-  if constexpr (EPI == EPI_QKV) {
+  if constexpr (QPF) {
     if (!loader) {
       const int rlq = wm * WM + 4 * (lane >> 4);
 #pragma unroll
@@ -206,20 +208,27 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
       l_off[j] = ks * SUB_BYTES + p * 1024;
     }
   }
+  // Rotated k order: each output tile walks its k-steps from its own offset, so the many
+  // workgroups that stream the SAME activation / weight panel at once are spread over different k
+  // columns (L2 channels) instead of all requesting one line together (rg ROT in
+  // scripts/exp/gemmlab.hip: 1-3 % on the decode shapes).  Slot t of the ring holds k-step kstep(t).
+  const int krot = nk > 1 ? (int)(((unsigned)(n_tile * 7 + m_tile * 3)) % (unsigned)nk) : 0;
+  auto kstep = [&](int t) { const int u = t + krot; return u >= nk ? u - nk : u; };
   auto issue = [&](int t) {
+    const int tk = kstep(t);
     if constexpr (NL > 0) {
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
 #pragma unroll
       for (int j = 0; j < GL; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + t * l_step[j]), (lds_void*)(base + l_off[j]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + tk * l_step[j]), (lds_void*)(base + l_off[j]), 16, 0, 0);
       return;
     }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (WK == 2 && ks != kg) continue;  // each k-group stages its own sub-tile
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + ks * SUB_BYTES;
-      const int ko = t * KSTEP + ks * BK;
-      const long kw = (long)(t * KS + ks) * wstep;
+      const int ko = tk * KSTEP + ks * BK;
+      const long kw = (long)(tk * KS + ks) * wstep;
 #pragma unroll
       for (int j = 0; j < GA; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + ko), (lds_void*)(base + (wave * GA + j) * 1024),
@@ -411,9 +420,10 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rl = rl0 + 16 * i + e, m = m0 + rl;
-        const int slot = q_slot[4 * i + e];
+        const int mq = min(m, M - 1);
+        const int slot = QPF ? q_slot[(4 * i + e) % QR] : a.slots[mq];
         if (wn == 0 && cl == 0) s_slot[rl] = slot;
-        const float* cs = a.cos_sin + (long)q_pos[4 * i + e] * d;
+        const float* cs = a.cos_sin + (long)(QPF ? q_pos[(4 * i + e) % QR] : a.pos[mq]) * d;
         const long blk = slot >> 4, off = slot & 15;
 #pragma unroll
         for (int jp = 0; jp < FN / 2; ++jp) {

@@ -32,7 +32,7 @@ import torch
 from .. import ops
 from ..models.configs import ModelConfig, get_model_config
 from ..models.llama import AttnMeta, LlamaModel
-from ..utils.faults import fault
+from ..utils.faults import diag, fault
 from ..parallel.comm import SINGLE, ParallelContext
 from ..utils.tracing import tracer
 from .sampling import SamplingParams
@@ -212,8 +212,8 @@ class LLMEngine:
         self._early_pf = None      # a prefill chunk queued under the last step of a decode burst
         self._pf_tok: Optional[torch.Tensor] = None   # pinned first tokens of a prefill chunk
         self._in_join_burst = False
-        # DLLM_SYNC_LOG=1: per pipelined step (host prep s, wait for the in-flight step s, launched)
-        self._sync_log: Optional[list] = [] if os.environ.get("DLLM_SYNC_LOG", "0") == "1" else None
+        # DLLM_DIAG=sync: per pipelined step (host prep s, wait for the in-flight step s, launched)
+        self._sync_log: Optional[list] = [] if diag("sync") else None
         pin = self.on_gpu
         # host mirror of the device block table (pinned); row R is the dummy row of padding tiles.
         self.bt_host_t = torch.zeros((R + 1, self.max_blocks), dtype=torch.int32, pin_memory=pin)
@@ -237,7 +237,7 @@ class LLMEngine:
         # Step I/O by kernels inside the step's graph (ops.step_fetch / step_store: the pinned
         # buffers are device-mapped), not by async copies: an H2D copy runs on an SDMA engine and
         # waited ~320 us per step for the previous step's read-back to signal it (r4 gap analysis).
-        self._gio = self.on_gpu and ops.native_available() and os.environ.get("DLLM_STEP_IO_KERNEL", "1") == "1"
+        self._gio = self.on_gpu and ops.native_available()   # step I/O by kernels inside the step graph
         self.dec_dev = torch.zeros(self._dec_n, dtype=torch.int32, device=self.device)
         # two pinned staging buffers: the pipelined decode (_decode_burst) fills one while the
         # previous step's async copy may still be reading the other
@@ -252,7 +252,7 @@ class LLMEngine:
         # the whole sampler runs inside the decode graph (ops.sample_rows) unless the vocab is
         # tensor-parallel (then the distributed arg-max / top-k of LlamaModel is used)
         # one-launch sampler inside the decode graph (TP: merged per-shard top-256 candidates, LlamaModel.sample)
-        self.fused_sampler = os.environ.get("DLLM_FUSED_SAMPLER", "1") == "1"
+        self.fused_sampler = True   # one-launch in-graph sampler (the host-side path stays for tests)
         self._seed_ctr = 0
         dv = self.dec_dev
         self.d_temp = dv[s0:s0 + mb].view(torch.float32)
@@ -313,26 +313,26 @@ class LLMEngine:
 
     # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),
     # tiles ordered longest context first (the dispatcher then starts the longest chains first).
-    # Opt-in (DLLM_ATTN_DYNAMIC=1): fixed grid depth, and each step the host writes a split length
-    # so the batch yields ~ATTN_TARGET_WGS workgroups; measured slower on MI355X because surplus
-    # early-exit blocks cost dispatch slots (csrc/kernels/attention.hip note).
-    ATTN_DYNAMIC = os.environ.get("DLLM_ATTN_DYNAMIC") == "1"
-    SORT_TILES = os.environ.get("DLLM_DECODE_SORT", "1") == "1"   # decode tiles longest context first
-    ATTN_TARGET_WGS = int(os.environ.get("DLLM_ATTN_TARGET_WGS", "2048"))
+    # ATTN_DYNAMIC (class attribute, off): fixed grid depth, and each step the host writes a split
+    # length so the batch yields ~ATTN_TARGET_WGS workgroups; measured slower on MI355X because
+    # surplus early-exit blocks cost dispatch slots (csrc/kernels/attention.hip note).
+    ATTN_DYNAMIC = False
+    SORT_TILES = True        # decode tiles longest context first
+    ATTN_TARGET_WGS = 2048
     # Default: persistent work-list attention (ops.decode_work_items): a fixed grid of at most
     # ATTN_PGRID workgroups walks ~ATTN_ITEMS_PER_WG equal key ranges each, longest first.
-    ATTN_WORKLIST = os.environ.get("DLLM_ATTN_WORKLIST", "1") == "1"
-    ATTN_PGRID = int(os.environ.get("DLLM_ATTN_PGRID", "512"))
-    ATTN_ITEMS_PER_WG = int(os.environ.get("DLLM_ATTN_ITEMS_PER_WG", "1"))
+    ATTN_WORKLIST = True
+    ATTN_PGRID = 512
+    ATTN_ITEMS_PER_WG = 1
     # Work list at every batch size: in a whole decode step (scripts/microbench.py decode, 1x
     # MI355X, TinyLlama) it cut B=1 from 1.14 to 0.89 ms and B=16 from 1.51 to 1.29 ms vs the
     # static split grid (a kernel-only sweep had B=16-64 about even)
-    ATTN_WL_MIN_BS = int(os.environ.get("DLLM_ATTN_WL_MIN_BS", "1"))
+    ATTN_WL_MIN_BS = 1
     # shortest key range of one work-list unit (split-K granularity)
     # (256: with the parallel split combine, batch 1-8 steps at 2k context are 2-3 % faster than at
     # 512 and equal at 8k, microbench decode sweep; it only matters while batch x context < 64k
     # tokens, above that the target unit count sets the chunk)
-    ATTN_MIN_CHUNK = int(os.environ.get("DLLM_ATTN_MIN_CHUNK", "256"))
+    ATTN_MIN_CHUNK = 256
     def _use_worklist(self, bs: int) -> bool:
         return self.attn_worklist and bs >= self.ATTN_WL_MIN_BS
 
@@ -1184,7 +1184,7 @@ class LLMEngine:
     # that stops on EOS at step k has already been launched in step k+1: that one row is computed
     # and discarded (its KV slot belongs to the finished sequence).  Count limits (max_new_tokens,
     # max_model_len) are known in advance and never cost a row.
-    PIPELINE = os.environ.get("DLLM_DECODE_PIPELINE", "1") == "1"
+    PIPELINE = True
     # New requests end a pipelined burst (to be admitted and prefilled) only once the burst has run
     # this many steps: a client that keeps submitting (turn pipelining) would otherwise cut every
     # burst to one or two steps and lose the host/GPU overlap; the added admission delay is at most
@@ -1192,13 +1192,13 @@ class LLMEngine:
     # into an idle engine, where it makes no difference).
     ADMIT_EVERY = max(1, int(os.environ.get("DLLM_ADMIT_EVERY", "1")))
 
-    # Tensor-parallel pools pipeline too (DLLM_TP_PIPELINE=0: off).  Every rank must take the same
+    # Tensor-parallel pools pipeline too (class attribute TP_PIPELINE).  Every rank must take the same
     # burst decisions, so a TP burst never looks at the leader-only inbox: it ends on the shared
     # stop rules (tokens, KV blocks and the mirrored waiting list are identical on every rank) or
     # after MIRROR_EVERY steps, when the next admission exchange is due.  The in-graph health vote
     # of the one-shot all-reduces is read back with each step's tokens; a trip ends the burst, the
     # step is re-run on the fallback collectives and the step already in flight is discarded.
-    TP_PIPELINE = os.environ.get("DLLM_TP_PIPELINE", "1") == "1"
+    TP_PIPELINE = True
 
     def _pipeline_ok(self) -> bool:
         return (self.PIPELINE and self.on_gpu and self.use_graphs and self.fused_sampler
@@ -1234,7 +1234,7 @@ class LLMEngine:
     # admission).  New sequences only take free rows and free blocks (nothing is released before
     # the burst has drained), and a prefix hit only shares full, committed blocks, never the slot
     # the in-flight step writes.  Single-GPU pools only (TP admissions follow the mirrored schedule).
-    EARLY_PREFILL = os.environ.get("DLLM_EARLY_PREFILL", "1") == "1"
+    EARLY_PREFILL = True
 
     def _early_admit(self, waiting: List[_Seq], prefilling: Optional[List[_Seq]], running: List[_Seq]) -> None:
         if (prefilling is None or self._early_pf is not None or not self.EARLY_PREFILL or self.par.enabled
@@ -1265,7 +1265,7 @@ class LLMEngine:
     # step after it stopped (when no in-flight step can still write its reserved slot), so rows
     # recycle without a drain.  Needs the step I/O kernels (per-row input ids from the host next to
     # gathered ones); single-GPU pools only.
-    BURST_JOIN = os.environ.get("DLLM_BURST_JOIN", "1") == "1"
+    BURST_JOIN = True
 
     def _take_joiners(self, prefilling: List[_Seq], running: List[_Seq], finished: List[_Seq],
                       preempted: List[_Seq]) -> List[_Seq]:

@@ -151,7 +151,7 @@ class LlamaModel:
         # MoE experts on the grouped LDS-tiled GEMM (csrc/kernels/moe.hip moe_ffn_tg): gate/up rows
         # of every expert interleaved in place for the SwiGLU epilogue
         self.moe_tg = bool(cfg.is_moe and self.device.type == "cuda" and ops.native_available()
-                           and cfg.hidden % 64 == 0 and self.I % 64 == 0 and os.environ.get("DLLM_MOE_TG", "1") == "1")
+                           and cfg.hidden % 64 == 0 and self.I % 64 == 0)
         if self.moe_tg:
             idx = gate_up_order(self.I).to(self.device)
             for L in self.layers:
@@ -431,10 +431,12 @@ class LlamaModel:
             r = torch.empty((T, H), dtype=self.dtype, device=input_ids.device)
             n = par.all_reduce_resadd(ops.embedding(input_ids, self.embed, self.vocab_shard.start, scatter=scatter),
                                       r, ssq_a, add=False)
-        # decode (one new token per sequence, TP 1): the QKV GEMM hands V over row-major and the
-        # attention kernel writes each sequence's newest V^T itself (ops.gemm.qkv_rope_cache)
+        # decode (one new token per sequence, TP 1, head_dim 64): the QKV GEMM hands V over row-major
+        # and the attention kernel writes each sequence's newest V^T itself (ops.gemm.qkv_rope_cache;
+        # for d = 96 / 128 the patch would cost the attention kernel a wave per SIMD)
         vn = (torch.empty((T, self.nkv * self.d), dtype=self.dtype, device=input_ids.device)
-              if (not tp and meta.all_last and meta.items is not None and input_ids.is_cuda) else None)
+              if (not tp and self.d == 64 and meta.all_last and meta.items is not None and input_ids.is_cuda)
+              else None)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             # column-parallel QKV (this rank's heads) with RMSNorm folded + RoPE + paged K/V write

@@ -142,7 +142,8 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
 
     ``v_new`` (decode, one query token per sequence): the new tokens' V row-major [T, nkv * d],
     NOT yet in the V^T cache (``gemm.qkv_rope_cache(v_new=...)``); the kernel writes each
-    sequence's newest V into the cache and uses it (CPU: the reference writes it first).
+    sequence's newest V into the cache and uses it (CPU: the reference writes it first).  GPU:
+    head_dim 64 with the work list only (the patch would cost d = 96 / 128 a wave per SIMD).
 
     ``splits`` is the split-K grid depth; with ``split_len`` (int32 device scalar, keys per split)
     each tile uses only ceil(its keys / split_len) of them (dynamic, balanced split-K).

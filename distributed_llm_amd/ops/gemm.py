@@ -66,7 +66,7 @@ EPI_PLAIN, EPI_RESADD, EPI_QKV, EPI_SWIGLU, EPI_GELU = 0, 1, 2, 3, 4
 # of the weight operand is one contiguous 1 KB instead of eight 128-B row pieces 4-11 KB apart
 # (profiles/r3_decode_gemm_panel.md).  The row-major weight stays for the GEMV / skinny / hipBLASLt
 # paths; models.llama keeps the panel copy only while both fit comfortably in HBM.
-W_PANEL = os.environ.get("DLLM_W_PANEL", "1") == "1"
+W_PANEL = True
 
 
 def panel_weight(w: torch.Tensor) -> torch.Tensor:
@@ -161,14 +161,16 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
-# Prefill-size buckets (M > MAX_M), opt-in (DLLM_PREFILL_TUNE=1): the fused ops' core is chosen per
+# Prefill-size buckets (M > MAX_M), opt-in (PREFILL_TUNE, autotune(prefill=True)): the fused ops' core is chosen per
 # (bucket, N, K) between one tgemm launch with the epilogue fused and hipBLASLt + the standalone
 # epilogue kernel; a prefill chunk uses the plan of the smallest bucket that holds it.  The probe
 # (scripts/exp/prefill_gemm_probe.py) has tgemm ahead on a few shapes (TinyLlama Wo at 2-4K rows,
 # gate|up at 8K: 9 %), but with those choices the flagship's prefill took 27 % longer (chunks of
 # ~5K rows run the 8K bucket's tile; profiles/r4_prefill_gemm.md), so hipBLASLt stays the default
 # core above MAX_M.
-PREFILL_MS = tuple(int(x) for x in os.environ.get("DLLM_PREFILL_TUNE_MS", "2048,4096,8192").split(",") if x)
+PREFILL_MS = (2048, 4096, 8192)
+PREFILL_TUNE = False   # measured slower end to end (above); autotune(prefill=True) opts in
+STREAM_K = False       # stream-K tgemm plans in the autotuner (see _tg_cands)
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8), (192, 128, 3, 1, 1, 8),
              (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4))
 
@@ -329,10 +331,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
         return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
     plan = _P.plans.get(_key(x, w, False))
     if plan is None:
-        if x.shape[0] > MAX_M and w.shape[1] % 64 == 0 and x.stride(0) % 8 == 0 and x.stride(1) == 1 \
-                and os.environ.get("DLLM_TG_PREFILL", "0") == "1":
-            plan = ("tg",) + tg_plan(x.shape[0], w.shape[0], w.shape[1])
-        elif x.shape[0] > MAX_M:
+        if x.shape[0] > MAX_M:
             plan = ("blas",)
         else:
             plan = _heuristic(x.shape[0], w.shape[0], w.shape[1])
@@ -342,19 +341,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
 def norm_linear(h: torch.Tensor, residual: torch.Tensor, spare: torch.Tensor, norm_w: torch.Tensor, eps: float,
                 w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """``linear(rmsnorm(h + residual) * norm_w, w)`` and the updated residual stream (unfused
-    layer path: tensor parallel, CPU).
-
-    Where the tuned plan for this shape is the GEMV (batch <= 8), one launch can do both
-    (csrc/kernels/gemv.hip NORM, opt-in DLLM_FUSED_NORM=1: measured SLOWER at batch 1,
-    profiles/r1_small_batch_decode.md); the new residual then goes to ``spare`` and is returned."""
-    M, N, K = h.shape[0], w.shape[0], w.shape[1]
-    if h.is_cuda and M <= MAX_M and os.environ.get("DLLM_GEMM") != "blas" \
-            and os.environ.get("DLLM_FUSED_NORM", "0") == "1":
-        plan = _P.plans.get((M, N, K, False))
-        if plan is not None and plan[0] == "gemv" and h.is_contiguous() and M * K * 2 <= 64 * 1024:
-            y = torch.empty((M, N), dtype=h.dtype, device=h.device)
-            _native(h).gemv_norm(h, residual, spare, norm_w, float(eps), w, y, plan[1])
-            return y, spare
+    layer path: tensor parallel, CPU).  (A one-launch GEMV form, gemv.hip NORM, measured SLOWER at
+    batch 1, profiles/r1_small_batch_decode.md; ``spare`` is kept for that interface.)"""
     from . import rms_norm
     x = rms_norm(h, norm_w, eps, residual=residual)
     return linear(x, w), residual
@@ -575,7 +563,7 @@ def _plan_key(k) -> str:
 
 
 def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False,
-             fused: Iterable[Tuple[int, int]] = ()) -> None:
+             fused: Iterable[Tuple[int, int]] = (), prefill: bool = False) -> None:
     """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest.
 
     ``fused``: the (N, K) shapes of one decoder layer's fused ops (QKV, Wo, gate|up, down); a
@@ -602,7 +590,7 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
     # the fused ops' tgemm plans stream the panel weight copies: time them in that layout
     _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set())
     _couple_gemv_choices(fused, list(ms), verbose)
-    if os.environ.get("DLLM_PREFILL_TUNE", "0") == "1":
+    if PREFILL_TUNE or prefill:
         _autotune_prefill(fused, dev, verbose)
     if cache:
         import json
@@ -695,7 +683,7 @@ def _tg_cands(M: int, N: int, K: int):
                     out.append((bm, bn, st, sp, ks, nw))
                     if ks == 2 and nw == 4 and st <= 3 and bm <= 128 and bn <= 128:
                         out.append((bm, bn, st, sp, ks, nw, 2))   # two k-groups of 4 waves
-    if N % 8 == 0 and os.environ.get("DLLM_TG_NL", "1") == "1":
+    if N % 8 == 0:
         for bm, bn, nw, st, nl, m_min in _TG_NL:
             if M < m_min:
                 continue
@@ -708,10 +696,10 @@ def _tg_cands(M: int, N: int, K: int):
                 out.append((bm, bn, st, sp, 1, nw, 1, nl))
     # stream-K forms (one workgroup per CU walking equal shares of tiles x k-steps) of the one-split
     # plans whose tile count leaves CUs idle (M = 320 gives a 64 x 64 grid 160 tiles for N = 2048).
-    # Opt-in (DLLM_TG_SK=1): measured, they never beat the one-unit plans on the TinyLlama shapes at
-    # M = 320-448, because the shared-operand L2 -> LDS traffic, not the idle CUs, sets the time
-    # (profiles/r3_decode_gemm_panel.md section 5)
-    if torch.cuda.is_available() and os.environ.get("DLLM_TG_SK", "0") == "1":
+    # Not offered (STREAM_K False): measured, they never beat the one-unit plans on the TinyLlama
+    # shapes at M = 320-448, because the shared-operand L2 -> LDS traffic, not the idle CUs, sets
+    # the time (profiles/r3_decode_gemm_panel.md section 5); the plans stay callable (tests)
+    if torch.cuda.is_available() and STREAM_K:
         g = _sk_grid(torch.cuda.current_device())
         for c in list(out):
             bm, bn, st, sp, ks, nw = c[:6]
@@ -728,7 +716,7 @@ def _tg_cands(M: int, N: int, K: int):
 
 
 def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
-    use_tg = os.environ.get("DLLM_GEMM_NO_TG") != "1"
+    use_tg = True
     for (N, K, sw) in shapes:
         copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
         ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(copies)]
@@ -744,7 +732,7 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
                 continue
             x = torch.randn(M, 2 * K if sw else K, device=dev).to(torch.bfloat16)
             cands = [("blas",)]
-            if M in _GEMV_MS and K % 8 == 0 and M * K * 2 <= 64 * 1024 and os.environ.get("DLLM_GEMM_NO_GEMV") != "1":
+            if M in _GEMV_MS and K % 8 == 0 and M * K * 2 <= 64 * 1024:
                 cands.extend(("gemv", r) for r in _GEMV_RS)
             for ntw in (_NTWS if M <= SKINNY_MAX_M else ()):
                 if M > 64 and ntw == 4:
@@ -778,7 +766,7 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
                 # fused-epilogue GEMV (one launch): timed in its RESADD form (the paired QKV /
                 # SwiGLU forms stream the same rows with the same per-wave loads)
                 gv = [c for c in res if c[0] == "gemv"]
-                if gv and N % 32 == 0 and os.environ.get("DLLM_GEMV_EPI", "1") == "1":
+                if gv and N % 32 == 0:
                     ext = _native(x)
                     rr = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
                     sq = torch.empty(max_slots(N, M), M, dtype=torch.float32, device=dev)

@@ -1,4 +1,6 @@
-"""Fault injection for tests: ONE environment variable,
+"""Fault injection for tests and bench diagnostics (``diag``, DLLM_DIAG).
+
+Faults: ONE environment variable,
 
     DLLM_FAULT="die_after=1,die_rank=2"          (comma-separated key=value pairs)
 
@@ -40,6 +42,19 @@ def fault(key: str, default: Any = None, cast=str) -> Any:
         spec = _cache[raw] = _parse(raw)
     v = spec.get(key)
     return default if v is None else cast(v)
+
+
+def diag(name: str):
+    """Diagnostics switch from ``DLLM_DIAG`` (comma-separated): ``sync`` (per-step host prep / wait
+    log of the pipelined step loop), ``cpu`` (per-thread CPU share of the bench window),
+    ``profile=PATH`` (cProfile of the bench's driver thread).  Returns the value for ``key=value``
+    entries, True for bare names, None when absent."""
+    raw = os.environ.get("DLLM_DIAG", "")
+    for part in raw.split(","):
+        k, _, v = part.strip().partition("=")
+        if k == name:
+            return v or True
+    return None
 
 
 def spec(**kw) -> str:

@@ -43,10 +43,11 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&noslots, M * 4));
   CHECK(hipMemset(noslots, 0xff, M * 4));
   const long blocks = 8192;
-  u16 *kc, *vc, *qo, *A, *Y;
+  u16 *kc, *vc, *qo, *A, *Y, *vrows;
   CHECK(hipMalloc(&kc, blocks * nkv * 16 * d * 2));
   CHECK(hipMalloc(&vc, blocks * nkv * 16 * d * 2));
   CHECK(hipMalloc(&qo, (long)M * nq * d * 2));
+  CHECK(hipMalloc(&vrows, (long)M * nkv * d * 2));
   CHECK(hipMalloc(&A, (long)M * I * 2));
   CHECK(hipMalloc(&Y, (long)M * 2 * I * 2));
   {
@@ -79,9 +80,10 @@ int main(int argc, char** argv) {
     }
     for (const Plan& p : plans) {
       // variants: 0 plain, 1 plain + RMSNorm row scale (ssq partials), 2 fused epilogue,
-      // 3 (QKV only) fused epilogue with every cache slot -1 (no K / V^T cache stores)
-      for (int e = 0; e < 4; ++e) {
-        if (e == 3 && sh.epi != dllm::EPI_QKV) continue;
+      // 3 (QKV only) fused epilogue with every cache slot -1 (no K / V^T cache stores),
+      // 4 (QKV only) V handed over row-major (v_rows, the decode form)
+      for (int e = 0; e < 5; ++e) {
+        if (e >= 3 && sh.epi != dllm::EPI_QKV) continue;
         if (e == 1 && sh.epi == dllm::EPI_RESADD) continue;
         const int epi = e >= 2 ? sh.epi : dllm::EPI_PLAIN;
         dllm::GemmArgs a{};
@@ -95,6 +97,7 @@ int main(int argc, char** argv) {
         if (epi == dllm::EPI_RESADD) { a.ssq_out = ssq_out; a.ssq_out_ld = M; }
         a.pos = pos; a.cos_sin = cs; a.slots = e == 3 ? noslots : slots; a.q_out = qo; a.kc = kc; a.vc = vc;
         a.nq = nq; a.nkv = nkv; a.d = d;
+        if (e == 4) { a.v_rows = vrows; a.v_ld = nkv * d; }
         const int rc = dllm_tgemm(&a, p.bm, p.bn, p.st, p.ks, p.nw, 1, epi, s, p.nl);
         if (rc != 0) continue;
         CHECK(hipStreamSynchronize(s));
@@ -123,7 +126,7 @@ int main(int argc, char** argv) {
         const double us = ms * 1000.0 / (reps * nlaunch);
         printf("{\"M\": %d, \"shape\": \"%s\", \"N\": %d, \"K\": %d, \"plan\": \"%dx%d st%d S%d ks%d nw%d nl%d\", \"epi\": \"%s\", \"us\": %.2f, \"TFs\": %.0f}\n",
                M, sh.name, sh.N, sh.K, p.bm, p.bn, p.st, p.splits, p.ks, p.nw, p.nl,
-               e == 0 ? "plain" : e == 1 ? "plain+rowscale" : e == 2 ? sh.name : "qkv-no-cache-writes", us,
+               e == 0 ? "plain" : e == 1 ? "plain+rowscale" : e == 2 ? sh.name : e == 3 ? "qkv-no-cache-writes" : "qkv-v-rows", us,
                2.0 * M * sh.N * sh.K / us / 1e6);
         fflush(stdout);
       }

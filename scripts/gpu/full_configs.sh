@@ -5,10 +5,10 @@
 # of weights on the card); config 4: Llama-3-8B x4 | Llama-3-70B TP=4 (~205 GB).  Throughput here
 # is 8 processes time-slicing one GPU: this proves the configurations run, it measures nothing.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/fullcfg
 mkdir -p $O
-export HSA_ENABLE_IPC_MODE_LEGACY=0 DLLM_REHEARSE_ONE_GPU=1 DLLM_W_PANEL=0 DLLM_AUTOTUNE=0 OMP_NUM_THREADS=2 \
+export HSA_ENABLE_IPC_MODE_LEGACY=0 DLLM_REHEARSE_ONE_GPU=1 DLLM_AUTOTUNE=0 OMP_NUM_THREADS=2 \
   MASTER_ADDR=127.0.0.1 DLLM_EMBEDDER=hash
 ( while true; do sleep 45; echo "tick $(date +%T) $(tail -c 200 $O/cfg*.log 2>/dev/null | tail -1 | cut -c1-120)"; done ) &
 TICK=$!

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Per-model routed bench line + rocprof kernel table on one MI355X:
-#   MODEL=llama-3-8b CONVS=128 STEPS=2 bash scripts/gpu_model_bench.sh
+#   MODEL=llama-3-8b CONVS=128 STEPS=2 bash scripts/gpu/model_bench.sh
 # Run 1 tunes the GEMM plans (saved); run 2 is the profiled one (kernel trace + stats, no PMC).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 M=${MODEL:?MODEL}
 CONVS=${CONVS:-128}

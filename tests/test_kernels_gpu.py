@@ -168,7 +168,7 @@ def test_paged_attention_worklist(nq, nkv, d, grid, target, min_chunk, ext):
     assert int(ws[2].abs().sum()) == 0
 
 
-@pytest.mark.parametrize("nq,nkv,d", [(32, 4, 64), (32, 8, 128), (32, 32, 96)])
+@pytest.mark.parametrize("nq,nkv,d", [(32, 4, 64), (32, 8, 64), (16, 16, 64)])
 @pytest.mark.parametrize("ext,grid", [(True, 7), (True, 512), (False, 64)])
 def test_paged_attention_decode_writes_newest_v(nq, nkv, d, ext, grid):
     """Decode hand-over (AttnArgs.v_new): each sequence's newest V arrives row-major and its V^T
@@ -204,6 +204,17 @@ def test_paged_attention_decode_writes_newest_v(nq, nkv, d, ext, grid):
     assert torch.equal(vc, vc_ref)          # every newest slot written, nothing else touched
     o3 = ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=z, workspace=ws, items=it, grid_items=grid)
     torch.testing.assert_close(o3.float(), o2.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_paged_attention_newest_v_refused_for_wide_heads():
+    """The v_new patch is built for head_dim 64 only; d = 128 must fail loudly, not skip the write."""
+    q, kc, vc, bt, qs, ql, cx, ts, tt = _attn_case(32, 8, 128, [(1, 40), (1, 7)], NB=16)
+    items = torch.tensor(ops.decode_work_items(np.array([40, 7]), 8, 4, 256, min_chunk=32), device=DEV)
+    ws = (torch.empty(2 * 8 * 4 * 16 * 128, device=DEV), torch.empty(2 * 8 * 4 * 16 * 2, device=DEV),
+          torch.zeros(2 * 8 + 2, dtype=torch.int32, device=DEV))
+    with pytest.raises(RuntimeError):
+        ops.paged_attention(q, kc, vc, bt, qs, ql, cx, ts, tt, splits=4, workspace=ws, items=items, grid_items=64,
+                            v_new=torch.zeros(2, 8 * 128, dtype=torch.bfloat16, device=DEV))
 
 
 def test_paged_attention_bidirectional():

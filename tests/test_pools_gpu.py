@@ -25,7 +25,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
-STEPS, WARMUP, CONVS = 4, 0, 24
+STEPS, WARMUP, CONVS = 4, 0, 24   # (the event-driver tests need WARMUP >= 0 only)
 COMMON = ["--steps", str(STEPS), "--warmup", str(WARMUP), "--kv-gb", "4", "--small-model", "tinyllama-1.1b",
           "--large-model", "llama-3.2-1b", "--small-new", "16", "--large-new", "24", "--greedy", "--no-graphs",
           "--strategy", "hybrid", "--pipeline", "0"]
@@ -143,7 +143,8 @@ def test_config5_colocated_mixtral_tp8_one_gpu(tmp_path):
     lay = res["layout"]
     assert lay["colocated"] and lay["large"]["replicas"] == [list(range(8))] and lay["large"]["model"] == "mixtral-8x7b"
     assert lay["small"]["replicas"] == [[r] for r in range(8)]
-    assert res["requests"] == 3 * 8 * 3 and res["pool_events"]["lost_turns"] == 0
+    assert res["config"]["turn_pipelining"] == "event-driver"
+    assert res["requests"] >= 3 * 8 * 3 and res["pool_events"]["lost_turns"] == 0
     assert 0.0 < res["small_tier_share"] < 1.0, "both tiers must serve"
 
 
@@ -163,4 +164,24 @@ def test_config4_large_leader_dies_mid_window_one_gpu(tmp_path):
     ev = res["pool_events"]
     assert ev["dead_ranks"] == [4] and ev["degraded"] and ev["failed_tiers"] == ["orin"], ev
     assert ev["failovers"] > 0 and ev["lost_turns"] == 0, ev
-    assert res["requests"] == 3 * 8 * 3 and sum(ev["failovers_by_step"]) == ev["failovers"]
+    # the event driver (the default): a failed turn is re-submitted to the small tier without
+    # stalling the other conversations' dispatch (Router.finish_ticket)
+    assert res["config"]["turn_pipelining"] == "event-driver"
+    assert res["requests"] >= 3 * 8 * 3 and sum(ev["failovers_by_step"]) == ev["failovers"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_pools_event_driver_n_ranks_one_gpu(world, tmp_path):
+    """The driver's N-rank pools command with the 1-GPU serving mode (event-driven turn pipelining,
+    --pipeline 2, the default): remote pools take non-blocking submissions and answer each request
+    on its own, so the JSON line reports the event driver and every conversation keeps turning."""
+    logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
+    os.makedirs(logdir, exist_ok=True)
+    args = [a for a in COMMON if a not in ("--pipeline", "0")]
+    res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world),
+                "--topology", "pools", "--convs", str(CONVS // world), *args],
+               os.path.join(logdir, f"pools_event_n{world}.log"), timeout=600)
+    assert res["n_gpus"] == world and res["config"]["turn_pipelining"] == "event-driver"
+    assert res["requests"] >= CONVS * STEPS and res["pool_events"]["lost_turns"] == 0
+    assert 0.0 < res["small_tier_share"] < 1.0 and res["p50_latency_ms"] > 0
