@@ -851,10 +851,11 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
            c10::optional<torch::Tensor> cos_sin, c10::optional<torch::Tensor> slots,
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
            int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk, int64_t nl,
-           c10::optional<torch::Tensor> sk_table, int64_t sk_cmax, c10::optional<torch::Tensor> v_rows) {
+           c10::optional<torch::Tensor> sk_table, int64_t sk_cmax, c10::optional<torch::Tensor> v_rows,
+           int64_t kdepth) {
   check_bf16(x, "x");
   check_bf16(w, "w");
-  if (nl > 0) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
+  if (nl > 0 && kdepth != 32) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
     const bool known = ks == 1 && wk == 1 &&
                        ((bm == 64 && bn == 64 && nw == 4 &&
                          ((nl == 2 && stages == 4) || ((nl == 4 || nl == 8) && (stages == 4 || stages == 8)))) ||
@@ -875,7 +876,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   TORCH_CHECK(wk == 1 || (wk == 2 && nw == 4 && ks == 2 && stages <= 3 && bm <= 128 && bn <= 128),
               "wk 2: two k-groups of 4 waves, ks 2, 2-3 stages, tiles up to 128 x 128");
   TORCH_CHECK(x.size(1) == K && K % (64 * ks) == 0, "x [M, K], K % (64 ks) == 0");
-  TORCH_CHECK(nl > 0 || ((bm == 64 || bm == 128 || ((bm == 192 || bm == 256) && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
+  TORCH_CHECK(nl > 0 || kdepth == 32 || ((bm == 64 || bm == 128 || ((bm == 192 || bm == 256) && nw == 8)) && (bn == 64 || bn == 128 || (bn == 256 && bm == 256)) &&
                   (stages == 2 || stages == 3 || ((stages == 4 || stages == 6) && ks == 1 && bm <= 128)) &&
                   (int64_t)stages * ks * (bm + bn) * 128 <= 150 * 1024),
               "tile / ring size");
@@ -983,6 +984,8 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
       a.v_ld = v_rows->stride(0);
     }
   }
+  TORCH_CHECK(kdepth == 64 || kdepth == 32, "tgemm: k depth 64 or 32");
+  a.kdepth = (int)kdepth;
   ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)wk, (int)epi, stream(), (int)nl), "tgemm");
 }
 

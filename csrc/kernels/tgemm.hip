@@ -85,7 +85,17 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + er
 // At decode-size M a stage's fill and its MFMA chain then overlap instead of alternating inside
 // each wave (profiles/r3_decode_gemm_lab.md: 5-30 % faster on the TinyLlama / Llama-3-8B decode
 // projections at M = 320-512).
-template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK, int NL, int WGM>
+// BKT: k depth of a staged sub-tile, 64 (one 128-B row line) or 32 (64-B rows: half the LDS per
+// stage, so the 256-row tiles of the prefill / wide-N plans fit a 4-6 stage ring; the swizzle then
+// permutes the 4 chunks of a row by (row >> 2) & 3 -> {0, 2, 3, 1}, which keeps every 16-lane
+// group of a fragment read on 16 distinct 16-B bank slots).
+template <int BKT>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (BKT == 64) return (r >> 1) & 7;
+  else return (0x1320 >> (4 * ((r >> 2) & 3))) & 3;
+}
+
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK, int NL, int WGM, int BKT>
 __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* smem, int M, const int S,
                                            const int SC, const int split, const int m_tile,
                                            const int n_tile, const int kbeg, const int nk) {
@@ -97,15 +107,17 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   constexpr int WM = BM / WGM, WN = BN / NWN;
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(FN % 2 == 0 && FM >= 1 && WM % 16 == 0 && NW % WGM == 0, "wave tile: >= 16 rows, a multiple of 32 columns");
-  constexpr int A_BYTES = BM * ROWB, SUB_BYTES = (BM + BN) * ROWB, STAGE_BYTES = KS * SUB_BYTES;
-  constexpr int GA = NL ? 1 : BM / (8 * NW), GB = NL ? 1 : BN / (8 * NW);  // global_load_lds per wave per sub-tile
-  constexpr int PPS = KS * (BM + BN) / 8;                                  // 1 KB pieces per stage
-  constexpr int GL = NL ? PPS / NL : 1;                                    // ... per loader wave
+  constexpr int RB = 2 * BKT, RPP = 1024 / RB, LPR = RB / 16;  // row bytes, rows per 1 KB piece, lanes per row
+  constexpr int A_BYTES = BM * RB, SUB_BYTES = (BM + BN) * RB, STAGE_BYTES = KS * SUB_BYTES;
+  constexpr int GA = NL ? 1 : BM / (RPP * NW), GB = NL ? 1 : BN / (RPP * NW);  // global_load_lds per wave per sub-tile
+  constexpr int PPS = KS * (BM + BN) / RPP;                                    // 1 KB pieces per stage
+  constexpr int GL = NL ? PPS / NL : 1;                                        // ... per loader wave
   static_assert(NL == 0 || PPS % NL == 0, "stage pieces must split evenly over the loader waves");
   constexpr int G = NL ? GL : (KS / WK) * (GA + GB);     // ring loads per (issuing) wave per stage
-  static_assert(NL > 0 || (GA >= 1 && GB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0),
+  static_assert(NL > 0 || (GA >= 1 && GB >= 1 && BM % (RPP * NW) == 0 && BN % (RPP * NW) == 0),
                 "tile too small for the wave count");
-  constexpr int KSTEP = BK * KS;
+  constexpr int KSTEP = BKT * KS;
+  constexpr int HALVES = BKT / 32;                        // MFMA k-steps per sub-tile
   constexpr int OW = (EPI == EPI_SWIGLU) ? BN / 2 : BN;  // staged output columns per row
   constexpr int OLD = OW + 8;                             // staged row stride (bf16)
   constexpr int RING = (STAGES * STAGE_BYTES > BM * OLD * 2) ? STAGES * STAGE_BYTES : BM * OLD * 2;
@@ -171,40 +183,40 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     }
   }
 
-  // ---- staging: wave w owns ring rows [8 (w*GA + j), +8) of A and [8 (w*GB + j), +8) of B;
-  // lane -> row + lane/8, LDS chunk lane%8 <- source chunk (lane%8) ^ ((row >> 1) & 7)
-  const int srow = lane >> 3, spos = lane & 7;
+  // ---- staging: wave w owns ring rows [RPP (w*GA + j), +RPP) of A and [RPP (w*GB + j), +RPP) of B;
+  // lane -> row + lane/LPR, LDS chunk lane%LPR <- source chunk (lane%LPR) ^ swz(row)
+  const int srow = lane / LPR, spos = lane % LPR;
   auto a_row = [&](int r) -> const u16* {  // A source of tile row r (k offset 0 of this split)
     const int row = min(m0 + r, M - 1);
     const long arow = a.g_perm != nullptr ? (long)(a.g_perm[row] / a.g_k) : (long)row;  // MoE: gathered rows
-    return a.A + arow * a.lda + kbeg + 8 * (spos ^ ((r >> 1) & 7));
+    return a.A + arow * a.lda + kbeg + 8 * (spos ^ swz<BKT>(r));
   };
-  // weight source of tile row r at k offset kbeg (row-major, or panel-major: row n of k panel p
-  // at (p N + n) 64); wstep = elements between consecutive 64-deep k sub-tiles of one row
-  const long wstep = a.w_panel ? 64L * N : 64L;
+  // weight source of tile row r without its k offset (row-major, or panel-major: row n of k panel
+  // p at (p N + n) 64); w_koff(k) = the offset of absolute k (a multiple of BKT) from there
+  const bool wp = a.w_panel != 0;
   auto b_row = [&](int r) -> const u16* {
     const long n = min(n0 + r, N - 1);
-    return Wb + (a.w_panel ? ((long)(kbeg / BK) * N + n) * BK : n * K + kbeg) + 8 * (spos ^ ((r >> 1) & 7));
+    return Wb + (wp ? n * 64 : n * K) + 8 * (spos ^ swz<BKT>(r));
   };
+  auto w_koff = [&](int k) -> long { return wp ? (long)(k >> 6) * 64 * N + (k & 63) : (long)k; };
   const u16* a_src[GA];
   const u16* b_src[GB];
   const u16* l_src[GL];   // loader waves: piece lw + NL j of the stage image ([A; B] per sub-tile)
-  long l_step[GL];        // ... and its source advance per ring stage (KS sub-tiles)
+  int l_k[GL];            // ... its k offset inside a stage (sub-tile ks * BKT), -1 - that for A
   int l_off[GL];
   if constexpr (NL == 0) {
 #pragma unroll
-    for (int j = 0; j < GA; ++j) a_src[j] = a_row(8 * (wave * GA + j) + srow);
+    for (int j = 0; j < GA; ++j) a_src[j] = a_row(RPP * (wave * GA + j) + srow);
 #pragma unroll
-    for (int j = 0; j < GB; ++j) b_src[j] = b_row(8 * (wave * GB + j) + srow);
+    for (int j = 0; j < GB; ++j) b_src[j] = b_row(RPP * (wave * GB + j) + srow);
   } else if (loader) {
     const int lw = wid - NC;
 #pragma unroll
     for (int j = 0; j < GL; ++j) {
-      const int g = lw + NL * j, ks = g / ((BM + BN) / 8), p = g % ((BM + BN) / 8);
-      const bool isa = p < BM / 8;
-      const long st = isa ? (long)BK : wstep;
-      l_src[j] = (isa ? a_row(8 * p + srow) : b_row(8 * (p - BM / 8) + srow)) + ks * st;
-      l_step[j] = st * KS;
+      const int g = lw + NL * j, ks = g / ((BM + BN) / RPP), p = g % ((BM + BN) / RPP);
+      const bool isa = p < BM / RPP;
+      l_src[j] = isa ? a_row(RPP * p + srow) : b_row(RPP * (p - BM / RPP) + srow);
+      l_k[j] = isa ? -1 - ks * BKT : ks * BKT;
       l_off[j] = ks * SUB_BYTES + p * 1024;
     }
   }
@@ -219,16 +231,18 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     if constexpr (NL > 0) {
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
 #pragma unroll
-      for (int j = 0; j < GL; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + tk * l_step[j]), (lds_void*)(base + l_off[j]), 16, 0, 0);
+      for (int j = 0; j < GL; ++j) {
+        const long off = l_k[j] < 0 ? (long)(tk * KSTEP - 1 - l_k[j]) : w_koff(kbeg + tk * KSTEP + l_k[j]);
+        __builtin_amdgcn_global_load_lds((const void*)(l_src[j] + off), (lds_void*)(base + l_off[j]), 16, 0, 0);
+      }
       return;
     }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (WK == 2 && ks != kg) continue;  // each k-group stages its own sub-tile
       unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + ks * SUB_BYTES;
-      const int ko = tk * KSTEP + ks * BK;
-      const long kw = (long)(tk * KS + ks) * wstep;
+      const int ko = tk * KSTEP + ks * BKT;
+      const long kw = w_koff(kbeg + ko);
 #pragma unroll
       for (int j = 0; j < GA; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + ko), (lds_void*)(base + (wave * GA + j) * 1024),
@@ -279,20 +293,20 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     }
     if (loader) continue;
 #pragma unroll
-    for (int s = 0; s < 2 * KS; ++s) {
-      if (WK == 2 && (s >> 1) != kg) continue;
-      const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + (s >> 1) * SUB_BYTES;
+    for (int s = 0; s < HALVES * KS; ++s) {
+      if (WK == 2 && (s / HALVES) != kg) continue;
+      const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + (s / HALVES) * SUB_BYTES;
       bf16x8 af[FM], bw[FN];
-      const int c = 4 * (s & 1) + (lane >> 4);
+      const int c = 4 * (s % HALVES) + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * WM + 16 * i + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(base + r * ROWB + ((c ^ ((r >> 1) & 7)) << 4));
+        af[i] = *reinterpret_cast<const bf16x8*>(base + r * RB + ((c ^ swz<BKT>(r)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * WN + 16 * j + (lane & 15);
-        bw[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + r * ROWB + ((c ^ ((r >> 1) & 7)) << 4));
+        bw[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + r * RB + ((c ^ swz<BKT>(r)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -546,7 +560,8 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   }
 }
 
-template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false>
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false,
+          int BKT = 64>
 __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) {
   static_assert(WK == 1 || (WK == 2 && KS == 2), "k-groups split the KS sub-tiles of a stage");
   static_assert(NL == 0 || WK == 1, "loader waves or k-groups, not both");
@@ -554,15 +569,8 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
   constexpr int WM = BM / WGM, WN = BN / NWN;
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(FN % 2 == 0 && FM >= 1 && WM % 16 == 0 && NW % WGM == 0, "wave tile: >= 16 rows, a multiple of 32 columns");
-  constexpr int A_BYTES = BM * ROWB, SUB_BYTES = (BM + BN) * ROWB, STAGE_BYTES = KS * SUB_BYTES;
-  constexpr int GA = NL ? 1 : BM / (8 * NW), GB = NL ? 1 : BN / (8 * NW);  // global_load_lds per wave per sub-tile
-  constexpr int PPS = KS * (BM + BN) / 8;                                  // 1 KB pieces per stage
-  constexpr int GL = NL ? PPS / NL : 1;                                    // ... per loader wave
-  static_assert(NL == 0 || PPS % NL == 0, "stage pieces must split evenly over the loader waves");
-  constexpr int G = NL ? GL : (KS / WK) * (GA + GB);     // ring loads per (issuing) wave per stage
-  static_assert(NL > 0 || (GA >= 1 && GB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0),
-                "tile too small for the wave count");
-  constexpr int KSTEP = BK * KS;
+  constexpr int STAGE_BYTES = KS * (BM + BN) * 2 * BKT;
+  constexpr int KSTEP = BKT * KS;
   constexpr int OW = (EPI == EPI_SWIGLU) ? BN / 2 : BN;  // staged output columns per row
   constexpr int OLD = OW + 8;                             // staged row stride (bf16)
   constexpr int RING = (STAGES * STAGE_BYTES > BM * OLD * 2) ? STAGES * STAGE_BYTES : BM * OLD * 2;
@@ -584,7 +592,7 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int split = wgid % S, rest = wgid / S;
     const int kbeg = split * a.kchunk;
-    tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM>(a, smem, a.M, S, S, split, rest % mt, rest / mt, kbeg,
+    tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM, BKT>(a, smem, a.M, S, S, split, rest % mt, rest / mt, kbeg,
                                                         max(0, (min(a.K, kbeg + a.kchunk) - kbeg) / KSTEP));
   } else {
     const int ng = gridDim.x, q8 = ng >> 3, r8 = ng & 7, xcd = bid & 7;
@@ -592,18 +600,19 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
     for (int sg = 0; sg < a.sk_segmax; ++sg) {
       const int4 e = *reinterpret_cast<const int4*>(a.sk_table + ((long)wl * a.sk_segmax + sg) * 4);
       if (e.x < 0) break;   // block-uniform: this workgroup's list ended
-      tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM>(a, smem, a.M, e.w >> 16, a.sk_cmax, e.w & 0xffff, e.x % mt,
+      tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM, BKT>(a, smem, a.M, e.w >> 16, a.sk_cmax, e.w & 0xffff, e.x % mt,
                                                           e.x / mt, e.y * KSTEP, e.z - e.y);
       __syncthreads();   // the next segment re-uses the ring, the row-scale partials and the flag
     }
   }
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false,
+          int BKT = 64>
 int launch_t(const GemmArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
   const int grid = SK ? a.sk_grid : mt * nt * a.splits;
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, SK>), dim3(grid),
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, SK, BKT>), dim3(grid),
                      dim3(64 * (NW * WK + NL)), 0, st, a);
   return (int)hipGetLastError();
 }
@@ -618,19 +627,33 @@ constexpr bool sk_plan() {
                      (BM == 128 && BN == 64 && NL == 4 && ST == 4));   // (160 x 128 spilled in the segment loop)
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, int BKT = 64>
 int launch_fit(const GemmArgs& a, hipStream_t st) {
-  if constexpr (ST * KS * (BM + BN) * ROWB > 150 * 1024) {
+  if constexpr (ST * KS * (BM + BN) * 2 * BKT > 150 * 1024) {
     return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
   } else {
     if (a.sk_table != nullptr) {
-      if constexpr (sk_plan<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>())
+      if constexpr (BKT == 64 && sk_plan<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>())
         return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, true>(a, st);
       else
         return -25;
     }
-    return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>(a, st);
+    return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, false, BKT>(a, st);
   }
+}
+
+// 32-deep k-steps (GemmArgs.kdepth = 32): the 256-row tiles with 4-6 stage rings, for prefill-size
+// M and the wide decode projections (gate/up), where a 64-deep ring of these tiles fits only 2-3
+// stages in the 160 KB LDS.  256 x 256: 8 compute waves of 128 x 64 (2 x 4); 256 x 128: 64 x 64 (4 x 2)
+template <int EPI>
+int by_tile_k32(int bm, int bn, int stages, int nw, int nl, const GemmArgs& a, hipStream_t st) {
+  // (256 x 256 with loader waves spills: 128 accumulators per lane leave no room at 3 waves/SIMD)
+  if (bm == 256 && bn == 256 && nw == 8 && stages == 4 && nl == 0) return launch_fit<256, 256, EPI, 4, 1, 8, 1, 0, 2, 32>(a, st);
+  if (bm == 256 && bn == 128 && nw == 8 && stages == 6) {
+    if (nl == 0) return launch_fit<256, 128, EPI, 6, 1, 8, 1, 0, 4, 32>(a, st);
+    if (nl == 8) return launch_fit<256, 128, EPI, 6, 1, 8, 1, 8, 4, 32>(a, st);
+  }
+  return -22;
 }
 
 // loader-wave tiles (NL > 0; KS 1): the decode-size plans the lab measured fastest
@@ -877,6 +900,23 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
   if (a.sk_table != nullptr && (!a.part || !a.counters || a.sk_grid < 1 || a.sk_segmax < 1 || a.sk_cmax < 1 ||
                                 a.g_tiles != nullptr || a.splits != 1))
     return -24;
+  if (a.kdepth == 32) {   // 32-deep k-step plans: KS 1, one k-group, no MoE gather, no stream-K
+    if (ks != 1 || wk != 1 || a.g_tiles != nullptr || a.sk_table != nullptr || a.K % BK || a.kchunk % BK ||
+        a.kchunk <= 0 || a.splits < 1 || a.lda % 8 || a.N % 8 || (a.Y && a.ldy % 8))
+      return -23;
+    if (a.splits > 1 && (!a.part || !a.counters)) return -2;
+    if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
+    if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
+    switch (epi) {
+      case EPI_PLAIN: return by_tile_k32<EPI_PLAIN>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_RESADD: return by_tile_k32<EPI_RESADD>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_QKV: return by_tile_k32<EPI_QKV>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_SWIGLU: return by_tile_k32<EPI_SWIGLU>(bm, bn, stages, nw, nl, a, stream);
+      case EPI_GELU: return by_tile_k32<EPI_GELU>(bm, bn, stages, nw, nl, a, stream);
+      default: return -6;
+    }
+  }
+  if (a.kdepth != 0 && a.kdepth != 64) return -26;
   if (nl > 0) {   // loader-wave plans: KS 1, one k-group, no MoE gather
     if (ks != 1 || wk != 1 || a.g_tiles != nullptr || a.K % BK || a.kchunk % BK || a.kchunk <= 0 || a.splits < 1 ||
         a.lda % 8 || a.N % 8 || (a.Y && a.ldy % 8))

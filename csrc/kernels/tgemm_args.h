@@ -56,6 +56,8 @@ struct GemmArgs {
   // slots per tile.  Null: one (tile, split) unit per workgroup.
   const int* sk_table;
   int sk_grid, sk_segmax, sk_cmax;
+  // k depth of a staged sub-tile: 0 / 64 (default), 32 (tgemm.hip by_tile_k32 plans)
+  int kdepth;
 };
 enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_GELU = 4 };
 }  // namespace dllm

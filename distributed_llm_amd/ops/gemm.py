@@ -54,6 +54,9 @@ _TG_NL = ((64, 64, 4, 4, 2, 1), (64, 64, 4, 4, 4, 1), (64, 64, 4, 8, 4, 1), (128
           (128, 128, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
           (64, 64, 4, 4, 8, 1), (64, 64, 4, 8, 8, 1), (128, 64, 4, 4, 8, 65), (128, 128, 4, 4, 8, 65),
           (160, 128, 8, 3, 6, 129), (256, 128, 8, 3, 8, 129))
+# 32-deep k-step plans (csrc/kernels/tgemm.hip by_tile_k32): (bm, bn, stages, loaders), 8 compute waves;
+# as plan tuples (bm, bn, stages, splits, 1, 8, 1, loaders, 0, 32)
+_TG_K32 = ((256, 256, 4, 0), (256, 128, 6, 0), (256, 128, 6, 8))
 # one-split plans with a stream-K instantiation (csrc/kernels/tgemm.hip sk_plan): (bm, bn, stages, ks, waves, loaders)
 _SK_PLANS = {(64, 64, 3, 2, 4, 0), (64, 64, 4, 1, 4, 0), (64, 64, 4, 1, 4, 4), (64, 64, 4, 1, 4, 8),
              (64, 128, 3, 1, 8, 0), (128, 64, 4, 1, 4, 4)}
@@ -172,7 +175,9 @@ PREFILL_MS = (2048, 4096, 8192)
 PREFILL_TUNE = False   # measured slower end to end (above); autotune(prefill=True) opts in
 STREAM_K = False       # stream-K tgemm plans in the autotuner (see _tg_cands)
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8), (192, 128, 3, 1, 1, 8),
-             (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4))
+             (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4),
+             # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
+             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32), (256, 128, 6, 1, 1, 8, 1, 8, 0, 32))
 
 
 def prefill_bucket(M: int) -> int:
@@ -290,12 +295,13 @@ def _sk_tensor(dev, M, N, K, bm, bn, ks):
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
            pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None,
            v_rows=None):
-    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves[, stream-K]]]])"""
+    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves[, stream-K[, k depth]]]]])"""
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     wk = plan[6] if len(plan) >= 7 else 1
     nl = plan[7] if len(plan) >= 8 else 0
     sk = len(plan) >= 9 and plan[8] == 1
+    bk = plan[9] if len(plan) >= 10 else 64
     M = x.shape[0]
     N, K = _nk(w)
     if K % (64 * ks):
@@ -312,7 +318,7 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
               pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl), tab, int(cmax),
-              v_rows)
+              v_rows, int(bk))
 
 
 def ref_silu_mul(gu):

@@ -177,7 +177,8 @@ def test_pools_event_driver_n_ranks_one_gpu(world, tmp_path):
     on its own, so the JSON line reports the event driver and every conversation keeps turning."""
     logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
     os.makedirs(logdir, exist_ok=True)
-    args = [a for a in COMMON if a not in ("--pipeline", "0")]
+    i = COMMON.index("--pipeline")
+    args = COMMON[:i] + COMMON[i + 2:]
     res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                 "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world),
                 "--topology", "pools", "--convs", str(CONVS // world), *args],

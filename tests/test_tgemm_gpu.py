@@ -22,8 +22,10 @@ PLANS = [p for p in ([(bm, bn, st, sp, 1, nw) for bm, bn, nw in G._TG_TILES for 
                       + [(bm, bn, st, sp, 2, 4, 2) for bm, bn in ((64, 64), (64, 128), (128, 64), (128, 128))
                          for st in (2, 3) for sp in (1, 2)]
                       # loader-wave plans (NL extra waves stream the ring, the rest only compute)
-                      + [(bm, bn, st, sp, 1, nw, 1, nl) for bm, bn, nw, st, nl, _ in G._TG_NL for sp in (1, 3)])
-         if p[2] * p[4] * (p[0] + p[1]) * 128 <= 150 * 1024]
+                      + [(bm, bn, st, sp, 1, nw, 1, nl) for bm, bn, nw, st, nl, _ in G._TG_NL for sp in (1, 3)]
+                      # 32-deep k-steps (64-B staged rows): the 256-row tiles with 4-6 stage rings
+                      + [(bm, bn, st, sp, 1, 8, 1, nl, 0, 32) for bm, bn, st, nl in G._TG_K32 for sp in (1, 3)])
+         if p[2] * p[4] * (p[0] + p[1]) * 2 * (p[9] if len(p) > 9 else 64) <= 150 * 1024]
 
 
 def _rnd(*shape, scale=1.0):
