@@ -548,12 +548,15 @@ def main() -> int:
     # this rank's GPU energy over the timed window (amdsmi's cumulative energy counter; no sampling
     # thread): board energy per generated token next to the reference's J/token
     meter, smi_idx, e0 = None, None, None
+    busy = None      # sampled GPU busy share over the window (amdsmi activity counter)
     if on_gpu:
-        from distributed_llm_amd.bench.power import PowerSampler, smi_index_for_cuda
+        from distributed_llm_amd.bench.power import BusySampler, PowerSampler, smi_index_for_cuda
         smi_idx = smi_index_for_cuda(local)
         meter = PowerSampler(gpus=[smi_idx])
         if not meter.available:
             meter = None
+        busy = BusySampler(smi_idx)
+    busy_pct = None
     records = []
     tokens = 0
     elapsed = 0.0
@@ -599,6 +602,8 @@ def main() -> int:
                 if on_gpu:
                     torch.cuda.synchronize()
                 e0 = meter.mark() if meter else None
+                if busy is not None:
+                    busy.start()
                 cpu0 = _thread_cpu() if diag("cpu") else None
                 t0 = time.perf_counter()
                 convs.records = records
@@ -611,6 +616,7 @@ def main() -> int:
                 elapsed = time.perf_counter() - t0
                 cpu1 = _thread_cpu() if cpu0 is not None else None
                 e1 = meter.mark() if meter else None
+                busy_pct = busy.stop() if busy is not None else None
                 st1 = [dict(e.stats()) for e in engines]
                 enc1 = encoder_stats()
             if cluster is not None:
@@ -621,6 +627,8 @@ def main() -> int:
             enc0 = encoder_stats()
             sync()
             e0 = meter.mark() if meter else None
+            if busy is not None:
+                busy.start()
             t0 = time.perf_counter()
             dump = [] if a.dump_responses else None
             for _ in range(a.steps):
@@ -631,6 +639,7 @@ def main() -> int:
             sync()
             elapsed = time.perf_counter() - t0
             e1 = meter.mark() if meter else None
+            busy_pct = busy.stop() if busy is not None else None
             st1 = [dict(e.stats()) for e in engines]
             enc1 = encoder_stats()
         if cluster is not None:
@@ -734,6 +743,10 @@ def main() -> int:
                                       / max(1, sum(b["decode"] - a_["decode"] for a_, b in zip(st0, st1))), 1),
             "engine_time_split_s": engine_time_split(st0, st1, elapsed_max),
         }
+        if busy_pct is not None:
+            # rank 0's GPU, sampled at 20 Hz over the timed window (no kernel trace: a traced run's
+            # host is slower and shows idle gaps the plain run does not have)
+            out["gpu_busy_sampled_pct"] = round(busy_pct, 1)
         if energy_j >= 0:
             # every rank's GPU over the timed window (energy counter deltas summed over ranks)
             out["gpu_energy_j"] = round(energy_j, 1)

@@ -133,6 +133,52 @@ class PowerSampler:
         return sum(energy_for_window_trapz(self.samples.get(g, []), start, end) for g in gpus)
 
 
+class BusySampler:
+    """GPU busy share over a window: amdsmi's graphics-engine activity (%, the firmware's own
+    utilisation counter) sampled by a thread at ``hz``.  Unlike a kernel trace it costs the host
+    nothing measurable, so the step loop runs as in the timed bench.  ``stop()`` returns the mean
+    (None when amdsmi or the counter is unavailable)."""
+
+    def __init__(self, smi_idx: int, hz: float = 20.0):
+        self.hz, self.vals = hz, []
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._h = None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self._smi = amdsmi
+            self._h = amdsmi.amdsmi_get_processor_handles()[smi_idx]
+            self._read()
+        except Exception:
+            self._h = None
+
+    def _read(self) -> float:
+        v = self._smi.amdsmi_get_gpu_activity(self._h).get("gfx_activity")
+        return float(v)
+
+    def _loop(self) -> None:
+        period = 1.0 / self.hz
+        while not self._stop.wait(period):
+            try:
+                self.vals.append(self._read())
+            except Exception:
+                pass
+
+    def start(self) -> "BusySampler":
+        if self._h is not None:
+            self._thread = threading.Thread(target=self._loop, daemon=True, name="busy-sampler")
+            self._thread.start()
+        return self
+
+    def stop(self) -> Optional[float]:
+        if self._thread is None:
+            return None
+        self._stop.set()
+        self._thread.join()
+        return sum(self.vals) / len(self.vals) if self.vals else None
+
+
 def smi_index_for_cuda(device: int) -> int:
     """amdsmi processor index of HIP device ``device`` (matched by PCI bus id: amdsmi lists every
     GPU the driver sees, HIP only the visible ones), falling back to the HIP index."""
