@@ -37,7 +37,7 @@ def main():
                 errs = {}
                 for p in K64 + K32:
                     for tag, wl in (("row", ws), ("pan", wps)):
-                        key = f"{tag}{p[:4]}{'k32' if len(p) > 9 else ''}nl{p[7] if len(p) > 7 else 0}"
+                        key = f"{tag}{p[:4]}{'k32' if len(p) > 9 else ''}w{p[5]}nl{p[7] if len(p) > 7 else 0}"
                         try:
                             res[key] = G._time(lambda i: G._tgemm(ext, x, wl[i % copies], G.EPI_PLAIN, p, y=y), iters=8)
                         except Exception:  # noqa: BLE001 - plan refused for this shape
