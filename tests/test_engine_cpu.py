@@ -229,3 +229,38 @@ def test_block_table_sync_covers_decode_grown_columns():
     assert (eng.bt_dev.cpu()[:, :eng._bt_hw] == eng.bt_host_t[:, :eng._bt_hw]).all()
     fresh = LLMEngine("tiny-llama-test", device="cpu", kv_cache_gb=0.05, max_num_seqs=1, seed=0)
     assert got == fresh.generate([prompt], sp)[0].token_ids
+
+
+def test_block_manager_places_sequences_in_runs():
+    """KV blocks of one sequence come out as consecutive runs (each new sequence starts a wholly
+    free 64-block segment, growth continues after its last block), also when sequences grow
+    interleaved and a later turn re-matches the cached prefix; the LIFO policy stays available."""
+    from distributed_llm_amd.engine.llm_engine import _need_runtime
+    rt = _need_runtime()
+    bm = rt.BlockManager(2000, 16, True)
+    ids = list(range(6))
+    for i in ids:
+        assert bm.allocate(i, list(range(1000 * i + 1, 1000 * i + 40)))[0]
+    for _ in range(300):                       # interleaved decode growth
+        bm.commit_append(ids, [5] * 6, [1] * 6)
+    for i in ids:
+        t = bm.block_table(i)
+        assert t == list(range(t[0], t[0] + len(t))), t
+    st = bm.stats()
+    assert st["segment_allocs"] == 6 and st["contiguous_allocs"] > 100
+    assert bm.check_invariants() == ""
+    # next turn of conversation 0: the history blocks are matched, the new ones continue the run
+    hist = list(range(1, 40)) + [5] * 300
+    t0 = bm.block_table(0)
+    bm.commit(0, len(hist))
+    bm.free(0)
+    t, cached = bm.allocate(100, hist + list(range(7000, 7100)))
+    assert cached > 0 and t[:len(t0) - 1] == t0[:len(t0) - 1]
+    assert t == list(range(t[0], t[0] + len(t)))
+    assert bm.check_invariants() == ""
+    lifo = rt.BlockManager(2000, 16, True, False)
+    for i in ids:
+        lifo.allocate(i, list(range(1000 * i + 1, 1000 * i + 40)))
+    for _ in range(40):
+        lifo.commit_append(ids, [5] * 6, [1] * 6)
+    assert lifo.stats()["segment_allocs"] == 0 and lifo.check_invariants() == ""
