@@ -401,6 +401,15 @@ STEP_LOOP_TIMERS = ("t_prefill_s", "t_admit_s", "t_decode_host_pre_s", "t_decode
 CLIENT_TIMERS = ("t_encode_s", "t_output_s")
 
 
+def kv_placement(st0, st1):
+    d = lambda k: sum(b.get(k, 0) - a_.get(k, 0) for a_, b in zip(st0, st1))
+    run, seg, tot = d("contiguous_allocs"), d("segment_allocs"), d("fresh_allocs")
+    # every new block either continues its sequence's run, opens a wholly free segment, or comes
+    # from the free list / LRU (scattered)
+    return {"new_blocks": int(tot), "run_share": round(run / tot, 3) if tot else None,
+            "segment_share": round(seg / tot, 3) if tot else None}
+
+
 def engine_time_split(st0, st1, window_s: float) -> dict:
     """Where the timed window went, per THREAD.  The step-loop timers are disjoint, so with one engine
     they partition its thread's window (``step_loop_other_s``: waiting for work, scheduling glue);
@@ -737,6 +746,9 @@ def main() -> int:
             "routing_overhead_ms_mean": round(statistics.mean(r["ovh"] for r in records), 3) if records else None,
             "ttft_ms_p50": round(statistics.median(r["ttft"] for r in records), 1) if records else None,
             "prefix_cache_hit_rate": round(hits / max(1, prompt), 3),
+            # new KV blocks that continued their sequence's run / opened a free segment / other
+            # (csrc/runtime/block_manager.h fresh(); profiles/r5_kv_placement.md)
+            "kv_block_placement": kv_placement(st0, st1),
             "engine_decode_tok_s": round(sum(b["decode_tokens"] - a_["decode_tokens"] for a_, b in zip(st0, st1))
                                          / max(elapsed_max, 1e-9), 1),
             "avg_decode_batch": round(sum(b["decode_tokens"] - a_["decode_tokens"] for a_, b in zip(st0, st1))

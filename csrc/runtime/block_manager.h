@@ -238,6 +238,7 @@ class BlockManager {
             {"free_blocks", (long long)n_free_},
             {"contiguous_allocs", contig_},
             {"segment_allocs", seg_allocs_},
+            {"fresh_allocs", fresh_allocs_},
             {"evictable_blocks", (long long)lru_.size()},
             {"cached_blocks", (long long)hash2block_.size()},
             {"active_seqs", (long long)seqs_.size()},
@@ -402,6 +403,7 @@ class BlockManager {
 
   // prefer: the block after the sequence's last one (-1: none)
   int fresh(int prefer = -1) {
+    ++fresh_allocs_;
     int b = -1;
     if (contiguous_ && prefer > 0 && prefer < (int)blocks_.size() && prefer % kSeg != 0 && free_flag_[prefer]) {
       b = prefer;   // continue the run (never into the next segment: that one may be wholly free)
@@ -448,7 +450,7 @@ class BlockManager {
   int n_free_ = 0;
   std::vector<int> seg_free_;      // free blocks per segment of kSeg
   std::vector<int> seg_stack_;     // segments that were wholly free when pushed (lazy)
-  long long contig_ = 0, seg_allocs_ = 0;
+  long long contig_ = 0, seg_allocs_ = 0, fresh_allocs_ = 0;
   std::list<int> lru_;  // front = most recently released
   std::unordered_map<uint64_t, int> hash2block_;
   std::unordered_map<int64_t, Seq> seqs_;
