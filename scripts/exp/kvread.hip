@@ -30,7 +30,21 @@ __global__ void k_seq(const uint4* __restrict__ a, long n16, uint32_t* out) {
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// NT: non-temporal loads (each K/V byte is read once per decode step by one workgroup)
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+template <typename T, bool NT>
+__device__ __forceinline__ T ldk(const T* p) {
+  if constexpr (NT) {
+    if constexpr (sizeof(T) == 16) return __builtin_bit_cast(T, __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p)));
+    else return __builtin_bit_cast(T, __builtin_nontemporal_load(reinterpret_cast<const u32x2v*>(p)));
+  } else {
+    return *p;
+  }
+}
+
 // head block = 16 keys x 64 dims bf16 = 2 KB; K [blocks][nkv][16][64], V [blocks][nkv][64][16]
+template <bool NT = false>
 __global__ void __launch_bounds__(512) k_attnlike(const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
                                                   const int* __restrict__ bt, int nb, int nkv, uint32_t* out) {
   const int seq = blockIdx.x / nkv, h = blockIdx.x % nkv;
@@ -44,10 +58,13 @@ __global__ void __launch_bounds__(512) k_attnlike(const uint16_t* __restrict__ k
     const uint16_t* v1 = vc + ((long)b1 * nkv + h) * BS * D + rl * BS + 4 * g;
     uint4 kr[4];
     uint2 vr[8];
-    kr[0] = *(const uint4*)(k0); kr[1] = *(const uint4*)(k0 + 32);
-    kr[2] = *(const uint4*)(k1); kr[3] = *(const uint4*)(k1 + 32);
+    kr[0] = ldk<uint4, NT>((const uint4*)(k0)); kr[1] = ldk<uint4, NT>((const uint4*)(k0 + 32));
+    kr[2] = ldk<uint4, NT>((const uint4*)(k1)); kr[3] = ldk<uint4, NT>((const uint4*)(k1 + 32));
 #pragma unroll
-    for (int n = 0; n < 4; ++n) { vr[n] = *(const uint2*)(v0 + 16 * n * BS); vr[4 + n] = *(const uint2*)(v1 + 16 * n * BS); }
+    for (int n = 0; n < 4; ++n) {
+      vr[n] = ldk<uint2, NT>((const uint2*)(v0 + 16 * n * BS));
+      vr[4 + n] = ldk<uint2, NT>((const uint2*)(v1 + 16 * n * BS));
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc ^= fold(kr[i]);
 #pragma unroll
@@ -155,8 +172,17 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&bt, (long)B * nb * 4)); CHECK(hipMalloc(&out, 64));
   std::vector<int> perm(NB - 8);
   for (long i = 0; i < NB - 8; ++i) perm[i] = (int)i;
-  const bool shuffled = argc > 3 ? atoi(argv[3]) != 0 : true;
-  if (shuffled) std::shuffle(perm.begin(), perm.end(), std::mt19937(1));
+  // placement: 0 every sequence's blocks consecutive, 1 random blocks, 2 runs of 64 consecutive
+  // blocks at random places (the block manager's segment placement)
+  const int shuffled = argc > 3 ? atoi(argv[3]) : 1;
+  if (shuffled == 1) std::shuffle(perm.begin(), perm.end(), std::mt19937(1));
+  if (shuffled == 2) {
+    const long nseg = (NB - 8) / 64;
+    std::vector<long> segs(nseg);
+    for (long i = 0; i < nseg; ++i) segs[i] = i;
+    std::shuffle(segs.begin(), segs.end(), std::mt19937(1));
+    for (long i = 0; i < nseg * 64; ++i) perm[i] = (int)(segs[i / 64] * 64 + i % 64);
+  }
   CHECK(hipMemcpy(bt, perm.data(), (long)B * nb * 4, hipMemcpyHostToDevice));
   const double bytes = (double)B * nb * nkv * BS * D * 2 * 2;
   auto rep = [&](const char* name, float ms) {
@@ -172,7 +198,9 @@ int main(int argc, char** argv) {
     printf("{\"exp\": \"kvread\", \"kernel\": \"seq\", \"bytes\": %.0f, \"us\": %.1f, \"TBps\": %.3f}\n", (double)elems * 4,
            ms * 1000, elems * 4.0 / (ms * 1e-3) / 1e12);
   }
-  rep("attnlike", timeit([&] { hipLaunchKernelGGL(k_attnlike, dim3(B * nkv), dim3(512), 0, 0, kc, vc, bt, nb, nkv, out); }));
+  rep("attnlike", timeit([&] { hipLaunchKernelGGL(k_attnlike<false>, dim3(B * nkv), dim3(512), 0, 0, kc, vc, bt, nb, nkv, out); }));
+  rep("attnlike_nt", timeit([&] { hipLaunchKernelGGL(k_attnlike<true>, dim3(B * nkv), dim3(512), 0, 0, kc, vc, bt, nb, nkv, out); }));
+  if (argc > 4) return 0;   // attnlike rows only
   rep("fullline", timeit([&] { hipLaunchKernelGGL(k_fullline, dim3(B * nkv), dim3(512), 0, 0, kc, vc, bt, nb, nkv, out); }));
   rep("allheads", timeit([&] { hipLaunchKernelGGL(k_allheads, dim3(B), dim3(512), 0, 0, kc, vc, bt, nb, nkv, out); }));
   for (int ns : {1, 2, 4}) {
