@@ -94,3 +94,18 @@ def test_bench_event_driven_turn_pipelining():
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert out["config"]["turn_pipelining"] == "event-driver" and out["config"]["admit_every"] == 4
     assert out["value"] > 0 and out["requests"] >= 2 * 4 - 4 and out["pool_events"]["lost_turns"] == 0
+
+
+def test_bench_helpers_busy_sampler_and_kv_placement():
+    """The busy sampler degrades to None where amdsmi / a GPU is missing (this container), and the
+    KV placement shares are deltas of the block manager's counters over the window."""
+    from distributed_llm_amd.bench.power import BusySampler
+    b = BusySampler(0, hz=100.0).start()
+    assert b.stop() is None or 0.0 <= b.stop() <= 100.0
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    st0 = [{"contiguous_allocs": 10, "segment_allocs": 1, "fresh_allocs": 20}]
+    st1 = [{"contiguous_allocs": 70, "segment_allocs": 3, "fresh_allocs": 100}]
+    got = bench.kv_placement(st0, st1)
+    assert got == {"new_blocks": 80, "run_share": 0.75, "segment_share": 0.025}
+    assert bench.kv_placement([{}], [{}])["run_share"] is None
