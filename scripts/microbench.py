@@ -332,7 +332,7 @@ if __name__ == "__main__":
                 print(json.dumps(bench_flash(L, nq, nkv, d)), flush=True)
             print(json.dumps(bench_flash(2048, nq, nkv, d, B=8)), flush=True)
     if "post" in what:
-        for M in (64, 128, 320, 512):
+        for M in (64, 512, 2048, 4096):
             print(json.dumps(bench_post(M)), flush=True)
     if "moe" in what:
         Ts = [int(x) for x in os.environ.get("MB_MOE_T", "1,16,64,256,1024,4096").split(",")]
