@@ -26,8 +26,10 @@ N > 1 GPUs default to BASELINE's multi-GPU configurations (``--topology pools``,
 at half size (Llama-3-8B x2 | Llama-3-70B TP=2), 8 GPUs config 4 (Llama-3-8B x4 | Llama-3-70B
 TP=4, perf router), and ``--baseline-config 5`` (``--topology colocated``) config 5 as written:
 Mixtral-8x7B TP=N over every GPU with a Llama-3.2-1B small replica co-located on each GPU.  Rank 0
-hosts the router and drives ``--convs x N`` conversations (``--convs`` defaults to 64 per GPU
-there); requests reach remote pools over the gloo control / data planes, RCCL carries the large
+hosts the router and drives ``--convs x N`` conversations (``--convs`` defaults to 128 per GPU
+there: with the event driver serving remote pools non-blockingly, 128 per GPU gave 17.3k vs 11.4k
+routed tok/s at 64 on the 2-rank config-3 rehearsal, while an 8B-tier GPU's 64 GB KV pool still
+holds 128 conversations at ~3K tokens of history each); requests reach remote pools over the gloo control / data planes, RCCL carries the large
 pool's tensor-parallel collectives.  The JSON line names the config (``baseline_config``) and the
 exact GPU layout (``layout``); values at different N are different model configurations, so they
 are not a scaling curve of one workload (``scaling_note``).  ``--topology replicated`` keeps the
@@ -78,7 +80,9 @@ def parse():
     ap.add_argument("--threshold", type=int, default=1000)
     ap.add_argument("--small-new", type=int, default=128)
     ap.add_argument("--large-new", type=int, default=384)
-    ap.add_argument("--kv-gb", type=float, default=64.0)
+    ap.add_argument("--kv-gb", type=float, default=None,
+                    help="KV cache per engine (GB); default 64, or 160 for a pool engine that owns its GPU "
+                         "(pools topology, N > 1: 128 conversations per GPU at ~3K tokens of history)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU plumbing run (tiny model)")
     ap.add_argument("--pipeline", type=int, default=2,
@@ -129,7 +133,7 @@ def resolve_config(a, world: int) -> int:
     if a.baseline_config is not None or a.topology is None:
         a.topology = topo
     if a.convs is None:
-        a.convs = 64 if (world > 1 and a.topology in ("pools", "colocated")) else 512
+        a.convs = 128 if (world > 1 and a.topology in ("pools", "colocated")) else 512
     a.small_model = a.small_model or sm or "llama-3.2-1b"
     a.large_model = a.large_model or lg or "llama-3-8b"
     if a.large_tp is None and tp is not None and world >= 2 * tp:
@@ -442,6 +446,7 @@ def main() -> int:
     # bench path (process group, per-rank engines and graphs, barriers, cross-rank reduction) on a
     # one-GPU box; RCCL itself refuses two ranks on one device.  Never used for reported numbers.
     rehearse = world > 1 and on_gpu and os.environ.get("DLLM_REHEARSE_ONE_GPU") == "1"
+    kv_gb = a.kv_gb if a.kv_gb is not None else 64.0
     if rehearse:
         local = 0
     coll_dev = "cpu" if (rehearse or not on_gpu) else f"cuda:{local}"
@@ -487,7 +492,7 @@ def main() -> int:
         from distributed_llm_amd.pools.base import EnginePool
         sm = a.small_model if on_gpu else "tiny-llama-test"
         lg = a.large_model if on_gpu else "tiny-llama-test"
-        kv = (a.kv_gb / 2) if on_gpu else 0.1
+        kv = (kv_gb / 2) if on_gpu else 0.1
         e_small = LLMEngine(mdl(sm), device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
                             use_graphs=not a.no_graphs, seed=0)
         e_large = LLMEngine(mdl(lg), device=dev, kv_cache_gb=kv, max_num_seqs=max(16, a.convs),
@@ -506,7 +511,7 @@ def main() -> int:
         from distributed_llm_amd.engine.llm_engine import LLMEngine
         from distributed_llm_amd.pools.base import EnginePool
         model = a.model if on_gpu else "tiny-llama-test"
-        engine = LLMEngine(mdl(model), device=dev, kv_cache_gb=a.kv_gb if on_gpu else 0.2,
+        engine = LLMEngine(mdl(model), device=dev, kv_cache_gb=kv_gb if on_gpu else 0.2,
                            max_num_seqs=max(16, a.convs), use_graphs=not a.no_graphs, seed=0)
         pools = {SMALL: EnginePool(SMALL, engine, max_new_tokens=a.small_new, temperature=0.0),
                  LARGE: EnginePool(LARGE, engine, max_new_tokens=a.large_new, **large_sampling)}
@@ -526,10 +531,14 @@ def main() -> int:
         n_small = len(topo.replicas[SMALL])
         # (a one-GPU rehearsal runs the collectives on gloo, which a hipGraph cannot capture)
         graphs = not (a.no_graphs or rehearse)
-        specs = {SMALL: TierSpec(mdl(sm), a.small_new, 0.0, kv_cache_gb=a.kv_gb if on_gpu else 0.1,
+        # a pool engine that owns its GPU (disjoint pools on a real node) gets a larger KV pool: the
+        # Llama-3-8B small replicas of config 4 hold 128 conversations x ~3K tokens x 128 KB
+        if a.kv_gb is None and topology == "pools" and not rehearse:
+            kv_gb = 160.0
+        specs = {SMALL: TierSpec(mdl(sm), a.small_new, 0.0, kv_cache_gb=kv_gb if on_gpu else 0.1,
                                  max_num_seqs=max(16, a.convs * world), graphs=graphs),
                  LARGE: TierSpec(mdl(lg), a.large_new, large_sampling["temperature"], large_sampling["top_k"],
-                                 large_sampling["top_p"], kv_cache_gb=a.kv_gb if on_gpu else 0.1,
+                                 large_sampling["top_p"], kv_cache_gb=kv_gb if on_gpu else 0.1,
                                  max_num_seqs=max(16, a.convs * world), graphs=graphs)}
         cluster = Cluster(topo, specs, device=dev)
         engines = list(cluster.engines.values())
