@@ -24,6 +24,7 @@ int dllm_gemv(const void*, long, const void*, void*, long, int, int, int, int, i
 int dllm_gelu(const void*, void*, long, hipStream_t);
 int dllm_mean_pool_l2(const void*, const int*, float*, int, int, int, hipStream_t);
 int dllm_moe_gate(const float*, int, int, int, int*, float*, hipStream_t);
+int dllm_moe_router(const void*, long, const void*, int, int, int, int, int*, float*, float*, hipStream_t);
 int dllm_scatter_pairs(int*, const int*, int, hipStream_t);
 int dllm_step_fetch(const int*, int*, int, int, int, int, const int*, const int*, int*, int, hipStream_t);
 int dllm_step_store(const int*, int*, int, hipStream_t);
@@ -344,6 +345,29 @@ void moe_gate(torch::Tensor logits, int64_t k, torch::Tensor ids, torch::Tensor 
   const int T = logits.size(0), E = logits.size(1);
   TORCH_CHECK(ids.numel() == (int64_t)T * k && w.numel() == (int64_t)T * k, "out shapes");
   ok(dllm_moe_gate(logits.data_ptr<float>(), T, E, k, ids.data_ptr<int>(), w.data_ptr<float>(), stream()), "moe_gate");
+}
+
+// fused router GEMV + top-k (batch-invariant): x [T, H] (row stride % 8), wg [E, H] -> ids/w [T, k]
+void moe_router(torch::Tensor x, torch::Tensor wg, int64_t k, torch::Tensor ids, torch::Tensor w,
+                c10::optional<torch::Tensor> logits) {
+  check_bf16(x, "x");
+  check_bf16(wg, "router weight");
+  check_i32(ids, "ids");
+  check_f32(w, "weights");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && wg.dim() == 2 && wg.is_contiguous() && wg.size(1) == x.size(1),
+              "x [T, H] row-major, wg [E, H] contiguous");
+  const int T = x.size(0), E = wg.size(0), H = x.size(1);
+  TORCH_CHECK(ids.numel() == (int64_t)T * k && w.numel() == (int64_t)T * k && ids.is_contiguous() && w.is_contiguous(),
+              "out shapes");
+  float* lp = nullptr;
+  if (logits.has_value()) {
+    check_f32(*logits, "logits");
+    TORCH_CHECK(logits->is_contiguous() && logits->numel() == (int64_t)T * E, "logits [T, E]");
+    lp = logits->data_ptr<float>();
+  }
+  ok(dllm_moe_router(x.data_ptr(), x.stride(0), wg.data_ptr(), T, E, H, k, ids.data_ptr<int>(), w.data_ptr<float>(),
+                     lp, stream()),
+     "moe_router");
 }
 
 // dst (int32, any shape, contiguous) flat[idx_i] = val_i for buf = [n, idx0, val0, ...]
@@ -1119,6 +1143,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("gelu", &gelu);
   m.def("mean_pool_l2", &mean_pool_l2);
   m.def("moe_gate", &moe_gate);
+  m.def("moe_router", &moe_router, py::arg("x"), py::arg("wg"), py::arg("k"), py::arg("ids"), py::arg("w"),
+        py::arg("logits") = py::none());
   m.def("argmax", &argmax);
   m.def("scatter_pairs", &scatter_pairs);
   m.def("step_fetch", &step_fetch);

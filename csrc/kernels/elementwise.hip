@@ -126,6 +126,69 @@ __global__ void moe_gate_kernel(const float* __restrict__ logits, int T, int E, 
   for (int i = 0; i < k; ++i) { sel[i] = __expf(sel[i] - m); s += sel[i]; }
   for (int i = 0; i < k; ++i) { ids[(long)t * k + i] = sid[i]; w[(long)t * k + i] = sel[i] / s; }
 }
+// Fused router: logits[t, e] = x[t] . wg[e] in fp32 (one wave per token: each lane holds XC 8-wide
+// chunks of its token's row in registers, every expert's dot product is summed in a fixed order and
+// reduced with an xor butterfly), then the same top-k / renormalised softmax as moe_gate_kernel.
+// A token's result depends only on its own row, never on how many tokens share the launch, so a
+// padded graph batch routes exactly like an eager one (a vendor GEMM picks its reduction split by M).
+template <int XC>
+__global__ void __launch_bounds__(256) moe_router_kernel(const u16* __restrict__ x, long x_stride,
+                                                         const u16* __restrict__ wg, int T, int E, int H, int k,
+                                                         int* __restrict__ ids, float* __restrict__ w,
+                                                         float* __restrict__ logits) {
+  __shared__ float lg[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int t = blockIdx.x * 4 + wv;
+  if (t >= T) return;  // whole wave; no block barrier below
+  const int nc = H >> 3;
+  float xf[XC][8];
+#pragma unroll
+  for (int c = 0; c < XC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) unpack8(ld16(x + (long)t * x_stride + 8 * ch), xf[c]);
+    else for (int q = 0; q < 8; ++q) xf[c][q] = 0.f;
+  }
+  for (int e = 0; e < E; ++e) {
+    uint4 wv8[XC];
+#pragma unroll
+    for (int c = 0; c < XC; ++c) {
+      const int ch = lane + 64 * c;
+      wv8[c] = ch < nc ? ld16(wg + (long)e * H + 8 * ch) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < XC; ++c) {
+      float f[8];
+      unpack8(wv8[c], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += xf[c][q] * f[q];
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) lg[wv][e] = s;
+  }
+  if (lane != 0) return;
+  const float* l = lg[wv];
+  if (logits != nullptr)
+    for (int e = 0; e < E; ++e) logits[(long)t * E + e] = l[e];
+  unsigned long long used = 0ull;
+  float sel[8];
+  int sid[8];
+  for (int i = 0; i < k; ++i) {
+    float best = -INFINITY;
+    int bi = 0;
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1ull) && l[e] > best) { best = l[e]; bi = e; }
+    used |= 1ull << bi;
+    sel[i] = best;
+    sid[i] = bi;
+  }
+  const float m = sel[0];
+  float s = 0.f;
+  for (int i = 0; i < k; ++i) { sel[i] = __expf(sel[i] - m); s += sel[i]; }
+  for (int i = 0; i < k; ++i) { ids[(long)t * k + i] = sid[i]; w[(long)t * k + i] = sel[i] / s; }
+}
+
 // buf = [n, idx0, val0, idx1, val1, ...]: dst[idx_i] = val_i.  n is read on the device, so a
 // captured decode graph applies a different number of block-table updates on every replay.
 __global__ void scatter_pairs_kernel(int* __restrict__ dst, const int* __restrict__ buf, int cap) {
@@ -223,6 +286,24 @@ extern "C" int dllm_moe_gate(const float* logits, int T, int E, int k, int* ids,
   if (E > 64 || k > 8 || k > E) return -1;
   if (T == 0) return 0;
   hipLaunchKernelGGL(moe_gate_kernel, dim3((T + 127) / 128), dim3(128), 0, stream, logits, T, E, k, ids, w);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dllm_moe_router(const void* x, long x_stride, const void* wg, int T, int E, int H, int k, int* ids,
+                               float* w, float* logits, hipStream_t stream) {
+  if (E > 64 || k > 8 || k > E || H % 8 != 0 || H > 8192 || x_stride % 8 != 0) return -1;
+  if (T == 0) return 0;
+  const dim3 grid((T + 3) / 4), block(256);
+  const int nc = H / 8;
+  if (nc <= 256)
+    hipLaunchKernelGGL(moe_router_kernel<4>, grid, block, 0, stream, (const u16*)x, x_stride, (const u16*)wg, T, E, H,
+                       k, ids, w, logits);
+  else if (nc <= 512)
+    hipLaunchKernelGGL(moe_router_kernel<8>, grid, block, 0, stream, (const u16*)x, x_stride, (const u16*)wg, T, E, H,
+                       k, ids, w, logits);
+  else
+    hipLaunchKernelGGL(moe_router_kernel<16>, grid, block, 0, stream, (const u16*)x, x_stride, (const u16*)wg, T, E,
+                       H, k, ids, w, logits);
   return (int)hipGetLastError();
 }
 

@@ -34,11 +34,15 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const int* __restrict__
                                                          int* __restrict__ tile_r0, int* __restrict__ tile_n,
                                                          int* __restrict__ n_tiles, int mt = MT,
                                                          int* __restrict__ inv = nullptr) {
-  __shared__ int cnt[64], off[65], cur[64];
-  const int tid = threadIdx.x;
+  // Pairs are placed in a stable order (pair index ascending within each expert): per chunk of
+  // blockDim pairs, a pair's slot = expert base + pairs of its expert in earlier chunks + in earlier
+  // waves of this chunk + lower lanes of its wave (ballot ranks), so the layout never depends on
+  // atomic arrival order.
+  __shared__ int cnt[64], off[65], cur[64], wcnt[16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
   if (tid < 64) { cnt[tid] = 0; cur[tid] = 0; }
   __syncthreads();
-  for (int p = tid; p < P; p += blockDim.x) atomicAdd(&cnt[min(max(ids[p], 0), E - 1)], 1);
+  for (int p = tid; p < P; p += blockDim.x) atomicAdd(&cnt[min(max(ids[p], 0), E - 1)], 1);  // order-free sum
   __syncthreads();
   if (tid == 0) {
     off[0] = 0;
@@ -53,11 +57,29 @@ __global__ void __launch_bounds__(1024) moe_route_kernel(const int* __restrict__
     *n_tiles = nt;
   }
   __syncthreads();
-  for (int p = tid; p < P; p += blockDim.x) {
-    const int e = min(max(ids[p], 0), E - 1);
-    const int pos = off[e] + atomicAdd(&cur[e], 1);
-    perm[pos] = p;
-    if (inv != nullptr) inv[p] = pos;
+  for (int base = 0; base < P; base += blockDim.x) {  // uniform trip count: every wave ballots
+    const int p = base + tid;
+    const int e = p < P ? min(max(ids[p], 0), E - 1) : -1;
+    int rank = 0;
+    for (int x = 0; x < E; ++x) {
+      const unsigned long long m = __ballot(e == x);
+      if (e == x) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wcnt[wv][x] = __popcll(m);
+    }
+    __syncthreads();
+    if (e >= 0) {
+      int pos = off[e] + cur[e] + rank;
+      for (int v = 0; v < wv; ++v) pos += wcnt[v][e];
+      perm[pos] = p;
+      if (inv != nullptr) inv[p] = pos;
+    }
+    __syncthreads();
+    if (tid < E) {
+      int s = 0;
+      for (int v = 0; v < nwv; ++v) s += wcnt[v][tid];
+      cur[tid] += s;
+    }
+    __syncthreads();
   }
 }
 

@@ -36,7 +36,6 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
-import torch.nn.functional as F
 
 from .. import ops
 from ..parallel.comm import SINGLE, ParallelContext, shard_range
@@ -331,10 +330,11 @@ class LlamaModel:
         return self._moe(L, x)
 
     def _moe(self, L, x: torch.Tensor) -> torch.Tensor:
-        """Top-k expert FFN: HIP gate kernel (softmax top-k) -> ops.moe_ffn (device-side token
-        permutation + grouped expert GEMMs, no host sync, so decode steps stay graph-captured).
-        Experts are TP-sharded along I; the caller all-reduces the partial sums."""
-        ids, w = ops.moe_gate(F.linear(x, L["wgate"]).float(), self.cfg.experts_per_token)
+        """Top-k expert FFN: HIP router kernel (fp32 projection + softmax top-k, batch-invariant)
+        -> ops.moe_ffn (device-side token permutation + grouped expert GEMMs, no host sync, so
+        decode steps stay graph-captured).  Experts are TP-sharded along I; the caller all-reduces
+        the partial sums."""
+        ids, w = ops.moe_router(x, L["wgate"], self.cfg.experts_per_token)
         if self.moe_tg:
             return ops.moe_ffn_tg(x, ids, w, L["w13"], L["w2"])
         return ops.moe_ffn(x, ids, w, L["w13"], L["w2"])
@@ -354,7 +354,7 @@ class LlamaModel:
         par, T = self.par, x.shape[0]
         lo, hi = token_slice(T, par.tp_rank, par.tp_size)
         xl = x[lo:hi]
-        ids, w = ops.moe_gate(F.linear(xl, L["wgate"]).float(), self.cfg.experts_per_token)
+        ids, w = ops.moe_router(xl, L["wgate"], self.cfg.experts_per_token)
         yl = ep_moe_ffn(xl, ids, w, L["w13_ep"], L["w2_ep"], self.cfg.n_experts, par.tp_group, par.tp_size)
         self.ep_calls += 1
         return all_gather_rows(yl, T, par.tp_group, par.tp_size)

@@ -402,6 +402,21 @@ def moe_gate(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     return ids, w
 
 
+def moe_router(x: torch.Tensor, wg: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Router projection + top-k in one kernel (csrc/kernels/elementwise.hip moe_router_kernel):
+    fp32 logits x . wg^T with a per-token fixed reduction order, so routing is batch-invariant (a
+    padded graph batch picks the same experts as the eager batch; a vendor GEMM's split varies
+    with M).  x [T, H] bf16, wg [E, H] bf16 -> ids [T, k] int32, renormalised weights [T, k] f32."""
+    ext = _native(x)
+    if ext is None or x.shape[1] > 8192 or x.stride(0) % 8:
+        return moe_gate(torch.nn.functional.linear(x.float(), wg.float()), k)
+    T = x.shape[0]
+    ids = torch.empty((T, k), dtype=torch.int32, device=x.device)
+    w = torch.empty((T, k), dtype=torch.float32, device=x.device)
+    ext.moe_router(x if x.stride(1) == 1 else x.contiguous(), wg.contiguous(), k, ids, w)
+    return ids, w
+
+
 def moe_ffn(x: torch.Tensor, ids: torch.Tensor, wts: torch.Tensor, w13: torch.Tensor,
             w2: torch.Tensor) -> torch.Tensor:
     """Top-k expert FFN (csrc/kernels/moe.hip): device-side routing + grouped MFMA GEMMs with the

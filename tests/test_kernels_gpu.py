@@ -481,6 +481,42 @@ def test_moe_ffn_grouped_tgemm(T, H, I, E, k, plan):
     assert err <= 2e-2 * max(1.0, want.abs().max().item()), err
 
 
+@pytest.mark.parametrize("H,E,k", [(256, 4, 2), (4096, 8, 2), (2048, 16, 4), (8192, 64, 8)])
+def test_moe_router_matches_fp32_and_is_batch_invariant(H, E, k):
+    """Fused router (fp32 projection + top-k) vs fp32 logits -> ref.moe_gate; a token's routing is
+    bitwise the same whether it runs alone, in a small batch or in a padded one."""
+    T = 37
+    g = torch.Generator(device="cuda").manual_seed(H + E)
+    x = (torch.randn(T, H, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    wg = (torch.randn(E, H, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    ids, w = ops.moe_router(x, wg, k)
+    lg = x.float() @ wg.float().t()
+    ri, rw = ref.moe_gate(lg, k)
+    top = lg.sort(-1, descending=True).values
+    clear = (top[:, k - 1] - top[:, k]) > 1e-3 * lg.abs().amax(-1)  # rows without a near-tie at the cut
+    assert clear.sum() > T // 2
+    assert torch.equal(ids[clear].long().sort(-1).values, ri[clear].long().sort(-1).values)
+    assert torch.allclose(w.sort(-1).values[clear], rw.float().sort(-1).values[clear], atol=1e-4)
+    for n in (1, 3, 16):
+        i2, w2 = ops.moe_router(x[:n], wg, k)
+        assert torch.equal(i2, ids[:n]) and torch.equal(w2, w[:n])
+
+
+@pytest.mark.parametrize("T", [5, 700, 1500])
+def test_moe_ffn_grouped_bitwise_repeatable(T):
+    """Routing places pairs in a stable order (no atomic arrival order), so repeated calls on the
+    same inputs are bitwise identical, across 1024-pair routing chunks too."""
+    H, I, E, k = 256, 128, 8, 2
+    g = torch.Generator(device="cuda").manual_seed(T)
+    x = (torch.randn(T, H, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    w13i = (torch.randn(E, 2 * I, H, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(E, H, I, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    ids, w = ops.moe_gate(torch.randn(T, E, device="cuda", generator=g), k)
+    y0 = ops.moe_ffn_tg(x, ids, w, w13i, w2)
+    for _ in range(8):
+        assert torch.equal(ops.moe_ffn_tg(x, ids, w, w13i, w2), y0)
+
+
 def test_moe_ffn_grouped_graph_capture_mixtral_layer():
     """Mixtral-8x7B expert shapes (H 4096, I 14336, E 8, top-2): one captured graph replays decode
     batches with fresh routing and matches the fp32 reference (checked on a row subset)."""
