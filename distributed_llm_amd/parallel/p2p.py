@@ -11,6 +11,10 @@ On one MI355X node, pools are process groups and the router talks to a pool lead
   * ``send_tokens`` / ``recv_tokens``: int32 token-id tensors (failover hand-off of a prompt);
   * ``bcast_obj``: leader -> TP group fan-out of a work item;
   * ``ping``: 4 KiB ping-pong health probe, timed.
+On an RCCL pair group every data-plane transfer runs on a side HIP stream of its own (``side_stream``):
+ProcessGroupNCCL orders a send/recv after the work queued on the CALLER's current stream, so on
+the compute stream a failover hand-off or a probe would wait behind the decode graphs in flight;
+on the side stream it waits only for its own staging copy.
 Every data-plane wait can be bounded (``timeout_s``: isend / irecv + ``Work.wait(timeout)``); a
 transfer past its deadline raises ``DataPlaneTimeout`` and the caller retires that pair group.
 The data plane defaults to gloo (parallel.cluster): token ids and pings are tiny, and on gloo a
@@ -19,9 +23,11 @@ whole router process.
 """
 from __future__ import annotations
 
+import contextlib
 import json
+import threading
 import time
-from typing import Any, Optional
+from typing import Any, Dict, Iterator, Optional
 
 import torch
 import torch.distributed as dist
@@ -34,25 +40,56 @@ def _dev(group) -> torch.device:
     return torch.device("cpu")
 
 
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+_SIDE_LOCK = threading.Lock()
+
+
+def side_stream(dev: torch.device) -> Optional["torch.cuda.Stream"]:
+    """The data plane's side stream on ``dev`` (one per device, created on first use); None on CPU."""
+    if dev.type != "cuda":
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    with _SIDE_LOCK:
+        s = _SIDE.get(idx)
+        if s is None:
+            s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+        return s
+
+
+@contextlib.contextmanager
+def on_side(dev: torch.device) -> Iterator[None]:
+    """Run the enclosed transfer on the side stream and wait for it before leaving, so whatever the
+    caller does next with the result (host copies, another stream) sees completed data."""
+    s = side_stream(dev)
+    if s is None:
+        yield
+        return
+    with torch.cuda.stream(s):
+        yield
+    s.synchronize()
+
+
 def send_bytes(data: bytes, dst: int, group=None, tag: int = 0) -> None:
     dev = _dev(group)
-    hdr = torch.tensor([len(data)], dtype=torch.int64, device=dev)
-    dist.send(hdr, dst, group=group, tag=tag)
-    if data:
-        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
-        dist.send(buf, dst, group=group, tag=tag)
+    with on_side(dev):
+        hdr = torch.tensor([len(data)], dtype=torch.int64, device=dev)
+        dist.send(hdr, dst, group=group, tag=tag)
+        if data:
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+            dist.send(buf, dst, group=group, tag=tag)
 
 
 def recv_bytes(src: int, group=None, tag: int = 0) -> bytes:
     dev = _dev(group)
-    hdr = torch.empty(1, dtype=torch.int64, device=dev)
-    dist.recv(hdr, src, group=group, tag=tag)
-    n = int(hdr.item())
-    if n == 0:
-        return b""
-    buf = torch.empty(n, dtype=torch.uint8, device=dev)
-    dist.recv(buf, src, group=group, tag=tag)
-    return bytes(buf.cpu().numpy().tobytes())
+    with on_side(dev):
+        hdr = torch.empty(1, dtype=torch.int64, device=dev)
+        dist.recv(hdr, src, group=group, tag=tag)
+        n = int(hdr.item())
+        if n == 0:
+            return b""
+        buf = torch.empty(n, dtype=torch.uint8, device=dev)
+        dist.recv(buf, src, group=group, tag=tag)
+        return bytes(buf.cpu().numpy().tobytes())
 
 
 def send_obj(obj: Any, dst: int, group=None, tag: int = 0) -> None:
@@ -109,19 +146,21 @@ def _recv(t: torch.Tensor, src: int, group, timeout_s: Optional[float], what: st
 def send_tokens(ids, dst: int, group=None, timeout_s: Optional[float] = None) -> None:
     """Ship int32 token ids (length header + payload); every wait is bounded by ``timeout_s``."""
     dev = _dev(group)
-    t = torch.as_tensor(ids, dtype=torch.int32).to(dev)
-    _send(torch.tensor([t.numel()], dtype=torch.int64, device=dev), dst, group, timeout_s, "token header send")
-    if t.numel():
-        _send(t, dst, group, timeout_s, "token send")
+    with on_side(dev):
+        t = torch.as_tensor(ids, dtype=torch.int32).to(dev)
+        _send(torch.tensor([t.numel()], dtype=torch.int64, device=dev), dst, group, timeout_s, "token header send")
+        if t.numel():
+            _send(t, dst, group, timeout_s, "token send")
 
 
 def recv_tokens(src: int, group=None, timeout_s: Optional[float] = None) -> torch.Tensor:
     dev = _dev(group)
-    hdr = torch.empty(1, dtype=torch.int64, device=dev)
-    _recv(hdr, src, group, timeout_s, "token header receive")
-    t = torch.empty(int(hdr.item()), dtype=torch.int32, device=dev)
-    if t.numel():
-        _recv(t, src, group, timeout_s, "token receive")
+    with on_side(dev):   # returns after the side stream drained: the ids are complete
+        hdr = torch.empty(1, dtype=torch.int64, device=dev)
+        _recv(hdr, src, group, timeout_s, "token header receive")
+        t = torch.empty(int(hdr.item()), dtype=torch.int32, device=dev)
+        if t.numel():
+            _recv(t, src, group, timeout_s, "token receive")
     return t
 
 
@@ -129,14 +168,13 @@ def ping(peer: int, group=None, nbytes: int = 4096, initiator: bool = True,
          timeout_s: Optional[float] = None) -> float:
     """4 KiB ping-pong; returns the round-trip time in microseconds on the initiator."""
     dev = _dev(group)
-    buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-    t0 = time.perf_counter()
-    if initiator:
-        _send(buf, peer, group, timeout_s, "ping send")
-        _recv(buf, peer, group, timeout_s, "ping receive")
-    else:
-        _recv(buf, peer, group, timeout_s, "ping receive")
-        _send(buf, peer, group, timeout_s, "ping send")
-    if dev.type == "cuda":
-        torch.cuda.current_stream().synchronize()
+    with on_side(dev):   # the round trip includes draining the side stream
+        buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        t0 = time.perf_counter()
+        if initiator:
+            _send(buf, peer, group, timeout_s, "ping send")
+            _recv(buf, peer, group, timeout_s, "ping receive")
+        else:
+            _recv(buf, peer, group, timeout_s, "ping receive")
+            _send(buf, peer, group, timeout_s, "ping send")
     return (time.perf_counter() - t0) * 1e6
