@@ -280,9 +280,75 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     s_rsp[rs_part * BM + rs_row] = s;  // published by the loop's first barrier (or the one below)
   }
 
+  // ---- ping-pong main loop of the 256 x 256 tile with 32-deep k-steps (8 waves = 2 per SIMD):
+  // wave group wm = 1 runs one barrier behind group 0, so on every SIMD one wave's LDS reads and
+  // ring refills overlap the other wave's MFMA burst (raised priority).  Per k-step two phases
+  // {memory: fragment reads (phase 0 also refills the slot read at t-1, phase 1 waits for slot t+1),
+  // lgkmcnt(0), barrier, 16 MFMAs, barrier}.  Ordering (barrier k of group 0 = barrier k-1 of
+  // group 1): every read of a slot retires before its wave's barrier, which both groups pass before
+  // the refill of that slot is issued one step later; slot t+1 is waited for (counted vmcnt) before
+  // the phase-1 barrier that every reader of it passes afterwards.
+  constexpr bool PP = NL == 0 && WK == 1 && KS == 1 && NW == 8 && WGM == 2 && BKT == 32 && FM == 8 && FN == 4 &&
+                      STAGES >= 3;
+  if constexpr (PP) {
+    const bool g1 = wm == 1;
+    wait_stages<G, (STAGES - 2 < 6 ? STAGES - 2 : 6)>(min(STAGES - 2, nk - 1));  // slot 0 landed
+    block_sync_lds();
+    if (g1) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int c = lane >> 4;
+    for (int t = 0; t < nk; ++t) {
+      const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
+      bf16x8 af[FM], bw[FN];
+      if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * WN + 16 * j + (lane & 15);
+        bw[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + r * RB + ((c ^ swz<BKT>(r)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM / 2; ++i) {
+        const int r = wm * WM + 16 * i + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(base + r * RB + ((c ^ swz<BKT>(r)) << 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = FM / 2; i < FM; ++i) {
+        const int r = wm * WM + 16 * i + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(base + r * RB + ((c ^ swz<BKT>(r)) << 4));
+      }
+      if (t + 1 < nk) wait_stages<G, (STAGES - 2 < 6 ? STAGES - 2 : 6)>(min(STAGES - 2, nk - 2 - t));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = FM / 2; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (!g1) __builtin_amdgcn_s_barrier();  // both groups leave with the same barrier count
+  }
   // ---- main loop: wait for tile t, barrier, refill the slot read at t-1, compute tile t
   // (NL > 0: the loader waves do the waits and refills, the compute waves only the MFMA part)
-  for (int t = 0; t < nk; ++t) {
+  for (int t = 0; t < (PP ? 0 : nk); ++t) {
     if (NL == 0 || loader) {
       // tile t landed once at most min(STAGES - 2, nk - 1 - t) later stages are still in flight
       wait_stages<G, (STAGES - 2 < 6 ? STAGES - 2 : 6)>(min(STAGES - 2, nk - 1 - t));
