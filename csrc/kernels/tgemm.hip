@@ -283,8 +283,8 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   // ---- ping-pong main loop of the 256 x 256 tile with 32-deep k-steps (8 waves = 2 per SIMD):
   // wave group wm = 1 runs one barrier behind group 0, so on every SIMD one wave's LDS reads and
   // ring refills overlap the other wave's MFMA burst (raised priority).  Per k-step two phases
-  // {memory: fragment reads (phase 0 also refills the slot read at t-1, phase 1 waits for slot t+1),
-  // lgkmcnt(0), barrier, 16 MFMAs, barrier}.  Ordering (barrier k of group 0 = barrier k-1 of
+  // {memory: fragment reads (phase 0 refills the A half of the slot read at t-1, phase 1 its B half
+  // and then waits for slot t+1), lgkmcnt(0), barrier, 16 MFMAs, barrier}.  Ordering (barrier k of group 0 = barrier k-1 of
   // group 1): every read of a slot retires before its wave's barrier, which both groups pass before
   // the refill of that slot is issued one step later; slot t+1 is waited for (counted vmcnt) before
   // the phase-1 barrier that every reader of it passes afterwards.
@@ -300,7 +300,15 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     for (int t = 0; t < nk; ++t) {
       const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES;
       bf16x8 af[FM], bw[FN];
-      if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+      const bool refill = t + STAGES - 1 < nk;
+      const int tk_r = kstep(t + STAGES - 1);
+      unsigned char* rbase = smem + ((t + STAGES - 1) % STAGES) * STAGE_BYTES;
+      if (refill) {  // the slot's A half now, its B half in phase 1 (two loads per lane per phase)
+#pragma unroll
+        for (int j = 0; j < GA; ++j)
+          __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + tk_r * KSTEP),
+                                           (lds_void*)(rbase + (wave * GA + j) * 1024), 16, 0, 0);
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * WN + 16 * j + (lane & 15);
@@ -328,6 +336,13 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
       for (int i = FM / 2; i < FM; ++i) {
         const int r = wm * WM + 16 * i + (lane & 15);
         af[i] = *reinterpret_cast<const bf16x8*>(base + r * RB + ((c ^ swz<BKT>(r)) << 4));
+      }
+      if (refill) {
+        const long kw = w_koff(kbeg + tk_r * KSTEP);
+#pragma unroll
+        for (int j = 0; j < GB; ++j)
+          __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + kw),
+                                           (lds_void*)(rbase + A_BYTES + (wave * GB + j) * 1024), 16, 0, 0);
       }
       if (t + 1 < nk) wait_stages<G, (STAGES - 2 < 6 ? STAGES - 2 : 6)>(min(STAGES - 2, nk - 2 - t));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
