@@ -408,7 +408,7 @@ def moe_router(x: torch.Tensor, wg: torch.Tensor, k: int) -> Tuple[torch.Tensor,
     padded graph batch picks the same experts as the eager batch; a vendor GEMM's split varies
     with M).  x [T, H] bf16, wg [E, H] bf16 -> ids [T, k] int32, renormalised weights [T, k] f32."""
     ext = _native(x)
-    if ext is None or x.shape[1] > 8192 or x.stride(0) % 8:
+    if ext is None or x.shape[1] > 8192 or x.shape[1] % 8 or x.stride(0) % 8 or x.data_ptr() % 16 or wg.data_ptr() % 16:
         return moe_gate(torch.nn.functional.linear(x.float(), wg.float()), k)
     T = x.shape[0]
     ids = torch.empty((T, k), dtype=torch.int32, device=x.device)

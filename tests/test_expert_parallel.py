@@ -117,3 +117,17 @@ def test_ep2_engine_matches_tp1():
         assert got[:3] == want[:3]
     same = sum(a == b for g, w in zip(res[0], ref) for a, b in zip(g, w))
     assert same >= 0.8 * sum(len(w) for w in ref)
+
+
+def test_moe_router_cpu_matches_fp32_gate():
+    """ops.moe_router off the GPU: fp32 projection + the same top-k / renormalised weights as
+    ops.moe_gate (the kernel's semantics); rows are independent of the batch they arrive in."""
+    from distributed_llm_amd import ops
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(9, 64, generator=g).bfloat16()
+    wg = torch.randn(8, 64, generator=g).bfloat16()
+    ids, w = ops.moe_router(x, wg, 2)
+    ri, rw = ops.moe_gate(x.float() @ wg.float().t(), 2)
+    assert torch.equal(ids, ri) and torch.allclose(w, rw)
+    i3, w3 = ops.moe_router(x[:3], wg, 2)
+    assert torch.equal(i3, ids[:3]) and torch.allclose(w3, w[:3])
