@@ -220,12 +220,11 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
       l_off[j] = ks * SUB_BYTES + p * 1024;
     }
   }
-  // Rotated k order: each output tile walks its k-steps from its own offset, so the many
-  // workgroups that stream the SAME activation / weight panel at once are spread over different k
-  // columns (L2 channels) instead of all requesting one line together (rg ROT in
-  // scripts/exp/gemmlab.hip: 1-3 % on the decode shapes).  Slot t of the ring holds k-step kstep(t).
-  const int krot = nk > 1 ? (int)(((unsigned)(n_tile * 7 + m_tile * 3)) % (unsigned)nk) : 0;
-  auto kstep = [&](int t) { const int u = t + krot; return u >= nk ? u - nk : u; };
+  // k-steps in the same order in every workgroup: the workgroups of an XCD that share an activation
+  // or weight tile then request its lines at about the same time and hit them in the XCD's L2.  (A
+  // rotated k-start per tile, tried this round, spread those requests over time: the 256 x 256
+  // prefill tile's L2 hit rate fell to 11 % against hipBLASLt's 81 %, profiles/r5_decode_gemm_lab.md.)
+  auto kstep = [&](int t) { return t; };
   auto issue = [&](int t) {
     const int tk = kstep(t);
     if constexpr (NL > 0) {

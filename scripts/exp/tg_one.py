@@ -1,5 +1,5 @@
-"""Run ONE tgemm plan on one shape a few times (for rocprofv3 --pmc passes).
-Usage: python scripts/exp/tg_one.py M N K bm,bn,stages,splits,ks,waves[,k-groups,nl,sk,kdepth] [reps]"""
+"""Run ONE tgemm plan (or hipBLASLt: plan "blas") on one shape a few times (for rocprofv3 --pmc passes).
+Usage: python scripts/exp/tg_one.py M N K bm,bn,stages,splits,ks,waves[,k-groups,nl,sk,kdepth]|blas [reps]"""
 import sys
 
 import torch
@@ -9,7 +9,7 @@ from distributed_llm_amd.ops import gemm as G
 
 def main():
     M, N, K = (int(v) for v in sys.argv[1:4])
-    plan = tuple(int(v) for v in sys.argv[4].split(","))
+    plan = None if sys.argv[4] == "blas" else tuple(int(v) for v in sys.argv[4].split(","))
     reps = int(sys.argv[5]) if len(sys.argv) > 5 else 10
     dev = torch.device("cuda:0")
     ext = G._native(torch.empty(1, device=dev))
@@ -17,7 +17,10 @@ def main():
     w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
     y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     for _ in range(reps):
-        G._tgemm(ext, x, w, G.EPI_PLAIN, plan, y=y)
+        if plan is None:
+            torch.matmul(x, w.t(), out=y)   # hipBLASLt
+        else:
+            G._tgemm(ext, x, w, G.EPI_PLAIN, plan, y=y)
     torch.cuda.synchronize()
     print("done", M, N, K, plan)
 
