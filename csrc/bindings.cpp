@@ -74,8 +74,9 @@ int dllm_qkv_post(const void*, long, const float*, int, long, float, float, cons
 int dllm_swiglu_post(const void*, long, const float*, int, long, float, float, void*, long, int, int, hipStream_t);
 int dllm_flash_prefill(const void*, const void*, const void*, const int*, const int*, const int*, const int*, const int*,
                        const int*, void*, int, int, int, int, int, int, float, int, float*, float*, int*, hipStream_t);
-int dllm_masked_cosine_argmax(const float*, const float*, const float*, const int*, int, int, int, float,
-                              unsigned long long*, hipStream_t);
+int dllm_cache_scan(const unsigned long long*, const int*, int, const float*, const int*, long, int, float,
+                    unsigned long long*, hipStream_t);
+int dllm_cache_write(const unsigned long long*, const long long*, const int*, int, float*, int*, int, hipStream_t);
 }
 
 namespace {
@@ -543,21 +544,53 @@ void cosine_scores(torch::Tensor q, torch::Tensor c, torch::Tensor s) {
      "cosine_scores");
 }
 
-void masked_cosine_argmax(torch::Tensor q, torch::Tensor table, torch::Tensor norms, torch::Tensor ctx, int64_t cid,
-                          double thr, torch::Tensor best) {
-  check_f32(q, "q");
+// one launch for up to 128 semantic-cache lookups (csrc/kernels/cosine.hip cache_scan_kernel):
+// qptrs = device addresses of the queries' f32 [d] vectors (kept alive by the caller), qcids = their
+// context ids; best[i] <- packed (orderable sim << 32 | ~row) key, 0 = no row >= thr
+void cache_scan(std::vector<int64_t> qptrs, std::vector<int64_t> qcids, torch::Tensor table, torch::Tensor ctx,
+                int64_t n_rows, double thr, torch::Tensor best) {
   check_f32(table, "table");
-  check_f32(norms, "norms");
   check_i32(ctx, "ctx");
   check_dev(best, "best");
-  TORCH_CHECK(best.scalar_type() == torch::kInt64 && best.numel() >= 1, "best: int64[1]");
-  TORCH_CHECK(table.dim() == 2 && table.size(1) == q.numel(), "table [N, d]");
-  const int N = table.size(0);
-  TORCH_CHECK(norms.numel() >= N && ctx.numel() >= N, "norms/ctx len");
-  ok(dllm_masked_cosine_argmax(q.data_ptr<float>(), table.data_ptr<float>(), norms.data_ptr<float>(),
-                               ctx.data_ptr<int>(), N, table.size(1), (int)cid, (float)thr,
-                               (unsigned long long*)best.data_ptr<int64_t>(), stream()),
-     "masked_cosine_argmax");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) % 4 == 0 && table.size(1) <= 1024, "table [N, d], d % 4 == 0, d <= 1024");
+  TORCH_CHECK(n_rows >= 0 && n_rows <= table.size(0) && ctx.numel() >= n_rows, "rows within table/ctx");
+  TORCH_CHECK(n_rows < 0xffffffffLL, "row index must fit the 32-bit key");
+  const int nq = (int)qptrs.size();
+  TORCH_CHECK(nq >= 1 && nq <= 128 && (int)qcids.size() == nq, "1..128 queries with one context id each");
+  TORCH_CHECK(best.scalar_type() == torch::kInt64 && best.is_contiguous() && best.numel() >= nq, "best: int64[nq]");
+  std::vector<unsigned long long> qp(nq);
+  std::vector<int> qc(nq);
+  for (int i = 0; i < nq; ++i) {
+    TORCH_CHECK(qptrs[i] != 0 && (qptrs[i] & 15) == 0, "query vectors must be 16-B aligned device memory");
+    qp[i] = (unsigned long long)qptrs[i];
+    qc[i] = (int)qcids[i];
+  }
+  ok(dllm_cache_scan(qp.data(), qc.data(), nq, table.data_ptr<float>(), ctx.data_ptr<int>(), (long)n_rows,
+                     (int)table.size(1), (float)thr, (unsigned long long*)best.data_ptr<int64_t>(), stream()),
+     "cache_scan");
+}
+
+// deferred routing-cache table writes, <= 64 per launch: row slots[i] <- f32 [d] at srcs[i] (0: keep),
+// ctx[slots[i]] <- cids[i]
+void cache_write(std::vector<int64_t> srcs, std::vector<int64_t> slots, std::vector<int64_t> cids, torch::Tensor table,
+                 torch::Tensor ctx) {
+  check_f32(table, "table");
+  check_i32(ctx, "ctx");
+  const int n = (int)srcs.size();
+  TORCH_CHECK(n <= 64 && (int)slots.size() == n && (int)cids.size() == n, "<= 64 writes");
+  std::vector<unsigned long long> sp(n);
+  std::vector<long long> sl(n);
+  std::vector<int> ci(n);
+  for (int i = 0; i < n; ++i) {
+    TORCH_CHECK(slots[i] >= 0 && slots[i] < table.size(0) && slots[i] < ctx.numel(), "slot out of range");
+    TORCH_CHECK((srcs[i] & 15) == 0, "source vectors must be 16-B aligned");
+    sp[i] = (unsigned long long)srcs[i];
+    sl[i] = slots[i];
+    ci[i] = (int)cids[i];
+  }
+  ok(dllm_cache_write(sp.data(), sl.data(), ci.data(), n, table.data_ptr<float>(), ctx.data_ptr<int>(),
+                      (int)table.size(1), stream()),
+     "cache_write");
 }
 // y[M, N] = x[M, K] . w[N, K]^T   (swiglu: x is [M, 2K] gate|up, silu(gate)*up computed on load)
 void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw, int64_t splits, bool swiglu,
@@ -1158,7 +1191,8 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("tp_cands", &tp_cands);
   m.def("tp_sample", &tp_sample);
   m.def("cosine_scores", &cosine_scores);
-  m.def("masked_cosine_argmax", &masked_cosine_argmax);
+  m.def("cache_scan", &cache_scan);
+  m.def("cache_write", &cache_write);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);
   m.def("gemv_norm", &gemv_norm);

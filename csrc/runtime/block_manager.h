@@ -237,6 +237,8 @@ class BlockManager {
     return {{"num_blocks", (long long)blocks_.size()},
             {"free_blocks", (long long)n_free_},
             {"contiguous_allocs", contig_},
+            {"inplace_evictions", inplace_},
+            {"roomy_segment_allocs", idle_allocs_},
             {"segment_allocs", seg_allocs_},
             {"fresh_allocs", fresh_allocs_},
             {"evictable_blocks", (long long)lru_.size()},
@@ -296,6 +298,10 @@ class BlockManager {
     }
     for (const auto& kv : hash2block_)
       if (!blocks_[kv.second].hashed || blocks_[kv.second].hash != kv.first) return "stale hash entry";
+    std::vector<int> held(held_.size(), 0);
+    for (size_t b = 0; b < blocks_.size(); ++b)
+      if (blocks_[b].ref > 0) ++held[b / kSeg];
+    if (held != held_) return "segment held count mismatch";
     return "";
   }
 
@@ -323,7 +329,7 @@ class BlockManager {
       lru_.erase(blk.lru_it);
       blk.in_lru = false;
     }
-    ++blk.ref;
+    if (blk.ref++ == 0) { ++held_[b / kSeg]; note_held(b / kSeg); }
   }
 
   // Free-block bookkeeping.  Decode attention reads each sequence's K/V block by block; blocks
@@ -334,6 +340,7 @@ class BlockManager {
   // take any free block (LIFO) or evict from the LRU.  free_ and seg_stack_ are stacks with lazy
   // deletion: an entry is valid only if its flag / count still says free.
   static constexpr int kSeg = 64;
+  static constexpr int kMaxHeld = 63, kMinStretch = 2;   // pop_roomy_segment candidates
   int seg_size(int sg) const { return std::min(kSeg, (int)blocks_.size() - sg * kSeg); }
 
   void init_free() {
@@ -347,6 +354,9 @@ class BlockManager {
     for (int i = n - 1; i >= 0; --i) free_.push_back(i);
     seg_stack_.clear();
     for (int sg = (int)seg_free_.size() - 1; sg >= 0; --sg) seg_stack_.push_back(sg);
+    held_.assign(seg_free_.size(), 0);
+    held_stacks_.assign(kMaxHeld, {});
+    for (int sg = (int)held_.size() - 1; sg >= 0; --sg) held_stacks_[0].push_back(sg);
   }
 
   void push_free(int b) {
@@ -401,30 +411,101 @@ class BlockManager {
     return -1;
   }
 
-  // prefer: the block after the sequence's last one (-1: none)
+  // A sequence that cannot continue its run starts a new one in the segment with the FEWEST held
+  // blocks (ref > 0), at the head of that segment's longest stretch of free / evictable blocks, and
+  // then grows through the stretch by in-place eviction (fresh()) - instead of scattering over
+  // single LRU-tail blocks.  held_stacks_[h] holds segments whose held count became h (lazy:
+  // an entry is valid only while the count still says h); segments with kMaxHeld or more held blocks, or no stretch of kMinStretch, are skipped.
+  int pop_roomy_segment() {
+    for (int h = 0; h < kMaxHeld; ++h) {
+      auto& st = held_stacks_[h];
+      while (!st.empty()) {
+        const int sg = st.back();
+        if (held_[sg] != h) { st.pop_back(); continue; }
+        // longest run of non-held blocks in the segment
+        const int lo = sg * kSeg, hi = lo + seg_size(sg);
+        int best = -1, best_len = 0;
+        for (int i = lo; i < hi;) {
+          if (blocks_[i].ref > 0) { ++i; continue; }
+          int j = i;
+          while (j < hi && blocks_[j].ref == 0) ++j;
+          if (j - i > best_len) { best_len = j - i; best = i; }
+          i = j;
+        }
+        if (best < 0 || best_len < kMinStretch) { st.pop_back(); continue; }  // too fragmented to help
+        if (free_flag_[best]) take_free(best);
+        else if (blocks_[best].in_lru) evict(best);
+        else { st.pop_back(); continue; }
+        ++idle_allocs_;
+        return best;
+      }
+    }
+    return -1;
+  }
+
+  void note_held(int sg) {
+    const int h = held_[sg];
+    if (h < kMaxHeld) {
+      held_stacks_[h].push_back(sg);
+      if (held_stacks_[h].size() > 4 * held_.size() + 64) compact_held(h);
+    }
+  }
+
+  void compact_held(int h) {
+    std::vector<uint8_t> seen(held_.size(), 0);
+    std::vector<int> v;
+    for (int sg : held_stacks_[h])
+      if (held_[sg] == h && !seen[sg]) { seen[sg] = 1; v.push_back(sg); }
+    held_stacks_[h].swap(v);
+  }
+
+  // take block b out of the LRU for new content (its hash, if any, is unregistered)
+  void evict(int b) {
+    Block& old = blocks_[b];
+    lru_.erase(old.lru_it);
+    old.in_lru = false;
+    if (old.hashed) {
+      hash2block_.erase(old.hash);
+      old.hashed = false;
+      old.parent = -1;
+    }
+  }
+
+  // prefer: the block after the sequence's last one (-1: none).  The run continues there when that
+  // block is free, or evictable: a cached block nobody holds (ref 0, in the LRU) is evicted IN PLACE.
+  // In the serving workload that block is almost always the sequence's own previous-turn decode
+  // block whose tokens did not re-tokenise to the same ids (so its hash can never match again) -
+  // the LRU would evict it eventually anyway, and taking it now keeps the conversation's K/V in one
+  // run (profiles/r6_kv_runs.md).  A run crosses into the next segment only when that segment is
+  // not wholly free (wholly free segments are kept for sequences that start a new run).
   int fresh(int prefer = -1) {
     ++fresh_allocs_;
     int b = -1;
-    if (contiguous_ && prefer > 0 && prefer < (int)blocks_.size() && prefer % kSeg != 0 && free_flag_[prefer]) {
-      b = prefer;   // continue the run (never into the next segment: that one may be wholly free)
-      take_free(b);
-      ++contig_;
+    if (contiguous_ && prefer > 0 && prefer < (int)blocks_.size()) {
+      if (true) {
+        if (free_flag_[prefer]) {
+          b = prefer;
+          take_free(b);
+          ++contig_;
+        } else if (blocks_[prefer].ref == 0 && blocks_[prefer].in_lru) {
+          b = prefer;
+          evict(b);
+          ++contig_;
+          ++inplace_;
+        }
+      }
     }
     if (b < 0 && contiguous_) b = pop_segment();
+    if (b < 0 && contiguous_) b = pop_roomy_segment();
     if (b < 0) b = pop_free();
     if (b < 0) {
       if (lru_.empty()) throw std::runtime_error("out of KV blocks");
       b = lru_.back();  // least recently used cached block
-      lru_.pop_back();
-      Block& old = blocks_[b];
-      old.in_lru = false;
-      if (old.hashed) {
-        hash2block_.erase(old.hash);
-        old.hashed = false;
-        old.parent = -1;
-      }
+      evict(b);
     }
     blocks_[b].ref = 1;
+    ++held_[b / kSeg];
+    note_held(b / kSeg);
     ++blocks_[b].gen;  // new content from here on: children registered under the old one go stale
     return b;
   }
@@ -432,6 +513,8 @@ class BlockManager {
   void release(int b) {
     Block& blk = blocks_[b];
     if (--blk.ref > 0) return;
+    --held_[b / kSeg];
+    note_held(b / kSeg);
     if (blk.hashed) {
       lru_.push_front(b);
       blk.lru_it = lru_.begin();
@@ -450,7 +533,9 @@ class BlockManager {
   int n_free_ = 0;
   std::vector<int> seg_free_;      // free blocks per segment of kSeg
   std::vector<int> seg_stack_;     // segments that were wholly free when pushed (lazy)
-  long long contig_ = 0, seg_allocs_ = 0, fresh_allocs_ = 0;
+  long long contig_ = 0, seg_allocs_ = 0, fresh_allocs_ = 0, inplace_ = 0, idle_allocs_ = 0;
+  std::vector<int> held_;          // blocks with ref > 0 per segment
+  std::vector<std::vector<int>> held_stacks_;  // segments by held count (lazy; see pop_roomy_segment)
   std::list<int> lru_;  // front = most recently released
   std::unordered_map<uint64_t, int> hash2block_;
   std::unordered_map<int64_t, Seq> seqs_;

@@ -180,7 +180,13 @@ int main(int argc, char** argv) {
   const std::string err = bm.check_invariants();
   if (!err.empty()) die(err.c_str(), iters);
   if (bm.num_free_blocks() != nblocks) die("blocks leaked after freeing everything", iters);
-  std::printf("ok iterations=%ld prefix_hits=%ld alloc_failures=%ld preempted=%ld collisions=%lld\n", iters, hits,
-              evict_pressure, preempt, bm.stats().at("hash_collisions"));
+  // the run-placement paths (in-place eviction of the block after a run, run restarts in the
+  // least-held segment) must have been exercised under the content model
+  const auto st = bm.stats();
+  if (iters >= 5000 && (st.at("inplace_evictions") == 0 || st.at("roomy_segment_allocs") == 0))
+    die("run placement paths not exercised", iters);
+  std::printf("ok iterations=%ld prefix_hits=%ld alloc_failures=%ld preempted=%ld collisions=%lld inplace=%lld "
+              "roomy=%lld\n", iters, hits, evict_pressure, preempt, st.at("hash_collisions"),
+              st.at("inplace_evictions"), st.at("roomy_segment_allocs"));
   return 0;
 }

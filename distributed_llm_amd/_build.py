@@ -76,9 +76,12 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
     jobs_list.append([hipcc, *common, *torch_inc, *py_inc, f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
                       "-DTORCH_EXTENSION_NAME=_hip_kernels", "-DTORCH_API_INCLUDE_EXTENSION_H",
                       "-c", bind, "-o", bind_obj])
-    with cf.ThreadPoolExecutor(max(1, min(jobs, len(jobs_list)))) as ex:
-        list(ex.map(_run, jobs_list))
     objs = [j[-1] for j in jobs_list]
+    # incremental: an object newer than its source and every kernel header is reused
+    srcs = kernels + [bind]
+    todo = [j for j, src in zip(jobs_list, srcs) if force or not _newer(j[-1], [src] + headers)]
+    with cf.ThreadPoolExecutor(max(1, min(jobs, len(todo) or 1))) as ex:
+        list(ex.map(_run, todo))
     libdir = ce.library_paths(device_type="cuda")[0]
     tmp = HIP_SO + ".tmp"
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-L", libdir,

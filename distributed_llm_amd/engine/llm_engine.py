@@ -72,6 +72,9 @@ class RequestOutput:
         return self.num_prompt - self.num_cached
 
 
+KV_RESERVE_GB = 16.0   # device memory left free next to a requested KV pool (_alloc_kv)
+
+
 @dataclass
 class _Seq:
     id: int
@@ -197,6 +200,14 @@ class LLMEngine:
                 kv_cache_gb = 0.6 * free / 2**30
             else:
                 kv_cache_gb = 0.25
+        elif self.device.type == "cuda":
+            # a requested size is an upper bound: what is free after this engine's weights (and any
+            # engine or TP shard already on the device), less KV_RESERVE_GB for graphs, split-K
+            # workspaces, prefill activations and the router encoder (a 160 GB default
+            # pool next to Llama-3-70B TP shards must not over-commit the 288 GB part)
+            free, _ = torch.cuda.mem_get_info(self.device)
+            kv_cache_gb = min(float(kv_cache_gb), max(0.5, free / 2**30 - KV_RESERVE_GB))
+        self.kv_cache_gb = float(kv_cache_gb)
         self.num_blocks = max(int(kv_cache_gb * 2**30) // per_block, self.max_blocks + 8)
         self.k_cache = torch.empty((L, self.num_blocks, m.nkv, BS, m.d), dtype=m.dtype, device=self.device)
         self.v_cache = torch.empty((L, self.num_blocks, m.nkv, m.d, BS), dtype=m.dtype, device=self.device)

@@ -199,6 +199,12 @@ class MiniLMEncoder:
 
     def encode(self, texts: List[str], max_len: int = 256) -> torch.Tensor:
         """[n, 384] f32 unit vectors on the device; memoised per text."""
+        out = self.encode_rows(texts, max_len)
+        return torch.stack(out) if out else torch.zeros((0, self.cfg.hidden), device=self.device)
+
+    def encode_rows(self, texts: List[str], max_len: int = 256) -> List[torch.Tensor]:
+        """``encode`` as one [384] row view per text, with no stacking launch: the rows belong to
+        forward outputs that are never written again (the routing cache keeps references)."""
         out: List[Optional[torch.Tensor]] = [None] * len(texts)
         todo: Dict[str, List[int]] = {}
         with self._lock:
@@ -229,4 +235,4 @@ class MiniLMEncoder:
                         self._memo[k] = e
                 while len(self._memo) > self._memo_size:
                     self._memo.popitem(last=False)
-        return torch.stack(out) if out else torch.zeros((0, self.cfg.hidden), device=self.device)
+        return out

@@ -14,7 +14,7 @@ from __future__ import annotations
 import math
 import os
 import struct
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -574,22 +574,80 @@ def cosine_scores(q: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     return s
 
 
-def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tensor, ctx: torch.Tensor, cid: int,
-                         thr: float) -> Tuple[int, float]:
-    """Best row of ``table`` with ctx id == cid and cosine >= thr -> (row, sim) or (-1, 0.0)."""
-    ext = _native(table)
-    if ext is None:
-        return ref.masked_cosine_argmax(q, table, norms, ctx, cid, thr)
-    best = torch.zeros(1, dtype=torch.int64, device=table.device)
-    ext.masked_cosine_argmax(q.float().contiguous(), table, norms, ctx, int(cid), float(thr), best)
-    key = int(best.item()) & 0xFFFFFFFFFFFFFFFF
+def _unpack_key(key: int) -> Tuple[int, float]:
+    key &= 0xFFFFFFFFFFFFFFFF
     if key == 0:
         return -1, 0.0
     row = 0xFFFFFFFF - (key & 0xFFFFFFFF)
     bits = key >> 32
     bits = (bits & 0x7FFFFFFF) if (bits & 0x80000000) else (~bits & 0xFFFFFFFF)
-    sim = struct.unpack("<f", struct.pack("<I", bits))[0]
-    return int(row), float(sim)
+    return int(row), float(struct.unpack("<f", struct.pack("<I", bits))[0])
+
+
+CACHE_SCAN_MAX_Q = 128   # queries per cache_scan launch (csrc/kernels/cosine.hip CQ)
+CACHE_WRITE_MAX = 64     # row writes per cache_write launch (CW)
+
+
+def cache_scan(queries: List[torch.Tensor], cids: List[int], table: torch.Tensor, ctx: torch.Tensor, n_rows: int,
+               thr: float) -> List[Tuple[int, float]]:
+    """Semantic-cache lookups of a routing batch: for each query (an f32 [d] vector) the row of
+    ``table[:n_rows]`` whose context id equals the query's with the highest cosine >= thr, as
+    (row, sim), or (-1, 0.0).  One launch per 128 queries and ONE host read-back for the batch;
+    only rows of the batch's contexts are read (csrc/kernels/cosine.hip cache_scan_kernel)."""
+    if not queries:
+        return []
+    ext = _native(table)
+    if ext is None:
+        return ref.cache_scan(queries, cids, table, ctx, n_rows, thr)
+    qs = [q if (q.dtype == torch.float32 and q.is_contiguous() and q.data_ptr() % 16 == 0) else
+          q.float().contiguous() for q in queries]
+    best = torch.empty(len(qs), dtype=torch.int64, device=table.device)
+    for i in range(0, len(qs), CACHE_SCAN_MAX_Q):
+        part = qs[i:i + CACHE_SCAN_MAX_Q]
+        ext.cache_scan([q.data_ptr() for q in part], [int(c) for c in cids[i:i + CACHE_SCAN_MAX_Q]], table, ctx,
+                       int(n_rows), float(thr), best[i:])
+    return [_unpack_key(k) for k in best.tolist()]
+
+
+def cache_write(writes: List[Tuple[int, Optional[torch.Tensor], int]], table: torch.Tensor, ctx: torch.Tensor) -> None:
+    """Apply deferred routing-cache table writes (slot, f32 [d] vector or None, context id) in
+    launches of 64: row ``slot`` <- the vector (None: keep the row's bytes), ``ctx[slot]`` <- id
+    (-1 removes the row from every lookup).  Slots must be unique within ``writes``."""
+    if not writes:
+        return
+    ext = _native(table)
+    if ext is None:
+        for slot, v, cid in writes:
+            if v is not None:
+                table[slot].copy_(v.reshape(-1))
+            ctx[slot] = cid
+        return
+    keep = []
+    for i in range(0, len(writes), CACHE_WRITE_MAX):
+        part = writes[i:i + CACHE_WRITE_MAX]
+        srcs = []
+        for _, v, _ in part:
+            if v is None:
+                srcs.append(0)
+                continue
+            if not (v.dtype == torch.float32 and v.is_contiguous() and v.data_ptr() % 16 == 0 and v.is_cuda):
+                v = v.to(table.device, torch.float32).contiguous()
+                keep.append(v)
+            srcs.append(v.data_ptr())
+        ext.cache_write(srcs, [int(s) for s, _, _ in part], [int(c) for _, _, c in part], table, ctx)
+    # (converted copies in ``keep`` may be freed now: the caching allocator hands their blocks only
+    # to work queued after these launches on the same stream)
+
+
+def masked_cosine_argmax(q: torch.Tensor, table: torch.Tensor, norms: torch.Tensor, ctx: torch.Tensor, cid: int,
+                         thr: float) -> Tuple[int, float]:
+    """Best row of ``table`` with ctx id == cid and cosine >= thr -> (row, sim) or (-1, 0.0) (one
+    query: ``cache_scan``; on the GPU the row norms are computed in the kernel, ``norms`` is the
+    host table's and is only used by the CPU reference)."""
+    ext = _native(table)
+    if ext is None:
+        return ref.masked_cosine_argmax(q, table, norms, ctx, cid, thr)
+    return cache_scan([q.reshape(-1)], [cid], table, ctx, table.shape[0], thr)[0]
 
 
 from .gemm import autotune as gemm_autotune, linear, linear_swiglu, norm_linear  # noqa: E402

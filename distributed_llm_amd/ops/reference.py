@@ -6,7 +6,7 @@ tests compare against.  Layout contracts are identical to the HIP kernels.
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -331,6 +331,28 @@ def masked_cosine_argmax(q, table, norms, ctx, cid, thr) -> Tuple[int, float]:
     j = int(torch.argmax(sims))
     s = float(sims[j])
     return (j, s) if s >= thr else (-1, 0.0)
+
+
+def cache_scan(queries, cids, table, ctx, n_rows, thr) -> List[Tuple[int, float]]:
+    """fp32 reference of ops.cache_scan: per query, the row of its context id with the highest
+    cosine >= thr (lowest row on ties; rows or queries of norm < 1e-9 never match) or (-1, 0.0)."""
+    t = table[:n_rows].float()
+    c = ctx[:n_rows]
+    rn = t.norm(dim=-1)
+    out = []
+    for q, cid in zip(queries, cids):
+        qf = q.float().reshape(-1)
+        nq = float(qf.norm())
+        mask = (c == int(cid)) & (rn >= 1e-9)
+        if nq < 1e-9 or not bool(mask.any()):
+            out.append((-1, 0.0))
+            continue
+        sims = (t @ qf) / (rn.clamp(min=1e-30) * nq)
+        sims = torch.where(mask, sims, torch.full_like(sims, -float("inf")))
+        j = int(torch.argmax(sims))
+        s = float(sims[j])
+        out.append((j, s) if s >= thr else (-1, 0.0))
+    return out
 
 
 def embedding(ids, table, lo=0):

@@ -271,9 +271,9 @@ class Router:
         results: List[Any] = [None] * len(histories)
         groups: Dict[str, List[int]] = {SMALL: [], LARGE: []}
         meta: Dict[int, Tuple[str, Dict[str, Any]]] = {}
-        self._prefetch_embeddings([self._split(h)[0] for h in histories])
-        for i, h in enumerate(histories):
-            query, context, ctx_hash = self._split(h)
+        splits = [self._split(h) for h in histories]
+        self._prefetch_embeddings([sp[0] for sp in splits], [sp[2] for sp in splits])
+        for i, (h, (query, context, ctx_hash)) in enumerate(zip(histories, splits)):
             hit = self._cached_payload(query)
             if hit is not None:
                 results[i] = hit
@@ -310,10 +310,10 @@ class Router:
     def _decide_batch(self, histories: Sequence[List[Dict[str, Any]]]) -> List[Tuple[str, Any, Any]]:
         """Routing half of ``route_batch``: ("hit", payload, None) for a response-cache hit,
         else ("route", query, decision)."""
-        self._prefetch_embeddings([self._split(h)[0] for h in histories])
+        splits = [self._split(h) for h in histories]
+        self._prefetch_embeddings([sp[0] for sp in splits], [sp[2] for sp in splits])
         out: List[Tuple[str, Any, Any]] = []
-        for h in histories:
-            query, context, ctx_hash = self._split(h)
+        for h, (query, context, ctx_hash) in zip(histories, splits):
             hit = self._cached_payload(query)
             if hit is not None:
                 out.append(("hit", hit, None))
@@ -375,6 +375,8 @@ class Router:
                 t["query"], t["dec"], t["device"] = a, dec, dec["device"]
                 if self._pool_down(dec["device"]):   # a tier known to be down: fail over up front
                     t["failover_from"], t["device"] = dec["device"], other_tier(dec["device"])
+                    # a double failure then reports the primary's error with no failover, as route_query
+                    t["primary_error"] = {"error": f"pool {dec['device']} unavailable"}
                 groups[t["device"]].append(i)
             tickets.append(t)
         for dev, idx in groups.items():
@@ -455,10 +457,11 @@ class Router:
         t["latency_ms"] = (time.perf_counter() - t["t0"]) * 1000.0
         return self._finish(t["query"], t["dec"], raw, which, lat, failed)
 
-    def _prefetch_embeddings(self, queries: List[str]) -> None:
+    def _prefetch_embeddings(self, queries: List[str], context_keys: Optional[List[str]] = None) -> None:
         """One batched encoder forward for every query of a batch (the GPU encoder keeps it for the
         batch's own lookups even with its memo off), so the semantic router and the semantic cache
-        do no per-query encoder launches."""
+        do no per-query encoder launches; then the batch's centroid scores and its semantic-cache
+        lookups are scored in one launch each (``prefetch_scores``, ``prefetch_cache``)."""
         emb = self.query_router.cache_embedder
         needs = self.query_router.cache_enabled or self.query_router.strategy in ("semantic", "hybrid")
         if emb is None or not needs or not queries:
@@ -467,6 +470,8 @@ class Router:
         try:
             enc(list(dict.fromkeys(queries)))
             self.query_router.prefetch_scores(queries)
+            if context_keys is not None:
+                self.query_router.prefetch_cache(queries, context_keys)
         except Exception as exc:  # routing still works, just unbatched
             logger.warning("batched embedding prefetch failed: %s", exc)
 

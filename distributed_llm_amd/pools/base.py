@@ -95,14 +95,14 @@ class PoolHandle:
     completed it.  Remote pools complete handles from their receiver thread; a deadline reaper
     fails handles a hung pool never answers (the reference's per-request ``timeout=(5, 180)``)."""
 
-    __slots__ = ("done", "reply", "notify", "deadline", "owner", "_lock")
+    __slots__ = ("done", "reply", "notify", "deadline", "rp", "_lock")
 
     def __init__(self, notify: Optional[Callable[["PoolHandle"], None]] = None, deadline: Optional[float] = None):
         self.done = threading.Event()
         self.reply: Optional[Dict[str, Any]] = None
         self.notify = notify
         self.deadline = deadline
-        self.owner = None            # ReplicatedPool: the replica that serves it
+        self.rp = None               # ReplicatedPool bookkeeping: {id(pool): [replica, released]}
         self._lock = threading.Lock()
 
     def complete(self, reply: Dict[str, Any]) -> bool:

@@ -441,8 +441,9 @@ class PoolLeader:
         # queues the finished sequence; this thread forms its payload and replies, so the engine's
         # step loop never blocks on the control-plane socket
         self._rq: "queue.Queue" = queue.Queue()
-        self._rid: Dict[int, int] = {}          # id(sequence) -> request id
-        self._rid_cv = threading.Condition()
+        # submits run on their own thread, in arrival order (tokenising a batch never delays the
+        # receiver loop's answers to health pings)
+        self._sub_ex = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dllm-pool-submit")
         self._rthread = threading.Thread(target=self._reply_loop, name="dllm-pool-reply", daemon=True)
         self._rthread.start()
 
@@ -509,31 +510,37 @@ class PoolLeader:
 
     def _submit(self, rids, prompts, params) -> None:
         """Admit requests into the engine's running batch without a worker thread each; every
-        request is answered on its own when it finishes (``_reply_loop``)."""
+        request is answered on its own when it finishes (``_reply_loop``).  The engine may finish
+        a request before ``submit`` returns, so each completion carries its batch's rid table and
+        an event set as soon as that table is filled: the reply thread waits for exactly that (no
+        timeout that could drop a reply)."""
         from ..engine.sampling import SamplingParams
+        table: Dict[int, int] = {}
+        ready = threading.Event()
         try:
-            seqs = self.engine.submit(prompts, SamplingParams.from_dict(params or {}), notify=self._rq.put)
-        except Exception as e:  # noqa: BLE001 - report, never kill the receiver loop
-            for rid in rids:
-                self._safe_reply({"id": rid, "error": f"engine failed: {e}"})
-            return
-        with self._rid_cv:
+            try:
+                seqs = self.engine.submit(prompts, SamplingParams.from_dict(params or {}),
+                                          notify=lambda s_: self._rq.put((s_, table, ready)))
+            except Exception as e:  # noqa: BLE001 - report, never kill the submit thread
+                for rid in rids:
+                    self._safe_reply({"id": rid, "error": f"engine failed: {e}"})
+                return
             for s_, rid in zip(seqs, rids):
-                self._rid[id(s_)] = rid
-            self._rid_cv.notify_all()
+                table[id(s_)] = rid
+        finally:
+            ready.set()
         for s_ in seqs:
             if s_.error is not None and s_.done.is_set() and s_.notify is None:   # rejected up front
-                self._rq.put(s_)
+                self._rq.put((s_, table, ready))
 
     def _reply_loop(self) -> None:
         while True:
-            s_ = self._rq.get()
-            if s_ is None:
+            item = self._rq.get()
+            if item is None:
                 return
-            with self._rid_cv:   # the engine may finish a request before _submit has mapped it
-                rid = self._rid.pop(id(s_), None)
-                while rid is None and self._rid_cv.wait(timeout=5.0):
-                    rid = self._rid.pop(id(s_), None)
+            s_, table, ready = item
+            ready.wait()   # set right after engine.submit returns (or raises)
+            rid = table.get(id(s_))
             if rid is None:
                 continue
             try:
@@ -555,6 +562,7 @@ class PoolLeader:
                 op = msg.get("op")
                 if op == "stop":
                     self._dq.put(None)
+                    self._sub_ex.shutdown(wait=True)
                     self._ex.shutdown(wait=True)
                     self._rq.put(None)
                     self._rthread.join(timeout=30)
@@ -590,7 +598,7 @@ class PoolLeader:
                     if die_after and self._gen_seen > die_after and (
                             die_rank is None or int(die_rank) == int(os.environ.get("RANK", "-1"))):
                         os._exit(17)   # fault injection (tests): this leader dies after N requests
-                    self._submit(msg["ids"], msg["prompts"], msg.get("params"))
+                    self._sub_ex.submit(self._submit, msg["ids"], msg["prompts"], msg.get("params"))
                 elif op in ("generate_ids", "submit_ids"):
                     self._dq.put(msg)
         finally:
@@ -611,8 +619,16 @@ class ReplicatedPool(PoolClient):
         self.inflight = [0] * len(replicas)
         self._lock = threading.Lock()
         self._ex = ThreadPoolExecutor(max_workers=len(replicas))
-        self._owner: Dict[int, int] = {}   # id(submitted handle) -> replica index (collect)
-        self._released: set = set()         # id(handle) already counted off its replica's load
+
+    def _state(self, h) -> list:
+        """[serving replica, released] of a handle this pool submitted, kept ON the handle (an
+        id()-keyed table would leak entries of never-collected handles and could hand a recycled
+        id a stale 'released' flag).  Keyed by this pool so nested replicated pools never mix."""
+        st = getattr(h, "rp", None)
+        if st is None:
+            st = {}
+            h.rp = st
+        return st.setdefault(id(self), [0, False])
 
     def _pick(self) -> int:
         with self._lock:
@@ -689,7 +705,8 @@ class ReplicatedPool(PoolClient):
                 from .base import ThreadSubmit
                 hs = ThreadSubmit.submit_batch(rep, hs_, overrides, notify=done_cb)
             for j, h in zip(idx, hs):
-                self._owner[id(h)] = k
+                with self._lock:
+                    self._state(h)[0] = k
                 out[j] = h
             for h in hs:   # finished already, or rejected up front (never notified): counted down now
                 if h.done.is_set():
@@ -699,9 +716,10 @@ class ReplicatedPool(PoolClient):
     def _release(self, h, k: int) -> None:
         """A submitted request stopped loading replica k (exactly once per handle)."""
         with self._lock:
-            if id(h) in self._released:
+            st = self._state(h)
+            if st[1]:
                 return
-            self._released.add(id(h))
+            st[1] = True
             self.inflight[k] -= 1
 
     def submit_failover(self, histories: Sequence[Any], notify=None) -> List[Any]:
@@ -711,10 +729,9 @@ class ReplicatedPool(PoolClient):
         out: List[Any] = [None] * len(handles)
         by: Dict[int, List[int]] = {}
         for j, h in enumerate(handles):
-            k = self._owner.pop(id(h), 0)
-            self._release(h, k)
             with self._lock:
-                self._released.discard(id(h))
+                k = self._state(h)[0]
+            self._release(h, k)   # idempotent: a later done callback does not count it again
             by.setdefault(k, []).append(j)
         for k, idx in by.items():
             rep = self.replicas[k]

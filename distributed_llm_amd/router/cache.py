@@ -145,8 +145,16 @@ def _host_vec(x) -> np.ndarray:
 class EmbeddingIndex:
     """Slot-indexed embedding table for vectorised / on-GPU semantic lookup.
 
-    ``device=None`` keeps a numpy table on the host; a torch device string keeps an HBM table
-    and uses the fused HIP scorer.
+    ``device=None`` keeps a numpy table on the host (vectorised numpy scoring).  A torch device
+    string keeps an HBM table [capacity, dim] f32 plus one context id per row, and:
+      * row writes are DEFERRED: ``put`` / ``remove`` only record (slot -> vector, context id);
+        ``flush`` applies every pending write in one ``ops.cache_write`` launch per 64 rows right
+        before the next scoring launch (no copy launch, norm reduction or host sync per insert);
+      * a lookup scores only rows of its context (``ops.cache_scan``: context ids read as 16-B
+        vectors, matching rows fetched and scored), and ``best_batch`` scores a whole routing
+        batch in one launch with one read-back.
+    ``dirty`` collects the context ids whose rows changed since the owner last cleared it (the
+    routing cache's batch prefetch uses it to know which prefetched results are still exact).
     """
 
     def __init__(self, dim: int = 384, capacity: int = 1024, device: Optional[str] = None):
@@ -162,6 +170,10 @@ class EmbeddingIndex:
         self._ctx_refs: Dict[int, int] = {}
         self._free_cids: List[int] = []
         self._slot_cid: Dict[int, int] = {}
+        self._pending: Dict[int, Tuple[Any, int]] = {}   # device mode: slot -> (vector | None, ctx id)
+        self.dirty: set = set()
+        self.track_dirty = False                          # on while a batch prefetch is outstanding
+        self.launches = {"write": 0, "scan": 0}           # device launches issued (bench / tests)
         self._alloc(capacity)
 
     def _alloc(self, capacity: int) -> None:
@@ -173,14 +185,16 @@ class EmbeddingIndex:
         else:
             import torch
             self.table = torch.zeros((capacity, self.dim), dtype=torch.float32, device=self.device)
-            self.norms = torch.zeros(capacity, dtype=torch.float32, device=self.device)
+            self.norms = None     # the GPU scorer computes row norms from the row it loads
             self.ctx = torch.full((capacity,), -1, dtype=torch.int32, device=self.device)
 
     def _grow(self) -> None:
+        self.flush()
         old_t, old_n, old_c, old_cap = self.table, self.norms, self.ctx, self.capacity
         self._alloc(old_cap * 2)
         self.table[:old_cap] = old_t
-        self.norms[:old_cap] = old_n
+        if old_n is not None:
+            self.norms[:old_cap] = old_n
         self.ctx[:old_cap] = old_c
 
     def ctx_id(self, key: str) -> int:
@@ -192,10 +206,15 @@ class EmbeddingIndex:
             self._ctx_refs[i] = 0
         return i
 
+    def cid_of(self, key: str) -> Optional[int]:
+        return self._ctx_ids.get(key)
+
     def _release(self, slot: int) -> None:
         cid = self._slot_cid.pop(slot, None)
         if cid is None:
             return
+        if self.track_dirty:
+            self.dirty.add(cid)
         self._ctx_refs[cid] -= 1
         if self._ctx_refs[cid] == 0:
             del self._ctx_refs[cid]
@@ -205,7 +224,7 @@ class EmbeddingIndex:
     def num_contexts(self) -> int:
         return len(self._ctx_ids)
 
-    def put(self, vec: np.ndarray, context_key: str, slot: int = -1) -> int:
+    def put(self, vec: Any, context_key: str, slot: int = -1) -> int:
         if slot < 0:
             if self._free:
                 slot = self._free.pop()
@@ -218,6 +237,8 @@ class EmbeddingIndex:
         cid = self.ctx_id(context_key)
         self._ctx_refs[cid] += 1
         self._slot_cid[slot] = cid
+        if self.track_dirty:
+            self.dirty.add(cid)
         if self.device is None:
             v = np.asarray(vec, dtype=np.float32).reshape(-1)
             self.table[slot] = v
@@ -225,23 +246,34 @@ class EmbeddingIndex:
             self.ctx[slot] = cid
         else:
             import torch
-            if isinstance(vec, torch.Tensor):   # device vector: async copies, no host sync
-                v = vec.to(self.device, torch.float32).reshape(-1)
-                self.table[slot].copy_(v)
-                self.norms[slot:slot + 1].copy_(torch.linalg.vector_norm(v).reshape(1))
+            if isinstance(vec, torch.Tensor):   # device vector: referenced until the next flush
+                v = vec.reshape(-1)
+                if v.device != self.table.device or v.dtype != torch.float32 or not v.is_contiguous():
+                    v = v.to(self.table.device, torch.float32).contiguous()
             else:
-                v = np.asarray(vec, dtype=np.float32).reshape(-1)
-                self.table[slot] = torch.from_numpy(v).to(self.device, non_blocking=True)
-                self.norms[slot] = float(np.linalg.norm(v))
-            self.ctx[slot] = cid
+                v = torch.from_numpy(np.asarray(vec, dtype=np.float32).reshape(-1).copy()).to(self.table.device)
+            self._pending[slot] = (v, cid)
         return slot
 
     def remove(self, slot: int) -> None:
         if slot < 0:
             return
-        self.ctx[slot] = -1
+        if self.device is None:
+            self.ctx[slot] = -1
+        else:
+            self._pending[slot] = (None, -1)
         self._release(slot)
         self._free.append(slot)
+
+    def flush(self) -> None:
+        """Apply the deferred device writes (one launch per 64 rows)."""
+        if not self._pending:
+            return
+        from .. import ops
+        writes = [(slot, v, cid) for slot, (v, cid) in self._pending.items()]
+        self._pending.clear()
+        ops.cache_write(writes, self.table, self.ctx)
+        self.launches["write"] += -(-len(writes) // ops.CACHE_WRITE_MAX)
 
     def clear(self) -> None:
         self._free.clear()
@@ -251,34 +283,58 @@ class EmbeddingIndex:
         self._ctx_refs.clear()
         self._free_cids.clear()
         self._slot_cid.clear()
-        self.ctx[:] = -1
+        self._pending.clear()
+        self.dirty.clear()
+        if self.device is None:
+            self.ctx[:] = -1
+        else:
+            self.ctx.fill_(-1)
+
+    def _best_host(self, q: Any, cid: int, threshold: float) -> Tuple[int, float]:
+        hi = self._next
+        qv = np.asarray(q, dtype=np.float32).reshape(-1)
+        nq = float(np.linalg.norm(qv))
+        if nq < 1e-9:
+            return -1, 0.0
+        mask = (self.ctx[:hi] == cid) & (self.norms[:hi] >= 1e-9)
+        if not mask.any():
+            return -1, 0.0
+        idx = np.nonzero(mask)[0]
+        sims = (self.table[idx] @ qv) / (self.norms[idx] * nq)
+        j = int(np.argmax(sims))
+        s = float(sims[j])
+        return (int(idx[j]), s) if s >= threshold else (-1, 0.0)
 
     def best(self, q: Any, context_key: str, threshold: float) -> Tuple[int, float]:
         """Best slot with cosine >= threshold among slots of ``context_key``; (-1, 0) if none."""
-        cid = self._ctx_ids.get(context_key)
-        if cid is None or self._next == 0:
-            return -1, 0.0
-        hi = self._next
+        return self.best_batch([q], [context_key], threshold)[0]
+
+    def best_batch(self, qs: List[Any], context_keys: List[str], threshold: float) -> List[Tuple[int, float]]:
+        """``best`` for a whole routing batch: on the GPU one scoring launch (per 128 queries) and
+        ONE read-back; queries whose context has no rows are answered on the host."""
+        out: List[Tuple[int, float]] = [(-1, 0.0)] * len(qs)
+        todo = [(i, self._ctx_ids.get(ck)) for i, ck in enumerate(context_keys)]
+        todo = [(i, cid) for i, cid in todo if cid is not None and qs[i] is not None]
+        if not todo or self._next == 0:
+            return out
         if self.device is None:
-            qv = np.asarray(q, dtype=np.float32).reshape(-1)
-            nq = float(np.linalg.norm(qv))
-            if nq < 1e-9:
-                return -1, 0.0
-            mask = (self.ctx[:hi] == cid) & (self.norms[:hi] >= 1e-9)
-            if not mask.any():
-                return -1, 0.0
-            idx = np.nonzero(mask)[0]
-            sims = (self.table[idx] @ qv) / (self.norms[idx] * nq)
-            j = int(np.argmax(sims))
-            s = float(sims[j])
-            return (int(idx[j]), s) if s >= threshold else (-1, 0.0)
+            for i, cid in todo:
+                out[i] = self._best_host(qs[i], cid, threshold)
+            return out
         from .. import ops
         import torch
-        qt = q if isinstance(q, torch.Tensor) else torch.from_numpy(np.asarray(q, np.float32))
-        qt = qt.to(self.device, torch.float32).reshape(-1)
-        slot, sim = ops.masked_cosine_argmax(qt, self.table[:hi], self.norms[:hi], self.ctx[:hi],
-                                             cid, threshold)
-        return slot, sim
+        self.flush()
+        qv = []
+        for i, _ in todo:
+            q = qs[i]
+            if not isinstance(q, torch.Tensor):
+                q = torch.from_numpy(np.asarray(q, dtype=np.float32).reshape(-1).copy())
+            qv.append(q.reshape(-1).to(self.table.device, torch.float32))
+        res = ops.cache_scan(qv, [cid for _, cid in todo], self.table, self.ctx, self._next, threshold)
+        self.launches["scan"] += -(-len(qv) // ops.CACHE_SCAN_MAX_Q)
+        for (i, _), r in zip(todo, res):
+            out[i] = r
+        return out
 
 
 class QueryCache:
@@ -307,6 +363,10 @@ class QueryCache:
         self._attempts = 0
         self._evictions = 0
         self._hybrid_fallbacks = 0
+        # batch prefetch (``prefetch``): (query, context_key) -> (slot, sim) scored together
+        self._pre: Dict[Tuple[str, str], Tuple[int, float]] = {}
+        self.prefetch_used = 0       # semantic lookups answered from a batch prefetch
+        self.prefetch_fallbacks = 0  # ... re-scored on their own (their context changed meanwhile)
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -327,9 +387,12 @@ class QueryCache:
         if emb is None:
             return
         if hasattr(emb, "detach") and self._index.device is not None:
-            # device embedding into the HBM index: stays on the GPU (no host round trip per insert);
-            # the entry keeps a private device copy, converted to host only by save / to_dict
-            arr = emb.detach().to(self._index.device, dtype=self._index.table.dtype).reshape(-1).clone()
+            # device embedding into the HBM index: stays on the GPU (no host round trip per insert).
+            # The encoder's rows are never written again (each forward allocates its output), so the
+            # entry keeps a reference, not a copy; converted to host only by save / to_dict
+            arr = emb.detach().reshape(-1)
+            if arr.device != self._index.table.device or arr.dtype != self._index.table.dtype:
+                arr = arr.to(self._index.table.device, dtype=self._index.table.dtype)
         else:
             arr = np.asarray(emb.detach().float().cpu().numpy() if hasattr(emb, "detach") else emb,
                              dtype=np.float32).reshape(-1).copy()
@@ -385,6 +448,9 @@ class QueryCache:
         self._evict_expired()
         h = self._make_hash(query, context_key)
         with self._lock:
+            pre = self._pre.pop((query, context_key), None) if self._pre else None
+            if not self._pre:   # the batch is consumed: stop tracking changed contexts
+                self._index.track_dirty = False
             cand = self._store.get(h)
             if cand is not None and cand.context_key == context_key:
                 if self._is_valid(cand):
@@ -395,7 +461,14 @@ class QueryCache:
                 self._delete_entry(h)
             if not self.use_semantic or q_emb is None:
                 return None
-            slot, _sim = self._index.best(q_emb, context_key, self.similarity_threshold)
+            cid = self._index.cid_of(context_key)
+            if pre is not None and (cid is None or cid not in self._index.dirty):
+                slot = pre[0]           # no row of this context changed since the batch was scored
+                self.prefetch_used += 1
+            else:
+                if pre is not None:
+                    self.prefetch_fallbacks += 1
+                slot, _sim = self._index.best(q_emb, context_key, self.similarity_threshold)
             if slot < 0:
                 return None
             bh = self._slot_to_hash.get(slot)
@@ -406,6 +479,30 @@ class QueryCache:
             self._store.move_to_end(bh)
             self._hits += 1
             return self._result(cand)
+
+    def prefetch(self, items: List[Tuple[str, str, Any]]) -> None:
+        """Score the semantic lookups of a whole routing batch at once: ``items`` = (query,
+        context_key, q_emb) in the order the batch will be routed.  On an HBM index this is one
+        launch and one read-back for the batch instead of one of each per lookup.  ``lookup``
+        then uses a query's prefetched result only while no row of its context has changed since
+        (an insert, replacement, TTL or LRU eviction in between marks the context dirty and that
+        lookup is re-scored on its own), so routing decisions are exactly those of per-query
+        lookups."""
+        if not self.use_semantic:
+            return
+        self._evict_expired()
+        with self._lock:
+            self._pre = {}
+            self._index.dirty.clear()
+            self._index.track_dirty = False
+            items = [(q, ck, e) for q, ck, e in items if e is not None]
+            if not items:
+                return
+            self._index.track_dirty = True
+            res = self._index.best_batch([e for _, _, e in items], [ck for _, ck, _ in items],
+                                         self.similarity_threshold)
+            for (q, ck, _), r in zip(items, res):
+                self._pre[(q, ck)] = r
 
     def insert(self, query: str, context_key: str, device: str, confidence: float = 1.0,
                method: str = "unknown", q_emb: Any = None, response_time: Optional[float] = None) -> None:
@@ -562,6 +659,7 @@ class QueryCache:
             self._slot_to_hash.clear()
             self._index.clear()
             self._expiry.clear()
+            self._pre = {}
             self._hits = self._attempts = self._evictions = self._hybrid_fallbacks = 0
 
     def __len__(self) -> int:

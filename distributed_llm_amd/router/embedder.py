@@ -111,6 +111,10 @@ class MiniLMEmbedder(Embedder):
         """Return a [n, dim] float32 device tensor (stays in HBM for the GPU scorer)."""
         return self.model.encode(list(texts), max_len=self.max_len)
 
+    def encode_rows(self, texts: Sequence[str]):
+        """One [dim] f32 device row per text (no stacking launch; memo rows are shared)."""
+        return self.model.encode_rows(list(texts), max_len=self.max_len)
+
     def encode(self, texts: Sequence[str]) -> np.ndarray:
         if not len(texts):
             return np.zeros((0, self.dim), dtype=np.float32)

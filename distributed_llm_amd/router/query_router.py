@@ -66,10 +66,22 @@ class QueryRouter:
         return self.strategy_name
 
     def _embed(self, query: str):
-        enc_t = getattr(self.cache_embedder, "encode_tensor", None)
-        if enc_t is not None and self.config.get("cache_index_device"):
-            return enc_t([query])[0]
+        rows = getattr(self.cache_embedder, "encode_rows", None)
+        if rows is not None and self.config.get("cache_index_device"):
+            return rows([query])[0]
         return self.cache_embedder.encode([query])[0]
+
+    def prefetch_cache(self, queries: List[str], context_keys: List[Optional[str]]) -> None:
+        """Score a routing batch's semantic-cache lookups together (QueryCache.prefetch: one GPU
+        launch + one read-back on an HBM index); ``route_query`` then consumes them in order."""
+        if not (self.cache_enabled and self.cache_embedder is not None and queries):
+            return
+        try:
+            items = [(q, ck or "default", self._embed(q)) for q, ck in zip(queries, context_keys)]
+        except Exception as exc:  # noqa: BLE001 - route_query retries per query and logs
+            logger.debug("cache prefetch skipped: %s", exc)
+            return
+        self._cache.prefetch(items)
 
     def prefetch_scores(self, queries: List[str]) -> None:
         """Batch the semantic centroid scoring of a routing batch (SemanticRouter.prefetch), for

@@ -130,3 +130,46 @@ def test_thread_submit_reports_a_raising_pool_as_errors():
         assert h.done.wait(10)
     assert all("boom" in h.payload()["error"] for h in hs)
     assert isinstance(Boom(SMALL), ThreadSubmit) and threading.active_count() >= 1
+
+
+def test_replicated_pool_load_returns_to_zero_without_collect():
+    """handles that are never collected must not leak bookkeeping or skew the load."""
+    reps = [EchoPool(SMALL, tokens_per_reply=2), EchoPool(SMALL, tokens_per_reply=2)]
+    rp = ReplicatedPool(SMALL, reps)
+    for rnd in range(20):
+        q = queue.SimpleQueue()
+        hs = rp.submit_batch([_conv(f"r{rnd} q{i}") for i in range(8)], notify=q.put)
+        for _ in hs:
+            q.get(timeout=10)
+        del hs
+    assert rp.inflight == [0, 0]
+    assert not any(k.startswith("_owner") or k.startswith("_released") for k in vars(rp))
+
+
+def test_replicated_pool_collect_before_done_counts_once():
+    reps = [SlowEcho(SMALL, marker="slow", delay_s=0.5), SlowEcho(SMALL, marker="slow", delay_s=0.5)]
+    rp = ReplicatedPool(SMALL, reps)
+    q = queue.SimpleQueue()
+    hs = rp.submit_batch([_conv("slow a"), _conv("slow b")], notify=q.put)
+    rp.collect(hs)             # not done yet: released now ...
+    assert rp.inflight == [0, 0]
+    for _ in hs:               # ... and the later completion callbacks do not count again
+        q.get(timeout=10)
+    assert rp.inflight == [0, 0]
+
+
+def test_both_tiers_down_reports_like_route_query():
+    """an up-front failover whose target fails too reports the primary's error and no
+    failover, as the blocking route_query does."""
+    class Dead(FaultInjectingPool):
+        alive = False
+    pools = {SMALL: FaultInjectingPool(EchoPool(SMALL), mode="error"), LARGE: Dead(EchoPool(LARGE), mode="error")}
+    r = Router("heuristic", config=dict(BENCHMARK_CFG), pools=pools)
+    q = queue.SimpleQueue()
+    t = r.dispatch_batch([_conv("Write a Python function for knapsack with dynamic programming")], notify=q.put)[0]
+    assert t["device"] == SMALL and t["failover_from"] == LARGE
+    if t.get("handle") is not None:
+        q.get(timeout=10)
+    payload, _, dev = r.finish_ticket(t, notify=q.put)
+    assert dev == LARGE and "failover_from" not in payload and not payload["ok"]
+    assert "unavailable" in str(payload.get("response", "")) + str(payload.get("raw", ""))

@@ -76,3 +76,72 @@ def test_batched_semantic_scores_match_per_query(monkeypatch):
         return out
 
     assert run(True) == run(False)
+
+
+def test_cache_scan_matches_fp32_reference():
+    """The batched scorer (one launch per 128 queries) against the fp32 torch reference: several
+    queries per context, more than 128 queries, a row count that is not a multiple of 4, zero rows,
+    removed rows (ctx -1) and a context with no rows."""
+    from distributed_llm_amd import ops
+    from distributed_llm_amd.ops import reference as ref
+    g = torch.Generator(device="cpu").manual_seed(3)
+    n, d = 4099, 384
+    table = torch.randn(n, d, generator=g).cuda()
+    ctx = torch.randint(0, 37, (n,), generator=g, dtype=torch.int32).cuda()
+    table[5] = 0.0
+    ctx[7:20] = -1
+    base = [int(x) for x in torch.randint(0, n, (150,), generator=g)]
+    qs = [(table[i] + 0.3 * torch.randn(d, generator=g).cuda()).contiguous() for i in base]
+    qs[3] = torch.zeros(d, device="cuda")
+    cids = [int(ctx[i]) if int(ctx[i]) >= 0 else 99 for i in base]
+    cids[10] = 1000   # no such context
+    got = ops.cache_scan(qs, cids, table, ctx, n, 0.7)
+    want = ref.cache_scan(qs, cids, table, ctx, n, 0.7)
+    hits = 0
+    for (gs, gv), (ws, wv) in zip(got, want):
+        assert gs == ws, (gs, ws, gv, wv)
+        assert abs(gv - wv) < 1e-4
+        hits += gs >= 0
+    assert hits > 100
+    # only the first rows: n_rows bounds the scan
+    got = ops.cache_scan(qs[:20], cids[:20], table, ctx, 1000, 0.7)
+    assert got == [(s, v) if s < 1000 else (-1, 0.0) for s, v in got]
+    assert [s for s, _ in got] == [s for s, _ in ref.cache_scan(qs[:20], cids[:20], table, ctx, 1000, 0.7)]
+
+
+def test_cache_write_applies_rows_and_removals():
+    from distributed_llm_amd import ops
+    table = torch.zeros(300, 64, device="cuda")
+    ctx = torch.full((300,), -1, dtype=torch.int32, device="cuda")
+    vecs = [torch.randn(64, device="cuda") for _ in range(100)]
+    ops.cache_write([(i * 3, v, i % 5) for i, v in enumerate(vecs)], table, ctx)   # two launches
+    for i, v in enumerate(vecs):
+        assert torch.equal(table[i * 3], v) and int(ctx[i * 3]) == i % 5
+    ops.cache_write([(0, None, -1), (3, None, 7)], table, ctx)
+    assert int(ctx[0]) == -1 and int(ctx[3]) == 7 and torch.equal(table[3], vecs[1])
+
+
+def test_device_prefetch_equals_per_query_and_batches_launches():
+    """The HBM index through QueryCache.prefetch routes exactly like per-query lookups (the CPU
+    version of this workload: tests/test_cache_prefetch.py) and issues one scoring launch per
+    batch plus one write launch per 64 inserts, instead of a launch (and a read-back) per lookup."""
+    import importlib.util
+    import pathlib
+    spec = importlib.util.spec_from_file_location(
+        "tcp", pathlib.Path(__file__).with_name("test_cache_prefetch.py"))
+    tcp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tcp)
+    batches = tcp._workload(seed=1)
+    to_dev = lambda v: torch.from_numpy(v).cuda()
+    a = QueryCache(max_size=40, ttl_seconds=3600, similarity_threshold=0.9, dim=32, index_device="cuda")
+    b = QueryCache(max_size=40, ttl_seconds=3600, similarity_threshold=0.9, dim=32, index_device="cuda")
+    h = QueryCache(max_size=40, ttl_seconds=3600, similarity_threshold=0.9, dim=32)
+    ta = tcp._run(a, batches, True, to_dev)
+    tb = tcp._run(b, batches, False, to_dev)
+    th = tcp._run(h, batches, False)
+    assert ta == tb == th
+    la = a._index.launches
+    assert a.prefetch_used > 100
+    # per batch: one prefetch scan, plus one per fallback lookup; writes batched per flush
+    assert la["scan"] <= len(batches) + a.prefetch_fallbacks + 1
+    assert la["scan"] < b._index.launches["scan"]
