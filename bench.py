@@ -21,7 +21,10 @@ so the decode batch stays full instead of draining to the large-tier answers at 
 turn; a *step* is then ``--convs`` completed turns, and only turns completed inside the timed
 window are counted.  ``--pipeline 0`` runs the turn-synchronous steps of rounds 1-3.
 
-N > 1 GPUs default to BASELINE's multi-GPU configurations (``--topology pools``, parallel.cluster):
+N > 1 GPUs run N config-2 replicas by default (``--topology replicated``: one engine and one routing
+driver per GPU, each with its own --convs conversations; per-GPU work is fixed, so values at N = 1, 2, 4, 8 form a weak-scaling
+curve of ONE workload).  BASELINE's multi-GPU configurations are selected with ``--baseline-config``
+(or ``--topology pools``, parallel.cluster):
 2 GPUs config 3 (Llama-3.2-1B small on GPU 0 | Llama-3-8B large on GPU 1), 4 GPUs config 4's models
 at half size (Llama-3-8B x2 | Llama-3-70B TP=2), 8 GPUs config 4 (Llama-3-8B x4 | Llama-3-70B
 TP=4, perf router), and ``--baseline-config 5`` (``--topology colocated``) config 5 as written:
@@ -31,9 +34,8 @@ there: with the event driver serving remote pools non-blockingly, 128 per GPU ga
 routed tok/s at 64 on the 2-rank config-3 rehearsal, while an 8B-tier GPU's 64 GB KV pool still
 holds 128 conversations at ~3K tokens of history each); requests reach remote pools over the gloo control / data planes, RCCL carries the large
 pool's tensor-parallel collectives.  The JSON line names the config (``baseline_config``) and the
-exact GPU layout (``layout``); values at different N are different model configurations, so they
-are not a scaling curve of one workload (``scaling_note``).  ``--topology replicated`` keeps the
-config-2 replicas at any N (N independent engines: weak scaling of one workload).
+exact GPU layout (``layout``); values of different configs are different model configurations,
+not a scaling curve (``scaling_note``).
 
 ``value`` = total generated tokens over all ranks / max rank wall time of the timed steps.
 """
@@ -50,6 +52,8 @@ import time
 
 from distributed_llm_amd.utils.faults import diag
 
+_T_PROC0 = time.perf_counter()   # process start (imports included) for the JSON's startup_s
+
 BASELINE_TOK_S = 10.57        # best published routed throughput (Jetson Nano+Orin)
 BASELINE_S_PER_QUERY = 39.6   # best published mean routed e2e latency per query
 
@@ -61,11 +65,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--topology", default=None, choices=["replicated", "pools", "colocated", "tiers"],
                     help="replicated: both tiers on one engine per GPU (BASELINE config 2; the 1-GPU default); "
-                         "pools: tiers on disjoint GPU subsets (configs 3-4; the N>1 default); colocated: large "
+                         "pools: tiers on disjoint GPU subsets (configs 3-4); colocated: large "
                          "TP group over every GPU + a small replica on each GPU (config 5); tiers: --small-model "
                          "and --large-model as two engines on every GPU")
     ap.add_argument("--baseline-config", type=int, default=None, choices=[2, 3, 4, 5],
-                    help="BASELINE.json config to run (default: 2 on 1 GPU, 3 on 2 GPUs, 4 on 4-8 GPUs); "
+                    help="BASELINE.json config to run (default 2 at every N; 3 needs 2 GPUs, 4 needs 4-8); "
                          "sets topology and models")
     ap.add_argument("--model", default="tinyllama-1.1b")
     ap.add_argument("--small-model", default=None, help="pools/tiers small tier (default per baseline config)")
@@ -121,7 +125,9 @@ def resolve_config(a, world: int) -> int:
     tagged on the JSON line."""
     cfg = a.baseline_config
     if a.topology is None and cfg is None:
-        a.topology = "pools" if world > 1 else "replicated"
+        # every N defaults to config 2 (one engine per GPU): the driver's N = 1 .. 8 runs are then
+        # one workload's weak-scaling curve; the multi-GPU configs 3-5 are --baseline-config runs
+        a.topology = "replicated"
     if cfg is None:
         if a.topology == "colocated":
             cfg = 5
@@ -554,6 +560,8 @@ def main() -> int:
                   "large": {"model": lg, "replicas": topo.replicas[LARGE], "tp": tp},
                   "colocated": topology == "colocated"}
 
+    t_ready = time.perf_counter()   # engines built, weights initialised, GEMMs tuned, graphs captured
+
     def sync():
         if cluster is not None:
             cluster.sync()
@@ -580,6 +588,7 @@ def main() -> int:
     elapsed = 0.0
     st0 = st1 = None
     e1 = None
+    t_window0 = None
     if cluster is not None and rank != 0:
         if meter:
             e0 = meter.mark()
@@ -624,6 +633,7 @@ def main() -> int:
                     busy.start()
                 cpu0 = _thread_cpu() if diag("cpu") else None
                 t0 = time.perf_counter()
+                t_window0 = t0
                 convs.records = records
                 start_count = convs.completed   # (turns completed during the opening barrier are warmup)
             convs.wait_turns(start_count + a.steps * n_convs)
@@ -648,6 +658,7 @@ def main() -> int:
             if busy is not None:
                 busy.start()
             t0 = time.perf_counter()
+            t_window0 = t0
             dump = [] if a.dump_responses else None
             for _ in range(a.steps):
                 convs.step(router, records, dump)
@@ -681,8 +692,10 @@ def main() -> int:
         import datetime
         store = dist.distributed_c10d._get_default_store()
         store.set(f"dllm_bench/{rank}", json.dumps({"tokens": float(tokens), "elapsed": elapsed, "energy": energy_j,
-                                                    "lats": lats}))
+                                                    "lats": lats, "init_s": t_ready - _T_PROC0,
+                                                    "startup_s": (t_window0 or t_ready) - _T_PROC0}))
         tokens_all, elapsed_max, e_sum, e_bad = 0.0, 0.0, 0.0, False
+        init_max, startup_max = t_ready - _T_PROC0, (t_window0 or t_ready) - _T_PROC0
         if rank == 0:
             got = []
             for r in range(world):
@@ -696,9 +709,12 @@ def main() -> int:
             e_bad = any(g["energy"] < 0 for g in got) or bool(dead_ranks)
             energy_j = -1.0 if e_bad else sum(g["energy"] for g in got)
             lats = sorted(x for g in got for x in g["lats"])
+            init_max = max([init_max] + [g.get("init_s", 0.0) for g in got])
+            startup_max = max([startup_max] + [g.get("startup_s", 0.0) for g in got])
             degraded = degraded or bool(dead_ranks)
     else:
         tokens_all, elapsed_max = float(tokens), elapsed
+        init_max, startup_max = t_ready - _T_PROC0, (t_window0 or t_ready) - _T_PROC0
     if rank == 0:
         value = tokens_all / max(elapsed_max, 1e-9)
         rates = sorted(r["tok"] * 1000.0 / r["lat"] for r in records if r["lat"] > 0 and r["tok"] > 0)
@@ -716,7 +732,7 @@ def main() -> int:
             "warmup": a.warmup,
             "ms_per_step": round(elapsed_max * 1000.0 / a.steps, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if topology in ("replicated", "tiers") else "config",
             "vs_baseline": round(value / BASELINE_TOK_S, 2),
             # vs_baseline divides this whole-job aggregate (all conversations, all GPUs) by the
             # reference's single-stream 10.57 tok/s; the like-for-like ratio is per stream:
@@ -726,9 +742,20 @@ def main() -> int:
             "per_stream_vs_baseline": round(per_stream / BASELINE_TOK_S, 2) if per_stream else None,
             "baseline_config": baseline_config,
             "layout": layout,
-            "scaling_note": ("N = 1 runs BASELINE config 2 and N > 1 the multi-GPU configs 3-5 by default: values "
-                             "at different N are different models and layouts, not one workload's scaling curve "
-                             "(--topology replicated: N config-2 replicas)"),
+            "per_gpu_tok_s": round(value / max(1, world), 2),
+            # process start -> engines ready (weights init, GEMM autotune, graph capture); -> timed window
+            # (plus the warmup turns); max over ranks
+            "init_s": round(init_max, 1),
+            "startup_s": round(startup_max, 1),
+            "scaling_note": ("every N runs BASELINE config 2 by default (one engine + routing driver per GPU, "
+                             "--convs conversations each): per-GPU work is fixed, so values at N = 1..8 are one "
+                             "workload's weak-scaling curve; BASELINE's multi-GPU configs run with "
+                             "--baseline-config 3 (2 GPUs), 4 (4-8 GPUs), 5 (co-located Mixtral TP=N) and are "
+                             "different models and layouts, not points of that curve"
+                             if topology == "replicated" else
+                             "BASELINE config %d (%s): a different model pair and layout than config 2, not a "
+                             "point of the config-2 weak-scaling curve (the default at every N)"
+                             % (baseline_config, topology)),
             "dtype": "bf16",
             "data": "synthetic: reference query sets replayed as growing conversations; random-init weights",
             "config": {"model": model_desc, "global_batch": a.convs * world,

@@ -12,10 +12,14 @@ Also the whole host path (EmbeddingIndex.best_batch: pybind descriptor, launch, 
 Usage: python scripts/cache_scorer_bench.py [--max-rows 1e8] > gpurun_out/cache_scorer.jsonl
 """
 import argparse
+import os
+import sys
 import json
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_llm_amd import ops
 from distributed_llm_amd.router.cache import EmbeddingIndex

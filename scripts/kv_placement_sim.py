@@ -12,8 +12,12 @@ history fills it (LRU eviction active), as on the GPU.
 Usage: python scripts/kv_placement_sim.py [--convs 128] [--steps 6000]
 """
 import argparse
+import os
+import sys
 import json
 import random
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_llm_amd.engine import _runtime
 

@@ -19,11 +19,12 @@ def _port():
         return s.getsockname()[1]
 
 
-# N > 1 defaults to BASELINE's multi-GPU configs (3 at 2 ranks, 4 at 4-8); replicas by flag;
-# config 5 = the large TP group over every rank with a small replica co-located on each
-@pytest.mark.parametrize("n,extra,par,cfg", [(1, [], "dp1", 2), (2, [], "pools:small1xtp1+large1xtp1", 3),
-                                             (2, ["--topology", "replicated"], "dp2", 2),
-                                             (4, [], "pools:small2xtp1+large1xtp2", 4),
+# every N defaults to config-2 replicas (a weak-scaling curve of one workload); BASELINE's
+# multi-GPU configs by flag (3 at 2 ranks, 4 at 4-8); config 5 = the large TP group over every
+# rank with a small replica co-located on each
+@pytest.mark.parametrize("n,extra,par,cfg", [(1, [], "dp1", 2), (2, [], "dp2", 2),
+                                             (2, ["--baseline-config", "3"], "pools:small1xtp1+large1xtp1", 3),
+                                             (4, ["--topology", "pools"], "pools:small2xtp1+large1xtp2", 4),
                                              (2, ["--baseline-config", "5"], "colocated:small2xtp1+large1xtp2", 5),
                                              (1, ["--topology", "tiers"], "dp1-colocated", 2)])
 def test_bench_json_line(n, extra, par, cfg):
@@ -42,7 +43,10 @@ def test_bench_json_line(n, extra, par, cfg):
     out = json.loads(lines[0])
     assert KEYS <= set(out)
     assert out["n_gpus"] == n and out["steps"] == 1 and out["warmup"] == 1
-    assert out["value"] > 0 and out["higher_is_better"] is True and out["scaling"] == "weak"
+    assert out["value"] > 0 and out["higher_is_better"] is True
+    assert out["scaling"] == ("weak" if cfg == 2 else "config")
+    assert out["per_gpu_tok_s"] * n == pytest.approx(out["value"], rel=1e-3)
+    assert 0 < out["init_s"] <= out["startup_s"]
     assert out["config"]["parallelism"].startswith(par)
     if out["config"]["turn_pipelining"]:
         # pipelined (the 1-GPU default): the window counts the turns completed inside it
@@ -71,7 +75,7 @@ def test_bench_survives_pool_leader_death():
                    MASTER_PORT=str(port), DLLM_EMBEDDER="hash", OMP_NUM_THREADS="1", DLLM_FAULT="die_rank=2,die_after=1")
         procs.append(subprocess.Popen([sys.executable, "bench.py", "--cpu", "--gpus", str(world), "--steps", "3",
                                        "--warmup", "1", "--convs", "3", "--small-new", "4", "--large-new", "6",
-                                       "--strategy", "hybrid"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                       "--strategy", "hybrid", "--topology", "pools"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.DEVNULL, text=True))
     outs = [p.communicate(timeout=300)[0] for p in procs]
     assert [p.returncode for p in procs] == [0, 0, 17, 0]
