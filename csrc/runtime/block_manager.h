@@ -51,6 +51,7 @@ struct Block {
   uint32_t gen = 0;         // bumped every time the block is (re)allocated by fresh()
   std::list<int>::iterator lru_it;
   bool in_lru = false;
+  uint64_t rel = 0;  // release tick when it entered the LRU (BlockManager::cold)
 };
 
 struct Seq {
@@ -341,6 +342,7 @@ class BlockManager {
   // deletion: an entry is valid only if its flag / count still says free.
   static constexpr int kSeg = 64;
   static constexpr int kMaxHeld = 63, kMinStretch = 2;   // pop_roomy_segment candidates
+  static constexpr uint64_t kColdFrac = 16;   // cold(): the oldest 1 / kColdFrac of the LRU's release span
   int seg_size(int sg) const { return std::min(kSeg, (int)blocks_.size() - sg * kSeg); }
 
   void init_free() {
@@ -425,10 +427,11 @@ class BlockManager {
         // longest run of non-held blocks in the segment
         const int lo = sg * kSeg, hi = lo + seg_size(sg);
         int best = -1, best_len = 0;
+        auto usable = [&](int x) { return free_flag_[x] || (blocks_[x].in_lru && cold(x)); };
         for (int i = lo; i < hi;) {
-          if (blocks_[i].ref > 0) { ++i; continue; }
+          if (!usable(i)) { ++i; continue; }
           int j = i;
-          while (j < hi && blocks_[j].ref == 0) ++j;
+          while (j < hi && usable(j)) ++j;
           if (j - i > best_len) { best_len = j - i; best = i; }
           i = j;
         }
@@ -459,6 +462,16 @@ class BlockManager {
     held_stacks_[h].swap(v);
   }
 
+  // An LRU block is COLD once at least half an LRU's worth of releases happened after it: a
+  // placement rule may then evict it out of LRU order.  Hot cached blocks (a conversation between
+  // two turns holds none of its history for a moment: all of it sits in the LRU) are left to the
+  // LRU order, which keeps them until they are the oldest (profiles/r6_kv_runs.md).
+  bool cold(int b) const {
+    if (lru_.empty()) return false;
+    const uint64_t oldest = blocks_[lru_.back()].rel;
+    return blocks_[b].rel - oldest <= (tick_ - oldest) / kColdFrac;
+  }
+
   // take block b out of the LRU for new content (its hash, if any, is unregistered)
   void evict(int b) {
     Block& old = blocks_[b];
@@ -487,7 +500,10 @@ class BlockManager {
           b = prefer;
           take_free(b);
           ++contig_;
-        } else if (blocks_[prefer].ref == 0 && blocks_[prefer].in_lru) {
+        } else if (blocks_[prefer].ref == 0 && blocks_[prefer].in_lru &&
+                   (blocks_[prefer].parent == prefer - 1 || cold(prefer))) {
+          // the sequence's own previous-turn continuation (its chain parent is the block before
+          // it: a stale decode block whose tokens did not re-tokenise the same), or a cold block
           b = prefer;
           evict(b);
           ++contig_;
@@ -519,6 +535,7 @@ class BlockManager {
       lru_.push_front(b);
       blk.lru_it = lru_.begin();
       blk.in_lru = true;
+      blk.rel = ++tick_;
     } else {
       push_free(b);
     }
@@ -534,6 +551,7 @@ class BlockManager {
   std::vector<int> seg_free_;      // free blocks per segment of kSeg
   std::vector<int> seg_stack_;     // segments that were wholly free when pushed (lazy)
   long long contig_ = 0, seg_allocs_ = 0, fresh_allocs_ = 0, inplace_ = 0, idle_allocs_ = 0;
+  uint64_t tick_ = 0;              // LRU releases so far (Block::rel)
   std::vector<int> held_;          // blocks with ref > 0 per segment
   std::vector<std::vector<int>> held_stacks_;  // segments by held count (lazy; see pop_roomy_segment)
   std::list<int> lru_;  // front = most recently released

@@ -22,13 +22,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llm_amd.engine import _runtime
 
 
-def simulate(convs=96, steps=5000, pool_blocks=None, seed=0, retok_same=0.3, contiguous=True, bs=16, ctx_cap=7000):
+def simulate(convs=96, steps=5000, pool_blocks=None, seed=0, retok_same=0.3, contiguous=True, bs=16, ctx_cap=7000,
+             gap=(0, 0)):
     rng = random.Random(seed)
     pool = pool_blocks or convs * 360
     bm = _runtime.BlockManager(pool, bs, True, contiguous)
     hist = [[rng.randrange(32000) for _ in range(rng.randrange(20, 80))] for _ in range(convs)]
     active = {}
+    waiting = {}                 # conversation -> step at which its next turn is dispatched
     nid = 0
+    step = 0
 
     def start(c):
         nonlocal nid
@@ -46,7 +49,7 @@ def simulate(convs=96, steps=5000, pool_blocks=None, seed=0, retok_same=0.3, con
     for c in range(convs):
         start(c)
     st0 = bm.stats()
-    for _ in range(steps):
+    for step in range(steps):
         cs = list(active)
         toks = [rng.randrange(32000) for _ in cs]
         slots = bm.commit_append([active[c]["id"] for c in cs], toks, [1] * len(cs))
@@ -62,10 +65,13 @@ def simulate(convs=96, steps=5000, pool_blocks=None, seed=0, retok_same=0.3, con
                 gen = a["gen"] if rng.random() < retok_same else [rng.randrange(32000) for _ in a["gen"]]
                 hist[c] = a["prompt"] + gen
                 del active[c]
-                start(c)
-        for c in range(convs):             # re-admit any that could not allocate
-            if c not in active:
-                start(c)
+                # the driver dispatches the next turn after a routing / admission gap, during which
+                # the conversation's blocks sit in the LRU (the bench: admission every 16 steps)
+                waiting[c] = step + rng.randint(*gap)
+        for c in range(convs):             # dispatch due turns; re-admit any that could not allocate
+            if c not in active and waiting.get(c, -1) <= step:
+                if start(c):
+                    waiting.pop(c, None)
     st1 = bm.stats()
     d = {k: st1.get(k, 0) - st0.get(k, 0) for k in ("contiguous_allocs", "segment_allocs", "fresh_allocs",
                                                     "prefix_hit_tokens", "prompt_tokens", "inplace_evictions",
