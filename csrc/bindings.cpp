@@ -40,6 +40,9 @@ int dllm_sample_split(const void*, long, int, int, int, const float*, const floa
                       long, int*, int*, hipStream_t);
 int dllm_sample_split_maxp();
 int dllm_sample_split_kmax();
+int dllm_skinny_epi(const void*, long, const void*, int, void*, long, int, int, int, int, int, int, float*, int*, void*,
+                    long, float*, long, const float*, int, long, float, float, const int*, const float*, const int*,
+                    void*, void*, void*, int, int, int, hipStream_t);
 int dllm_skinny_gemm(const void*, long, const void*, void*, long, int, int, int, int, int, int, float*, int*,
                      hipStream_t);
 int dllm_moe_max_tiles(int, int);
@@ -619,6 +622,101 @@ void skinny_gemm(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t ntw,
         part.data_ptr<float>(), counters.data_ptr<int>(), stream()),
      "skinny_gemm");
 }
+// Small-batch (M <= 16) MFMA GEMM with a fused decoder epilogue (csrc/kernels/skinny_gemm.hip
+// skinny_epi_kernel): epi 0 plain (y), 1 residual add (res in place + per-tile row sums -> ssq_out),
+// 2 QKV (RoPE, q_out, paged K / V^T), 3 SwiGLU (y = act [M, N/2]).  w: [N, K] or the panel copy
+// [K/64, N, 64].  Returns the row-sum slots written (RESADD) or 0.
+int64_t skinny_epi(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int64_t ntw, int64_t splits,
+                   int64_t epi, torch::Tensor part, torch::Tensor counters, c10::optional<torch::Tensor> res,
+                   c10::optional<torch::Tensor> ssq_out, c10::optional<torch::Tensor> ssq_in, int64_t ssq_n,
+                   double scale, double eps, c10::optional<torch::Tensor> pos, c10::optional<torch::Tensor> cos_sin,
+                   c10::optional<torch::Tensor> slots, c10::optional<torch::Tensor> q_out,
+                   c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc, int64_t nq, int64_t nkv, int64_t d) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_f32(part, "part");
+  check_i32(counters, "counters");
+  const bool panel = w.dim() == 3;
+  TORCH_CHECK(((w.dim() == 2) || (panel && w.size(2) == 64)) && w.is_contiguous(), "w: [N, K] or [K / 64, N, 64]");
+  const int M = x.size(0), N = panel ? w.size(1) : w.size(0), K = panel ? w.size(0) * 64 : w.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) == K, "x [M, K], 16-B rows");
+  TORCH_CHECK(M >= 1 && M <= 16 && K % 64 == 0, "M in [1, 16], K % 64 == 0");
+  TORCH_CHECK(ntw == 1 || ntw == 2, "ntw 1 or 2");
+  TORCH_CHECK(epi >= 0 && epi <= 3 && (epi < 2 || ntw == 2), "epi 0-3; QKV / SwiGLU need ntw 2");
+  const int nc = 16 * (int)ntw, tiles = (N + nc - 1) / nc;
+  int kchunk = (K + (int)splits - 1) / (int)splits;
+  kchunk = (kchunk + 31) & ~31;
+  const int S = (K + kchunk - 1) / kchunk;
+  if (S > 1) {
+    TORCH_CHECK(part.numel() >= (int64_t)S * tiles * nc * 16, "split-K workspace too small");
+    TORCH_CHECK(counters.numel() >= tiles, "counter buffer too small");
+  }
+  void* yp = nullptr;
+  long ldy = 0;
+  if (epi == 0 || epi == 3) {
+    TORCH_CHECK(y.has_value(), "y required");
+    check_bf16(*y, "y");
+    TORCH_CHECK(y->dim() == 2 && y->stride(1) == 1 && y->size(0) == M && y->size(1) == (epi == 3 ? N / 2 : N), "y shape");
+    yp = y->data_ptr();
+    ldy = y->stride(0);
+  }
+  void* rp = nullptr;
+  long ldr = 0;
+  float* so = nullptr;
+  long so_ld = 0;
+  if (epi == 1) {
+    TORCH_CHECK(res.has_value() && ssq_out.has_value(), "residual epilogue: res and ssq_out");
+    check_bf16(*res, "res");
+    check_f32(*ssq_out, "ssq_out");
+    TORCH_CHECK(res->dim() == 2 && res->stride(1) == 1 && res->size(0) == M && res->size(1) == N, "res [M, N]");
+    TORCH_CHECK(ssq_out->dim() == 2 && ssq_out->size(0) >= tiles && ssq_out->size(1) >= M, "ssq_out [>= tiles, >= M]");
+    rp = res->data_ptr();
+    ldr = res->stride(0);
+    so = ssq_out->data_ptr<float>();
+    so_ld = ssq_out->size(1);
+  }
+  const float* si = nullptr;
+  long si_ld = 0;
+  if (epi >= 2) {
+    TORCH_CHECK(ssq_in.has_value(), "row-scaled epilogue: ssq_in");
+    check_f32(*ssq_in, "ssq_in");
+    TORCH_CHECK(ssq_in->dim() == 2 && ssq_in->size(1) >= M && ssq_n >= 1 && ssq_n <= ssq_in->size(0), "ssq_in [slots, >= M]");
+    si = ssq_in->data_ptr<float>();
+    si_ld = ssq_in->size(1);
+  }
+  const int *pp = nullptr, *sl = nullptr;
+  const float* cs = nullptr;
+  void *qo = nullptr, *kp = nullptr, *vp = nullptr;
+  if (epi == 2) {
+    TORCH_CHECK(pos.has_value() && cos_sin.has_value() && slots.has_value() && q_out.has_value() && kc.has_value() &&
+                    vc.has_value(), "qkv epilogue operands");
+    check_i32(*pos, "positions");
+    check_i32(*slots, "slots");
+    check_f32(*cos_sin, "cos_sin");
+    check_bf16(*q_out, "q_out");
+    check_bf16(*kc, "k_cache");
+    check_bf16(*vc, "v_cache");
+    TORCH_CHECK(d % 32 == 0 && N == (nq + 2 * nkv) * d, "qkv: N == (nq + 2 nkv) d, d % 32 == 0");
+    TORCH_CHECK(pos->numel() >= M && slots->numel() >= M && cos_sin->dim() == 2 && cos_sin->size(1) == d,
+                "positions / slots / cos_sin");
+    TORCH_CHECK(q_out->is_contiguous() && q_out->numel() >= (int64_t)M * nq * d, "q_out [M, nq, d]");
+    TORCH_CHECK(kc->is_contiguous() && vc->is_contiguous() && kc->dim() == 4 && kc->size(1) == nkv &&
+                    kc->size(2) == 16 && kc->size(3) == d && vc->size(1) == nkv && vc->size(2) == d && vc->size(3) == 16,
+                "cache layout: K [blocks, nkv, 16, d], V [blocks, nkv, d, 16]");
+    pp = pos->data_ptr<int>();
+    sl = slots->data_ptr<int>();
+    cs = cos_sin->data_ptr<float>();
+    qo = q_out->data_ptr();
+    kp = kc->data_ptr();
+    vp = vc->data_ptr();
+  }
+  ok(dllm_skinny_epi(x.data_ptr(), x.stride(0), w.data_ptr(), panel ? 1 : 0, yp, ldy, M, N, K, (int)ntw, (int)splits,
+                     (int)epi, part.data_ptr<float>(), counters.data_ptr<int>(), rp, ldr, so, so_ld, si, (int)ssq_n, si_ld,
+                     (float)scale, (float)eps, pp, cs, sl, qo, kp, vp, (int)nq, (int)nkv, (int)d, stream()),
+     "skinny_epi");
+  return epi == 1 ? tiles : 0;
+}
+
 // Small-batch GEMV (M in {1, 2, 4, 8}; csrc/kernels/gemv.hip): y = x . w^T (x = silu(g)*u if swiglu).
 void gemv(torch::Tensor x, torch::Tensor w, torch::Tensor y, int64_t R, bool swiglu) {
   check_bf16(x, "x");
@@ -909,10 +1007,28 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
            c10::optional<torch::Tensor> q_out, c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
            int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> bias, int64_t wk, int64_t nl,
            c10::optional<torch::Tensor> sk_table, int64_t sk_cmax, c10::optional<torch::Tensor> v_rows,
-           int64_t kdepth) {
+           int64_t kdepth, int64_t mfma, int64_t raster) {
   check_bf16(x, "x");
   check_bf16(w, "w");
-  if (nl > 0 && kdepth != 32) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
+  TORCH_CHECK(mfma == 16 || mfma == 32, "tgemm: mfma 16 or 32");
+  if (mfma == 32) {   // tgemm.hip by_tile_m32: the whitelist, so a bad plan gets a clear error
+    const bool known = wk == 1 && kdepth == 64 &&
+                       ((nl == 0 && ks == 2 && stages == 3 && ((bm == 64 && bn == 64 && nw == 4) ||
+                                                               (bm == 64 && bn == 128 && nw == 8))) ||
+                        (nl == 0 && ks == 1 && bm == 256 && bn == 256 && nw == 8 && stages == 2) ||
+                        (nl == 8 && ks == 1 && bm == 128 && bn == 64 && nw == 4 && stages == 4) ||
+                        (nl == 8 && ks == 1 && bm == 256 && bn == 128 && nw == 8 && stages == 3));
+    TORCH_CHECK(known, "tgemm: no 32x32x16 plan (", bm, "x", bn, ", ", stages, " stages, ks ", ks, ", ", nw, "+", nl,
+                " waves)");
+    TORCH_CHECK(!sk_table.has_value(), "tgemm: 32x32x16 plans have no stream-K form");
+  }
+  if (kdepth == 32) {   // tgemm.hip by_tile_k32: explicit whitelist
+    const bool known = ks == 1 && wk == 1 && nw == 8 &&
+                       ((bm == 256 && bn == 256 && stages == 4 && nl == 0) ||
+                        (bm == 256 && bn == 128 && stages == 6 && (nl == 0 || nl == 8)));
+    TORCH_CHECK(known, "tgemm: no 32-deep plan (", bm, "x", bn, ", ", stages, " stages, ", nw, "+", nl, " waves)");
+  }
+  if (nl > 0 && kdepth != 32 && mfma == 16) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
     const bool known = ks == 1 && wk == 1 &&
                        ((bm == 64 && bn == 64 && nw == 4 &&
                          ((nl == 2 && stages == 4) || ((nl == 4 || nl == 8) && (stages == 4 || stages == 8)))) ||
@@ -1043,6 +1159,9 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   }
   TORCH_CHECK(kdepth == 64 || kdepth == 32, "tgemm: k depth 64 or 32");
   a.kdepth = (int)kdepth;
+  a.mfma = (int)mfma;
+  TORCH_CHECK(raster >= 0 && raster <= 64, "tgemm: raster 0..64");
+  a.raster = (int)raster;
   ok(dllm_tgemm(&a, (int)bm, (int)bn, (int)stages, (int)ks, (int)nw, (int)wk, (int)epi, stream(), (int)nl), "tgemm");
 }
 
@@ -1194,6 +1313,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("cache_scan", &cache_scan);
   m.def("cache_write", &cache_write);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_epi", &skinny_epi);
   m.def("gemv", &gemv);
   m.def("gemv_norm", &gemv_norm);
   m.def("gemv_slots", &gemv_slots);

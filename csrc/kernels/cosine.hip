@@ -69,9 +69,10 @@ __global__ void __launch_bounds__(256) cache_scan_kernel(CacheScan b, const floa
   __syncthreads();
   const int nu = b.nu, nf4 = d >> 2, lane = threadIdx.x & 63;
   const long nwave = (long)gridDim.x * (blockDim.x >> 6);
-  for (long r0 = ((long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256; r0 < N; r0 += nwave * 256) {
+  // the next iteration's context ids are requested before this iteration's matches are scored, so
+  // a wave that finds a match does not serialise its id stream behind the row fetch
+  auto load_ids = [&](long r0, int (&c)[4]) {
     const long rb = r0 + 4 * lane;
-    int c[4];
     if (rb + 3 < N) {
       const int4 v = *reinterpret_cast<const int4*>(ctx + rb);
       c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
@@ -79,6 +80,15 @@ __global__ void __launch_bounds__(256) cache_scan_kernel(CacheScan b, const floa
 #pragma unroll
       for (int k = 0; k < 4; ++k) c[k] = rb + k < N ? ctx[rb + k] : -1;
     }
+  };
+  long r0 = ((long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 256;
+  int cn[4];
+  if (r0 < N) load_ids(r0, cn);
+  for (; r0 < N; r0 += nwave * 256) {
+    int c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = cn[k];
+    if (r0 + nwave * 256 < N) load_ids(r0 + nwave * 256, cn);
     int u[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

@@ -39,6 +39,12 @@ namespace {
 
 enum { GV_PLAIN = 0, GV_RESADD = 1, GV_QKV = 2, GV_SWIGLU = 3 };
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// acc + x.lo * w.lo + x.hi * w.hi for two packed bf16 pairs (v_dot2c_f32_bf16)
+__device__ __forceinline__ float dot2bf(uint32_t x, uint32_t w, float acc) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, x), __builtin_bit_cast(bf16x2, w), acc, false);
+}
+
 struct EpiArgs {                 // fused output epilogues (EPI != GV_PLAIN)
   u16* res;                      // RESADD: residual stream [M, ldr], updated in place
   long ldr;
@@ -195,20 +201,22 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
     for (int u = 0; u < UNR; ++u) {
       const int k = kb + u * STEP + 8 * lane;
       if (k < K) {
-        float wf[R][8];
-#pragma unroll
-        for (int r = 0; r < R; ++r) unpack8(w[u][r], wf[r]);
+        // packed bf16 dot products (v_dot2c_f32_bf16: two exact bf16 products added into the f32
+        // accumulator, no unpacking): 4 VALU ops per (row, column, 16-B piece) instead of 8 FMAs plus
+        // 16 conversions - at 8 rows the unpacked form was VALU-bound (8.5 ops per weight byte)
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          float xf[8];
-          if constexpr (XG)
-            unpack8(xg[u][m], xf);
-          else
-            unpack8(ld16(xs + (long)m * K + k), xf);
+          const uint4 xv = XG ? xg[u][m] : ld16(xs + (long)m * K + k);
 #pragma unroll
-          for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[m][r] = fmaf(xf[j], wf[r][j], acc[m][r]);
+          for (int r = 0; r < R; ++r) {
+            const uint4 wv = w[u][r];
+            float a = acc[m][r];
+            a = dot2bf(xv.x, wv.x, a);
+            a = dot2bf(xv.y, wv.y, a);
+            a = dot2bf(xv.z, wv.z, a);
+            a = dot2bf(xv.w, wv.w, a);
+            acc[m][r] = a;
+          }
         }
       }
     }

@@ -95,7 +95,13 @@ __device__ __forceinline__ int swz(int r) {
   else return (0x1320 >> (4 * ((r >> 2) & 3))) & 3;
 }
 
-template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK, int NL, int WGM, int BKT>
+// MF: MFMA shape of the wave tile, 16 (mfma_f32_16x16x32_bf16, FM x FN 16 x 16 fragments) or 32
+// (mfma_f32_32x32x16_bf16, (WM / 32) x (WN / 32) 32 x 32 blocks: half the MFMA instructions for the
+// same tile and the SAME LDS fragment bytes per FLOP - each lane still reads one 16-B k-slice of
+// one row per fragment; the swizzle stays conflict-free for the 32-row reads, see below).  With
+// MF 32 every epilogue stages its bf16 values through LDS (a RoPE / SwiGLU partner column c ^ 16
+// is in lane ^ 16 of the same register: one shuffle), then the common copy-out runs.
+template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK, int NL, int WGM, int BKT, int MF = 16>
 __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* smem, int M, const int S,
                                            const int SC, const int split, const int m_tile,
                                            const int n_tile, const int kbeg, const int nk) {
@@ -166,7 +172,7 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   // starts with them in registers: its RoPE table reads are then ONE round trip, not two dependent
   // ones (pos -> cos/sin), and the K copy-out reads its slots from LDS.  Decode-sized tiles only
   // (FM <= 2): 2 FM*4 live registers across the ring spill the large prefill tiles
-  constexpr bool QPF = EPI == EPI_QKV && FM <= 2;
+  constexpr bool QPF = EPI == EPI_QKV && FM <= 2 && MF == 16;
   constexpr int QR = QPF ? FM * 4 : 1;
   int q_pos[QR], q_slot[QR];
   if constexpr (QPF) {
@@ -253,11 +259,23 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
     }
   };
 
-  f32x4 acc[FM][FN];
+  static_assert(MF == 16 || (MF == 32 && WM % 32 == 0 && WN % 32 == 0 && WK == 1), "32 x 32 blocks: 32-aligned wave tiles, one k-group");
+  constexpr int FM32 = MF == 32 ? WM / 32 : 1, FN32 = MF == 32 ? WN / 32 : 1;
+  f32x4 acc[FM][FN];   // (MF 32: unused, eliminated)
+  f32x16 acc32[FM32][FN32];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM32; ++i)
+#pragma unroll
+      for (int j = 0; j < FN32; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc32[i][j][v] = 0.f;
+  }
 
   if (NL == 0 || loader) {
 #pragma unroll
@@ -287,8 +305,8 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   // group 1): every read of a slot retires before its wave's barrier, which both groups pass before
   // the refill of that slot is issued one step later; slot t+1 is waited for (counted vmcnt) before
   // the phase-1 barrier that every reader of it passes afterwards.
-  constexpr bool PP = NL == 0 && WK == 1 && KS == 1 && NW == 8 && WGM == 2 && BKT == 32 && FM == 8 && FN == 4 &&
-                      STAGES >= 3;
+  constexpr bool PP = MF == 16 && NL == 0 && WK == 1 && KS == 1 && NW == 8 && WGM == 2 && BKT == 32 && FM == 8 &&
+                      FN == 4 && STAGES >= 3;
   if constexpr (PP) {
     const bool g1 = wm == 1;
     wait_stages<G, (STAGES - 2 < 6 ? STAGES - 2 : 6)>(min(STAGES - 2, nk - 1));  // slot 0 landed
@@ -372,6 +390,34 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
       if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
     }
     if (loader) continue;
+    if constexpr (MF == 32) {
+      // 32 x 32 x 16 blocks: lane l holds A[row l & 31][k 8 (l >> 5) .. +7] of a 16-deep k slice and
+      // B likewise (B[k][n] = W[n][k]).  A 16-lane group of ds_read_b128 reads 16 rows of one chunk:
+      // with the (r >> 1) & 7 swizzle (64-deep rows) the 16-B slots 8 (r & 1) + (c ^ ((r >> 1) & 7)) of
+      // those rows are 16 distinct ones, and with the 32-deep permutation 4 (r & 3) + (c ^ p((r >> 2) & 3))
+      // likewise - conflict-free, as the 16 x 16 reads.
+#pragma unroll
+      for (int s = 0; s < (BKT / 16) * KS; ++s) {
+        const unsigned char* base = smem + (t % STAGES) * STAGE_BYTES + (s / (BKT / 16)) * SUB_BYTES;
+        const int c = 2 * (s % (BKT / 16)) + (lane >> 5);
+        bf16x8 af[FM32], bw[FN32];
+#pragma unroll
+        for (int i = 0; i < FM32; ++i) {
+          const int r = wm * WM + 32 * i + (lane & 31);
+          af[i] = *reinterpret_cast<const bf16x8*>(base + r * RB + ((c ^ swz<BKT>(r)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN32; ++j) {
+          const int r = wn * WN + 32 * j + (lane & 31);
+          bw[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + r * RB + ((c ^ swz<BKT>(r)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < FM32; ++i)
+#pragma unroll
+          for (int j = 0; j < FN32; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bw[j], acc32[i][j], 0, 0, 0);
+      }
+    } else {
 #pragma unroll
     for (int s = 0; s < HALVES * KS; ++s) {
       if (WK == 2 && (s / HALVES) != kg) continue;
@@ -393,6 +439,7 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+    }
     }
   }
   __syncthreads();  // ring idle (every load waited), rinv partials visible
@@ -420,8 +467,47 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   }
 
   // ---- split-K: write-through f32 slabs, ticket per output tile; the last arriver sums all
-  // slabs in split order (deterministic) and runs the epilogue
-  if (S > 1) {
+  // slabs in split order (deterministic) and runs the epilogue.  Slab layout (either MF):
+  // column-major [BN][BM] f32, four consecutive rows per 16-B store
+  if constexpr (MF == 32) {
+    if (S > 1) {
+      const int tile_id = n_tile * mt + m_tile;
+      const long slab = (long)BM * BN;
+      const unsigned bytes = (unsigned)min((long)mt * nt * SC * slab * 4, 0x7fffffffL);
+      const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.part, bytes);
+      const long my = ((long)tile_id * SC + split) * slab;
+      if (fw) {
+#pragma unroll
+        for (int i = 0; i < FM32; ++i)
+#pragma unroll
+          for (int j = 0; j < FN32; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = wm * WM + 32 * i + 8 * q + 4 * (lane >> 5), c = wn * WN + 32 * j + (lane & 31);
+              st_wt16(pr, (unsigned)((my + (long)c * BM + r) * 4),
+                      make_float4(acc32[i][j][4 * q], acc32[i][j][4 * q + 1], acc32[i][j][4 * q + 2], acc32[i][j][4 * q + 3]));
+            }
+      }
+      if (!ticket_last(&a.counters[tile_id], S, s_last)) return;
+      if (fw) {
+#pragma unroll
+        for (int i = 0; i < FM32; ++i)
+#pragma unroll
+          for (int j = 0; j < FN32; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = wm * WM + 32 * i + 8 * q + 4 * (lane >> 5), c = wn * WN + 32 * j + (lane & 31);
+              float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+              for (int sp = 0; sp < S; ++sp) {
+                const float4 x = ld_wt16(pr, (unsigned)((((long)tile_id * SC + sp) * slab + (long)c * BM + r) * 4));
+                v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
+              }
+              acc32[i][j][4 * q] = v.x; acc32[i][j][4 * q + 1] = v.y;
+              acc32[i][j][4 * q + 2] = v.z; acc32[i][j][4 * q + 3] = v.w;
+            }
+      }
+    }
+  } else if (S > 1) {
     const int tile_id = n_tile * mt + m_tile;
     const long slab = (long)BM * BN;
     const unsigned bytes = (unsigned)min((long)mt * nt * SC * slab * 4, 0x7fffffffL);
@@ -480,7 +566,7 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   const int cl = lane & 15;
   float rinv[FM][4];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < (MF == 16 ? FM : 0); ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float r = 1.f;
@@ -502,13 +588,83 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
   u16* so = reinterpret_cast<u16*>(smem);
   const bool full_n = n0 + BN <= N;  // (N % 8 == 0 is required on the host side for vector stores)
 
+  if constexpr (MF == 32) {
+    // 32 x 32 blocks: element v of acc32[i][j] is row wm*WM + 32 i + (v & 3) + 8 (v >> 2) + 4 (lane >> 5),
+    // column wn*WN + 32 j + (lane & 31).  Every epilogue value goes to the LDS image `so` here (the
+    // partner column c ^ 16 of a RoPE / SwiGLU pair sits in lane ^ 16, same rows); the copy-out
+    // passes below are the MF-independent ones.
+    const int lc = lane & 31, c16 = lane & 15, hi = (lane >> 4) & 1;
+    float bcol[FN32];
+#pragma unroll
+    for (int j = 0; j < FN32; ++j) {
+      const int n = n0 + wn * WN + 32 * j + lc;
+      bcol[j] = (EPI != EPI_SWIGLU && EPI != EPI_QKV && a.bias != nullptr && n < N) ? bf2f(a.bias[n]) : 0.f;
+    }
+    if (fw) {
+#pragma unroll
+      for (int i = 0; i < FM32; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int rl = wm * WM + 32 * i + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+          float ri = 1.f;
+          if (has_rs) {
+            float sum = 0.f;
+#pragma unroll
+            for (int p = 0; p < TPR; ++p) sum += s_rsp[p * BM + rl];
+            ri = rsqrtf(sum * a.norm_scale + a.eps);
+          }
+          if constexpr (EPI == EPI_QKV) {
+            const int d = a.d, hd = d / 2, nkv = a.nkv, qcols = a.nq * d, kcols = nkv * d;
+            const int m = m0 + rl, mq = min(m, M - 1);
+            const int slot = a.slots[mq];
+            if (wn == 0 && lc == 0) reinterpret_cast<int*>(s_red)[rl] = slot;
+            const float* cs = a.cos_sin + (long)a.pos[mq] * d;
+#pragma unroll
+            for (int j = 0; j < FN32; ++j) {
+              const int cb = wn * WN + 32 * j, nb = n0 + cb;
+              const float xs = bfr(acc32[i][j][v] * ri);
+              const float xp = __shfl_xor(xs, 16, 64);
+              if (nb >= N) continue;   // wave-uniform
+              if (nb < qcols + kcols) {
+                const int cc = nb < qcols ? nb : nb - qcols;
+                const int d1 = 16 * ((cc % d) >> 5) + c16;
+                const float co = cs[d1], si = cs[hd + d1];
+                // first half (x1 = own, x2 = partner): x1 co - x2 si; second half: x2 co + x1 si
+                so[rl * OLD + cb + lc] = f2bf(hi ? xs * co + xp * si : xs * co - xp * si);
+              } else if (a.v_rows != nullptr) {
+                so[rl * OLD + cb + lc] = f2bf(xs);
+              } else if (m < M && slot >= 0) {
+                const int cc = nb - qcols - kcols;
+                u16* vo = a.vc + (((long)(slot >> 4) * nkv + cc / d) * d) * 16 + (slot & 15);
+                vo[(long)(cc % d + lc) * 16] = f2bf(xs);
+              }
+            }
+          } else if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+            for (int j = 0; j < FN32; ++j) {
+              const float xs = bfr(acc32[i][j][v] * ri);
+              const float xp = __shfl_xor(xs, 16, 64);
+              if (!hi) so[rl * OLD + (wn * WN + 32 * j) / 2 + c16] = f2bf(silu(xs) * xp);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < FN32; ++j) {
+              float x = acc32[i][j][v] * ri + bcol[j];
+              if constexpr (EPI == EPI_GELU) x = gelu_erf(bfr(x));
+              so[rl * OLD + wn * WN + 32 * j + lc] = f2bf(x);
+            }
+          }
+        }
+    }
+  }
+
   if constexpr (EPI == EPI_QKV) {
     // RoPE in registers (pairs in adjacent fragments of one lane), V written straight from the
     // registers (transposed cache layout: no row vectors to form), q/k staged.
     const int d = a.d, hd = d / 2, nq = a.nq, nkv = a.nkv;
     const int qcols = nq * d, kcols = nkv * d;
     int* s_slot = reinterpret_cast<int*>(s_red);   // [BM] cache slot per tile row (copy-out)
-    if (fw) {
+    if (fw && MF == 16) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -576,9 +732,9 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + wn * WN + 16 * j + cl;
-      bcol[j] = (EPI != EPI_SWIGLU && a.bias != nullptr && n < N) ? bf2f(a.bias[n]) : 0.f;
+      bcol[j] = (MF == 16 && EPI != EPI_SWIGLU && a.bias != nullptr && n < N) ? bf2f(a.bias[n]) : 0.f;
     }
-    if (fw) {
+    if (fw && MF == 16) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -641,7 +797,7 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
 }
 
 template <int BM, int BN, int EPI, int STAGES, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false,
-          int BKT = 64>
+          int BKT = 64, int MF = 16>
 __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) {
   static_assert(WK == 1 || (WK == 2 && KS == 2), "k-groups split the KS sub-tiles of a stage");
   static_assert(NL == 0 || WK == 1, "loader waves or k-groups, not both");
@@ -672,7 +828,14 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int split = wgid % S, rest = wgid / S;
     const int kbeg = split * a.kchunk;
-    tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM, BKT>(a, smem, a.M, S, S, split, rest % mt, rest / mt, kbeg,
+    int m_t = rest % mt, n_t = rest / mt;
+    if (a.raster > 1 && mt > a.raster) {   // grouped raster (GemmArgs.raster)
+      const int gsz = a.raster * nt, first = (rest / gsz) * a.raster;
+      const int gm = min(mt - first, a.raster), in = rest % gsz;
+      m_t = first + in % gm;
+      n_t = in / gm;
+    }
+    tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM, BKT, MF>(a, smem, a.M, S, S, split, m_t, n_t, kbeg,
                                                         max(0, (min(a.K, kbeg + a.kchunk) - kbeg) / KSTEP));
   } else {
     const int ng = gridDim.x, q8 = ng >> 3, r8 = ng & 7, xcd = bid & 7;
@@ -680,7 +843,7 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
     for (int sg = 0; sg < a.sk_segmax; ++sg) {
       const int4 e = *reinterpret_cast<const int4*>(a.sk_table + ((long)wl * a.sk_segmax + sg) * 4);
       if (e.x < 0) break;   // block-uniform: this workgroup's list ended
-      tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM, BKT>(a, smem, a.M, e.w >> 16, a.sk_cmax, e.w & 0xffff, e.x % mt,
+      tgemm_unit<BM, BN, EPI, STAGES, KS, NW, WK, NL, WGM, BKT, MF>(a, smem, a.M, e.w >> 16, a.sk_cmax, e.w & 0xffff, e.x % mt,
                                                           e.x / mt, e.y * KSTEP, e.z - e.y);
       __syncthreads();   // the next segment re-uses the ring, the row-scale partials and the flag
     }
@@ -688,11 +851,11 @@ __global__ void __launch_bounds__(64 * (NW * WK + NL)) tgemm_kernel(GemmArgs a) 
 }
 
 template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, bool SK = false,
-          int BKT = 64>
+          int BKT = 64, int MF = 16>
 int launch_t(const GemmArgs& a, hipStream_t st) {
   const int mt = (a.M + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
   const int grid = SK ? a.sk_grid : mt * nt * a.splits;
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, SK, BKT>), dim3(grid),
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, SK, BKT, MF>), dim3(grid),
                      dim3(64 * (NW * WK + NL)), 0, st, a);
   return (int)hipGetLastError();
 }
@@ -707,19 +870,37 @@ constexpr bool sk_plan() {
                      (BM == 128 && BN == 64 && NL == 4 && ST == 4));   // (160 x 128 spilled in the segment loop)
 }
 
-template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, int BKT = 64>
+template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, int BKT = 64, int MF = 16>
 int launch_fit(const GemmArgs& a, hipStream_t st) {
   if constexpr (ST * KS * (BM + BN) * 2 * BKT > 150 * 1024) {
     return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
   } else {
     if (a.sk_table != nullptr) {
-      if constexpr (BKT == 64 && sk_plan<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>())
+      if constexpr (BKT == 64 && MF == 16 && sk_plan<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>())
         return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, true>(a, st);
       else
         return -25;
     }
-    return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, false, BKT>(a, st);
+    return launch_t<BM, BN, EPI, ST, KS, NW, WK, NL, WGM, false, BKT, MF>(a, st);
   }
+}
+
+// 32 x 32 x 16 MFMA plans (GemmArgs.mfma = 32): the decode tiles the autotuner picks on the
+// flagship (64 x 64 / 64 x 128 with k-step 128, the 128 x 64 and 256 x 128 loader-wave tiles) and
+// the 256 x 256 prefill tile; chosen per shape by measurement like every other plan
+template <int EPI>
+int by_tile_m32(int bm, int bn, int stages, int ks, int nw, int nl, const GemmArgs& a, hipStream_t st) {
+  if (nl == 0 && ks == 2 && stages == 3) {
+    if (bm == 64 && bn == 64 && nw == 4) return launch_fit<64, 64, EPI, 3, 2, 4, 1, 0, 2, 64, 32>(a, st);
+    if (bm == 64 && bn == 128 && nw == 8) return launch_fit<64, 128, EPI, 3, 2, 8, 1, 0, 2, 64, 32>(a, st);
+  }
+  if (nl == 0 && ks == 1 && bm == 256 && bn == 256 && nw == 8 && stages == 2)
+    return launch_fit<256, 256, EPI, 2, 1, 8, 1, 0, 2, 64, 32>(a, st);
+  if (nl == 8 && ks == 1 && bm == 128 && bn == 64 && nw == 4 && stages == 4)
+    return launch_fit<128, 64, EPI, 4, 1, 4, 1, 8, 2, 64, 32>(a, st);
+  if (nl == 8 && ks == 1 && bm == 256 && bn == 128 && nw == 8 && stages == 3)
+    return launch_fit<256, 128, EPI, 3, 1, 8, 1, 8, 4, 64, 32>(a, st);
+  return -27;
 }
 
 // 32-deep k-steps (GemmArgs.kdepth = 32): the 256-row tiles with 4-6 stage rings, for prefill-size
@@ -980,6 +1161,24 @@ extern "C" int dllm_tgemm(const void* args, int bm, int bn, int stages, int ks, 
   if (a.sk_table != nullptr && (!a.part || !a.counters || a.sk_grid < 1 || a.sk_segmax < 1 || a.sk_cmax < 1 ||
                                 a.g_tiles != nullptr || a.splits != 1))
     return -24;
+  if (a.mfma == 32) {     // 32 x 32 x 16 MFMA plans: one k-group, no MoE gather, no stream-K, k-step 64
+    if (wk != 1 || a.g_tiles != nullptr || a.sk_table != nullptr || (a.kdepth != 0 && a.kdepth != 64) ||
+        a.K % (BK * ks) || a.kchunk % (BK * ks) || a.kchunk <= 0 || a.splits < 1 || a.lda % 8 || a.N % 8 ||
+        (a.Y && a.ldy % 8))
+      return -23;
+    if (a.splits > 1 && (!a.part || !a.counters)) return -2;
+    if ((epi == EPI_QKV || epi == EPI_SWIGLU) && (a.N % 32)) return -3;
+    if (epi == EPI_QKV && (a.d % 32 || !a.q_out || !a.kc || !a.vc || !a.pos || !a.slots || !a.cos_sin)) return -4;
+    switch (epi) {
+      case EPI_PLAIN: return by_tile_m32<EPI_PLAIN>(bm, bn, stages, ks, nw, nl, a, stream);
+      case EPI_RESADD: return by_tile_m32<EPI_RESADD>(bm, bn, stages, ks, nw, nl, a, stream);
+      case EPI_QKV: return by_tile_m32<EPI_QKV>(bm, bn, stages, ks, nw, nl, a, stream);
+      case EPI_SWIGLU: return by_tile_m32<EPI_SWIGLU>(bm, bn, stages, ks, nw, nl, a, stream);
+      case EPI_GELU: return by_tile_m32<EPI_GELU>(bm, bn, stages, ks, nw, nl, a, stream);
+      default: return -6;
+    }
+  }
+  if (a.mfma != 0 && a.mfma != 16) return -28;
   if (a.kdepth == 32) {   // 32-deep k-step plans: KS 1, one k-group, no MoE gather, no stream-K
     if (ks != 1 || wk != 1 || a.g_tiles != nullptr || a.sk_table != nullptr || a.K % BK || a.kchunk % BK ||
         a.kchunk <= 0 || a.splits < 1 || a.lda % 8 || a.N % 8 || (a.Y && a.ldy % 8))

@@ -58,6 +58,13 @@ struct GemmArgs {
   int sk_grid, sk_segmax, sk_cmax;
   // k depth of a staged sub-tile: 0 / 64 (default), 32 (tgemm.hip by_tile_k32 plans)
   int kdepth;
+  // MFMA of the wave tiles: 0 / 16 (mfma_f32_16x16x32_bf16, default), 32 (mfma_f32_32x32x16_bf16,
+  // tgemm.hip by_tile_m32 plans)
+  int mfma;
+  // tile raster: 0 / 1 = n-major (consecutive workgroups of an XCD share a weight tile), G > 1 =
+  // groups of G m-tile rows (an XCD's consecutive workgroups cover G m-tiles x (32 / G) n-tiles, so
+  // they share G activation and 32 / G weight panels; tgemm.hip tgemm_kernel)
+  int raster;
 };
 enum { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKV = 2, EPI_SWIGLU = 3, EPI_GELU = 4 };
 }  // namespace dllm

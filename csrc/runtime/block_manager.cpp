@@ -11,8 +11,8 @@ using dllm::BlockManager;
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "distributed_llm_amd native serving runtime (paged-KV block manager)";
   py::class_<BlockManager>(m, "BlockManager")
-      .def(py::init<int, int, bool, bool>(), py::arg("num_blocks"), py::arg("block_size") = 16,
-           py::arg("prefix_cache") = true, py::arg("contiguous") = true)
+      .def(py::init<int, int, bool, int>(), py::arg("num_blocks"), py::arg("block_size") = 16,
+           py::arg("prefix_cache") = true, py::arg("placement") = 2)
       .def_property_readonly("block_size", &BlockManager::block_size)
       .def_property_readonly("num_blocks", &BlockManager::num_blocks)
       .def("num_free_blocks", &BlockManager::num_free_blocks)

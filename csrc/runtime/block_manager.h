@@ -66,9 +66,11 @@ struct Seq {
 
 class BlockManager {
  public:
-  // contiguous: place a sequence's blocks in runs (see fresh()); false: plain LIFO free list
-  BlockManager(int num_blocks, int block_size, bool prefix_cache, bool contiguous = true)
-      : bs_(block_size), prefix_(prefix_cache), contiguous_(contiguous), blocks_(num_blocks),
+  // placement (see fresh()): 0 plain LIFO free list; 1 round-5 runs (continue into a FREE next block
+  // inside the segment, else open a wholly free segment); 2 (default) round-6 runs (continue through
+  // an evictable next block too, restart in the least-held segment's longest free / cold stretch)
+  BlockManager(int num_blocks, int block_size, bool prefix_cache, int placement = 2)
+      : bs_(block_size), prefix_(prefix_cache), placement_(placement), contiguous_(placement > 0), blocks_(num_blocks),
         tok_store_(prefix_cache ? (size_t)num_blocks * block_size : 0) {
     if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad sizes");
     init_free();
@@ -494,8 +496,13 @@ class BlockManager {
   int fresh(int prefer = -1) {
     ++fresh_allocs_;
     int b = -1;
-    if (contiguous_ && prefer > 0 && prefer < (int)blocks_.size()) {
-      if (true) {
+    if (placement_ == 1 && prefer > 0 && prefer < (int)blocks_.size() && prefer % kSeg != 0 && free_flag_[prefer]) {
+      b = prefer;   // round-5 rule (A/B baseline)
+      take_free(b);
+      ++contig_;
+    }
+    if (placement_ >= 2 && prefer > 0 && prefer < (int)blocks_.size()) {
+      {
         if (free_flag_[prefer]) {
           b = prefer;
           take_free(b);
@@ -512,7 +519,7 @@ class BlockManager {
       }
     }
     if (b < 0 && contiguous_) b = pop_segment();
-    if (b < 0 && contiguous_) b = pop_roomy_segment();
+    if (b < 0 && placement_ >= 2) b = pop_roomy_segment();
     if (b < 0) b = pop_free();
     if (b < 0) {
       if (lru_.empty()) throw std::runtime_error("out of KV blocks");
@@ -543,6 +550,7 @@ class BlockManager {
 
   int bs_;
   bool prefix_;
+  int placement_;
   bool contiguous_;
   std::vector<Block> blocks_;
   std::vector<int> free_;          // stack of free blocks (lazy deletion, see init_free)

@@ -147,7 +147,7 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         self.max_blocks = (self.max_model_len + BS - 1) // BS
         self._alloc_kv(kv_cache_gb)
-        self.bm = _need_runtime().BlockManager(self.num_blocks, BS, prefix_cache, self.KV_CONTIGUOUS)
+        self.bm = _need_runtime().BlockManager(self.num_blocks, BS, prefix_cache, int(self.KV_PLACEMENT))
         self._ids = itertools.count()
         self._lock = threading.Lock()          # held by the thread currently driving the step loop
         self._inbox: List[_Seq] = []            # submitted, not yet seen by the driver
@@ -1197,8 +1197,9 @@ class LLMEngine:
     # max_model_len) are known in advance and never cost a row.
     PIPELINE = True
     # KV blocks placed in per-sequence runs (csrc/runtime/block_manager.h fresh()): decode attention
-    # streams a sequence's blocks in order, and runs read faster than scattered blocks
-    KV_CONTIGUOUS = True
+    # streams a sequence's blocks in order, and runs read faster than scattered blocks.  0 LIFO,
+    # 1 round-5 runs, 2 round-6 runs (in-place continuation, least-held-segment restarts; the default)
+    KV_PLACEMENT = 2
     # New requests end a pipelined burst (to be admitted and prefilled) only once the burst has run
     # this many steps: a client that keeps submitting (turn pipelining) would otherwise cut every
     # burst to one or two steps and lose the host/GPU overlap; the added admission delay is at most

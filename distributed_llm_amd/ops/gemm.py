@@ -41,6 +41,8 @@ SKINNY_MAX_M = 128
 _SPLITS = (1, 2, 4, 8, 16)
 _NTWS = (1, 2, 4)
 _GEMV_MS = (1, 2, 4, 8)   # csrc/kernels/gemv.hip instantiations (decode buckets below 16)
+SKE_MAX_M = 16            # small-batch MFMA GEMM with fused epilogues (skinny_gemm.hip skinny_epi_kernel)
+_SKE_SPLITS = (1, 2, 4, 8)
 _GEMV_RS = (1, 2, 4)
 _TG_TILES = ((64, 64, 4), (64, 128, 4), (128, 64, 4), (128, 128, 4), (64, 128, 8), (128, 128, 8), (192, 128, 8),
              (256, 128, 8),
@@ -57,6 +59,11 @@ _TG_NL = ((64, 64, 4, 4, 2, 1), (64, 64, 4, 4, 4, 1), (64, 64, 4, 8, 4, 1), (128
 # 32-deep k-step plans (csrc/kernels/tgemm.hip by_tile_k32): (bm, bn, stages, loaders), 8 compute waves;
 # as plan tuples (bm, bn, stages, splits, 1, 8, 1, loaders, 0, 32)
 _TG_K32 = ((256, 256, 4, 0), (256, 128, 6, 0), (256, 128, 6, 8))
+# 32 x 32 x 16 MFMA plans (csrc/kernels/tgemm.hip by_tile_m32), as full plan tuples with k depth 64 and
+# mfma 32: the flagship's decode tiles and the 256 x 256 prefill tile; measured against everything else
+_TG_M32 = ((64, 64, 3, 1, 2, 4, 1, 0, 0, 64, 32), (64, 128, 3, 1, 2, 8, 1, 0, 0, 64, 32),
+           (128, 64, 4, 1, 1, 4, 1, 8, 0, 64, 32), (256, 128, 3, 1, 1, 8, 1, 8, 0, 64, 32),
+           (256, 256, 2, 1, 1, 8, 1, 0, 0, 64, 32))
 # one-split plans with a stream-K instantiation (csrc/kernels/tgemm.hip sk_plan): (bm, bn, stages, ks, waves, loaders)
 _SK_PLANS = {(64, 64, 3, 2, 4, 0), (64, 64, 4, 1, 4, 0), (64, 64, 4, 1, 4, 4), (64, 64, 4, 1, 4, 8),
              (64, 128, 3, 1, 8, 0), (128, 64, 4, 1, 4, 4)}
@@ -177,7 +184,9 @@ STREAM_K = False       # stream-K tgemm plans in the autotuner (see _tg_cands)
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8), (192, 128, 3, 1, 1, 8),
              (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
-             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32), (256, 128, 6, 1, 1, 8, 1, 8, 0, 32))
+             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32), (256, 128, 6, 1, 1, 8, 1, 8, 0, 32),
+             # the 256 x 256 tile on 32 x 32 x 16 MFMA blocks
+             (256, 256, 2, 1, 1, 8, 1, 0, 0, 64, 32))
 
 
 def prefill_bucket(M: int) -> int:
@@ -295,13 +304,15 @@ def _sk_tensor(dev, M, N, K, bm, bn, ks):
 def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, eps=0.0, ssq_out=None,
            pos=None, cos_sin=None, slots=None, q_out=None, kc=None, vc=None, nq=0, nkv=0, d=0, bias=None,
            v_rows=None):
-    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves[, stream-K[, k depth]]]]])"""
+    """plan = (bm, bn, stages, splits[, ks, waves[, k-groups[, loader waves[, stream-K[, k depth[, mfma[, raster]]]]]]])"""
     bm, bn, st, sp = plan[:4]
     ks, nw = (plan[4], plan[5]) if len(plan) >= 6 else (1, 4)
     wk = plan[6] if len(plan) >= 7 else 1
     nl = plan[7] if len(plan) >= 8 else 0
     sk = len(plan) >= 9 and plan[8] == 1
     bk = plan[9] if len(plan) >= 10 else 64
+    mf = plan[10] if len(plan) >= 11 else 16
+    raster = plan[11] if len(plan) >= 12 else 0
     M = x.shape[0]
     N, K = _nk(w)
     if K % (64 * ks):
@@ -318,7 +329,7 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
         part, cnt = _P.workspace(x.device, floats, tiles)
     ext.tgemm(x, w, y, epi, bm, bn, st, sp, ks, nw, part, cnt, ssq_in, int(ssq_n), float(norm_scale), float(eps), ssq_out,
               pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv), int(d), bias, int(wk), int(nl), tab, int(cmax),
-              v_rows, int(bk))
+              v_rows, int(bk), int(mf), int(raster))
 
 
 def ref_silu_mul(gu):
@@ -406,6 +417,38 @@ def fused_gemv_r(x: torch.Tensor, N: int) -> int:
     return 0
 
 
+def fused_ske(x: torch.Tensor, N: int, K: int) -> int:
+    """Split count of the small-batch fused-epilogue MFMA GEMM (skinny_epi, 32-column tiles) if the
+    autotuner picked it for this fused op's shape (``fused_core`` = ``skE<splits>``; forced by
+    ``DLLM_FUSED_CORE=skE<splits>``), else 0."""
+    M = x.shape[0]
+    if not (0 < M <= SKE_MAX_M) or K % 64 or N % 32 or x.stride(1) != 1 or x.stride(0) % 8:
+        return 0
+    env = os.environ.get("DLLM_FUSED_CORE")
+    c = env if env and env.startswith("skE") else _P.fused_core.get((M, N, K))
+    if isinstance(c, str) and c.startswith("skE") and c[3:].isdigit():
+        return int(c[3:])
+    return 0
+
+
+def _ske_ws(x: torch.Tensor, N: int, K: int, splits: int):
+    tiles = -(-N // 32)
+    kchunk = ((-(-K // splits)) + 31) // 32 * 32
+    S = -(-K // kchunk)
+    return _P.workspace(x.device, (S * tiles * 32 * 16) if S > 1 else 0, tiles)
+
+
+def skinny_epi(x: torch.Tensor, w: torch.Tensor, epi: int, splits: int, y=None, res=None, ssq_out=None, ssq_in=None,
+               ssq_n: int = 0, scale: float = 0.0, eps: float = 0.0, pos=None, cos_sin=None, slots=None, q_out=None,
+               kc=None, vc=None, nq: int = 0, nkv: int = 0, d: int = 0) -> int:
+    """One launch of the small-batch fused-epilogue GEMM (``w`` row-major or the panel copy)."""
+    N, K = _nk(w)
+    part, cnt = _ske_ws(x, N, K, splits)
+    return int(_native(x).skinny_epi(x, w, y, 2, int(splits), int(epi), part, cnt, res, ssq_out, ssq_in, int(ssq_n),
+                                     float(scale), float(eps), pos, cos_sin, slots, q_out, kc, vc, int(nq), int(nkv),
+                                     int(d)))
+
+
 def _core(x: torch.Tensor, w: torch.Tensor, wp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Plain product for the split (core + epilogue) form of a fused op: the tuned plan of this
     shape (M <= MAX_M), hipBLASLt above."""
@@ -435,6 +478,11 @@ def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: i
         _native(r).gemv_qkv(r, w, ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q, k_cache,
                             v_cache, nq, nkv, d, R)
         return out(False)
+    sp = fused_ske(r, w.shape[0], H)
+    if sp:
+        skinny_epi(r, wp if wp is not None else w, EPI_QKV, sp, ssq_in=ssq, ssq_n=ssq_n, scale=1.0 / H, eps=eps,
+                   pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv, d=d)
+        return out(False)
     if use_vendor_core(T, w.shape[0], H):
         _native(r).qkv_post(_core(r, w, wp), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
                             k_cache, v_cache, nq, nkv, d)
@@ -453,6 +501,9 @@ def matmul_resadd(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ssq_
     R = fused_gemv_r(x, N) if M else 0
     if R:
         return int(_native(x).gemv_resadd(x, w, residual, ssq_out, R))
+    sp = fused_ske(x, N, K) if M else 0
+    if sp:
+        return skinny_epi(x, wp if wp is not None else w, EPI_RESADD, sp, res=residual, ssq_out=ssq_out)
     if M and use_vendor_core(M, N, K):
         return int(_native(x).res_add_ssq(_core(x, w, wp), residual, ssq_out))
     plan = tg_plan(M, N, K)
@@ -470,6 +521,11 @@ def swiglu_matmul(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: in
     R = fused_gemv_r(r, w.shape[0]) if T else 0
     if R:
         _native(r).gemv_swiglu(r, w, ssq, int(ssq_n), 1.0 / H, float(eps), act, R)
+        return act
+    sp = fused_ske(r, w.shape[0], H) if T else 0
+    if sp:
+        skinny_epi(r, wp if wp is not None else w, EPI_SWIGLU, sp, y=act, ssq_in=ssq, ssq_n=ssq_n, scale=1.0 / H,
+                   eps=eps)
         return act
     if T and use_vendor_core(T, w.shape[0], H):
         _native(r).swiglu_post(_core(r, w, wp), ssq, int(ssq_n), 1.0 / H, float(eps), act)
@@ -519,8 +575,11 @@ def linear_bias_residual(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, r
 
 def max_slots(N: int, M: int = 0) -> int:
     """Rows a partial-row-sum buffer needs for a residual producer of N columns: one per 64-column
-    tgemm tile, or at batch <= 8 one per fused-GEMV workgroup (N / 4 at R = 1)."""
-    return -(-N // 4) if 0 < M <= max(_GEMV_MS) else -(-N // 64)
+    tgemm tile, at batch <= 8 one per fused-GEMV workgroup (N / 4 at R = 1), at batch <= 16 one
+    per 32-column small-batch MFMA tile (skinny_epi)."""
+    if 0 < M <= max(_GEMV_MS):
+        return -(-N // 4)
+    return -(-N // 32) if 0 < M <= SKE_MAX_M else -(-N // 64)
 
 
 # ----------------------------------------------------------------------------- autotuning
@@ -655,7 +714,7 @@ def _couple_gemv_choices(fused, ms, verbose: bool) -> None:
         for prod, cons in pairs:
             kp, kc = (M,) + tuple(prod), (M,) + tuple(cons)
             cp, cc = _P.fused_core.get(kp), _P.fused_core.get(kc)
-            if cp is None or not cp.startswith("gemv") or (cc is not None and cc.startswith("gemv")):
+            if cp is None or not cp.startswith("gemv") or (cc is not None and cc.startswith(("gemv", "skE"))):
                 continue
             opts = {c: t for c, t in _P.fused_opts.get(kp, {}).items() if not c.startswith("gemv")}
             _P.fused_core[kp] = min(opts, key=opts.get) if opts else "lin"
@@ -700,6 +759,19 @@ def _tg_cands(M: int, N: int, K: int):
                 if _need_tg(M, N, K, bm, bn, sp)[0] > WS_FLOATS:
                     continue
                 out.append((bm, bn, st, sp, 1, nw, 1, nl))
+    # 32 x 32 x 16 MFMA forms of the flagship's tiles, with the splits their 16 x 16 forms take
+    if N % 8 == 0:
+        for p in _TG_M32:
+            bm, bn, st, _, ks, nw, wk, nl = p[:8]
+            if (bm >= 128 and M <= 64) or (bm == 256 and M <= 128) or K % (64 * ks):
+                continue
+            tiles = -(-M // bm) * -(-N // bn)
+            for sp in (1, 2, 3, 4):
+                if sp > 1 and (K // sp < 256 * ks or tiles * sp > 2048 or _tg_splits(K, sp, ks) != sp):
+                    continue
+                if _need_tg(M, N, K, bm, bn, sp, ks)[0] > WS_FLOATS:
+                    continue
+                out.append((bm, bn, st, sp) + tuple(p[4:]))
     # stream-K forms (one workgroup per CU walking equal shares of tiles x k-steps) of the one-split
     # plans whose tile count leaves CUs idle (M = 320 gives a 64 x 64 grid 160 tiles for N = 2048).
     # Not offered (STREAM_K False): measured, they never beat the one-unit plans on the TinyLlama
@@ -778,6 +850,20 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
                     sq = torch.empty(max_slots(N, M), M, dtype=torch.float32, device=dev)
                     for c in gv:
                         opts["gemv%d" % c[1]] = _time(lambda i: ext.gemv_resadd(x, ws[i % copies], rr, sq, c[1]))
+                # small-batch MFMA GEMM with the epilogue fused (one launch), timed in its RESADD form
+                # on the weight layout the fused ops stream (the panel copy where the model keeps one)
+                if M <= SKE_MAX_M and N % 32 == 0 and K % 64 == 0:
+                    rr = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+                    sq = torch.empty(max_slots(N, M), M, dtype=torch.float32, device=dev)
+                    src = wps if wps is not None else ws
+                    for sp in _SKE_SPLITS:
+                        if sp > 1 and K // sp < 256:
+                            continue
+                        try:
+                            opts["skE%d" % sp] = _time(lambda i: skinny_epi(x, src[i % copies], EPI_RESADD, sp, res=rr,
+                                                                             ssq_out=sq))
+                        except Exception:  # noqa: BLE001 - workspace / shape refused
+                            pass
                 _P.fused_core[tkey] = min(opts, key=opts.get)
                 _P.fused_opts[tkey] = opts
             if verbose:

@@ -1,5 +1,5 @@
 """bench.py with class / module constants overridden, for same-box A/B runs of a default:
-    python scripts/exp/bench_ab.py engine.KV_CONTIGUOUS=0 gemm.PREFILL_TUNE=1 -- --steps 20 --warmup 5
+    python scripts/exp/bench_ab.py engine.KV_PLACEMENT=1 gemm.PREFILL_TUNE=1 -- --steps 20 --warmup 5
 ``engine.X`` sets LLMEngine.X, ``gemm.X`` sets distributed_llm_amd.ops.gemm.X (ints; 0/1 for flags).
 Everything after ``--`` goes to bench.py."""
 import os

@@ -26,7 +26,7 @@ def simulate(convs=96, steps=5000, pool_blocks=None, seed=0, retok_same=0.3, con
              gap=(0, 0)):
     rng = random.Random(seed)
     pool = pool_blocks or convs * 360
-    bm = _runtime.BlockManager(pool, bs, True, contiguous)
+    bm = _runtime.BlockManager(pool, bs, True, int(contiguous) if not isinstance(contiguous, bool) else (2 if contiguous else 0))
     hist = [[rng.randrange(32000) for _ in range(rng.randrange(20, 80))] for _ in range(convs)]
     active = {}
     waiting = {}                 # conversation -> step at which its next turn is dispatched

@@ -24,7 +24,9 @@ PLANS = [p for p in ([(bm, bn, st, sp, 1, nw) for bm, bn, nw in G._TG_TILES for 
                       # loader-wave plans (NL extra waves stream the ring, the rest only compute)
                       + [(bm, bn, st, sp, 1, nw, 1, nl) for bm, bn, nw, st, nl, _ in G._TG_NL for sp in (1, 3)]
                       # 32-deep k-steps (64-B staged rows): the 256-row tiles with 4-6 stage rings
-                      + [(bm, bn, st, sp, 1, 8, 1, nl, 0, 32) for bm, bn, st, nl in G._TG_K32 for sp in (1, 3)])
+                      + [(bm, bn, st, sp, 1, 8, 1, nl, 0, 32) for bm, bn, st, nl in G._TG_K32 for sp in (1, 3)]
+                      # 32 x 32 x 16 MFMA wave tiles (by_tile_m32), every epilogue, with and without split-K
+                      + [p[:3] + (sp,) + p[4:] for p in G._TG_M32 for sp in (1, 3)])
          if p[2] * p[4] * (p[0] + p[1]) * 2 * (p[9] if len(p) > 9 else 64) <= 150 * 1024]
 
 
@@ -416,3 +418,90 @@ def test_stream_k_fused_epilogues(plan, monkeypatch):
     for a_, b_ in zip(*outs):
         torch.testing.assert_close(a_.float(), b_.float(), atol=2e-2 * (a_.float().abs().max().item() + 1e-6),
                                    rtol=2e-2)
+
+
+# ---- small-batch MFMA GEMM with the fused epilogues (skinny_gemm.hip skinny_epi_kernel, M <= 16)
+SKE_SPLITS = [1, 3]
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("panel", [False, True])
+@pytest.mark.parametrize("sp", SKE_SPLITS)
+@pytest.mark.parametrize("N,K", [(256, 512), (2048, 2048), (2048, 5632), (96, 320)])
+def test_skinny_epi_plain_and_resadd(M, panel, sp, N, K):
+    if K % 64:
+        pytest.skip("panel / skE weights need K % 64 == 0")
+    torch.manual_seed(M * 7 + N + sp)
+    G.reserve("cuda")
+    x, w, r = _rnd(M, K), _rnd(N, K, scale=0.05), _rnd(M, N)
+    wl = G.panel_weight(w) if panel else w
+    y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    G.skinny_epi(x, wl, G.EPI_PLAIN, sp, y=y)
+    want = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), want, atol=2e-2 * want.abs().max().item(), rtol=2e-2)
+    r0 = r.clone()
+    ssq = torch.full((G.max_slots(N, M), M), float("nan"), device="cuda")
+    n = G.skinny_epi(x, wl, G.EPI_RESADD, sp, res=r, ssq_out=ssq)
+    assert n == math.ceil(N / 32)
+    want = (want.to(torch.bfloat16).float() + r0.float()).to(torch.bfloat16)
+    torch.testing.assert_close(r.float(), want.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(ssq[:n].sum(0), (r.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 4, 8, 16])
+@pytest.mark.parametrize("panel", [False, True])
+@pytest.mark.parametrize("sp", SKE_SPLITS)
+@pytest.mark.parametrize("d,nq,nkv,H", [(64, 8, 2, 256), (128, 32, 8, 4096), (64, 32, 4, 2048)])
+def test_skinny_epi_qkv(M, panel, sp, d, nq, nkv, H):
+    """QKV form: folded RMSNorm row scale, RoPE on the permuted (c, c + 16) pairs, q out, K and V^T
+    into the paged caches; vs rmsnorm -> fp32 GEMM -> rope + cache write (as test_gemv_qkv)."""
+    torch.manual_seed(M + d + sp)
+    G.reserve("cuda")
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wqkv = _rnd((nq + 2 * nkv) * d, H, scale=0.05)
+    wf = fuse_qkv_weight(wqkv, ln, nq, nkv, d)
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
+    n = ops.gemm.res_add_ssq(None, r, ssq)
+    cos_sin = ops.rope_cos_sin(4096, d, 10000.0, "cuda")
+    pos = torch.randint(0, 4000, (M,), device="cuda", dtype=torch.int32)
+    nblk = 4
+    slots = torch.randperm(nblk * 16, device="cuda")[:M].to(torch.int32)
+    if M > 2:
+        slots[1] = -1
+    kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
+    q = torch.empty(M, nq, d, dtype=torch.bfloat16, device="cuda")
+    G.skinny_epi(r, G.panel_weight(wf) if panel else wf, G.EPI_QKV, sp, ssq_in=ssq, ssq_n=n, scale=1.0 / H, eps=1e-5,
+                 pos=pos, cos_sin=cos_sin, slots=slots, q_out=q, kc=kc, vc=vc, nq=nq, nkv=nkv, d=d)
+    x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
+    qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
+    kr = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16)
+    vr = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16)
+    qr = ref.rope_and_cache(qkv, pos.cpu(), cos_sin.cpu(), slots.cpu(), kr, vr, nq, nkv, d)
+    tol = max(4e-2, 8e-3 * qr.float().abs().max().item())
+    torch.testing.assert_close(q.cpu().float(), qr.float(), atol=tol, rtol=3e-2)
+    torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=tol, rtol=3e-2)
+    torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=tol, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 5, 8, 16])
+@pytest.mark.parametrize("panel", [False, True])
+@pytest.mark.parametrize("sp", SKE_SPLITS)
+@pytest.mark.parametrize("H,I", [(256, 320), (2048, 5632)])
+def test_skinny_epi_swiglu(M, panel, sp, H, I):
+    torch.manual_seed(M + I + sp)
+    G.reserve("cuda")
+    r = _rnd(M, H)
+    ln = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = _rnd(2 * I, H, scale=0.05)
+    wf = fuse_gate_up_weight(wgu, ln)
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
+    n = ops.gemm.res_add_ssq(None, r, ssq)
+    act = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    G.skinny_epi(r, G.panel_weight(wf) if panel else wf, G.EPI_SWIGLU, sp, y=act, ssq_in=ssq, ssq_n=n, scale=1.0 / H,
+                 eps=1e-5)
+    x = ref.rms_norm(r.cpu(), ln.cpu(), 1e-5)
+    want = ref.silu_mul((x.float() @ wgu.cpu().float().t()).to(torch.bfloat16))
+    tol = max(3e-2, 8e-3 * want.abs().max().item())
+    torch.testing.assert_close(act.cpu().float(), want.float(), atol=tol, rtol=3e-2)
