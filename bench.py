@@ -416,8 +416,13 @@ def kv_placement(st0, st1):
     run, seg, tot = d("contiguous_allocs"), d("segment_allocs"), d("fresh_allocs")
     # every new block either continues its sequence's run, opens a wholly free segment, or comes
     # from the free list / LRU (scattered)
-    return {"new_blocks": int(tot), "run_share": round(run / tot, 3) if tot else None,
-            "segment_share": round(seg / tot, 3) if tot else None}
+    out = {"new_blocks": int(tot), "run_share": round(run / tot, 3) if tot else None,
+           "segment_share": round(seg / tot, 3) if tot else None}
+    # why the others did not continue: no previous block (a sequence's first), next block held by a
+    # live sequence, next block cached but hot (block_manager.h fresh)
+    for k in ("roomy_segment_allocs", "inplace_evictions", "run_miss_first", "run_miss_held", "run_miss_hot"):
+        out[k.replace("_allocs", "").replace("_evictions", "") + "_share"] = round(d(k) / tot, 3) if tot else None
+    return out
 
 
 def engine_time_split(st0, st1, window_s: float) -> dict:

@@ -1011,29 +1011,23 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   check_bf16(x, "x");
   check_bf16(w, "w");
   TORCH_CHECK(mfma == 16 || mfma == 32, "tgemm: mfma 16 or 32");
-  if (mfma == 32) {   // tgemm.hip by_tile_m32: the whitelist, so a bad plan gets a clear error
+  if (mfma == 32) {   // tgemm.hip by_tile_m32 minus kPruned: the whitelist, so a bad plan gets a clear error
     const bool known = wk == 1 && kdepth == 64 &&
                        ((nl == 0 && ks == 2 && stages == 3 && ((bm == 64 && bn == 64 && nw == 4) ||
-                                                               (bm == 64 && bn == 128 && nw == 8))) ||
-                        (nl == 0 && ks == 1 && bm == 256 && bn == 256 && nw == 8 && stages == 2) ||
-                        (nl == 8 && ks == 1 && bm == 128 && bn == 64 && nw == 4 && stages == 4) ||
-                        (nl == 8 && ks == 1 && bm == 256 && bn == 128 && nw == 8 && stages == 3));
+                                                               (bm == 64 && bn == 128 && nw == 8))));
     TORCH_CHECK(known, "tgemm: no 32x32x16 plan (", bm, "x", bn, ", ", stages, " stages, ks ", ks, ", ", nw, "+", nl,
                 " waves)");
     TORCH_CHECK(!sk_table.has_value(), "tgemm: 32x32x16 plans have no stream-K form");
   }
-  if (kdepth == 32) {   // tgemm.hip by_tile_k32: explicit whitelist
-    const bool known = ks == 1 && wk == 1 && nw == 8 &&
-                       ((bm == 256 && bn == 256 && stages == 4 && nl == 0) ||
-                        (bm == 256 && bn == 128 && stages == 6 && (nl == 0 || nl == 8)));
+  if (kdepth == 32) {   // tgemm.hip by_tile_k32 minus kPruned: explicit whitelist
+    const bool known = ks == 1 && wk == 1 && nw == 8 && bm == 256 && bn == 256 && stages == 4 && nl == 0;
     TORCH_CHECK(known, "tgemm: no 32-deep plan (", bm, "x", bn, ", ", stages, " stages, ", nw, "+", nl, " waves)");
   }
-  if (nl > 0 && kdepth != 32 && mfma == 16) {  // loader-wave plans (tgemm.hip by_tile_nl): KS 1, one k-group
+  if (nl > 0 && kdepth != 32 && mfma == 16) {  // loader-wave plans (tgemm.hip by_tile_nl minus kPruned): KS 1, one k-group
     const bool known = ks == 1 && wk == 1 &&
-                       ((bm == 64 && bn == 64 && nw == 4 &&
-                         ((nl == 2 && stages == 4) || ((nl == 4 || nl == 8) && (stages == 4 || stages == 8)))) ||
+                       ((bm == 64 && bn == 64 && nw == 4 && ((nl == 4 && stages == 4) || (nl == 8 && (stages == 4 || stages == 8)))) ||
                         (bm == 128 && bn == 64 && nw == 4 && (nl == 4 || nl == 8) && stages == 4) ||
-                        (bm == 128 && bn == 128 && nw == 4 && (nl == 4 || nl == 8) && stages == 4) ||
+                        (bm == 128 && bn == 128 && nw == 4 && nl == 8 && stages == 4) ||
                         (bm == 160 && bn == 128 && nw == 8 && (nl == 4 || nl == 6) && stages == 3) ||
                         (bm == 256 && bn == 128 && nw == 8 && (nl == 4 || nl == 8) && stages == 3));
     TORCH_CHECK(known, "tgemm: no loader-wave plan (", bm, "x", bn, ", ", stages, " stages, ", nw, "+", nl, " waves)");

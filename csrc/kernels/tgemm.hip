@@ -860,20 +860,54 @@ int launch_t(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// the stream-K instantiations: the one-split plans the autotuner pairs with a stream-K table
-// (ops.gemm._tg_cands); any other plan asked for in stream-K mode is refused (-25)
+// the stream-K instantiations: the one-split plans measured in stream-K mode, PLAIN epilogue only
+// (they never beat the one-unit plans, profiles/r3_decode_gemm_panel.md section 5, so the autotuner
+// does not offer them; tests/test_tgemm_gpu.py keeps the path honest); any other plan asked for in
+// stream-K mode is refused (-25)
 template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK, int NL, int WGM>
 constexpr bool sk_plan() {
-  return WK == 1 && ((BM == 64 && BN == 64 && ((NL == 0 && NW == 4 && ((ST == 3 && KS == 2) || (ST == 4 && KS == 1))) ||
-                                              (NL == 4 && ST == 4) || (NL == 8 && ST == 4))) ||
-                     (BM == 64 && BN == 128 && NL == 0 && NW == 8 && ST == 3 && KS == 1) ||
-                     (BM == 128 && BN == 64 && NL == 4 && ST == 4));   // (160 x 128 spilled in the segment loop)
+  return EPI == EPI_PLAIN && WK == 1 &&
+         ((BM == 64 && BN == 64 && ((NL == 0 && NW == 4 && ((ST == 3 && KS == 2) || (ST == 4 && KS == 1))) ||
+                                    (NL == 4 && ST == 4) || (NL == 8 && ST == 4))) ||
+          (BM == 64 && BN == 128 && NL == 0 && NW == 8 && ST == 3 && KS == 1) ||
+          (BM == 128 && BN == 64 && NL == 4 && ST == 4));   // (160 x 128 spilled in the segment loop)
+}
+
+// Plans no measured shape ever selected: not instantiated, refused with -28.  The evidence is every
+// autotune plan file of rounds 2-6 (42 files: TinyLlama, Llama-3-8B, Phi-3-mini, the MoE layers,
+// decode buckets 1-512 and prefill buckets) plus ops.MOE_PLANS (profiles/r6_prune.md).
+// ops.gemm._TG_PRUNED mirrors this
+// table so the autotuner never proposes them.  Fields: BM, BN, stages, KS, compute waves, WK, NL,
+// k depth, MFMA size.
+struct PlanKey { int bm, bn, st, ks, nw, wk, nl, bkt, mf; };
+constexpr PlanKey kPruned[] = {
+    {64, 128, 6, 1, 4, 1, 0, 64, 16},  {64, 128, 2, 2, 4, 1, 0, 64, 16},  {128, 64, 3, 1, 4, 1, 0, 64, 16},
+    {128, 64, 4, 1, 4, 1, 0, 64, 16},  {128, 64, 6, 1, 4, 1, 0, 64, 16},  {128, 64, 2, 2, 4, 1, 0, 64, 16},
+    {128, 64, 3, 2, 4, 1, 0, 64, 16},  {128, 128, 3, 1, 4, 1, 0, 64, 16}, {128, 128, 4, 1, 4, 1, 0, 64, 16},
+    {128, 128, 2, 2, 4, 1, 0, 64, 16}, {64, 128, 2, 1, 8, 1, 0, 64, 16},  {64, 128, 2, 2, 8, 1, 0, 64, 16},
+    {128, 128, 2, 1, 8, 1, 0, 64, 16}, {128, 128, 2, 2, 8, 1, 0, 64, 16}, {192, 128, 2, 1, 8, 1, 0, 64, 16},
+    {256, 128, 2, 1, 8, 1, 0, 64, 16}, {64, 128, 2, 2, 4, 2, 0, 64, 16},
+    {128, 64, 2, 2, 4, 2, 0, 64, 16},  {128, 64, 3, 2, 4, 2, 0, 64, 16},  {128, 128, 2, 2, 4, 2, 0, 64, 16},
+    {64, 64, 4, 1, 4, 1, 2, 64, 16},   {64, 64, 8, 1, 4, 1, 4, 64, 16},   {128, 128, 4, 1, 4, 1, 4, 64, 16},
+    {256, 128, 6, 1, 8, 1, 0, 32, 16}, {256, 128, 6, 1, 8, 1, 8, 32, 16}, {128, 64, 4, 1, 4, 1, 8, 64, 32},
+    {256, 128, 3, 1, 8, 1, 8, 64, 32}, {256, 256, 2, 1, 8, 1, 0, 64, 32},
+};
+
+template <int BM, int BN, int ST, int KS, int NW, int WK, int NL, int BKT, int MF>
+constexpr bool pruned() {
+  for (const PlanKey& p : kPruned)
+    if (p.bm == BM && p.bn == BN && p.st == ST && p.ks == KS && p.nw == NW && p.wk == WK && p.nl == NL &&
+        p.bkt == BKT && p.mf == MF)
+      return true;
+  return false;
 }
 
 template <int BM, int BN, int EPI, int ST, int KS, int NW, int WK = 1, int NL = 0, int WGM = 2, int BKT = 64, int MF = 16>
 int launch_fit(const GemmArgs& a, hipStream_t st) {
   if constexpr (ST * KS * (BM + BN) * 2 * BKT > 150 * 1024) {
     return -9;  // ring does not fit the 160 KB LDS (with the epilogue scratch)
+  } else if constexpr (pruned<BM, BN, ST, KS, NW, WK, NL, BKT, MF>()) {
+    return -28;
   } else {
     if (a.sk_table != nullptr) {
       if constexpr (BKT == 64 && MF == 16 && sk_plan<BM, BN, EPI, ST, KS, NW, WK, NL, WGM>())
@@ -887,7 +921,8 @@ int launch_fit(const GemmArgs& a, hipStream_t st) {
 
 // 32 x 32 x 16 MFMA plans (GemmArgs.mfma = 32): the decode tiles the autotuner picks on the
 // flagship (64 x 64 / 64 x 128 with k-step 128, the 128 x 64 and 256 x 128 loader-wave tiles) and
-// the 256 x 256 prefill tile; chosen per shape by measurement like every other plan
+// the 256 x 256 prefill tile; chosen per shape by measurement like every other plan.  Only the
+// 64-row forms are built (kPruned): the others lost 6-16 % to 16 x 16 x 32 (r6_gemm_fill_path.md)
 template <int EPI>
 int by_tile_m32(int bm, int bn, int stages, int ks, int nw, int nl, const GemmArgs& a, hipStream_t st) {
   if (nl == 0 && ks == 2 && stages == 3) {

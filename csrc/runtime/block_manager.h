@@ -241,6 +241,9 @@ class BlockManager {
             {"free_blocks", (long long)n_free_},
             {"contiguous_allocs", contig_},
             {"inplace_evictions", inplace_},
+            {"run_miss_first", miss_first_},
+            {"run_miss_held", miss_held_},
+            {"run_miss_hot", miss_hot_},
             {"roomy_segment_allocs", idle_allocs_},
             {"segment_allocs", seg_allocs_},
             {"fresh_allocs", fresh_allocs_},
@@ -515,9 +518,14 @@ class BlockManager {
           evict(b);
           ++contig_;
           ++inplace_;
+        } else if (blocks_[prefer].ref > 0) {
+          ++miss_held_;
+        } else {
+          ++miss_hot_;
         }
       }
     }
+    if (b < 0 && (prefer <= 0 || prefer >= (int)blocks_.size())) ++miss_first_;
     if (b < 0 && contiguous_) b = pop_segment();
     if (b < 0 && placement_ >= 2) b = pop_roomy_segment();
     if (b < 0) b = pop_free();
@@ -559,6 +567,7 @@ class BlockManager {
   std::vector<int> seg_free_;      // free blocks per segment of kSeg
   std::vector<int> seg_stack_;     // segments that were wholly free when pushed (lazy)
   long long contig_ = 0, seg_allocs_ = 0, fresh_allocs_ = 0, inplace_ = 0, idle_allocs_ = 0;
+  long long miss_first_ = 0, miss_held_ = 0, miss_hot_ = 0;   // why a new block did not continue its run
   uint64_t tick_ = 0;              // LRU releases so far (Block::rel)
   std::vector<int> held_;          // blocks with ref > 0 per segment
   std::vector<std::vector<int>> held_stacks_;  // segments by held count (lazy; see pop_roomy_segment)

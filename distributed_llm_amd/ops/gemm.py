@@ -52,19 +52,41 @@ _TG_SPLITS = (1, 2, 3, 4, 6, 8)
 # M is the smallest batch each is tried at (larger tiles only pay once M fills them)
 # (8 loader waves: a CU's LDS-DMA intake grows with the waves issuing it, ~75 GB/s at 4 and ~140 GB/s
 # at 8 on contiguous pieces, scripts/exp/intake.hip; profiles/r3_decode_gemm_panel.md)
-_TG_NL = ((64, 64, 4, 4, 2, 1), (64, 64, 4, 4, 4, 1), (64, 64, 4, 8, 4, 1), (128, 64, 4, 4, 4, 65),
-          (128, 128, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
+_TG_NL = ((64, 64, 4, 4, 4, 1), (128, 64, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
           (64, 64, 4, 4, 8, 1), (64, 64, 4, 8, 8, 1), (128, 64, 4, 4, 8, 65), (128, 128, 4, 4, 8, 65),
           (160, 128, 8, 3, 6, 129), (256, 128, 8, 3, 8, 129))
 # 32-deep k-step plans (csrc/kernels/tgemm.hip by_tile_k32): (bm, bn, stages, loaders), 8 compute waves;
 # as plan tuples (bm, bn, stages, splits, 1, 8, 1, loaders, 0, 32)
-_TG_K32 = ((256, 256, 4, 0), (256, 128, 6, 0), (256, 128, 6, 8))
+_TG_K32 = ((256, 256, 4, 0),)
 # 32 x 32 x 16 MFMA plans (csrc/kernels/tgemm.hip by_tile_m32), as full plan tuples with k depth 64 and
-# mfma 32: the flagship's decode tiles and the 256 x 256 prefill tile; measured against everything else
-_TG_M32 = ((64, 64, 3, 1, 2, 4, 1, 0, 0, 64, 32), (64, 128, 3, 1, 2, 8, 1, 0, 0, 64, 32),
-           (128, 64, 4, 1, 1, 4, 1, 8, 0, 64, 32), (256, 128, 3, 1, 1, 8, 1, 8, 0, 64, 32),
-           (256, 256, 2, 1, 1, 8, 1, 0, 0, 64, 32))
-# one-split plans with a stream-K instantiation (csrc/kernels/tgemm.hip sk_plan): (bm, bn, stages, ks, waves, loaders)
+# mfma 32: the flagship's 64-row decode tiles, measured against everything else (the 128- and 256-row
+# forms lost 6-16 % to 16 x 16 x 32 and are pruned: profiles/r6_gemm_fill_path.md, r6_prune.md)
+_TG_M32 = ((64, 64, 3, 1, 2, 4, 1, 0, 0, 64, 32), (64, 128, 3, 1, 2, 8, 1, 0, 0, 64, 32))
+# plans no measured shape ever selected, not instantiated (csrc/kernels/tgemm.hip kPruned, same table):
+# (bm, bn, stages, ks, waves, wk, loaders, k depth, mfma); profiles/r6_prune.md
+_TG_PRUNED = frozenset({
+    (64, 128, 6, 1, 4, 1, 0, 64, 16), (64, 128, 2, 2, 4, 1, 0, 64, 16), (128, 64, 3, 1, 4, 1, 0, 64, 16),
+    (128, 64, 4, 1, 4, 1, 0, 64, 16), (128, 64, 6, 1, 4, 1, 0, 64, 16), (128, 64, 2, 2, 4, 1, 0, 64, 16),
+    (128, 64, 3, 2, 4, 1, 0, 64, 16), (128, 128, 3, 1, 4, 1, 0, 64, 16), (128, 128, 4, 1, 4, 1, 0, 64, 16),
+    (128, 128, 2, 2, 4, 1, 0, 64, 16), (64, 128, 2, 1, 8, 1, 0, 64, 16), (64, 128, 2, 2, 8, 1, 0, 64, 16),
+    (128, 128, 2, 1, 8, 1, 0, 64, 16), (128, 128, 2, 2, 8, 1, 0, 64, 16), (192, 128, 2, 1, 8, 1, 0, 64, 16),
+    (256, 128, 2, 1, 8, 1, 0, 64, 16), (64, 128, 2, 2, 4, 2, 0, 64, 16),
+    (128, 64, 2, 2, 4, 2, 0, 64, 16), (128, 64, 3, 2, 4, 2, 0, 64, 16), (128, 128, 2, 2, 4, 2, 0, 64, 16),
+    (64, 64, 4, 1, 4, 1, 2, 64, 16), (64, 64, 8, 1, 4, 1, 4, 64, 16), (128, 128, 4, 1, 4, 1, 4, 64, 16),
+    (256, 128, 6, 1, 8, 1, 0, 32, 16), (256, 128, 6, 1, 8, 1, 8, 32, 16), (128, 64, 4, 1, 4, 1, 8, 64, 32),
+    (256, 128, 3, 1, 8, 1, 8, 64, 32), (256, 256, 2, 1, 8, 1, 0, 64, 32),
+})
+
+
+def tg_built(plan) -> bool:
+    """False for a plan tuple (bm, bn, stages, splits, ks, waves[, wk, loaders, sk, k depth, mfma, raster])
+    whose kernel is pruned from the build."""
+    p = tuple(plan) + (1, 0, 0, 64, 16)[max(0, len(plan) - 6):]
+    return (p[0], p[1], p[2], p[4], p[5], p[6], p[7], p[9], p[10]) not in _TG_PRUNED
+
+
+# one-split plans with a stream-K instantiation (csrc/kernels/tgemm.hip sk_plan, PLAIN epilogue only):
+# (bm, bn, stages, ks, waves, loaders)
 _SK_PLANS = {(64, 64, 3, 2, 4, 0), (64, 64, 4, 1, 4, 0), (64, 64, 4, 1, 4, 4), (64, 64, 4, 1, 4, 8),
              (64, 128, 3, 1, 8, 0), (128, 64, 4, 1, 4, 4)}
 WS_FLOATS = 16 << 20      # 64 MiB of f32 split-K slabs per (device, owner)
@@ -180,13 +202,9 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
 # core above MAX_M.
 PREFILL_MS = (2048, 4096, 8192)
 PREFILL_TUNE = False   # measured slower end to end (above); autotune(prefill=True) opts in
-STREAM_K = False       # stream-K tgemm plans in the autotuner (see _tg_cands)
-_PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8), (192, 128, 3, 1, 1, 8),
-             (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4),
+_PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
-             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32), (256, 128, 6, 1, 1, 8, 1, 8, 0, 32),
-             # the 256 x 256 tile on 32 x 32 x 16 MFMA blocks
-             (256, 256, 2, 1, 1, 8, 1, 0, 0, 64, 32))
+             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32))
 
 
 def prefill_bucket(M: int) -> int:
@@ -206,8 +224,8 @@ def tg_plan(M: int, N: int, K: int) -> Tuple[int, ...]:
     if p is not None:
         return tuple(p) + (1, 4)[len(p) - 4:] if len(p) < 6 else tuple(p)
     mt128, nt128 = -(-M // 128), -(-N // 128)
-    if mt128 * nt128 >= 224:
-        return (128, 128, 3, 1, 1, 4)
+    if mt128 * nt128 >= 224:   # 8 waves: ~10 % ahead of 4 (profiles/r2_tgemm_tune_8b_shapes.log:25)
+        return (128, 128, 3, 1, 1, 8)
     mt64, nt64 = -(-M // 64), -(-N // 64)
     if mt64 * nt128 >= 200:
         return (64, 128, 3, 1, 1, 4)
@@ -313,6 +331,8 @@ def _tgemm(ext, x, w, epi, plan, y=None, ssq_in=None, ssq_n=0, norm_scale=0.0, e
     bk = plan[9] if len(plan) >= 10 else 64
     mf = plan[10] if len(plan) >= 11 else 16
     raster = plan[11] if len(plan) >= 12 else 0
+    if sk and epi != EPI_PLAIN:
+        raise ValueError("tgemm: stream-K plans are built for the PLAIN epilogue only")
     M = x.shape[0]
     N, K = _nk(w)
     if K % (64 * ks):
@@ -772,25 +792,11 @@ def _tg_cands(M: int, N: int, K: int):
                 if _need_tg(M, N, K, bm, bn, sp, ks)[0] > WS_FLOATS:
                     continue
                 out.append((bm, bn, st, sp) + tuple(p[4:]))
-    # stream-K forms (one workgroup per CU walking equal shares of tiles x k-steps) of the one-split
-    # plans whose tile count leaves CUs idle (M = 320 gives a 64 x 64 grid 160 tiles for N = 2048).
-    # Not offered (STREAM_K False): measured, they never beat the one-unit plans on the TinyLlama
-    # shapes at M = 320-448, because the shared-operand L2 -> LDS traffic, not the idle CUs, sets
-    # the time (profiles/r3_decode_gemm_panel.md section 5); the plans stay callable (tests)
-    if torch.cuda.is_available() and STREAM_K:
-        g = _sk_grid(torch.cuda.current_device())
-        for c in list(out):
-            bm, bn, st, sp, ks, nw = c[:6]
-            if sp != 1 or (len(c) >= 7 and c[6] != 1):
-                continue
-            tiles = -(-M // bm) * -(-N // bn)
-            if tiles % g == 0 or tiles >= 2 * g or tiles * (K // (64 * ks)) < 2 * g:
-                continue
-            nl = c[7] if len(c) >= 8 else 0
-            if (bm, bn, st, ks, nw, nl) not in _SK_PLANS:
-                continue
-            out.append((bm, bn, st, 1, ks, nw, 1, nl, 1))
-    return out
+    # Stream-K forms (one workgroup per CU walking equal shares of tiles x k-steps, _SK_PLANS) are not
+    # offered: measured, they never beat the one-unit plans on the TinyLlama shapes at M = 320-448,
+    # because the shared-operand L2 -> LDS traffic, not the idle CUs, sets the time
+    # (profiles/r3_decode_gemm_panel.md section 5).  They stay built for the PLAIN epilogue (tests).
+    return [c for c in out if tg_built(c)]
 
 
 def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:

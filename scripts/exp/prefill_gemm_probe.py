@@ -14,6 +14,7 @@ SHAPES = {"tinyllama": [(2560, 2048), (2048, 2048), (11264, 2048), (2048, 5632)]
           "llama3-8b": [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]}
 PLANS = [(256, 256, 2, 1, 1, 8), (256, 256, 3, 1, 1, 8), (256, 128, 3, 1, 1, 8), (256, 128, 2, 1, 1, 8),
          (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 4), (128, 128, 2, 1, 2, 4)]
+PLANS = [p for p in PLANS if G.tg_built(p)]   # (pruned plans are not built: profiles/r6_prune.md)
 
 
 def main():

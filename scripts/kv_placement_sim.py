@@ -75,13 +75,17 @@ def simulate(convs=96, steps=5000, pool_blocks=None, seed=0, retok_same=0.3, con
     st1 = bm.stats()
     d = {k: st1.get(k, 0) - st0.get(k, 0) for k in ("contiguous_allocs", "segment_allocs", "fresh_allocs",
                                                     "prefix_hit_tokens", "prompt_tokens", "inplace_evictions",
-                                                    "roomy_segment_allocs")}
+                                                    "roomy_segment_allocs", "run_miss_first", "run_miss_held",
+                                                    "run_miss_hot")}
     err = bm.check_invariants()
     return {"pool_blocks": pool, "convs": convs, "new_blocks": d["fresh_allocs"],
             "run_share": round(d["contiguous_allocs"] / max(1, d["fresh_allocs"]), 3),
             "segment_share": round(d["segment_allocs"] / max(1, d["fresh_allocs"]), 3),
             "roomy_segment_share": round(d["roomy_segment_allocs"] / max(1, d["fresh_allocs"]), 3),
             "inplace_share": round(d["inplace_evictions"] / max(1, d["fresh_allocs"]), 3),
+            "miss_first_share": round(d["run_miss_first"] / max(1, d["fresh_allocs"]), 3),
+            "miss_held_share": round(d["run_miss_held"] / max(1, d["fresh_allocs"]), 3),
+            "miss_hot_share": round(d["run_miss_hot"] / max(1, d["fresh_allocs"]), 3),
             "prefix_hit_rate": round(d["prefix_hit_tokens"] / max(1, d["prompt_tokens"]), 3),
             "invariants": err or "ok"}
 
@@ -91,7 +95,9 @@ if __name__ == "__main__":
     ap.add_argument("--convs", type=int, default=96)
     ap.add_argument("--steps", type=int, default=5000)
     ap.add_argument("--pool", type=int, default=0)
+    ap.add_argument("--gap", type=int, nargs=2, default=(5, 40), help="turn gap range in steps")
     a = ap.parse_args()
-    for contiguous in (False, True):
-        print(json.dumps(dict(simulate(a.convs, a.steps, a.pool or None, contiguous=contiguous),
-                              contiguous=contiguous)))
+    for gap in ((0, 0), tuple(a.gap)):
+        for mode in (0, 1, 2):   # block_manager.h placement: 0 LIFO, 1 round-5 runs, 2 round-6 (default)
+            print(json.dumps(dict(simulate(a.convs, a.steps, a.pool or None, contiguous=mode, gap=gap),
+                                  placement=mode, gap=list(gap))), flush=True)

@@ -108,8 +108,11 @@ def test_bench_helpers_busy_sampler_and_kv_placement():
     assert b.stop() is None or 0.0 <= b.stop() <= 100.0
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    st0 = [{"contiguous_allocs": 10, "segment_allocs": 1, "fresh_allocs": 20}]
-    st1 = [{"contiguous_allocs": 70, "segment_allocs": 3, "fresh_allocs": 100}]
+    st0 = [{"contiguous_allocs": 10, "segment_allocs": 1, "fresh_allocs": 20, "run_miss_held": 2}]
+    st1 = [{"contiguous_allocs": 70, "segment_allocs": 3, "fresh_allocs": 100, "run_miss_held": 10,
+            "inplace_evictions": 20}]
     got = bench.kv_placement(st0, st1)
-    assert got == {"new_blocks": 80, "run_share": 0.75, "segment_share": 0.025}
+    assert {k: got[k] for k in ("new_blocks", "run_share", "segment_share")} == \
+        {"new_blocks": 80, "run_share": 0.75, "segment_share": 0.025}
+    assert got["run_miss_held_share"] == 0.1 and got["inplace_share"] == 0.25 and got["run_miss_hot_share"] == 0.0
     assert bench.kv_placement([{}], [{}])["run_share"] is None

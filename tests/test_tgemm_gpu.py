@@ -27,7 +27,7 @@ PLANS = [p for p in ([(bm, bn, st, sp, 1, nw) for bm, bn, nw in G._TG_TILES for 
                       + [(bm, bn, st, sp, 1, 8, 1, nl, 0, 32) for bm, bn, st, nl in G._TG_K32 for sp in (1, 3)]
                       # 32 x 32 x 16 MFMA wave tiles (by_tile_m32), every epilogue, with and without split-K
                       + [p[:3] + (sp,) + p[4:] for p in G._TG_M32 for sp in (1, 3)])
-         if p[2] * p[4] * (p[0] + p[1]) * 2 * (p[9] if len(p) > 9 else 64) <= 150 * 1024]
+         if p[2] * p[4] * (p[0] + p[1]) * 2 * (p[9] if len(p) > 9 else 64) <= 150 * 1024 and G.tg_built(p)]
 
 
 def _rnd(*shape, scale=1.0):
@@ -383,41 +383,20 @@ def test_stream_k_plain(plan, M, N, K):
     assert torch.equal(y, y2)
 
 
-@pytest.mark.parametrize("plan", SK_PLANS)
-def test_stream_k_fused_epilogues(plan, monkeypatch):
-    """RESADD (+ row sums), SwiGLU and QKV (+ RoPE, paged K/V) epilogues under a stream-K plan
-    equal the same ops under a one-unit plan up to the fp32 summation order."""
-    torch.manual_seed(77)
+def test_stream_k_fused_and_pruned_plans_refused():
+    """Stream-K plans are built for the PLAIN epilogue only, and the pruned plans (tgemm.hip kPruned)
+    not at all: both are refused with an error, never launched."""
     G.reserve("cuda")
-    M, H, I = 320, 512, 1024
-    nq, nkv, d = 8, 2, 64
-    base = (plan[0], plan[1], plan[2], 1, plan[4], plan[5], 1, plan[7])
-    r0, w_gu, w_d = _rnd(M, H), _rnd(2 * I, H, scale=0.05), _rnd(H, I, scale=0.05)
-    wqkv = _rnd((nq + 2 * nkv) * d, H, scale=0.05)
-    ssq = torch.rand(4, M, device="cuda") * 10 + 1
-    pos = torch.randint(0, 1000, (M,), dtype=torch.int32, device="cuda")
-    cos_sin = ops.rope_cos_sin(2048, d, 10000.0, torch.device("cuda"))
-    nb = M // 16 + 2
-    slots = torch.randperm(nb * 16, device="cuda")[:M].to(torch.int32)
-    outs = []
-    for p in (base, plan):
-        for key in ((M, 2 * I, H), (M, H, I), (M, wqkv.shape[0], H)):
-            G._P.tg_plans[key] = p
-            G._P.fused_core[key] = "tg"
-        act = G.swiglu_matmul(r0, w_gu, ssq, 4, 1e-5)
-        r = r0.clone()
-        so = torch.zeros(64, M, device="cuda")
-        n = G.matmul_resadd(act, w_d, r, so)
-        kc = torch.zeros(nb, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
-        vc = torch.zeros(nb, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
-        q = G.qkv_rope_cache(r0, wqkv, ssq, 4, 1e-5, pos, cos_sin, slots, kc, vc, nq, nkv, d)
-        outs.append((act, r, so[:n], q, kc, vc))
-    for key in ((M, 2 * I, H), (M, H, I), (M, wqkv.shape[0], H)):
-        G._P.tg_plans.pop(key, None)
-        G._P.fused_core.pop(key, None)
-    for a_, b_ in zip(*outs):
-        torch.testing.assert_close(a_.float(), b_.float(), atol=2e-2 * (a_.float().abs().max().item() + 1e-6),
-                                   rtol=2e-2)
+    x, w = _rnd(320, 512), _rnd(1024, 512, scale=0.05)
+    y = torch.empty(320, 1024, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        G._tgemm(_ext(), x, w, G.EPI_RESADD, SK_PLANS[0], y=y, ssq_out=torch.zeros(64, 320, device="cuda"))
+    for key in sorted(G._TG_PRUNED):
+        bm, bn, st, ks, nw, wk, nl, bk, mf = key
+        plan = (bm, bn, st, 1, ks, nw, wk, nl, 0, bk, mf)
+        assert not G.tg_built(plan)
+        with pytest.raises(RuntimeError):
+            G._tgemm(_ext(), x, w, G.EPI_PLAIN, plan, y=y)
 
 
 # ---- small-batch MFMA GEMM with the fused epilogues (skinny_gemm.hip skinny_epi_kernel, M <= 16)
