@@ -411,6 +411,11 @@ STEP_LOOP_TIMERS = ("t_prefill_s", "t_admit_s", "t_decode_host_pre_s", "t_decode
 CLIENT_TIMERS = ("t_encode_s", "t_output_s")
 
 
+def _peak_mem_gb(on_gpu: bool):
+    """This process's peak PyTorch device allocation (weights, KV pool, workspaces, graphs), GB."""
+    return round(torch.cuda.max_memory_allocated() / 2**30, 2) if on_gpu else None
+
+
 def kv_placement(st0, st1):
     d = lambda k: sum(b.get(k, 0) - a_.get(k, 0) for a_, b in zip(st0, st1))
     run, seg, tot = d("contiguous_allocs"), d("segment_allocs"), d("fresh_allocs")
@@ -540,8 +545,9 @@ def main() -> int:
         sm = a.small_model if on_gpu else "tiny-llama-test"
         lg = a.large_model if on_gpu else "tiny-moe-test"
         n_small = len(topo.replicas[SMALL])
-        # (a one-GPU rehearsal runs the collectives on gloo, which a hipGraph cannot capture)
-        graphs = not (a.no_graphs or rehearse)
+        # (a one-GPU rehearsal runs the TP collectives on gloo, which a hipGraph cannot capture; pools
+        # without TP groups capture their decode graphs as on a real node)
+        graphs = not (a.no_graphs or (rehearse and max(len(g) for g in topo.replicas[LARGE]) > 1))
         # a pool engine that owns its GPU (disjoint pools on a real node) gets a larger KV pool: the
         # Llama-3-8B small replicas of config 4 hold 128 conversations x ~3K tokens x 128 KB
         if a.kv_gb is None and topology == "pools" and not rehearse:
@@ -698,7 +704,8 @@ def main() -> int:
         store = dist.distributed_c10d._get_default_store()
         store.set(f"dllm_bench/{rank}", json.dumps({"tokens": float(tokens), "elapsed": elapsed, "energy": energy_j,
                                                     "lats": lats, "init_s": t_ready - _T_PROC0,
-                                                    "startup_s": (t_window0 or t_ready) - _T_PROC0}))
+                                                    "startup_s": (t_window0 or t_ready) - _T_PROC0,
+                                                    "mem_gb": _peak_mem_gb(on_gpu)}))
         tokens_all, elapsed_max, e_sum, e_bad = 0.0, 0.0, 0.0, False
         init_max, startup_max = t_ready - _T_PROC0, (t_window0 or t_ready) - _T_PROC0
         if rank == 0:
@@ -716,10 +723,12 @@ def main() -> int:
             lats = sorted(x for g in got for x in g["lats"])
             init_max = max([init_max] + [g.get("init_s", 0.0) for g in got])
             startup_max = max([startup_max] + [g.get("startup_s", 0.0) for g in got])
+            rank_mem_gb = [g.get("mem_gb") for g in got]
             degraded = degraded or bool(dead_ranks)
     else:
         tokens_all, elapsed_max = float(tokens), elapsed
         init_max, startup_max = t_ready - _T_PROC0, (t_window0 or t_ready) - _T_PROC0
+        rank_mem_gb = [_peak_mem_gb(on_gpu)]
     if rank == 0:
         value = tokens_all / max(elapsed_max, 1e-9)
         rates = sorted(r["tok"] * 1000.0 / r["lat"] for r in records if r["lat"] > 0 and r["tok"] > 0)
@@ -751,6 +760,7 @@ def main() -> int:
             # process start -> engines ready (weights init, GEMM autotune, graph capture); -> timed window
             # (plus the warmup turns); max over ranks
             "init_s": round(init_max, 1),
+            "peak_device_mem_gb_by_rank": rank_mem_gb,
             "startup_s": round(startup_max, 1),
             "scaling_note": ("every N runs BASELINE config 2 by default (one engine + routing driver per GPU, "
                              "--convs conversations each): per-GPU work is fixed, so values at N = 1..8 are one "
@@ -765,6 +775,7 @@ def main() -> int:
             "data": "synthetic: reference query sets replayed as growing conversations; random-init weights",
             "config": {"model": model_desc, "global_batch": a.convs * world,
                        "seq_len": "growing conversation (<=16384)", "parallelism": parallelism,
+                       "decode_graphs": bool(engines) and all(getattr(e, "use_graphs", False) for e in engines),
                        "strategy": a.strategy, "semantic_cache": True, "response_cache": False,
                        "perf_explore": bool(cfg.get("perf_explore")),
                        "penalise_failed_primary": bool(cfg.get("penalise_failed_primary")),

@@ -68,7 +68,8 @@ int dllm_encoder_attention(const void*, const int*, void*, int, int, int, int, f
 int dllm_embed_ln(const int*, const void*, const void*, const void*, const void*, const void*, void*, int, int, int, int,
                   float, hipStream_t);
 int dllm_res_add_ssq(const void*, long, void*, long, float*, long, int, int, int, hipStream_t);
-int dllm_gemv_slots(int, int);
+int dllm_gemv_slots(int, int, int);
+void dllm_gemv_set_grid(int, int, int);
 int dllm_gemv_epi(const void*, long, const void*, void*, long, int, int, int, int, int, void*, long, float*, long,
                   const float*, int, long, float, float, const int*, const float*, const int*, void*, void*, void*, int,
                   int, int, hipStream_t);
@@ -775,14 +776,17 @@ static void check_ssq_in(const torch::Tensor& ssq, int64_t ssq_n, int64_t M) {
               "ssq [slots, >= M]");
 }
 
-int64_t gemv_slots(int64_t N, int64_t R) { return dllm_gemv_slots((int)N, (int)R); }
+int64_t gemv_slots(int64_t M, int64_t N, int64_t R) { return dllm_gemv_slots((int)M, (int)N, (int)R); }
+void gemv_set_grid(int64_t min_blocks, int64_t xdiv, int64_t n_min) {
+  dllm_gemv_set_grid((int)min_blocks, (int)xdiv, (int)n_min);
+}
 
 int64_t gemv_resadd(torch::Tensor x, torch::Tensor w, torch::Tensor r, torch::Tensor ssq_out, int64_t R) {
   gemv_epi_checks(x, w, R, "gemv_resadd");
   check_bf16(r, "r");
   check_f32(ssq_out, "ssq_out");
   const int M = x.size(0), N = w.size(0), K = w.size(1);
-  const int slots = dllm_gemv_slots(N, (int)R);
+  const int slots = dllm_gemv_slots(M, N, (int)R);
   TORCH_CHECK(r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N && r.stride(0) % 8 == 0, "r [M, N]");
   TORCH_CHECK(ssq_out.dim() == 2 && ssq_out.stride(1) == 1 && ssq_out.size(0) >= slots && ssq_out.size(1) >= M,
               "ssq_out [>= slots, >= M]");
@@ -1311,6 +1315,7 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("gemv", &gemv);
   m.def("gemv_norm", &gemv_norm);
   m.def("gemv_slots", &gemv_slots);
+  m.def("gemv_set_grid", &gemv_set_grid);
   m.def("gemv_resadd", &gemv_resadd);
   m.def("gemv_qkv", &gemv_qkv);
   m.def("gemv_swiglu", &gemv_swiglu);

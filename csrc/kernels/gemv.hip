@@ -35,6 +35,8 @@
 // Chosen per (M, N, K) by the host autotuner (ops.gemm) only where it beats the other plans.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 enum { GV_PLAIN = 0, GV_RESADD = 1, GV_QKV = 2, GV_SWIGLU = 3 };
@@ -70,6 +72,8 @@ struct NormArgs {         // NORM: X is the sub-layer output h; the kernel forms
   float eps;
 };
 
+__host__ __device__ constexpr unsigned gemv_blocks_rt(int N, int R) { return (unsigned)((N + 4 * R - 1) / (4 * R)); }
+
 template <int M, int R, int UNR, bool SWIGLU, bool NORM, int EPI, bool XG = false>
 __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, long ldx, const u16* __restrict__ W,
                                                    u16* __restrict__ Y, long ldy, int N, int K, NormArgs na,
@@ -83,17 +87,24 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
   float* s_red = s_ep + 4 * R * M;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr bool PAIRED = EPI == GV_QKV || EPI == GV_SWIGLU;
-  int n0;
-  if constexpr (PAIRED) {
-    // 8/R workgroups per 32-column group; each takes 2R first-half columns (waves 0, 1) and the
-    // 2R second-half columns 16 further on (waves 2, 3)
-    constexpr int PER = 8 / R;
-    const int g = blockIdx.x / PER, j0 = (blockIdx.x % PER) * 2 * R;
-    n0 = g * 32 + (wave >> 1) * 16 + j0 + (wave & 1) * R;
-  } else {
-    n0 = (blockIdx.x * 4 + wave) * R;
-  }
-  const bool active = n0 < N;  // inactive waves still stage X and pass the barrier
+  // Virtual blocks: the launch may cap the grid below the column blocks (gemv_grid), and then a
+  // workgroup walks blocks vb, vb + gridDim.x, ... with X staged ONCE: at batch 2-8 a per-block
+  // X stage moved as many bytes from L2 as the weights themselves (M x K per 4R columns)
+  const int nvb = (int)gemv_blocks_rt(N, R);
+  auto col0 = [&](int vb) {
+    if constexpr (PAIRED) {
+      // 8/R blocks per 32-column group; each takes 2R first-half columns (waves 0, 1) and the
+      // 2R second-half columns 16 further on (waves 2, 3)
+      constexpr int PER = 8 / R;
+      const int g = vb / PER, j0 = (vb % PER) * 2 * R;
+      return g * 32 + (wave >> 1) * 16 + j0 + (wave & 1) * R;
+    } else {
+      return (vb * 4 + wave) * R;
+    }
+  };
+  int vb = blockIdx.x;
+  int n0 = col0(vb);
+  bool active = n0 < N;  // inactive waves still stage X and pass the barriers
   const u16* wr[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) wr[r] = W + (long)min(n0 + r, N - 1) * K;
@@ -103,17 +114,17 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
   uint4 w[UNR][R], wn[UNR][R];
   // XG (batch 1, plain X): X travels with W in every trip (L1/L2 hits, no LDS stage, no barrier)
   uint4 xg[XG ? UNR : 1][XG ? M : 1], xgn[XG ? UNR : 1][XG ? M : 1];
-#define DLLM_GEMV_LOAD(DST, XDST, KB)                                                                \
+#define DLLM_GEMV_LOAD(DST, XDST, KB, ROWS, ACT)                                                     \
   _Pragma("unroll") for (int u = 0; u < UNR; ++u) {                                                 \
     const int k_ = (KB) + u * STEP + 8 * lane;                                                      \
     _Pragma("unroll") for (int r = 0; r < R; ++r) DST[u][r] =                                       \
-        (active && k_ < K) ? __builtin_bit_cast(uint4, ldnt_bf16x8(wr[r] + k_)) : make_uint4(0, 0, 0, 0); \
+        ((ACT) && k_ < K) ? __builtin_bit_cast(uint4, ldnt_bf16x8(ROWS[r] + k_)) : make_uint4(0, 0, 0, 0); \
     if constexpr (XG) {                                                                             \
       _Pragma("unroll") for (int m = 0; m < M; ++m) XDST[u][m] =                                    \
-          (active && k_ < K) ? ld16(X + (long)m * ldx + k_) : make_uint4(0, 0, 0, 0);               \
+          ((ACT) && k_ < K) ? ld16(X + (long)m * ldx + k_) : make_uint4(0, 0, 0, 0);                \
     }                                                                                               \
   }
-  DLLM_GEMV_LOAD(w, xg, 0)  // the first trip of W is in flight while X is staged
+  DLLM_GEMV_LOAD(w, xg, 0, wr, active)  // the first trip of W is in flight while X is staged
   if constexpr (PAIRED) {
     // folded RMSNorm row scale: lane-parallel sum of the producer's partial sums, wave w -> rows w, w + 4
     // (a GEMV producer leaves one slot per workgroup, e.g. 512 at N = 2048: 8 independent loads
@@ -190,13 +201,26 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
   }
   if constexpr (!XG) __syncthreads();
 
+  float v2sum = 0.f;  // RESADD: this lane's row sums of r^2 over the workgroup's blocks
+  for (;;) {
+  const int vn = vb + (int)gridDim.x;  // the workgroup's next block (its first W trip overlaps this one)
+  const int n0n = vn < nvb ? col0(vn) : N;
+  const bool activen = n0n < N;
+  const u16* wrn[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) wrn[r] = W + (long)min(n0n + r, N - 1) * K;
   float acc[M][R];
 #pragma unroll
   for (int m = 0; m < M; ++m)
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[m][r] = 0.f;
   for (int kb = 0; kb < K; kb += TRIP) {
-    if (kb + TRIP < K) { DLLM_GEMV_LOAD(wn, xgn, kb + TRIP) }  // next trip in flight during this one
+    // next trip in flight during this one: this block's, else the next block's first
+    if (kb + TRIP < K) {
+      DLLM_GEMV_LOAD(wn, xgn, kb + TRIP, wr, active)
+    } else if (vn < nvb) {
+      DLLM_GEMV_LOAD(wn, xgn, 0, wrn, activen)
+    }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int k = kb + u * STEP + 8 * lane;
@@ -230,7 +254,6 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
       }
     }
   }
-#undef DLLM_GEMV_LOAD
 #pragma unroll
   for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -250,11 +273,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
       }
     }
   } else if constexpr (EPI == GV_RESADD) {
-    // r = bf16(bf16(acc) + r) (res_add_ssq numerics), then this workgroup's partial row sums of
-    // r^2.  Lane (m, r) = (lane / R, lane % R) owns one output, so a wave's residual
-    // read-modify-writes go out together (one round trip, not M x R dependent ones from lane 0);
-    // after the butterfly every lane holds every acc[m][r].
-    float v2 = 0.f;
+    // r = bf16(bf16(acc) + r) (res_add_ssq numerics), summed into this lane's r^2.  Lane (m, r) =
+    // (lane / R, lane % R) owns one output, so a wave's residual read-modify-writes go out together
+    // (one round trip, not M x R dependent ones from lane 0); after the butterfly every lane holds
+    // every acc[m][r].
     if (active && lane < M * R) {
       const int lm = lane / R, lr = lane % R;
       float a = 0.f;
@@ -267,16 +289,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
         u16* p = ea.res + (long)lm * ea.ldr + n0 + lr;
         const float v = bf2f(f2bf(bf2f(f2bf(a)) + bf2f(*p)));
         *p = f2bf(v);
-        v2 = v * v;
+        v2sum += v * v;
       }
-    }
-#pragma unroll
-    for (int o = 1; o < R; o <<= 1) v2 += __shfl_xor(v2, o, 64);  // the R lanes of a row (aligned groups)
-    if (lane < M * R && lane % R == 0) s_red[wave * M + lane / R] = v2;  // inactive waves store zeros
-    __syncthreads();
-    if (threadIdx.x < M) {
-      const int m = threadIdx.x;
-      ea.ssq_out[(long)blockIdx.x * ea.ssq_out_ld + m] = s_red[m] + s_red[M + m] + s_red[2 * M + m] + s_red[3 * M + m];
     }
   } else {
     // paired modes: accumulators meet in LDS, thread (p, m) owns pair p of row m
@@ -290,7 +304,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
     if (threadIdx.x < 2 * R * M) {
       constexpr int PER = 8 / R;
       const int m = threadIdx.x % M, p = threadIdx.x / M;
-      const int g = blockIdx.x / PER, j = (blockIdx.x % PER) * 2 * R + p;  // column offset in the group
+      const int g = vb / PER, j = (vb % PER) * 2 * R + p;  // column offset in the group
       const float x1 = s_ep[p * M + m], x2 = s_ep[(2 * R + p) * M + m];      // columns 32g + j, + 16
       const float ri = s_ri[m];
       if constexpr (EPI == GV_SWIGLU) {
@@ -321,11 +335,45 @@ __global__ void __launch_bounds__(256) gemv_kernel(const u16* __restrict__ X, lo
         }
       }
     }
+    if (vn < nvb) __syncthreads();  // s_ep is rewritten by the next block (uniform condition)
+  }
+  if (vn >= nvb) break;
+  vb = vn;
+  n0 = n0n;
+  active = activen;
+#pragma unroll
+  for (int r = 0; r < R; ++r) wr[r] = wrn[r];
+  }
+#undef DLLM_GEMV_LOAD
+  if constexpr (EPI == GV_RESADD) {
+    // this workgroup's partial row sums of r^2 over all its blocks: one slot per workgroup
+#pragma unroll
+    for (int o = 1; o < R; o <<= 1) v2sum += __shfl_xor(v2sum, o, 64);  // the R lanes of a row (aligned groups)
+    if (lane < M * R && lane % R == 0) s_red[wave * M + lane / R] = v2sum;  // inactive waves store zeros
+    __syncthreads();
+    if (threadIdx.x < M) {
+      const int m = threadIdx.x;
+      ea.ssq_out[(long)blockIdx.x * ea.ssq_out_ld + m] = s_red[m] + s_red[M + m] + s_red[2 * M + m] + s_red[3 * M + m];
+    }
   }
 }
 
 template <int R>
-constexpr unsigned gemv_blocks(int N) { return (unsigned)((N + 4 * R - 1) / (4 * R)); }
+constexpr unsigned gemv_blocks(int N) { return gemv_blocks_rt(N, R); }
+
+// Grid of a batch 2-8 launch with N >= g_grid_nmin: at most max(g_grid_min, N / (g_grid_xdiv M))
+// workgroups, so the X bytes every workgroup stages (M x K) stay <= 1 / g_grid_xdiv of the weight
+// bytes.  Batch 1 (X rides with W, no stage), narrower N and g_grid_xdiv = 0 keep one workgroup per
+// column block.  Measured (profiles/r6_small_batch.md, scripts/exp/gemv_probe.py): the cap takes
+// 7-27 % off the wide gate|up projections at batch 2-8 and costs 5-35 % on the narrow ones
+// (QKV / Wo / down), whose grids it would shrink below the CU count's worth of bytes in flight.
+int g_grid_min = 512, g_grid_xdiv = 4, g_grid_nmin = 8192;
+unsigned gemv_grid(int M, int N, int R) {
+  const unsigned nvb = gemv_blocks_rt(N, R);
+  if (M == 1 || g_grid_xdiv <= 0 || N < g_grid_nmin) return nvb;
+  const unsigned want = (unsigned)std::max(g_grid_min, (N + g_grid_xdiv * M - 1) / (g_grid_xdiv * M));
+  return std::min(nvb, want);
+}
 
 template <int M, int R, bool SW, bool NORM, int EPI>
 void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int N, int K, const NormArgs& na,
@@ -351,16 +399,16 @@ void launch_gemv(const void* x, long ldx, const void* w, void* y, long ldy, int 
   if constexpr (M <= 2 && R == 1) {
     if (K > 2048 && K <= 6144 && gemv_blocks<R>(N) <= 512) {
       if (K <= 4096)
-        hipLaunchKernelGGL((gemv_kernel<M, R, 8, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
+        hipLaunchKernelGGL((gemv_kernel<M, R, 8, SW, NORM, EPI>), dim3(gemv_grid(M, N, R)), dim3(256), lds, stream,
                            (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
       else
-        hipLaunchKernelGGL((gemv_kernel<M, R, 12, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
+        hipLaunchKernelGGL((gemv_kernel<M, R, 12, SW, NORM, EPI>), dim3(gemv_grid(M, N, R)), dim3(256), lds, stream,
                            (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
       return;
     }
   }
   constexpr int UNR = M <= 4 ? 4 : 2;
-  hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM, EPI>), dim3(gemv_blocks<R>(N)), dim3(256), lds, stream,
+  hipLaunchKernelGGL((gemv_kernel<M, R, UNR, SW, NORM, EPI>), dim3(gemv_grid(M, N, R)), dim3(256), lds, stream,
                      (const u16*)x, ldx, (const u16*)w, (u16*)y, ldy, N, K, na, ea);
 }
 
@@ -412,9 +460,17 @@ extern "C" int dllm_gemv(const void* x, long ldx, const void* w, void* y, long l
   return (int)hipGetLastError();
 }
 
-// Number of partial row-sum slots a GV_RESADD launch of N columns writes (one per workgroup).
-extern "C" int dllm_gemv_slots(int N, int R) {
-  return R == 1 ? (int)gemv_blocks<1>(N) : R == 2 ? (int)gemv_blocks<2>(N) : R == 4 ? (int)gemv_blocks<4>(N) : -1;
+// Number of partial row-sum slots a GV_RESADD launch of M x N writes (one per workgroup).
+extern "C" int dllm_gemv_slots(int M, int N, int R) {
+  return (R == 1 || R == 2 || R == 4) ? (int)gemv_grid(M, N, R) : -1;
+}
+
+// Grid policy of the batch 2-8 launches (gemv_grid); xdiv 0 = one workgroup per column block.
+// Set before any graph capture: a captured launch keeps the grid it was captured with.
+extern "C" void dllm_gemv_set_grid(int min_blocks, int xdiv, int n_min) {
+  g_grid_min = min_blocks > 0 ? min_blocks : 1;
+  g_grid_xdiv = xdiv;
+  g_grid_nmin = n_min;
 }
 
 // GEMV with a fused decoder epilogue (epi: 1 RESADD, 2 QKV, 3 SWIGLU; see the header).
@@ -423,7 +479,7 @@ extern "C" int dllm_gemv_slots(int N, int R) {
 //   SWIGLU: w = interleaved gate|up rows (N = 2I), y = act [M, I]
 // Host contract (csrc/bindings.cpp checks it): M in {1, 2, 4, 8}, R in {1, 2, 4}, K % 8 == 0,
 // M x K x 2 B <= 64 KB, N % 32 == 0 for QKV / SWIGLU (and d % 32 == 0 for QKV), ssq_out rows >=
-// dllm_gemv_slots(N, R) for RESADD.
+// dllm_gemv_slots(M, N, R) for RESADD.
 extern "C" int dllm_gemv_epi(const void* x, long ldx, const void* w, void* y, long ldy, int M, int N, int K, int R,
                              int epi, void* res, long ldr, float* ssq_out, long ssq_out_ld, const float* ssq_in,
                              int ssq_n, long ssq_in_ld, float scale, float eps, const int* pos, const float* cos_sin,

@@ -15,6 +15,8 @@
 //              issues its NEXT phase's weight rows before it waits at a seam (run-ahead in VGPRs:
 //              weights do not depend on the seam)
 //   persist0 : the same launch without the run-ahead (loads issued after each seam)
+//   persist_xcd_seam : persist with the XCD-hierarchical seam (grid_seam_h: 8 group counters, 8
+//              arrivals on the global one, per-group release flags)
 // Both forms use the same row -> wave -> lane mapping and reduction order, so r must be bitwise
 // equal.  Prints one JSON line per variant: us per layer.
 // Build: hipcc --offload-arch=gfx950 -O3 -o expbin/player scripts/exp/player.hip
@@ -165,7 +167,45 @@ __device__ __forceinline__ void grid_seam(unsigned* ctr, unsigned* tmo) {
   __syncthreads();
 }
 
-template <bool RUNAHEAD>
+// XCD-hierarchical seam (review item 7, round 5): the 256 workgroups arrive in 8 groups of 32 (blockIdx % 8:
+// the dispatcher deals workgroups to the 8 XCDs round-robin, so a group is one XCD's workgroups).  Each
+// group counts its own arrivals (ctr[1 + g]); only the group's last arriver touches the global counter
+// (ctr[0], 8 arrivals instead of 256) and waits for it, then raises the group's release flag
+// (ctr[9 + g]) that the other 31 poll.  Same payload rules and bounded spins as grid_seam.
+constexpr int SEAM_WORDS_H = 32;
+__device__ __forceinline__ void grid_seam_h(unsigned* ctr, unsigned* tmo) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int g = blockIdx.x & 7;
+    const unsigned prev = __hip_atomic_fetch_add(ctr + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    if (prev == (unsigned)(WG / 8) - 1) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) { __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+      }
+      __hip_atomic_store(ctr + 9 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(ctr + 9 + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) { __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <bool H>
+__device__ __forceinline__ void seam(unsigned* ctr, int i, unsigned* tmo) {
+  if constexpr (H) grid_seam_h(ctr + i * SEAM_WORDS_H, tmo);
+  else grid_seam(ctr + i * 4, tmo);
+}
+
+template <bool RUNAHEAD, bool HSEAM = false>
 __global__ void __launch_bounds__(256, 1) k_layer(Layer L, const u16* xa, float* r, float* act, unsigned* bar,
                                                    unsigned* tmo) {
   __shared__ __attribute__((aligned(16))) float xs[I];
@@ -193,7 +233,7 @@ __global__ void __launch_bounds__(256, 1) k_layer(Layer L, const u16* xa, float*
     const float y = dot_row<NCH>(wa[j], xs, lane);
     if (lane == 0) st_agent(r + row, r[row] + y);
   }
-  grid_seam(bar + 0, tmo);
+  seam<HSEAM>(bar, 0, tmo);
   // ---- phase B: gate/up
   if constexpr (!RUNAHEAD) {
 #pragma unroll
@@ -235,7 +275,7 @@ __global__ void __launch_bounds__(256, 1) k_layer(Layer L, const u16* xa, float*
       if (lane == 0) st_agent(act + p, silu_mul(g, u));
     }
   }
-  grid_seam(bar + 4, tmo);
+  seam<HSEAM>(bar, 1, tmo);
   // ---- phase C: down
   if constexpr (!RUNAHEAD) {
     load_row<NCI>(wc[0], L.wd + (long)gw * I, lane);
@@ -287,7 +327,7 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&r, H * 4));
   CHECK(hipMalloc(&r0, H * 4));
   CHECK(hipMalloc(&act, I * 4));
-  CHECK(hipMalloc(&bar, NL * 8 * 4));
+  CHECK(hipMalloc(&bar, NL * 2 * SEAM_WORDS_H * 4));
   CHECK(hipMalloc(&tmo, 4));
   CHECK(hipMemset(tmo, 0, 4));
   {
@@ -301,29 +341,32 @@ int main(int argc, char** argv) {
     hipGraph_t g;
     hipGraphExec_t ge;
     CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
-    if (mode != 0) CHECK(hipMemsetAsync(bar, 0, NL * 8 * 4, st));
+    if (mode != 0) CHECK(hipMemsetAsync(bar, 0, NL * 2 * SEAM_WORDS_H * 4, st));
     for (int l = 0; l < NL; ++l) {
       if (mode == 0) {
         hipLaunchKernelGGL(k_wo, dim3(WG), dim3(256), 0, st, Ls[l], xa, r);
         hipLaunchKernelGGL(k_gu, dim3(WG), dim3(256), 0, st, Ls[l], r, act);
         hipLaunchKernelGGL(k_d, dim3(WG), dim3(256), 0, st, Ls[l], act, r);
       } else if (mode == 1) {
-        hipLaunchKernelGGL(k_layer<true>, dim3(WG), dim3(256), 0, st, Ls[l], xa, r, act, bar + 8 * l, tmo);
+        hipLaunchKernelGGL((k_layer<true, false>), dim3(WG), dim3(256), 0, st, Ls[l], xa, r, act, bar + 8 * l, tmo);
+      } else if (mode == 2) {
+        hipLaunchKernelGGL((k_layer<false, false>), dim3(WG), dim3(256), 0, st, Ls[l], xa, r, act, bar + 8 * l, tmo);
       } else {
-        hipLaunchKernelGGL(k_layer<false>, dim3(WG), dim3(256), 0, st, Ls[l], xa, r, act, bar + 8 * l, tmo);
+        hipLaunchKernelGGL((k_layer<true, true>), dim3(WG), dim3(256), 0, st, Ls[l], xa, r, act,
+                           bar + 2 * SEAM_WORDS_H * l, tmo);
       }
     }
     CHECK(hipStreamEndCapture(st, &g));
     CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     return ge;
   };
-  const char* names[3] = {"launches", "persist", "persist0"};
-  std::vector<float> out[3];
-  float us[3];
+  const char* names[4] = {"launches", "persist", "persist0", "persist_xcd_seam"};
+  std::vector<float> out[4];
+  float us[4];
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 4; ++mode) {
     hipGraphExec_t ge = capture(mode);
     // correctness pass from r0
     CHECK(hipMemcpyAsync(r, r0, H * 4, hipMemcpyDeviceToDevice, st));
@@ -347,7 +390,7 @@ int main(int argc, char** argv) {
   }
   unsigned htmo;
   CHECK(hipMemcpy(&htmo, tmo, 4, hipMemcpyDeviceToHost));
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 4; ++mode) {
     double md = 0, mx = 0;
     for (int i = 0; i < H; ++i) {
       md = fmax(md, fabs(out[mode][i] - out[0][i]));

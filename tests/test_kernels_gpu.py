@@ -649,7 +649,8 @@ def test_embedding_with_block_table_scatter(T, n):
 @pytest.mark.parametrize("N,K,swiglu", [(2560, 2048, False), (2048, 5632, True), (1000, 520, False), (37, 1032, True),
                                          (4096, 3000, True)])
 @pytest.mark.parametrize("R", [1, 2, 4])
-def test_gemv(M, N, K, swiglu, R):
+@pytest.mark.parametrize("grid", [(512, 4, 8192), (8, 64, 0), (1, 0, 0)], ids=["default", "tight", "off"])
+def test_gemv(M, N, K, swiglu, R, grid):
     """Small-batch GEMV (csrc/kernels/gemv.hip) vs an fp32 reference; SwiGLU formed on the load;
     N not a multiple of the column block and K not a multiple of 512 exercise the tails."""
     from distributed_llm_amd.ops import gemm as G
@@ -660,7 +661,12 @@ def test_gemv(M, N, K, swiglu, R):
     w = bf(N, K, scale=0.05)
     xe = ref.silu_mul(x).float() if swiglu else x.float()
     want = xe @ w.float().t()
-    got = G._run_plan(("gemv", R), x, w, swiglu, None)
+    ext = ops._load()
+    ext.gemv_set_grid(*grid)   # batch 2-8 grid policy (gemv.hip gemv_grid); restored below
+    try:
+        got = G._run_plan(("gemv", R), x, w, swiglu, None)
+    finally:
+        ext.gemv_set_grid(512, 4, 8192)
     torch.testing.assert_close(got.float(), want, atol=3e-2, rtol=2e-2)
 
 
