@@ -440,6 +440,21 @@ __device__ __forceinline__ void tgemm_unit(const GemmArgs& a, unsigned char* sme
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
     }
+#if defined(DLLM_TG_SCHED) && DLLM_TG_SCHED == 1
+    // lab build only (scripts/exp/gemmlab.hip): one fragment read between consecutive MFMAs, the
+    // first k-step's reads up front (hipBLASLt's one-memory-op-per-MFMA-gap order)
+    if constexpr (WK == 1) {
+      constexpr int NMF = HALVES * KS * FM * FN, NDS = HALVES * KS * (FM + FN);
+      __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
+#pragma unroll
+      for (int q = 0; q < NMF; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (q < NDS - (FM + FN)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+#elif defined(DLLM_TG_SCHED) && DLLM_TG_SCHED == 2
+    __builtin_amdgcn_iglp_opt(0);
+#endif
     }
   }
   __syncthreads();  // ring idle (every load waited), rinv partials visible
