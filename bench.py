@@ -413,7 +413,10 @@ CLIENT_TIMERS = ("t_encode_s", "t_output_s")
 
 def _peak_mem_gb(on_gpu: bool):
     """This process's peak PyTorch device allocation (weights, KV pool, workspaces, graphs), GB."""
-    return round(torch.cuda.max_memory_allocated() / 2**30, 2) if on_gpu else None
+    if not on_gpu:
+        return None
+    import torch
+    return round(torch.cuda.max_memory_allocated() / 2**30, 2)
 
 
 def kv_placement(st0, st1):

@@ -204,7 +204,12 @@ PREFILL_MS = (2048, 4096, 8192)
 PREFILL_TUNE = False   # measured slower end to end (above); autotune(prefill=True) opts in
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
-             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32))
+             (256, 256, 4, 1, 1, 8, 1, 0, 0, 32),
+             # grouped tile raster (plan element 12: m-tiles per group), the 8-loader 256 x 128 tile: the
+             # fastest tgemm forms at 2-8K rows in scripts/exp/raster_probe.py (profiles/r6_gemm_fill_path.md)
+             (256, 256, 2, 1, 1, 8, 1, 0, 0, 64, 16, 8), (256, 256, 4, 1, 1, 8, 1, 0, 0, 32, 16, 8),
+             (256, 128, 3, 1, 1, 8, 1, 8, 0, 64, 16, 0), (256, 128, 3, 1, 1, 8, 1, 8, 0, 64, 16, 2),
+             (256, 128, 3, 1, 1, 8, 1, 8, 0, 64, 16, 8))
 
 
 def prefill_bucket(M: int) -> int:
