@@ -265,9 +265,15 @@ class PipelinedConversations(Conversations):
 
     def wait_turns(self, n: int, records=None) -> None:
         """Block until ``n`` turns have completed in total; from then on record into ``records``."""
+        # DLLM_VERBOSE=1: a progress line every 30 s (long rehearsals; gpurun's silence watchdog)
+        verbose = os.environ.get("DLLM_VERBOSE") == "1"
+        last = time.perf_counter()
         with self._cv:
             while self.completed < n and not self.errors:
-                self._cv.wait()
+                self._cv.wait(timeout=30.0 if verbose else None)
+                if verbose and time.perf_counter() - last >= 30.0:
+                    last = time.perf_counter()
+                    print(f"bench: {self.completed} / {n} turns completed", file=sys.stderr, flush=True)
             if self.errors:
                 raise self.errors[0]
             self.records = records
@@ -409,6 +415,27 @@ class EventConversations(PipelinedConversations):
 STEP_LOOP_TIMERS = ("t_prefill_s", "t_admit_s", "t_decode_host_pre_s", "t_decode_gpu_wait_s",
                     "t_decode_host_post_s", "t_complete_s")
 CLIENT_TIMERS = ("t_encode_s", "t_output_s")
+
+
+def _collective_cross_check(tokens, elapsed, dev, world):
+    """(backend, tokens summed, window max) from two all-reduces on ``dev`` (RCCL on a GPU node, gloo
+    on CPU); None if they did not finish within 60 s."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    try:
+        s_t = torch.tensor([float(tokens)], dtype=torch.float64, device=dev)
+        m_t = torch.tensor([float(elapsed)], dtype=torch.float64, device=dev)
+        w1 = dist.all_reduce(s_t, op=dist.ReduceOp.SUM, async_op=True)
+        w2 = dist.all_reduce(m_t, op=dist.ReduceOp.MAX, async_op=True)
+        w1.wait(timeout=datetime.timedelta(seconds=60))
+        w2.wait(timeout=datetime.timedelta(seconds=60))
+        if s_t.is_cuda:
+            torch.cuda.synchronize()
+        return {"backend": str(dist.get_backend()), "ranks": world, "tokens_sum": s_t.item(),
+                "elapsed_max_s": m_t.item()}
+    except Exception as e:  # noqa: BLE001 - reported, never fatal: the store reduction is authoritative
+        return {"backend": str(dist.get_backend()), "error": repr(e)[:200]}
 
 
 def _peak_mem_gb(on_gpu: bool):
@@ -699,6 +726,11 @@ def main() -> int:
         energy_j = 0.0   # every rank read the SAME card's counter: count it once (rank 0's)
     dead_ranks = []
     degraded = bool(cluster is not None and cluster.degraded)
+    # replicated ranks also reduce (tokens, window) through the process group's own collectives
+    # (RCCL on a GPU node: the driver's N > 1 runs then execute RCCL all-reduces across devices)
+    # and rank 0 checks them against the store reduction below
+    coll = _collective_cross_check(tokens, elapsed, dev, world) if (
+        world > 1 and not rehearse and topology == "replicated" and not degraded) else None
     if world > 1:
         # cross-rank reduction through the rendezvous store (hosted by rank 0's process): a pool
         # rank lost mid-run (fault injection, a dead GPU) leaves a missing key instead of hanging
@@ -762,6 +794,9 @@ def main() -> int:
             "per_gpu_tok_s": round(value / max(1, world), 2),
             # process start -> engines ready (weights init, GEMM autotune, graph capture); -> timed window
             # (plus the warmup turns); max over ranks
+            "collective_cross_check": (dict(coll, matches_store=bool(
+                "tokens_sum" in coll and abs(coll["tokens_sum"] - tokens_all) < 0.5
+                and abs(coll["elapsed_max_s"] - elapsed_max) < 1e-6)) if coll else None),
             "init_s": round(init_max, 1),
             "peak_device_mem_gb_by_rank": rank_mem_gb,
             "startup_s": round(startup_max, 1),

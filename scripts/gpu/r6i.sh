@@ -16,6 +16,5 @@ import json; d=json.load(open('gpurun_out/r6i/$name.json'))
 print('$name', d['value'], d['baseline_config'], d['config']['parallelism'], 'graphs', d['config'].get('decode_graphs'), 'init', d['init_s'], 'startup', d['startup_s'], 'mem', d.get('peak_device_mem_gb_by_rank'))"
 }
 rocm-smi --showmeminfo vram > gpurun_out/r6i/vram_before.txt 2>&1 || true
-run rep2 420 2 --steps 3 --warmup 1 --convs 128 --kv-gb 16 && \
 export DLLM_VERBOSE=1 && \
-run cfg4 1000 8 --baseline-config 4 --steps 2 --warmup 0 --convs 8 --kv-gb 2
+run cfg4 1000 8 --baseline-config 4 --steps 2 --warmup 0 --convs 8 --kv-gb 2 --small-new 32 --large-new 48

@@ -55,6 +55,11 @@ def test_bench_json_line(n, extra, par, cfg):
         assert out["requests"] == 2 * n
     assert out["p50_latency_ms"] > 0
     assert out["baseline_config"] == cfg
+    cc = out["collective_cross_check"]
+    if n > 1 and cfg == 2:   # replicas also reduce through the process group (gloo here, RCCL on a node)
+        assert cc["backend"] == "gloo" and cc["ranks"] == n and cc["matches_store"] is True
+    else:
+        assert cc is None
     lay = out["layout"]
     assert set(lay) >= {"small", "large"} and lay["small"]["replicas"] and lay["large"]["replicas"]
     if cfg == 5:   # every rank hosts a small replica AND a shard of the large TP group
@@ -116,3 +121,14 @@ def test_bench_helpers_busy_sampler_and_kv_placement():
         {"new_blocks": 80, "run_share": 0.75, "segment_share": 0.025}
     assert got["run_miss_held_share"] == 0.1 and got["inplace_share"] == 0.25 and got["run_miss_hot_share"] == 0.0
     assert bench.kv_placement([{}], [{}])["run_share"] is None
+
+
+def test_peak_mem_helper_gpu_branch(monkeypatch):
+    """The GPU branch of the per-rank memory report runs without a GPU here (allocator stubbed):
+    the helper must not depend on module-level imports that bench.py defers to main()."""
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.setattr(torch.cuda, "max_memory_allocated", lambda *a, **k: 3 * 2**30)
+    assert bench._peak_mem_gb(True) == 3.0
+    assert bench._peak_mem_gb(False) is None
