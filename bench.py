@@ -455,8 +455,11 @@ def kv_placement(st0, st1):
            "segment_share": round(seg / tot, 3) if tot else None}
     # why the others did not continue: no previous block (a sequence's first), next block held by a
     # live sequence, next block cached but hot (block_manager.h fresh)
-    for k in ("roomy_segment_allocs", "inplace_evictions", "run_miss_first", "run_miss_held", "run_miss_hot"):
+    for k in ("roomy_segment_allocs", "inplace_evictions", "run_miss_first", "run_miss_held", "run_miss_hot",
+              "run_miss_held_shared", "run_miss_held_segstart"):
         out[k.replace("_allocs", "").replace("_evictions", "") + "_share"] = round(d(k) / tot, 3) if tot else None
+    roomy = d("roomy_segment_allocs")
+    out["roomy_stretch_mean_blocks"] = round(d("roomy_stretch_blocks") / roomy, 1) if roomy else None
     return out
 
 
@@ -575,23 +578,25 @@ def main() -> int:
         sm = a.small_model if on_gpu else "tiny-llama-test"
         lg = a.large_model if on_gpu else "tiny-moe-test"
         n_small = len(topo.replicas[SMALL])
-        # (a one-GPU rehearsal runs the TP collectives on gloo, which a hipGraph cannot capture; pools
+        # (a one-GPU rehearsal runs the TP collectives on gloo, which a hipGraph cannot capture; tiers
         # without TP groups capture their decode graphs as on a real node)
-        graphs = not (a.no_graphs or (rehearse and max(len(g) for g in topo.replicas[LARGE]) > 1))
+        graphs = {t: not (a.no_graphs or (rehearse and max(len(g) for g in topo.replicas[t]) > 1))
+                  for t in (SMALL, LARGE)}
         # a pool engine that owns its GPU (disjoint pools on a real node) gets a larger KV pool: the
         # Llama-3-8B small replicas of config 4 hold 128 conversations x ~3K tokens x 128 KB
         if a.kv_gb is None and topology == "pools" and not rehearse:
             kv_gb = 160.0
         specs = {SMALL: TierSpec(mdl(sm), a.small_new, 0.0, kv_cache_gb=kv_gb if on_gpu else 0.1,
-                                 max_num_seqs=max(16, a.convs * world), graphs=graphs),
+                                 max_num_seqs=max(16, a.convs * world), graphs=graphs[SMALL]),
                  LARGE: TierSpec(mdl(lg), a.large_new, large_sampling["temperature"], large_sampling["top_k"],
                                  large_sampling["top_p"], kv_cache_gb=kv_gb if on_gpu else 0.1,
-                                 max_num_seqs=max(16, a.convs * world), graphs=graphs)}
+                                 max_num_seqs=max(16, a.convs * world), graphs=graphs[LARGE])}
         cluster = Cluster(topo, specs, device=dev)
         engines = list(cluster.engines.values())
-        if on_gpu and graphs:
+        if on_gpu:
             for e in engines:
-                e.capture_all(max_bs=e._bucket(min(e.R, max(16, a.convs * world))))
+                if e.use_graphs:
+                    e.capture_all(max_bs=e._bucket(min(e.R, max(16, a.convs * world))))
         tp = len(topo.replicas[LARGE][0])
         where = "small replicas co-located on the large pool's GPUs" if topology == "colocated" else "disjoint GPU pools"
         model_desc = f"{sm} small x{n_small} + {lg} large TP={tp} ({where})"
@@ -814,6 +819,7 @@ def main() -> int:
             "config": {"model": model_desc, "global_batch": a.convs * world,
                        "seq_len": "growing conversation (<=16384)", "parallelism": parallelism,
                        "decode_graphs": bool(engines) and all(getattr(e, "use_graphs", False) for e in engines),
+                       # (rank 0's engines; in a one-GPU rehearsal only TP tiers run eager)
                        "strategy": a.strategy, "semantic_cache": True, "response_cache": False,
                        "perf_explore": bool(cfg.get("perf_explore")),
                        "penalise_failed_primary": bool(cfg.get("penalise_failed_primary")),

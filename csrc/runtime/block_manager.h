@@ -244,6 +244,9 @@ class BlockManager {
             {"run_miss_first", miss_first_},
             {"run_miss_held", miss_held_},
             {"run_miss_hot", miss_hot_},
+            {"run_miss_held_shared", miss_held_shared_},
+            {"run_miss_held_segstart", miss_held_segstart_},
+            {"roomy_stretch_blocks", roomy_len_sum_},
             {"roomy_segment_allocs", idle_allocs_},
             {"segment_allocs", seg_allocs_},
             {"fresh_allocs", fresh_allocs_},
@@ -445,6 +448,7 @@ class BlockManager {
         else if (blocks_[best].in_lru) evict(best);
         else { st.pop_back(); continue; }
         ++idle_allocs_;
+        roomy_len_sum_ += best_len;
         return best;
       }
     }
@@ -520,6 +524,8 @@ class BlockManager {
           ++inplace_;
         } else if (blocks_[prefer].ref > 0) {
           ++miss_held_;
+          if (blocks_[prefer].ref > 1) ++miss_held_shared_;      // a prefix block several sequences share
+          if (prefer % kSeg == 0) ++miss_held_segstart_;         // the run reached a segment boundary
         } else {
           ++miss_hot_;
         }
@@ -568,6 +574,7 @@ class BlockManager {
   std::vector<int> seg_stack_;     // segments that were wholly free when pushed (lazy)
   long long contig_ = 0, seg_allocs_ = 0, fresh_allocs_ = 0, inplace_ = 0, idle_allocs_ = 0;
   long long miss_first_ = 0, miss_held_ = 0, miss_hot_ = 0;   // why a new block did not continue its run
+  long long miss_held_shared_ = 0, miss_held_segstart_ = 0, roomy_len_sum_ = 0;   // (diagnostics)
   uint64_t tick_ = 0;              // LRU releases so far (Block::rel)
   std::vector<int> held_;          // blocks with ref > 0 per segment
   std::vector<std::vector<int>> held_stacks_;  // segments by held count (lazy; see pop_roomy_segment)

@@ -186,3 +186,21 @@ def test_pools_event_driver_n_ranks_one_gpu(world, tmp_path):
     assert res["n_gpus"] == world and res["config"]["turn_pipelining"] == "event-driver"
     assert res["requests"] >= CONVS * STEPS and res["pool_events"]["lost_turns"] == 0
     assert 0.0 < res["small_tier_share"] < 1.0 and res["p50_latency_ms"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_replicated_full_depth_graphs_n_ranks_one_gpu(world, tmp_path):
+    """The driver's default N-GPU command (config-2 replicas) rehearsed with FULL-depth TinyLlama and
+    decode graphs ON in every rank (review item 6, round 5): the JSON reports the graphs, every
+    rank's start-up and peak device memory, and the per-GPU value."""
+    logdir = os.environ.get("DLLM_TEST_LOGDIR") or str(tmp_path)
+    os.makedirs(logdir, exist_ok=True)
+    res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world),
+                "--steps", "1", "--warmup", "1", "--convs", "16", "--kv-gb", "4", "--small-new", "16",
+                "--large-new", "24"], os.path.join(logdir, f"replicated_n{world}.log"), timeout=600)
+    assert res["n_gpus"] == world and res.get("rehearsal_one_gpu") is True and res["baseline_config"] == 2
+    assert res["config"]["decode_graphs"] is True and res["config"]["parallelism"] == f"dp{world}"
+    assert len(res["peak_device_mem_gb_by_rank"]) == world and all(m > 2.0 for m in res["peak_device_mem_gb_by_rank"])
+    assert 0 < res["init_s"] <= res["startup_s"] and res["per_gpu_tok_s"] * world == pytest.approx(res["value"], rel=1e-3)
+    assert res["collective_cross_check"] is None   # (gloo rehearsal: the cross-check runs on real multi-GPU nodes)
