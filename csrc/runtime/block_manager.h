@@ -444,6 +444,14 @@ class BlockManager {
           i = j;
         }
         if (best < 0 || best_len < kMinStretch) { st.pop_back(); continue; }  // too fragmented to help
+        // A held block right before the stretch is most likely a live run's tail that grows into
+        // it: start half-way in, so both runs have room (starting at the head put the new run's
+        // first block where the live run needed its next one: 32 % of the flagship's new blocks
+        // missed their run on a held next block, profiles/r6_kv_runs.md)
+        if (best > lo && blocks_[best - 1].ref > 0 && best_len >= 2 * kMinStretch) {
+          best += best_len / 2;
+          best_len -= best_len / 2;
+        }
         if (free_flag_[best]) take_free(best);
         else if (blocks_[best].in_lru) evict(best);
         else { st.pop_back(); continue; }

@@ -193,15 +193,16 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
     return ("skinny", ntw, splits)
 
 
-# Prefill-size buckets (M > MAX_M), opt-in (PREFILL_TUNE, autotune(prefill=True)): the fused ops' core is chosen per
-# (bucket, N, K) between one tgemm launch with the epilogue fused and hipBLASLt + the standalone
-# epilogue kernel; a prefill chunk uses the plan of the smallest bucket that holds it.  The probe
-# (scripts/exp/prefill_gemm_probe.py) has tgemm ahead on a few shapes (TinyLlama Wo at 2-4K rows,
-# gate|up at 8K: 9 %), but with those choices the flagship's prefill took 27 % longer (chunks of
-# ~5K rows run the 8K bucket's tile; profiles/r4_prefill_gemm.md), so hipBLASLt stays the default
-# core above MAX_M.
+# Prefill-size buckets (M > MAX_M, PREFILL_TUNE): the fused ops' core is chosen per (bucket, N, K)
+# between one tgemm launch with the epilogue fused and hipBLASLt + the standalone epilogue kernel;
+# a prefill chunk uses the plan of the smallest bucket that holds it.  Rounds 4-5 measured it
+# slower or neutral end to end (profiles/r4_prefill_gemm.md); with the grouped tile raster and the
+# 8-loader 256 x 128 plans among the candidates (round 6) tgemm takes 8 of TinyLlama's 12 (bucket,
+# shape) pairs (gate|up at 8K rows: 368 vs 448 us).  End to end it is within noise (+0.3 % over 7
+# same-box arms of the driver command, prefill step time lower in 2 of 3; profiles/r6_prefill_core.md),
+# and it is the default: the fused-epilogue kernel runs where it measured faster, hipBLASLt elsewhere.
 PREFILL_MS = (2048, 4096, 8192)
-PREFILL_TUNE = False   # measured slower end to end (above); autotune(prefill=True) opts in
+PREFILL_TUNE = True
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
              (256, 256, 4, 1, 1, 8, 1, 0, 0, 32),
