@@ -319,7 +319,8 @@ class LLMEngine:
         fused = [tuple(L[n].shape) for n in ("wqkv_f", "wo", "wgu_f", "wd") if m.fused and n in L]
         with ops.gemm.workspace_owner(self._ws_owner):
             ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= ops.gemm.MAX_M], self.device,
-                              verbose=os.environ.get("DLLM_VERBOSE") == "1", fused=fused)
+                              verbose=os.environ.get("DLLM_VERBOSE") == "1", fused=fused,
+                              qkv_dims=(m.nq, m.nkv, m.d) if fused else None)
             ops.gemm.reserve(self.device)
 
     # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),

@@ -203,6 +203,8 @@ def _heuristic(M: int, N: int, K: int) -> Tuple:
 # and it is the default: the fused-epilogue kernel runs where it measured faster, hipBLASLt elsewhere.
 PREFILL_MS = (2048, 4096, 8192)
 PREFILL_TUNE = True
+# decode buckets: the fused ops' core options are timed through the fused ops (_retime_fused)
+FUSED_INSITU = True
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
              (256, 256, 4, 1, 1, 8, 1, 0, 0, 32),
@@ -654,12 +656,14 @@ def _plan_key(k) -> str:
 
 
 def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False,
-             fused: Iterable[Tuple[int, int]] = (), prefill: bool = False) -> None:
+             fused: Iterable[Tuple[int, int]] = (), prefill: bool = False, qkv_dims=None) -> None:
     """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest.
 
     ``fused``: the (N, K) shapes of one decoder layer's fused ops (QKV, Wo, gate|up, down); a
     residual producer keeps the fused GEMV only where its consumer runs it too
-    (``_couple_gemv_choices``)."""
+    (``_couple_gemv_choices``).  Their fused-op cores are timed through the fused ops themselves
+    (``_retime_fused``); ``qkv_dims`` = (nq, nkv, d) of the QKV op (None: QKV keeps the stand-in
+    timings)."""
     dev = torch.device(device)
     if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
         return
@@ -679,7 +683,11 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
     shapes = list(shapes)
     fused = list(fused)
     # the fused ops' tgemm plans stream the panel weight copies: time them in that layout
-    _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set())
+    roles = {}
+    if len(fused) == 4:   # (QKV, Wo, gate|up, down) of a dense layer
+        roles = {tuple(fused[0]): "qkv", tuple(fused[1]): "resadd", tuple(fused[2]): "swiglu",
+                 tuple(fused[3]): "resadd"}
+    _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set(), roles, qkv_dims)
     _couple_gemv_choices(fused, list(ms), verbose)
     if PREFILL_TUNE or prefill:
         _autotune_prefill(fused, dev, verbose)
@@ -805,7 +813,54 @@ def _tg_cands(M: int, N: int, K: int):
     return [c for c in out if tg_built(c)]
 
 
-def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
+def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
+    """Time every fused-core option of a decoder-layer shape through the fused op itself: its real
+    epilogue and its row-scale prologue over the producer's partial row sums.  The stand-in timings
+    (PLAIN tgemm, RESADD GEMV / skinny_epi) missed those: gate|up at batch 4 chose a tgemm timed at
+    13.6 us that ran 17.3 us inside the step graph (profiles/r6_small_batch.md)."""
+    M, N, K = tkey
+    copies = len(ws)
+    wsrc = lambda i: (ws[i % copies], wps[i % copies] if wps is not None else None)
+    slots_in = -(-K // 32)   # the producer's partial row sums (as many as a skinny_epi producer leaves)
+    ssq = torch.rand(slots_in, M, device=dev) + 1.0
+    if role == "resadd":
+        res = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        so = torch.empty(max_slots(N, M), M, dtype=torch.float32, device=dev)
+        fn = lambda i: matmul_resadd(x, wsrc(i)[0], res, so, wp=wsrc(i)[1])
+    elif role == "swiglu":
+        fn = lambda i: swiglu_matmul(x, wsrc(i)[0], ssq, slots_in, 1e-5, wp=wsrc(i)[1])
+    elif role == "qkv" and qkv_dims is not None:
+        nq, nkv, d = qkv_dims
+        if (nq + 2 * nkv) * d != N:
+            return None
+        nblk = -(-M // 16) + 1
+        kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device=dev)
+        pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
+        sl = torch.arange(M, dtype=torch.int32, device=dev)
+        cs = torch.rand(4096, d, device=dev)
+        fn = lambda i: qkv_rope_cache(x, wsrc(i)[0], ssq, slots_in, 1e-5, pos, cs, sl, kc, vc, nq, nkv, d,
+                                      wp=wsrc(i)[1])
+    else:
+        return None
+    saved = _P.fused_core.get(tkey)
+    out = {}
+    try:
+        for opt in opts:
+            _P.fused_core[tkey] = opt
+            try:
+                out[opt] = _time(fn)
+            except Exception:  # noqa: BLE001 - option not runnable for this shape
+                out[opt] = float("inf")
+    finally:
+        if saved is None:
+            _P.fused_core.pop(tkey, None)
+        else:
+            _P.fused_core[tkey] = saved
+    return out
+
+
+def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset(), roles=None, qkv_dims=None) -> None:
     use_tg = True
     for (N, K, sw) in shapes:
         copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
@@ -876,6 +931,11 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
                                                                              ssq_out=sq))
                         except Exception:  # noqa: BLE001 - workspace / shape refused
                             pass
+                role = (roles or {}).get((N, K))
+                if FUSED_INSITU and role is not None and M <= MAX_M and os.environ.get("DLLM_FUSED_CORE") is None:
+                    insitu = _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev)
+                    if insitu:
+                        opts = insitu
                 _P.fused_core[tkey] = min(opts, key=opts.get)
                 _P.fused_opts[tkey] = opts
             if verbose:
@@ -885,7 +945,9 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset()) -> None:
                 top = sorted(tgc, key=res.get)[:4]
                 extra += " | tg top: " + " ".join(f"{c[1:]}:{res[c]:.1f}" for c in top)
                 if post is not None:
-                    extra += f" | post {post:.1f}us -> core {_P.fused_core[tkey]}"
+                    extra += (f" | post {post:.1f}us | fused " +
+                              " ".join(f"{k}:{v:.1f}" for k, v in _P.fused_opts[tkey].items()) +
+                              f" -> core {_P.fused_core[tkey]}")
                 print(f"gemm M={M} N={N} K={K} swiglu={sw}: best={best} {res[best]:.1f}us "
                       f"({N * K * 2 / res[best] / 1e3:.0f} GB/s, {2 * M * N * K / res[best] / 1e6:.0f} TF/s; "
                       f"blas {res[('blas',)]:.1f}us; {extra})", flush=True)
