@@ -839,8 +839,11 @@ def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
         pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
         sl = torch.arange(M, dtype=torch.int32, device=dev)
         cs = torch.rand(4096, d, device=dev)
+        # (d = 64 decode hands V over row-major, as models.llama does: the one-launch cores then skip
+        # the strided V^T cache writes)
+        vn = torch.empty(M, nkv * d, dtype=torch.bfloat16, device=dev) if d == 64 else None
         fn = lambda i: qkv_rope_cache(x, wsrc(i)[0], ssq, slots_in, 1e-5, pos, cs, sl, kc, vc, nq, nkv, d,
-                                      wp=wsrc(i)[1])
+                                      wp=wsrc(i)[1], v_new=vn)
     else:
         return None
     saved = _P.fused_core.get(tkey)

@@ -498,3 +498,24 @@ def test_skinny_epi_swiglu(M, panel, sp, H, I):
     want = ref.silu_mul((x.float() @ wgu.cpu().float().t()).to(torch.bfloat16))
     tol = max(3e-2, 8e-3 * want.abs().max().item())
     torch.testing.assert_close(act.cpu().float(), want.float(), atol=tol, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [4, 64])
+def test_fused_core_timed_in_situ(M):
+    """The autotuner times every fused-op core option of a decoder layer through the fused op
+    itself (ops.gemm._retime_fused): each option runs, and the chosen core is the fastest of them."""
+    G.reserve("cuda")
+    H, I, nq, nkv, d = 512, 1024, 8, 2, 64
+    fused = [((nq + 2 * nkv) * d, H), (H, nq * d), (2 * I, H), (H, I)]
+    shapes = sorted({(n, k, False) for n, k in fused})
+    saved = (dict(G._P.fused_core), dict(G._P.fused_opts), dict(G._P.tg_plans), dict(G._P.plans))
+    try:
+        G.autotune(shapes, [M], "cuda", fused=fused, qkv_dims=(nq, nkv, d))
+        for n, k in fused:
+            opts = G._P.fused_opts[(M, n, k)]
+            assert opts and all(math.isfinite(t) and t > 0 for t in opts.values()), opts
+            assert G._P.fused_core[(M, n, k)] == min(opts, key=opts.get)
+    finally:
+        for dst, src in zip((G._P.fused_core, G._P.fused_opts, G._P.tg_plans, G._P.plans), saved):
+            dst.clear()
+            dst.update(src)
