@@ -833,11 +833,14 @@ def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
         nq, nkv, d = qkv_dims
         if (nq + 2 * nkv) * d != N:
             return None
-        nblk = -(-M // 16) + 1
+        # the step writes each row's K / V into its own block of a large pool: scattered slots in a
+        # 64 MiB-per-cache pool (contiguous slots in a tiny cache timed the split form's K / V^T
+        # writes 3.5 us per call faster than they run in the flagship's step)
+        nblk = max(-(-M // 16) + 1, (64 << 20) // (nkv * 16 * d * 2))
         kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device=dev)
         vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device=dev)
-        pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
-        sl = torch.arange(M, dtype=torch.int32, device=dev)
+        pos = torch.randint(100, 4000, (M,), dtype=torch.int32, device=dev)
+        sl = (torch.randperm(nblk, device=dev)[:M] * 16 + torch.randint(0, 16, (M,), device=dev)).to(torch.int32)
         cs = torch.rand(4096, d, device=dev)
         # (d = 64 decode hands V over row-major, as models.llama does: the one-launch cores then skip
         # the strided V^T cache writes)
@@ -849,12 +852,14 @@ def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
     saved = _P.fused_core.get(tkey)
     out = {}
     try:
-        for opt in opts:
-            _P.fused_core[tkey] = opt
-            try:
-                out[opt] = _time(fn)
-            except Exception:  # noqa: BLE001 - option not runnable for this shape
-                out[opt] = float("inf")
+        for _ in range(2):   # two interleaved passes, the faster of each option's two times
+            for opt in opts:
+                _P.fused_core[tkey] = opt
+                try:
+                    t = _time(fn)
+                except Exception:  # noqa: BLE001 - option not runnable for this shape
+                    t = float("inf")
+                out[opt] = min(out.get(opt, float("inf")), t)
     finally:
         if saved is None:
             _P.fused_core.pop(tkey, None)
