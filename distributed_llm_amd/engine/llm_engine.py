@@ -320,7 +320,8 @@ class LLMEngine:
         with ops.gemm.workspace_owner(self._ws_owner):
             ops.gemm_autotune(sorted(shapes), [b for b in self.buckets if b <= ops.gemm.MAX_M], self.device,
                               verbose=os.environ.get("DLLM_VERBOSE") == "1", fused=fused,
-                              qkv_dims=(m.nq, m.nkv, m.d) if fused else None)
+                              qkv_dims=(m.nq, m.nkv, m.d) if fused else None,
+                              qkv_cache=self.kv_caches[0] if fused else None)
             ops.gemm.reserve(self.device)
 
     # Decode attention split-K.  Default: a static split count sized to the batch (_splits_for),

@@ -656,14 +656,15 @@ def _plan_key(k) -> str:
 
 
 def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device, verbose: bool = False,
-             fused: Iterable[Tuple[int, int]] = (), prefill: bool = False, qkv_dims=None) -> None:
+             fused: Iterable[Tuple[int, int]] = (), prefill: bool = False, qkv_dims=None, qkv_cache=None) -> None:
     """Measure every candidate plan for each (M, N, K, swiglu) and keep the fastest.
 
     ``fused``: the (N, K) shapes of one decoder layer's fused ops (QKV, Wo, gate|up, down); a
     residual producer keeps the fused GEMV only where its consumer runs it too
     (``_couple_gemv_choices``).  Their fused-op cores are timed through the fused ops themselves
     (``_retime_fused``); ``qkv_dims`` = (nq, nkv, d) of the QKV op (None: QKV keeps the stand-in
-    timings)."""
+    timings); ``qkv_cache`` = one layer's (K, V^T) caches of the engine, which the QKV timing writes
+    into at scattered free blocks (the TLB reach of a whole serving pool, not of a small buffer)."""
     dev = torch.device(device)
     if dev.type != "cuda" or os.environ.get("DLLM_GEMM") == "blas":
         return
@@ -687,7 +688,8 @@ def autotune(shapes: Iterable[Tuple[int, int, bool]], ms: Iterable[int], device,
     if len(fused) == 4:   # (QKV, Wo, gate|up, down) of a dense layer
         roles = {tuple(fused[0]): "qkv", tuple(fused[1]): "resadd", tuple(fused[2]): "swiglu",
                  tuple(fused[3]): "resadd"}
-    _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set(), roles, qkv_dims)
+    _autotune(shapes, list(ms), dev, verbose, {tuple(f) for f in fused} if W_PANEL else set(), roles, qkv_dims,
+              qkv_cache)
     _couple_gemv_choices(fused, list(ms), verbose)
     if PREFILL_TUNE or prefill:
         _autotune_prefill(fused, dev, verbose)
@@ -813,7 +815,7 @@ def _tg_cands(M: int, N: int, K: int):
     return [c for c in out if tg_built(c)]
 
 
-def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
+def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev, qkv_cache=None):
     """Time every fused-core option of a decoder-layer shape through the fused op itself: its real
     epilogue and its row-scale prologue over the producer's partial row sums.  The stand-in timings
     (PLAIN tgemm, RESADD GEMV / skinny_epi) missed those: gate|up at batch 4 chose a tgemm timed at
@@ -833,12 +835,17 @@ def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
         nq, nkv, d = qkv_dims
         if (nq + 2 * nkv) * d != N:
             return None
-        # the step writes each row's K / V into its own block of a large pool: scattered slots in a
-        # 64 MiB-per-cache pool (contiguous slots in a tiny cache timed the split form's K / V^T
-        # writes 3.5 us per call faster than they run in the flagship's step)
-        nblk = max(-(-M // 16) + 1, (64 << 20) // (nkv * 16 * d * 2))
-        kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device=dev)
-        vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device=dev)
+        # the step writes each row's K / V into its own block of a large pool: scattered slots in the
+        # engine's own cache (else a 64 MiB pool; contiguous slots in a tiny cache timed the split
+        # form's K / V^T writes 3.5 us per call faster than they run in the flagship's step)
+        if (qkv_cache is not None and tuple(qkv_cache[0].shape[1:]) == (nkv, 16, d)
+                and qkv_cache[0].shape[0] >= M + 1):
+            kc, vc = qkv_cache
+            nblk = kc.shape[0]
+        else:
+            nblk = max(-(-M // 16) + 1, (64 << 20) // (nkv * 16 * d * 2))
+            kc = torch.zeros(nblk, nkv, 16, d, dtype=torch.bfloat16, device=dev)
+            vc = torch.zeros(nblk, nkv, d, 16, dtype=torch.bfloat16, device=dev)
         pos = torch.randint(100, 4000, (M,), dtype=torch.int32, device=dev)
         sl = (torch.randperm(nblk, device=dev)[:M] * 16 + torch.randint(0, 16, (M,), device=dev)).to(torch.int32)
         cs = torch.rand(4096, d, device=dev)
@@ -868,7 +875,8 @@ def _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev):
     return out
 
 
-def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset(), roles=None, qkv_dims=None) -> None:
+def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset(), roles=None, qkv_dims=None,
+              qkv_cache=None) -> None:
     use_tg = True
     for (N, K, sw) in shapes:
         copies = max(2, min(64, math.ceil((768 << 20) / (N * K * 2))))
@@ -941,7 +949,7 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset(), roles=No
                             pass
                 role = (roles or {}).get((N, K))
                 if FUSED_INSITU and role is not None and M <= MAX_M and os.environ.get("DLLM_FUSED_CORE") is None:
-                    insitu = _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev)
+                    insitu = _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev, qkv_cache)
                     if insitu:
                         opts = insitu
                 _P.fused_core[tkey] = min(opts, key=opts.get)
