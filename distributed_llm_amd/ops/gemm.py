@@ -205,6 +205,11 @@ PREFILL_MS = (2048, 4096, 8192)
 PREFILL_TUNE = True
 # decode buckets: the fused ops' core options are timed through the fused ops (_retime_fused)
 FUSED_INSITU = True
+# the split form (vendor / plain GEMM + standalone epilogue kernel) wins a fused op only when it is
+# more than 3 % faster than the best one-launch core: measured in the flagship's step, the split
+# QKV ran 24.6 us against 21-23 us timed in situ (the one-launch tgemm: 22.3 us in the step, 21.5-22
+# in situ), so near-ties flipped the choice run to run (profiles/r6_small_batch.md)
+SPLIT_MARGIN = 1.03
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
              (256, 256, 4, 1, 1, 8, 1, 0, 0, 32),
@@ -952,7 +957,11 @@ def _autotune(shapes, ms, dev, verbose: bool, panel_shapes=frozenset(), roles=No
                     insitu = _retime_fused(tkey, role, opts, x, ws, wps, qkv_dims, dev, qkv_cache)
                     if insitu:
                         opts = insitu
-                _P.fused_core[tkey] = min(opts, key=opts.get)
+                core = min(opts, key=opts.get)
+                one = {c: t for c, t in opts.items() if c != "lin"}
+                if core == "lin" and one and min(one.values()) <= SPLIT_MARGIN * opts["lin"]:
+                    core = min(one, key=one.get)
+                _P.fused_core[tkey] = core
                 _P.fused_opts[tkey] = opts
             if verbose:
                 bk = {k: min((c for c in res if c[0] == k), key=res.get, default=None)

@@ -514,7 +514,10 @@ def test_fused_core_timed_in_situ(M):
         for n, k in fused:
             opts = G._P.fused_opts[(M, n, k)]
             assert opts and all(math.isfinite(t) and t > 0 for t in opts.values()), opts
-            assert G._P.fused_core[(M, n, k)] == min(opts, key=opts.get)
+            core, best = G._P.fused_core[(M, n, k)], min(opts, key=opts.get)
+            # the fastest option, or a one-launch core within SPLIT_MARGIN of a faster split form
+            assert core == best or (best == "lin" and core != "lin" and opts[core] <= G.SPLIT_MARGIN * opts["lin"]
+                                    and opts[core] == min(t for c, t in opts.items() if c != "lin"))
     finally:
         for dst, src in zip((G._P.fused_core, G._P.fused_opts, G._P.tg_plans, G._P.plans), saved):
             dst.clear()
