@@ -206,9 +206,8 @@ PREFILL_TUNE = True
 # decode buckets: the fused ops' core options are timed through the fused ops (_retime_fused)
 FUSED_INSITU = True
 # the split form (vendor / plain GEMM + standalone epilogue kernel) wins a fused op only when it is
-# more than 3 % faster than the best one-launch core: measured in the flagship's step, the split
-# QKV ran 24.6 us against 21-23 us timed in situ (the one-launch tgemm: 22.3 us in the step, 21.5-22
-# in situ), so near-ties flipped the choice run to run (profiles/r6_small_batch.md)
+# more than 3 % faster than the best one-launch core: on near-ties (QKV at the 512 bucket, 21-23 us
+# either way in situ) the choice flipped run to run (profiles/r6_small_batch.md)
 SPLIT_MARGIN = 1.03
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
