@@ -44,3 +44,24 @@ def test_fixed_plan_lists_are_built():
     for p in ops.MOE_PLANS.values():   # (bm, bn13, st13, ks13, nw13, bn2, st2, ks2, nw2)
         assert G.tg_built((p[0], p[1], p[2], 1, p[3], p[4]))
         assert G.tg_built((p[0], p[5], p[6], 1, p[7], p[8]))
+
+
+def test_gemv_grid_policy_host():
+    """Batch 2-8 GEMV grid (csrc/kernels/gemv.hip gemv_grid): capped at max(512, N / 4M) workgroups
+    from N = 8192 on, one workgroup per 4R columns otherwise and at batch 1.  Host-side launch
+    geometry: the native library answers without a GPU."""
+    try:
+        ext = ops._load()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip(f"native library not built here: {e}")
+    blocks = lambda N, R: -(-N // (4 * R))
+    for M in (1, 2, 4, 8):
+        for N in (2048, 2560, 6144, 8192, 11264, 28672, 32000, 128256):
+            for R in (1, 2, 4):
+                want = blocks(N, R) if (M == 1 or N < 8192) else min(blocks(N, R), max(512, -(-N // (4 * M))))
+                assert ext.gemv_slots(M, N, R) == want, (M, N, R)
+    ext.gemv_set_grid(1, 0, 0)   # policy off: one workgroup per column block everywhere
+    try:
+        assert ext.gemv_slots(8, 28672, 1) == blocks(28672, 1)
+    finally:
+        ext.gemv_set_grid(512, 4, 8192)
