@@ -1029,7 +1029,8 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
   }
   if (nl > 0 && kdepth != 32 && mfma == 16) {  // loader-wave plans (tgemm.hip by_tile_nl minus kPruned): KS 1, one k-group
     const bool known = ks == 1 && wk == 1 &&
-                       ((bm == 64 && bn == 64 && nw == 4 && ((nl == 4 && stages == 4) || (nl == 8 && (stages == 4 || stages == 8)))) ||
+                       ((bm == 16 && bn == 128 && nw == 4 && nl == 6 && (stages == 4 || stages == 8)) ||
+                        (bm == 64 && bn == 64 && nw == 4 && ((nl == 4 && stages == 4) || (nl == 8 && (stages == 4 || stages == 8)))) ||
                         (bm == 128 && bn == 64 && nw == 4 && (nl == 4 || nl == 8) && stages == 4) ||
                         (bm == 128 && bn == 128 && nw == 4 && nl == 8 && stages == 4) ||
                         (bm == 160 && bn == 128 && nw == 8 && (nl == 4 || nl == 6) && stages == 3) ||

@@ -970,6 +970,12 @@ int by_tile_k32(int bm, int bn, int stages, int nw, int nl, const GemmArgs& a, h
 // loader-wave tiles (NL > 0; KS 1): the decode-size plans the lab measured fastest
 template <int EPI>
 int by_tile_nl(int bm, int bn, int stages, int nw, int nl, const GemmArgs& a, hipStream_t st) {
+  // batch <= 16: a 16-row tile (one 16 x 16 x 32 MFMA row block per wave, 4 waves across 128 columns,
+  // WGM 1) streamed by 6 loader waves: the activation ring rows are 16, not 64 padded ones
+  if (bm == 16 && bn == 128 && nw == 4 && nl == 6) {
+    if (stages == 4) return launch_fit<16, 128, EPI, 4, 1, 4, 1, 6, 1>(a, st);
+    if (stages == 8) return launch_fit<16, 128, EPI, 8, 1, 4, 1, 6, 1>(a, st);
+  }
   if (bm == 64 && bn == 64 && nw == 4) {
     if (nl == 2 && stages == 4) return launch_fit<64, 64, EPI, 4, 1, 4, 1, 2>(a, st);
     if (nl == 4 && stages == 4) return launch_fit<64, 64, EPI, 4, 1, 4, 1, 4>(a, st);

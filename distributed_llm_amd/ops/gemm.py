@@ -52,7 +52,8 @@ _TG_SPLITS = (1, 2, 3, 4, 6, 8)
 # M is the smallest batch each is tried at (larger tiles only pay once M fills them)
 # (8 loader waves: a CU's LDS-DMA intake grows with the waves issuing it, ~75 GB/s at 4 and ~140 GB/s
 # at 8 on contiguous pieces, scripts/exp/intake.hip; profiles/r3_decode_gemm_panel.md)
-_TG_NL = ((64, 64, 4, 4, 4, 1), (128, 64, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
+_TG_NL = ((16, 128, 4, 4, 6, 1), (16, 128, 4, 8, 6, 1),   # batch <= 16 only (TG_NL16_MAX_M): 16-row tiles
+          (64, 64, 4, 4, 4, 1), (128, 64, 4, 4, 4, 65), (160, 128, 8, 3, 4, 129), (256, 128, 8, 3, 4, 129),
           (64, 64, 4, 4, 8, 1), (64, 64, 4, 8, 8, 1), (128, 64, 4, 4, 8, 65), (128, 128, 4, 4, 8, 65),
           (160, 128, 8, 3, 6, 129), (256, 128, 8, 3, 8, 129))
 # 32-deep k-step plans (csrc/kernels/tgemm.hip by_tile_k32): (bm, bn, stages, loaders), 8 compute waves;
@@ -790,7 +791,7 @@ def _tg_cands(M: int, N: int, K: int):
                         out.append((bm, bn, st, sp, ks, nw, 2))   # two k-groups of 4 waves
     if N % 8 == 0:
         for bm, bn, nw, st, nl, m_min in _TG_NL:
-            if M < m_min:
+            if M < m_min or (bm == 16 and M > 16):
                 continue
             tiles = -(-M // bm) * -(-N // bn)
             for sp in (1, 2, 3, 4):
