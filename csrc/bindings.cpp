@@ -74,7 +74,7 @@ int dllm_gemv_epi(const void*, long, const void*, void*, long, int, int, int, in
                   const float*, int, long, float, float, const int*, const float*, const int*, void*, void*, void*, int,
                   int, int, hipStream_t);
 int dllm_qkv_post(const void*, long, const float*, int, long, float, float, const int*, const float*, const int*, void*,
-                  void*, void*, int, int, int, int, hipStream_t);
+                  void*, void*, void*, int, int, int, int, hipStream_t);
 int dllm_swiglu_post(const void*, long, const float*, int, long, float, float, void*, long, int, int, hipStream_t);
 int dllm_flash_prefill(const void*, const void*, const void*, const int*, const int*, const int*, const int*, const int*,
                        const int*, void*, int, int, int, int, int, int, float, int, float*, float*, int*, hipStream_t);
@@ -1167,7 +1167,7 @@ void tgemm(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> y, int
 // standalone EPI_QKV / EPI_SWIGLU for a vendor-GEMM output y (prefill)
 void qkv_post(torch::Tensor y, torch::Tensor ssq, int64_t ssq_n, double scale, double eps, torch::Tensor pos,
               torch::Tensor cos_sin, torch::Tensor slots, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc,
-              int64_t nq, int64_t nkv, int64_t d) {
+              int64_t nq, int64_t nkv, int64_t d, c10::optional<torch::Tensor> v_rows) {
   check_bf16(y, "y");
   check_f32(ssq, "ssq");
   check_i32(pos, "positions");
@@ -1182,9 +1182,15 @@ void qkv_post(torch::Tensor y, torch::Tensor ssq, int64_t ssq_n, double scale, d
   TORCH_CHECK(kc.is_contiguous() && vc.is_contiguous() && kc.size(1) == nkv && kc.size(2) == 16 && kc.size(3) == d &&
                   vc.size(2) == d && vc.size(3) == 16,
               "cache layout");
+  void* vr = nullptr;
+  if (v_rows.has_value() && v_rows->defined()) {   // decode: V row-major, the attention kernel writes V^T
+    check_bf16(*v_rows, "v_rows");
+    TORCH_CHECK(v_rows->is_contiguous() && v_rows->numel() >= (int64_t)M * nkv * d, "v_rows [M, nkv d]");
+    vr = v_rows->data_ptr();
+  }
   ok(dllm_qkv_post(y.data_ptr(), y.stride(0), ssq.data_ptr<float>(), ssq_n, ssq.size(1), (float)scale, (float)eps,
                    pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(), q_out.data_ptr(), kc.data_ptr(),
-                   vc.data_ptr(), M, nq, nkv, d, stream()),
+                   vc.data_ptr(), vr, M, nq, nkv, d, stream()),
      "qkv_post");
 }
 
@@ -1267,7 +1273,9 @@ PYBIND11_MODULE(_hip_kernels, m) {
   m.def("moe_ffn_tg", &moe_ffn_tg);
   m.def("tgemm", &tgemm);
   m.def("res_add_ssq", &res_add_ssq);
-  m.def("qkv_post", &qkv_post);
+  m.def("qkv_post", &qkv_post, py::arg("y"), py::arg("ssq"), py::arg("ssq_n"), py::arg("scale"), py::arg("eps"),
+        py::arg("pos"), py::arg("cos_sin"), py::arg("slots"), py::arg("q_out"), py::arg("kc"), py::arg("vc"),
+        py::arg("nq"), py::arg("nkv"), py::arg("d"), py::arg("v_rows") = py::none());
   m.def("swiglu_post", &swiglu_post);
   m.def("car_alloc", &car_alloc);
   m.def("car_handle", &car_handle);

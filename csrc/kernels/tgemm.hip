@@ -1104,23 +1104,31 @@ __device__ __forceinline__ float row_rinv(const float* ssq, int n, long ld, int 
   return rsqrtf(s * scale + eps);
 }
 
-// one block per (row, 2048-column slice); a thread handles 8 RoPE pairs (q/k: 16-B loads of both halves of a 32-column
-// group) or 8 V columns
+// one block per row; a thread handles units of that row: 8 RoPE pairs (q/k: 16-B loads of both
+// halves of a 32-column group, (c, c + 16)) or 8 V columns.  Units are numbered densely (no thread
+// idles on the second half of a RoPE group) and one block covers the row: the previous layout (one
+// block per (row, 2048-column slice), the owning thread of each half-group only) left half the
+// q/k threads and most of the second slice idle and cost 8.9 us per call at the decode buckets
+// (profiles/r6_end_kernels.md).  v_rows (decode, d = 64): V goes row-major to v_rows [M, nkv d],
+// coalesced, and the decode attention kernel writes each sequence's newest V^T itself
+// (gemm.qkv_rope_cache v_new), instead of 2-byte stores 32 B apart into the V^T cache.
 __global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y, long ldy, const float* __restrict__ ssq,
                                                        int ssq_n, long ssq_ld, float scale, float eps,
                                                        const int* __restrict__ pos, const float* __restrict__ cos_sin,
                                                        const int* __restrict__ slots, u16* __restrict__ q_out,
-                                                       u16* __restrict__ kc, u16* __restrict__ vc, int nq, int nkv, int d) {
+                                                       u16* __restrict__ kc, u16* __restrict__ vc, u16* __restrict__ v_rows,
+                                                       int nq, int nkv, int d) {
   const int m = blockIdx.x;
   const float ri = ssq ? row_rinv(ssq, ssq_n, ssq_ld, m, scale, eps) : 1.f;
-  const int hd = d / 2, qcols = nq * d, kcols = nkv * d, N = qcols + kcols + nkv * d;
+  const int hd = d / 2, qcols = nq * d, kcols = nkv * d, vcols = nkv * d;
+  const int rope_units = (qcols + kcols) / 16, units = rope_units + vcols / 8;
   const int slot = slots[m];
   const long blk = slot >> 4, off = slot & 15;
   const float* cs = cos_sin + (long)pos[m] * d;
   const u16* yr = y + (long)m * ldy;
-  for (int c = (blockIdx.y * blockDim.x + threadIdx.x) * 8; c < N; c += gridDim.y * blockDim.x * 8) {
-    if (c < qcols + kcols) {
-      if ((c & 31) >= 16) continue;  // the thread owning the group's first half rotates both halves
+  for (int u = threadIdx.x; u < units; u += blockDim.x) {
+    if (u < rope_units) {
+      const int c = 32 * (u >> 1) + 8 * (u & 1);
       float x1[8], x2[8];
       unpack8(ld16(yr + c), x1);
       unpack8(ld16(yr + c + 16), x2);
@@ -1128,13 +1136,17 @@ __global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y
       const int cc = isq ? c : c - qcols;
       const int head = cc / d, o = cc % d;
       const int d1 = 16 * (o >> 5) + (o & 15);
+      float co[8], si[8];
+      *(float4*)&co[0] = *(const float4*)(cs + d1);
+      *(float4*)&co[4] = *(const float4*)(cs + d1 + 4);
+      *(float4*)&si[0] = *(const float4*)(cs + hd + d1);
+      *(float4*)&si[4] = *(const float4*)(cs + hd + d1 + 4);
       float r1[8], r2[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float a1 = bfr(x1[j] * ri), a2 = bfr(x2[j] * ri);
-        const float co = cs[d1 + j], si = cs[hd + d1 + j];
-        r1[j] = a1 * co - a2 * si;
-        r2[j] = a2 * co + a1 * si;
+        r1[j] = a1 * co[j] - a2 * si[j];
+        r2[j] = a2 * co[j] + a1 * si[j];
       }
       u16* dst = isq ? q_out + ((long)m * nq + head) * d
                      : (slot >= 0 ? kc + ((blk * nkv + head) * 16 + off) * d : nullptr);
@@ -1142,13 +1154,20 @@ __global__ void __launch_bounds__(256) qkv_post_kernel(const u16* __restrict__ y
         st16(dst + d1, pack8(r1));
         st16(dst + hd + d1, pack8(r2));
       }
-    } else if (slot >= 0) {
+    } else {
+      const int cc = 8 * (u - rope_units);
       float v[8];
-      unpack8(ld16(yr + c), v);
-      const int cc = c - qcols - kcols, head = cc / d, dim = cc % d;
-      u16* vo = vc + ((blk * nkv + head) * d) * 16 + off;
+      unpack8(ld16(yr + qcols + kcols + cc), v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vo[(long)(dim + j) * 16] = f2bf(v[j] * ri);
+      for (int j = 0; j < 8; ++j) v[j] *= ri;
+      if (v_rows) {
+        st16(v_rows + (long)m * vcols + cc, pack8(v));
+      } else if (slot >= 0) {
+        const int head = cc / d, dim = cc % d;
+        u16* vo = vc + ((blk * nkv + head) * d) * 16 + off;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vo[(long)(dim + j) * 16] = f2bf(v[j]);
+      }
     }
   }
 }
@@ -1174,12 +1193,13 @@ __global__ void __launch_bounds__(256) swiglu_post_kernel(const u16* __restrict_
 
 extern "C" int dllm_qkv_post(const void* y, long ldy, const float* ssq, int ssq_n, long ssq_ld, float scale, float eps,
                              const int* pos, const float* cos_sin, const int* slots, void* q_out, void* kc, void* vc,
-                             int M, int nq, int nkv, int d, hipStream_t stream) {
+                             void* v_rows, int M, int nq, int nkv, int d, hipStream_t stream) {
   if (d % 32 || ldy % 8) return -1;
   if (M <= 0) return 0;
-  const int N = (nq + 2 * nkv) * d;
-  hipLaunchKernelGGL(qkv_post_kernel, dim3(M, (N + 2047) / 2048), dim3(256), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale, eps,
-                     pos, cos_sin, slots, (u16*)q_out, (u16*)kc, (u16*)vc, nq, nkv, d);
+  const int units = (nq + nkv) * d / 16 + nkv * d / 8;
+  const int threads = units <= 128 ? 128 : 256;
+  hipLaunchKernelGGL(qkv_post_kernel, dim3(M), dim3(threads), 0, stream, (const u16*)y, ldy, ssq, ssq_n, ssq_ld, scale, eps,
+                     pos, cos_sin, slots, (u16*)q_out, (u16*)kc, (u16*)vc, (u16*)v_rows, nq, nkv, d);
   return (int)hipGetLastError();
 }
 

@@ -210,6 +210,9 @@ FUSED_INSITU = True
 # more than 3 % faster than the best one-launch core: on near-ties (QKV at the 512 bucket, 21-23 us
 # either way in situ) the choice flipped run to run (profiles/r6_small_batch.md)
 SPLIT_MARGIN = 1.03
+# decode (v_new given): the standalone QKV epilogue hands V over row-major too, as the one-launch
+# tgemm does, and the attention kernel writes the newest V^T (no 2-byte stores 32 B apart)
+QKV_POST_VROWS = True
 _PF_PLANS = ((256, 256, 2, 1, 1, 8), (256, 128, 3, 1, 1, 8), (192, 128, 3, 1, 1, 8), (128, 128, 3, 1, 1, 8),
              # 32-deep k-steps: 5-13 % ahead of the 64-deep tiles at 2-4K rows (profiles/r5_decode_gemm_lab.md)
              (256, 256, 4, 1, 1, 8, 1, 0, 0, 32),
@@ -517,9 +520,10 @@ def qkv_rope_cache(r: torch.Tensor, w: torch.Tensor, ssq: torch.Tensor, ssq_n: i
                    pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv, d=d)
         return out(False)
     if use_vendor_core(T, w.shape[0], H):
+        vr = v_new if QKV_POST_VROWS else None
         _native(r).qkv_post(_core(r, w, wp), ssq, int(ssq_n), 1.0 / H, float(eps), positions, cos_sin, slots, q,
-                            k_cache, v_cache, nq, nkv, d)
-        return out(False)
+                            k_cache, v_cache, nq, nkv, d, vr)
+        return out(vr is not None)
     _tgemm(_native(r), r, wp if wp is not None else w, EPI_QKV, tg_plan(T, w.shape[0], H), ssq_in=ssq, ssq_n=ssq_n, norm_scale=1.0 / H,
            eps=eps, pos=positions, cos_sin=cos_sin, slots=slots, q_out=q, kc=k_cache, vc=v_cache, nq=nq, nkv=nkv,
            d=d, v_rows=v_new)

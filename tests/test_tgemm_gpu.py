@@ -235,6 +235,49 @@ def test_fused_ops_both_cores(core, M, monkeypatch):
     torch.testing.assert_close(ssq3[:n3].sum(0).cpu(), (r.cpu().float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("M", [5, 77, 512])
+@pytest.mark.parametrize("nq,nkv,d", [(4, 2, 64), (32, 4, 64), (8, 2, 128)])
+def test_qkv_post_v_rows(M, nq, nkv, d, monkeypatch):
+    """Vendor core + standalone QKV epilogue (qkv_post) in the decode hand-over form: q and K as
+    the reference, V row-major into v_new (what the attention kernel moves into V^T), the V^T
+    cache untouched; without v_new, V^T written as before."""
+    monkeypatch.setenv("DLLM_FUSED_CORE", "blas")
+    torch.manual_seed(M + nq + d)
+    H = 256
+    G.reserve("cuda")
+    r = _rnd(M, H)
+    ln1 = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wqkv = _rnd((nq + 2 * nkv) * d, H, scale=0.05)
+    ssq = torch.empty(G.max_slots(H, M), M, device="cuda")
+    ops.gemm.res_add_ssq(None, r, ssq[0])
+    cos_sin = ops.rope_cos_sin(1024, d, 10000.0, "cuda")
+    pos = torch.randint(0, 1000, (M,), device="cuda", dtype=torch.int32)
+    nb = (M + 15) // 16 + 4
+    slots = torch.randperm(nb * 16, device="cuda")[:M].to(torch.int32)
+    wf = fuse_qkv_weight(wqkv, ln1, nq, nkv, d)
+    x = ref.rms_norm(r.cpu(), ln1.cpu(), 1e-5)
+    qkv = (x.float() @ wqkv.cpu().float().t()).to(torch.bfloat16)
+    kr = torch.zeros(nb, nkv, 16, d, dtype=torch.bfloat16)
+    vr = torch.zeros(nb, nkv, d, 16, dtype=torch.bfloat16)
+    qr = ref.rope_and_cache(qkv, pos.cpu(), cos_sin.cpu(), slots.cpu(), kr, vr, nq, nkv, d)
+    s_cpu = slots.cpu().long()
+    v_rows_ref = vr[s_cpu // 16, :, :, s_cpu % 16].reshape(M, nkv * d)
+    for with_v in (True, False):
+        kc = torch.zeros(nb, nkv, 16, d, dtype=torch.bfloat16, device="cuda")
+        vc = torch.zeros(nb, nkv, d, 16, dtype=torch.bfloat16, device="cuda")
+        vn = torch.full((M, nkv * d), float("nan"), dtype=torch.bfloat16, device="cuda") if with_v else None
+        out = G.qkv_rope_cache(r, wf, ssq, 1, 1e-5, pos, cos_sin, slots, kc, vc, nq, nkv, d, v_new=vn)
+        q, used = out if with_v else (out, None)
+        torch.testing.assert_close(q.cpu().float(), qr.float(), atol=4e-2, rtol=3e-2)
+        torch.testing.assert_close(kc.cpu().float(), kr.float(), atol=4e-2, rtol=3e-2)
+        if with_v:
+            assert used is vn
+            torch.testing.assert_close(vn.cpu().float(), v_rows_ref.float(), atol=4e-2, rtol=3e-2)
+            assert not vc.any()
+        else:
+            torch.testing.assert_close(vc.cpu().float(), vr.float(), atol=4e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
 @pytest.mark.parametrize("R", [1, 2, 4])
 @pytest.mark.parametrize("N,K", [(256, 512), (2048, 2048), (4096, 5632), (2048, 5632), (1024, 3000), (1024, 14336)])
