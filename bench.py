@@ -479,6 +479,9 @@ def engine_time_split(st0, st1, window_s: float) -> dict:
 
 def main() -> int:
     a = parse()
+    if os.environ.get("DLLM_STACK_DUMP_S"):   # diagnostics: every thread's stack after S seconds (hang hunting)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DLLM_STACK_DUMP_S"]), exit=False)
     import torch
     import torch.distributed as dist
     from distributed_llm_amd.config import LARGE, PRODUCTION_CFG, SMALL

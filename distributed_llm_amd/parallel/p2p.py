@@ -69,14 +69,16 @@ def on_side(dev: torch.device) -> Iterator[None]:
     s.synchronize()
 
 
-def send_bytes(data: bytes, dst: int, group=None, tag: int = 0) -> None:
+def send_bytes(data: bytes, dst: int, group=None, tag: int = 0, timeout_s: Optional[float] = None) -> None:
+    """``timeout_s``: bound each transfer's wait (a send to a peer that died mid-conversation can
+    block in gloo instead of raising); raises :class:`DataPlaneTimeout` when it passes."""
     dev = _dev(group)
     with on_side(dev):
         hdr = torch.tensor([len(data)], dtype=torch.int64, device=dev)
-        dist.send(hdr, dst, group=group, tag=tag)
+        _wait(dist.isend(hdr, dst, group=group, tag=tag), timeout_s, "send header")
         if data:
             buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
-            dist.send(buf, dst, group=group, tag=tag)
+            _wait(dist.isend(buf, dst, group=group, tag=tag), timeout_s, "send payload")
 
 
 def recv_bytes(src: int, group=None, tag: int = 0) -> bytes:
@@ -92,8 +94,8 @@ def recv_bytes(src: int, group=None, tag: int = 0) -> bytes:
         return bytes(buf.cpu().numpy().tobytes())
 
 
-def send_obj(obj: Any, dst: int, group=None, tag: int = 0) -> None:
-    send_bytes(json.dumps(obj).encode("utf-8"), dst, group, tag)
+def send_obj(obj: Any, dst: int, group=None, tag: int = 0, timeout_s: Optional[float] = None) -> None:
+    send_bytes(json.dumps(obj).encode("utf-8"), dst, group, tag, timeout_s)
 
 
 def recv_obj(src: int, group=None, tag: int = 0) -> Any:

@@ -143,9 +143,20 @@ class RemotePool(PoolClient):
                 ent.reply = {"error": why}
                 ent.event.set()
 
+    # bound on one control-plane send: a gloo send to a leader that died mid-conversation can block
+    # instead of raising (seen in the config-4 leader-death rehearsal: the router's dispatch thread
+    # hung in the send while the receiver thread had already seen the connection close)
+    CTRL_SEND_TIMEOUT_S = 30.0
+
     def _send(self, msg: Dict[str, Any]) -> None:
+        if not self.transport_ok:   # the receiver saw the connection close: never touch the pair again
+            raise RuntimeError(f"pool {self.name} transport closed")
         with self._send_lock:
-            p2p.send_obj(msg, self.leader, self.ctrl, tag=TAG_REQ)
+            try:
+                p2p.send_obj(msg, self.leader, self.ctrl, tag=TAG_REQ, timeout_s=self.CTRL_SEND_TIMEOUT_S)
+            except p2p.DataPlaneTimeout as e:   # a control-plane failure, not a data-plane one
+                self.transport_ok = False
+                raise RuntimeError(f"pool {self.name} control send: {e}") from e
 
     def data_ok(self) -> bool:
         return self.data is not None and self.data_error is None and self.alive
@@ -404,8 +415,13 @@ class RemotePool(PoolClient):
 
     # ------------------------------------------------------------------ lifecycle
     def sync(self) -> None:
-        """Barrier hand-off (bench timing): the leader barriers with its members and the node."""
-        self._send({"op": "sync", "id": 0})
+        """Barrier hand-off (bench timing): the leader barriers with its members and the node.  A
+        leader that died (e.g. in the warmup) fails its pool here instead of raising in the router:
+        the node barrier that follows then marks the node degraded."""
+        try:
+            self._send({"op": "sync", "id": 0})
+        except Exception as e:  # noqa: BLE001 - transport gone
+            self._fail_all(f"pool {self.name} sync failed: {e}")
 
     def stop(self) -> None:
         self._probe_stop.set()
