@@ -254,7 +254,30 @@ def _router_submit(ctrl, data):
             "tokens": [r.get("num_tokens") for r in res], "submit_s": submit_s}
 
 
-_ROUTER = {"concurrent": _router_concurrent, "kill": _router_kill, "hang": _router_hang,
+def _router_dead_sync(ctrl, data):
+    """The leader dies on a request (fault injection).  Afterwards the router's control-plane use of
+    that pool must fail fast instead of raising or blocking in gloo: ``sync()`` (the bench's
+    window-opening barrier hand-off) fails the pool quietly, and a later submission completes at once
+    with an error (the send checks the transport flag the receiver cleared)."""
+    from distributed_llm_amd.pools.remote import RemotePool
+    rp = RemotePool("orin", 1, ctrl, data, max_new_tokens=4, timeout_s=60)
+    r = rp.process_batch([[{"role": "user", "content": "request __die__"}]])[0]
+    t0 = time.perf_counter()
+    while rp.transport_ok and time.perf_counter() - t0 < 20:
+        time.sleep(0.05)
+    sync_err = None
+    try:
+        rp.sync()
+    except Exception as e:  # noqa: BLE001 - the regression: sync raised into the bench
+        sync_err = repr(e)
+    t1 = time.perf_counter()
+    hs = rp.submit_batch([[{"role": "user", "content": "after"}]])
+    res = rp.collect(hs)
+    return {"first": r.get("error"), "transport_ok": rp.transport_ok, "sync_err": sync_err,
+            "after_err": res[0].get("error"), "after_dt": time.perf_counter() - t1, "alive": rp.alive}
+
+
+_ROUTER = {"dead_sync": _router_dead_sync, "concurrent": _router_concurrent, "kill": _router_kill, "hang": _router_hang,
            "handoff": _router_handoff, "data_die": _router_die_in_data_ping, "revive": _router_revive,
            "stuck_lock": _router_stuck_data_lock, "submit": _router_submit}
 
@@ -336,3 +359,11 @@ def test_submit_batch_completes_each_request_on_its_own():
     assert out["order"][-1] == "long", out["order"]          # submitted earlier, finished last
     assert out["tokens"][0] == 200 and out["tokens"][1:4] == [3, 3, 3] and out["tokens"][4] == 4
     assert out["submit_s"] < 5.0                              # submission never waits for generation
+
+
+def test_dead_leader_sync_and_sends_fail_fast():
+    out = _run("dead_sync", env={"DLLM_FAULT": "die_on=__die__"})
+    assert out["first"], out                                  # the request on the dying leader failed
+    assert out["transport_ok"] is False and out["alive"] is False, out
+    assert out["sync_err"] is None, out                       # sync() did not raise into the caller
+    assert out["after_err"] and out["after_dt"] < 5.0, out    # a later send fails at once, no gloo wait
